@@ -1,0 +1,171 @@
+/*
+ * lego_frontend.h — C-ABI of the MI355X-native LeGO-LOAM-BOR front end.
+ *
+ * Drop-in boundary for the reference's per-scan hot path:
+ *   ImageProjection::cloudHandler            (LeGO-LOAM/src/imageProjection.h:16, .cpp:153-174)
+ *   FeatureAssociation::runFeatureAssociation (LeGO-LOAM/src/featureAssociation.h:19, .cpp:1386-1450)
+ * and the two value types that cross the reference's thread boundary:
+ *   ProjectionOut + cloud_msgs::cloud_info   (LeGO-LOAM/include/lego_loam/utility.h:64-70, cloud_msgs/msg/cloud_info.msg:1-13)
+ *   AssociationOut                           (utility.h:73-80)
+ *
+ * Plain C, plain pointers and sizes; no torch / ROS / PCL types.  Every entry point
+ * returns an int status (LEGO_OK = 0, < 0 = error) and never throws.  Output arrays
+ * referenced by the *_out structs are owned by the context / batch and stay valid until
+ * the next call on the same object.  A context or batch is single-threaded (the
+ * reference's one-writer/one-reader Channel contract, channel.h:8-10).
+ *
+ * The product path is the HIP path on a gfx950 device.  There is no CPU fallback:
+ * creating a context without a usable device returns LEGO_EDEVICE.
+ */
+#ifndef LEGO_FRONTEND_H
+#define LEGO_FRONTEND_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LEGO_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------ */
+#define LEGO_OK          0
+#define LEGO_EINVAL     -1   /* bad parameter / shape                                   */
+#define LEGO_ENOMEM     -2   /* host or device allocation failed                         */
+#define LEGO_EDEVICE    -3   /* no HIP device / kernel launch or runtime failure          */
+#define LEGO_ENOTSUP    -4   /* configuration not supported (e.g. fp_mode != 0)           */
+#define LEGO_EEMPTY     -5   /* empty input cloud (reference: UB in findStartEndAngle)    */
+
+/* ---- per-scan status bits reported by the association stage ------------------- */
+#define LEGO_ST_INIT            0x001  /* first scan: checkSystemInitialization (fa.cpp:1181-1209)   */
+#define LEGO_ST_LM_SKIPPED      0x002  /* Last clouds too small, LM skipped (fa.cpp:1214)            */
+#define LEGO_ST_DEGENERATE      0x004  /* eigenvalue degeneracy hit in a solve (fa.cpp:869-898)      */
+#define LEGO_ST_STALE_TREE      0x008  /* ref UB: kd-tree not rebuilt but LM ran (fa.cpp:1214,1356)   */
+#define LEGO_ST_FWD_OOB         0x010  /* ref UB: forward scan bound > |Last| (fa.cpp:522,661)        */
+#define LEGO_ST_NN_TIE          0x020  /* exact 1-NN distance tie (nanoflann first-visited unpinned)  */
+#define LEGO_ST_STALE_IND_OOB   0x040  /* ref UB: stale smoothness entry indexes past the cloud       */
+#define LEGO_ST_EMITTED         0x080  /* AssociationOut sent to mapping this cycle (fa.cpp:1432)     */
+#define LEGO_ST_VOXEL_OVERFLOW  0x100  /* PCL VoxelGrid index overflow: cloud copied unfiltered       */
+#define LEGO_ST_DEGEN_UB        0x200  /* ref UB: degenerate at iter>0 uses uninit matP (fa.cpp:894)  */
+
+/* ---- parameters: the reference's loam_config.yaml keys ------------------------- */
+typedef struct lego_params {
+  int32_t num_vertical_scans;              /* V   laser/num_vertical_scans       loam_config.yaml:5  */
+  int32_t num_horizontal_scans;            /* H   laser/num_horizontal_scans     :6                 */
+  int32_t ground_scan_index;               /* G   laser/ground_scan_index        :7                 */
+  float   vertical_angle_bottom;           /* deg laser/vertical_angle_bottom    :8                 */
+  float   vertical_angle_top;              /* deg laser/vertical_angle_top       :9                 */
+  float   sensor_mount_angle;              /* deg laser/sensor_mount_angle       :10                */
+  float   scan_period;                     /* s   laser/scan_period              :11                */
+  int32_t segment_valid_point_num;         /*     imageProjection/...            :14                */
+  int32_t segment_valid_line_num;          /*                                    :15                */
+  float   segment_theta;                   /* deg                                :16                */
+  float   edge_threshold;                  /*     featureAssociation/...         :19                */
+  float   surf_threshold;                  /*                                    :20                */
+  float   nearest_feature_search_distance; /* m                                  :21                */
+  int32_t mapping_frequency_divider;       /*     mapping/...                    :25                */
+  int32_t fp_mode;                         /* libm overload model: 0 = float
+                                              overloads of unqualified sin/cos/atan2 (only mode
+                                              implemented), 1 = double promotion (LEGO_ENOTSUP)  */
+} lego_params;
+
+/* pcl::PointXYZI payload (utility.h:46); 16 B, the device layout of every cloud. */
+typedef struct lego_point { float x, y, z, intensity; } lego_point;
+
+/* ProjectionOut (utility.h:64-70) + cloud_msgs::cloud_info (cloud_info.msg:1-13). */
+typedef struct lego_projection_out {
+  int32_t n_segmented;                       /* |segmented_cloud|  (M)                      */
+  int32_t n_outlier;                         /* |outlier_cloud|                             */
+  int32_t n_scan;                            /* |scan_msg| (2-D scan, imageProjection.cpp:312-330) */
+  const lego_point* segmented_cloud;         /* [M]                                         */
+  const lego_point* outlier_cloud;           /* [n_outlier]                                 */
+  const lego_point* scan_msg;                /* [n_scan]                                    */
+  const int32_t* start_ring_index;           /* cloud_info.startRingIndex [V]               */
+  const int32_t* end_ring_index;             /* cloud_info.endRingIndex   [V]               */
+  float start_orientation;                   /* cloud_info.startOrientation                 */
+  float end_orientation;                     /* cloud_info.endOrientation                   */
+  float orientation_diff;                    /* cloud_info.orientationDiff                  */
+  const uint8_t*  segmented_cloud_ground_flag; /* [M]  (ROS bool[] = uint8)                 */
+  const uint32_t* segmented_cloud_col_ind;     /* [M]                                       */
+  const float*    segmented_cloud_range;       /* [M]                                       */
+  /* diagnostics (the reference's _label_mat/_ground_mat/_range_mat), row-major V x H */
+  const int32_t* label_mat;
+  const int8_t*  ground_mat;
+  const float*   range_mat;
+} lego_projection_out;
+
+/* One FeatureAssociation loop body: odometry + feature clouds + AssociationOut. */
+typedef struct lego_association_out {
+  int32_t status;                            /* LEGO_ST_* bits                              */
+  int32_t n_sharp, n_less_sharp, n_flat, n_less_flat;
+  const lego_point* corner_points_sharp;     /* fa.cpp:297  (after adjustDistortion frame)  */
+  const lego_point* corner_points_less_sharp;/* fa.cpp:298,301                              */
+  const lego_point* surf_points_flat;        /* fa.cpp:337                                  */
+  const lego_point* surf_points_less_flat;   /* fa.cpp:381 (VoxelGrid per ring)             */
+  const int32_t* sharp_ind;                  /* indices into the segmented cloud            */
+  const int32_t* less_sharp_ind;
+  const int32_t* flat_ind;
+  float transform_cur[6];                    /* featureAssociation.h:96                     */
+  float transform_sum[6];                    /* featureAssociation.h:97                     */
+  double odom_orientation[4];                /* /laser_odom_to_init quaternion x,y,z,w (fa.cpp:1287-1294) */
+  double odom_position[3];
+  int32_t lm_iter_surf, lm_iter_corner;      /* iterations run (<=25 each)                  */
+  int32_t n_corner_last, n_surf_last, n_outlier_last;
+  const lego_point* cloud_corner_last;       /* AssociationOut::cloud_corner_last           */
+  const lego_point* cloud_surf_last;         /* AssociationOut::cloud_surf_last             */
+  const lego_point* cloud_outlier_last;      /* AssociationOut::cloud_outlier_last (axis-swapped, fa.cpp:1273-1283) */
+} lego_association_out;
+
+typedef struct lego_ctx   lego_ctx;    /* one sequence: ImageProjection + FeatureAssociation state */
+typedef struct lego_batch lego_batch;  /* S independent sequences advanced one scan per step      */
+
+/* ---- parameters ---------------------------------------------------------------- */
+int32_t lego_abi_version(void);
+/* The reference's loam_config.yaml (VLP-16). */
+void lego_params_vlp16(lego_params* p);
+/* HDL-64E-like synthetic config: V=64 evenly spaced -24.8..+2.0 deg, H=2048, G=55. */
+void lego_params_hdl64(lego_params* p);
+int  lego_params_validate(const lego_params* p);
+/* Number of visible HIP devices (0 when none). */
+int32_t lego_device_count(void);
+
+/* ---- single-sequence drop-in (replaces ImageProjection + FeatureAssociation) ----- */
+/* ImageProjection ctor + FeatureAssociation ctor (imageProjection.cpp:32-104, featureAssociation.cpp:41-88). */
+int  lego_ctx_create(const lego_params* p, int32_t device, lego_ctx** out);
+void lego_ctx_destroy(lego_ctx* ctx);
+/* ImageProjection::cloudHandler minus ROS (imageProjection.cpp:153-174).  Points are read zero-copy
+ * from a strided host buffer (PointCloud2 data: x,y,z float32 at the given byte offsets).  Non-finite
+ * points are dropped (removeNaNFromPointCloud, :160-161).  Returns the ProjectionOut (:538-547). */
+int  lego_cloud_handler(lego_ctx* ctx, const void* points, int32_t n_points, int32_t point_step,
+                        int32_t off_x, int32_t off_y, int32_t off_z, lego_projection_out* out);
+/* One runFeatureAssociation iteration (featureAssociation.cpp:1389-1448) on the projection the last
+ * lego_cloud_handler call produced (device-resident; the reference's Channel<ProjectionOut> hop). */
+int  lego_feature_association(lego_ctx* ctx, lego_association_out* out);
+/* Same, on a ProjectionOut supplied by the caller (host arrays), e.g. from another producer. */
+int  lego_feature_association_from(lego_ctx* ctx, const lego_projection_out* in, lego_association_out* out);
+
+/* ---- batched multi-sequence engine (throughput path) ------------------------------ */
+int  lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, int32_t max_points,
+                       lego_batch** out);
+void lego_batch_destroy(lego_batch* b);
+/* Advance every stream by one scan.  d_points: DEVICE array of lego_point (x,y,z,intensity);
+ * stream s's scan is d_points[d_offsets[s] .. d_offsets[s] + d_counts[s]).  d_offsets / d_counts are
+ * DEVICE arrays (int64 / int32) of length n_streams.  Asynchronous on hip_stream (NULL = default). */
+int  lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_offsets,
+                     const int32_t* d_counts, void* hip_stream);
+int  lego_batch_sync(lego_batch* b);
+/* Copy one stream's last projection / association outputs to host (blocking). */
+int  lego_batch_read(lego_batch* b, int32_t s, lego_projection_out* proj, lego_association_out* assoc);
+/* Poses of all streams: out[s*12 + 0..5] = transformCur, [6..11] = transformSum; status[s]. */
+int  lego_batch_read_poses(lego_batch* b, float* out, int32_t* status);
+/* Reset every stream to the freshly constructed state (systemInitedLM = false, transforms 0). */
+int  lego_batch_reset(lego_batch* b);
+/* Kernel timing of the last step (ms, measured with hipEvents on the step's stream):
+ * [0] project, [1] segment, [2] distortion+smoothness+occlusion, [3] features, [4] concat, [5] LM. */
+int  lego_batch_stage_times(lego_batch* b, float* ms6);
+int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LEGO_FRONTEND_H */

@@ -1,0 +1,60 @@
+"""Build the in-tree native libraries (no JIT cache: the .so files travel with the repo snapshot).
+
+  liblego_frontend.so  product: HIP kernels for gfx950 + C-ABI (include/lego_frontend.h)
+  liblego_synth.so     synthetic VLP-16 / HDL-64E sweep generator (tests / bench input)
+
+Usage: python lego-loam-bor_amd/build.py [--force]
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "lego_amd")
+REPO = os.path.dirname(HERE)
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("LEGO_OFFLOAD_ARCH", "gfx950")
+
+FRONTEND_SRC = ["lego_kernels.hip", "lego_frontend.hip"]
+FRONTEND_DEPS = FRONTEND_SRC + ["lego_device.h", "lego_introsort.h"]
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "--offload-arch=" + ARCH,
+             # numerics contract: no FMA contraction, IEEE division/sqrt
+             "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+             "-Wno-unused-result", "-Wno-unused-value"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_frontend(force=False):
+    target = os.path.join(OUT, "liblego_frontend.so")
+    deps = [os.path.join(CSRC, f) for f in FRONTEND_DEPS] + [os.path.join(REPO, "include", "lego_frontend.h")]
+    if force or _stale(target, deps):
+        cmd = [HIPCC] + HIP_FLAGS + [os.path.join(CSRC, f) for f in FRONTEND_SRC] + ["-o", target]
+        print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+    return target
+
+
+def build_synth(force=False):
+    target = os.path.join(OUT, "liblego_synth.so")
+    src = os.path.join(CSRC, "synth.cpp")
+    if force or _stale(target, [src]):
+        cmd = ["g++", "-std=c++14", "-O3", "-fPIC", "-shared", "-fopenmp", src, "-o", target]
+        print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+    return target
+
+
+def build_all(force=False):
+    build_synth(force)
+    build_frontend(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,553 @@
+// lego_frontend.hip — host engine + C-ABI (include/lego_frontend.h).
+//
+// A lego_batch owns S independent sequences ("streams") laid out stream-major in HBM and advances
+// all of them by one scan per step with one launch per stage (lego_kernels.hip).  A lego_ctx is a
+// batch of one plus host staging: the drop-in for one ImageProjection + FeatureAssociation pair.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <cfloat>
+#include <new>
+#include <vector>
+
+#include "../../include/lego_frontend.h"
+#include "lego_device.h"
+
+int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
+                      const int32_t* cnts, hipStream_t st);
+int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
+int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
+int lg_launch_extract(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
+int lg_launch_concat(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
+int lg_launch_lm(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
+
+namespace {
+
+const double DEG_TO_RAD = M_PI / 180.0;  // utility.h:50
+
+// ImageProjection / FeatureAssociation ctor arithmetic with the reference's types
+// (imageProjection.cpp:57-84, featureAssociation.cpp:69-81); glibc float trig for the
+// labelComponents constants (:414, :463), as the reference evaluates them per call.
+LgParams derive(const lego_params& p) {
+  LgParams P;
+  memset(&P, 0, sizeof(P));
+  P.V = p.num_vertical_scans;
+  P.H = p.num_horizontal_scans;
+  P.G = p.ground_scan_index;
+  P.VH = P.V * P.H;
+  float ang_bottom = p.vertical_angle_bottom;
+  float top = p.vertical_angle_top;
+  P.ang_res_x = (M_PI * 2) / (P.H);
+  P.ang_res_y = DEG_TO_RAD * (top - ang_bottom) / float(P.V - 1);
+  P.ang_bottom = -(ang_bottom - 0.1) * DEG_TO_RAD;
+  float theta = p.segment_theta;
+  theta *= DEG_TO_RAD;
+  float mount = p.sensor_mount_angle;
+  mount *= DEG_TO_RAD;
+  P.mount = mount;
+  P.theta_thr = tanf(theta);
+  P.sinX = sinf(P.ang_res_x);
+  P.cosX = cosf(P.ang_res_x);
+  P.sinY = sinf(P.ang_res_y);
+  P.cosY = cosf(P.ang_res_y);
+  P.seg_valid_pt = p.segment_valid_point_num;
+  P.seg_valid_line = p.segment_valid_line_num;
+  P.scan_period = p.scan_period;
+  P.edge_thr = p.edge_threshold;
+  P.surf_thr = p.surf_threshold;
+  float nd = p.nearest_feature_search_distance;
+  P.nn_dist_sqr = nd * nd;
+  P.map_div = p.mapping_frequency_divider;
+  P.cap_sharp = 12;   // 2 per segment x 6 (fa.cpp:295)
+  P.cap_lsharp = 120; // 20 per segment x 6 (fa.cpp:299)
+  P.cap_flat = 24;    // 4 per segment x 6 (fa.cpp:340)
+  return P;
+}
+
+template <typename T>
+int dalloc(T** p, size_t n, std::vector<void*>& owned) {
+  if (n == 0) n = 1;
+  if (hipMalloc((void**)p, n * sizeof(T)) != hipSuccess) return LEGO_ENOMEM;
+  owned.push_back((void*)*p);
+  return LEGO_OK;
+}
+
+template <typename T>
+int d2h(std::vector<T>& h, const T* d, size_t n) {
+  h.resize(n > 0 ? n : 1);
+  if (n == 0) return LEGO_OK;
+  return hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost) == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+}
+
+}  // namespace
+
+struct lego_batch {
+  lego_params params;
+  LgParams P;
+  LgBufs B;
+  int S = 0;
+  int max_points = 0;
+  int device = 0;
+  std::vector<void*> owned;
+  hipEvent_t ev[8];
+  bool timing = false;
+  bool events = false;
+  hipStream_t last_stream = nullptr;
+  // host mirrors for lego_batch_read
+  std::vector<lego_point> h_seg, h_out, h_scan, h_sharp, h_lsharp, h_flat, h_lflat, h_clast, h_slast, h_olast;
+  std::vector<int32_t> h_rs, h_re, h_label, h_sharp_ind, h_lsharp_ind, h_flat_ind;
+  std::vector<uint8_t> h_gflag;
+  std::vector<uint32_t> h_col;
+  std::vector<float> h_range_seg, h_range;
+  std::vector<int8_t> h_ground;
+  ~lego_batch() {
+    hipSetDevice(device);
+    for (void* p : owned) hipFree(p);
+    if (events)
+      for (int i = 0; i < 8; ++i) hipEventDestroy(ev[i]);
+  }
+};
+
+struct lego_ctx {
+  lego_batch* b = nullptr;
+  float4* d_pts = nullptr;
+  int64_t* d_off = nullptr;
+  int32_t* d_cnt = nullptr;
+  int cap = 0;
+  std::vector<float4> h_pts;
+  ~lego_ctx() {
+    if (b) {
+      hipSetDevice(b->device);
+      if (d_pts) hipFree(d_pts);
+      if (d_off) hipFree(d_off);
+      if (d_cnt) hipFree(d_cnt);
+      delete b;
+    }
+  }
+};
+
+extern "C" {
+
+int32_t lego_abi_version(void) { return LEGO_ABI_VERSION; }
+
+void lego_params_vlp16(lego_params* p) {  // LeGO-LOAM/config/loam_config.yaml
+  p->num_vertical_scans = 16;
+  p->num_horizontal_scans = 1800;
+  p->ground_scan_index = 7;
+  p->vertical_angle_bottom = -15.f;
+  p->vertical_angle_top = 15.f;
+  p->sensor_mount_angle = 0.f;
+  p->scan_period = 0.1f;
+  p->segment_valid_point_num = 5;
+  p->segment_valid_line_num = 3;
+  p->segment_theta = 60.f;
+  p->edge_threshold = 0.1f;
+  p->surf_threshold = 0.1f;
+  p->nearest_feature_search_distance = 5.f;
+  p->mapping_frequency_divider = 5;
+  p->fp_mode = 0;
+}
+
+void lego_params_hdl64(lego_params* p) {
+  lego_params_vlp16(p);
+  p->num_vertical_scans = 64;
+  p->num_horizontal_scans = 2048;
+  p->ground_scan_index = 55;
+  p->vertical_angle_bottom = -24.8f;
+  p->vertical_angle_top = 2.0f;
+}
+
+int lego_params_validate(const lego_params* p) {
+  if (!p) return LEGO_EINVAL;
+  if (p->fp_mode != 0) return LEGO_ENOTSUP;
+  if (p->num_vertical_scans < 2 || p->num_vertical_scans > 64) return LEGO_EINVAL;
+  if (p->num_horizontal_scans < 16 || p->num_horizontal_scans > 2048) return LEGO_EINVAL;
+  if (p->ground_scan_index < 0 || p->ground_scan_index >= p->num_vertical_scans) return LEGO_EINVAL;
+  if (p->mapping_frequency_divider < 1) return LEGO_EINVAL;
+  if (!(p->vertical_angle_top > p->vertical_angle_bottom)) return LEGO_EINVAL;
+  return LEGO_OK;
+}
+
+int32_t lego_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, int32_t max_points,
+                      lego_batch** out) {
+  if (!out) return LEGO_EINVAL;
+  *out = nullptr;
+  int rc = lego_params_validate(p);
+  if (rc != LEGO_OK) return rc;
+  if (n_streams < 1 || max_points < 1) return LEGO_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return LEGO_EDEVICE;
+  if (hipSetDevice(device) != hipSuccess) return LEGO_EDEVICE;
+  lego_batch* b = new (std::nothrow) lego_batch();
+  if (!b) return LEGO_ENOMEM;
+  b->params = *p;
+  b->P = derive(*p);
+  b->S = n_streams;
+  b->max_points = max_points;
+  b->device = device;
+  const LgParams& P = b->P;
+  LgBufs& B = b->B;
+  memset(&B, 0, sizeof(B));
+  const size_t S = n_streams, VH = P.VH, V = P.V, H = P.H;
+  std::vector<void*>& o = b->owned;
+  bool lds_proj = (size_t)(P.VH + 64) * 4 <= 160 * 1024;
+  bool lds_seg = P.V <= 16 && lds_proj;
+  rc = LEGO_OK;
+#define A(ptr, n) if (rc == LEGO_OK) rc = dalloc(&B.ptr, (n), o)
+  A(range, S * VH); A(cloud, S * VH); A(ground, S * VH); A(label, S * VH);
+  A(winner, lds_proj ? 1 : S * VH);
+  A(cc_parent, lds_seg ? 1 : S * VH); A(cc_cnt, lds_seg ? 1 : S * VH); A(cc_mask, lds_seg ? 1 : S * VH);
+  A(scan_cand, S * H); A(orient, S * 4);
+  A(seg_pts, S * VH); A(seg_range, S * VH); A(seg_col, S * VH); A(seg_ground, S * VH);
+  A(ring_start, S * V); A(ring_end, S * V); A(outlier, S * VH); A(scan_msg, S * H); A(counts, S * CNT_N);
+  A(curv, S * VH); A(picked, S * VH); A(flabel, S * VH); A(smooth, S * VH); A(seg_fa, S * VH); A(outlier_fa, S * VH);
+  A(r_sharp, S * V * P.cap_sharp); A(r_sharp_ind, S * V * P.cap_sharp);
+  A(r_lsharp, S * V * P.cap_lsharp); A(r_lsharp_ind, S * V * P.cap_lsharp);
+  A(r_flat, S * V * P.cap_flat); A(r_flat_ind, S * V * P.cap_flat);
+  A(r_lflat, S * V * H); A(r_counts, S * V * 4); A(r_status, S * V);
+  A(f_sharp, S * V * P.cap_sharp); A(f_sharp_ind, S * V * P.cap_sharp);
+  A(f_lsharp, S * V * P.cap_lsharp); A(f_lsharp_ind, S * V * P.cap_lsharp);
+  A(f_flat, S * V * P.cap_flat); A(f_flat_ind, S * V * P.cap_flat);
+  A(f_lflat, S * VH);
+  A(corner_last, S * 2 * V * P.cap_lsharp); A(surf_last, S * 2 * VH);
+  A(state, S);
+#undef A
+  if (rc != LEGO_OK) {
+    delete b;
+    return rc;
+  }
+  rc = lego_batch_reset(b);
+  if (rc != LEGO_OK) {
+    delete b;
+    return rc;
+  }
+  *out = b;
+  return LEGO_OK;
+}
+
+void lego_batch_destroy(lego_batch* b) { delete b; }
+
+int lego_batch_reset(lego_batch* b) {
+  if (!b) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  const size_t S = b->S, VH = b->P.VH;
+  LgBufs& B = b->B;
+  // FeatureAssociation's vectors are value-initialised (fa.cpp:96-128); transforms zero (:135-138)
+  if (hipMemset(B.curv, 0, S * VH * sizeof(float)) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemset(B.picked, 0, S * VH) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemset(B.flabel, 0, S * VH) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemset(B.smooth, 0, S * VH * sizeof(int2)) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemset(B.counts, 0, S * CNT_N * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  return LEGO_OK;
+}
+
+int lego_batch_set_timing(lego_batch* b, int32_t enabled) {
+  if (!b) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  if (enabled && !b->events) {
+    for (int i = 0; i < 8; ++i)
+      if (hipEventCreate(&b->ev[i]) != hipSuccess) return LEGO_EDEVICE;
+    b->events = true;
+  }
+  b->timing = enabled != 0;
+  return LEGO_OK;
+}
+
+static int run_projection(lego_batch* b, const float4* pts, const int64_t* offs, const int32_t* cnts, hipStream_t st) {
+  int rc = lg_launch_project(b->P, b->B, b->S, pts, offs, cnts, st);
+  if (rc) return rc;
+  if (b->timing) hipEventRecord(b->ev[1], st);
+  rc = lg_launch_segment(b->P, b->B, b->S, st);
+  if (rc) return rc;
+  if (b->timing) hipEventRecord(b->ev[2], st);
+  return LEGO_OK;
+}
+
+static int run_association(lego_batch* b, hipStream_t st) {
+  int rc = lg_launch_fa_prep(b->P, b->B, b->S, st);
+  if (rc) return rc;
+  if (b->timing) hipEventRecord(b->ev[3], st);
+  rc = lg_launch_extract(b->P, b->B, b->S, st);
+  if (rc) return rc;
+  if (b->timing) hipEventRecord(b->ev[4], st);
+  rc = lg_launch_concat(b->P, b->B, b->S, st);
+  if (rc) return rc;
+  if (b->timing) hipEventRecord(b->ev[5], st);
+  rc = lg_launch_lm(b->P, b->B, b->S, st);
+  if (rc) return rc;
+  if (b->timing) hipEventRecord(b->ev[6], st);
+  return LEGO_OK;
+}
+
+int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_offsets, const int32_t* d_counts,
+                    void* hip_stream) {
+  if (!b || !d_points || !d_offsets || !d_counts) return LEGO_EINVAL;
+  if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
+  hipStream_t st = (hipStream_t)hip_stream;
+  b->last_stream = st;
+  if (b->timing) hipEventRecord(b->ev[0], st);
+  int rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st);
+  if (rc) return rc;
+  return run_association(b, st);
+}
+
+int lego_batch_sync(lego_batch* b) {
+  if (!b) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  return hipDeviceSynchronize() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+}
+
+int lego_batch_stage_times(lego_batch* b, float* ms6) {
+  if (!b || !ms6 || !b->timing) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  if (hipEventSynchronize(b->ev[6]) != hipSuccess) return LEGO_EDEVICE;
+  for (int i = 0; i < 6; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, b->ev[i], b->ev[i + 1]) != hipSuccess) return LEGO_EDEVICE;
+    ms6[i] = ms;
+  }
+  return LEGO_OK;
+}
+
+static int read_proj(lego_batch* b, int s, lego_projection_out* o) {
+  const LgParams& P = b->P;
+  const LgBufs& B = b->B;
+  const size_t VH = P.VH;
+  int32_t cnt[CNT_N];
+  if (hipMemcpy(cnt, B.counts + (size_t)s * CNT_N, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
+  float ori[4];
+  if (hipMemcpy(ori, B.orient + (size_t)s * 4, sizeof(ori), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
+  const int M = cnt[CNT_M];
+  int rc = LEGO_OK;
+  rc |= d2h(b->h_seg, (const lego_point*)(B.seg_pts + s * VH), M);
+  rc |= d2h(b->h_out, (const lego_point*)(B.outlier + s * VH), cnt[CNT_OUTLIER]);
+  rc |= d2h(b->h_scan, (const lego_point*)(B.scan_msg + (size_t)s * P.H), cnt[CNT_SCAN]);
+  rc |= d2h(b->h_rs, B.ring_start + (size_t)s * P.V, P.V);
+  rc |= d2h(b->h_re, B.ring_end + (size_t)s * P.V, P.V);
+  rc |= d2h(b->h_gflag, B.seg_ground + s * VH, M);
+  rc |= d2h(b->h_col, B.seg_col + s * VH, M);
+  rc |= d2h(b->h_range_seg, B.seg_range + s * VH, M);
+  rc |= d2h(b->h_label, B.label + s * VH, VH);
+  rc |= d2h(b->h_ground, B.ground + s * VH, VH);
+  rc |= d2h(b->h_range, B.range + s * VH, VH);
+  if (rc) return LEGO_EDEVICE;
+  o->n_segmented = M;
+  o->n_outlier = cnt[CNT_OUTLIER];
+  o->n_scan = cnt[CNT_SCAN];
+  o->segmented_cloud = b->h_seg.data();
+  o->outlier_cloud = b->h_out.data();
+  o->scan_msg = b->h_scan.data();
+  o->start_ring_index = b->h_rs.data();
+  o->end_ring_index = b->h_re.data();
+  o->start_orientation = ori[0];
+  o->end_orientation = ori[1];
+  o->orientation_diff = ori[2];
+  o->segmented_cloud_ground_flag = b->h_gflag.data();
+  o->segmented_cloud_col_ind = b->h_col.data();
+  o->segmented_cloud_range = b->h_range_seg.data();
+  o->label_mat = b->h_label.data();
+  o->ground_mat = b->h_ground.data();
+  o->range_mat = b->h_range.data();
+  return LEGO_OK;
+}
+
+static int read_assoc(lego_batch* b, int s, lego_association_out* o) {
+  const LgParams& P = b->P;
+  const LgBufs& B = b->B;
+  const size_t VH = P.VH, V = P.V;
+  int32_t cnt[CNT_N];
+  LgState S;
+  if (hipMemcpy(cnt, B.counts + (size_t)s * CNT_N, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemcpy(&S, B.state + s, sizeof(S), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
+  int rc = LEGO_OK;
+  rc |= d2h(b->h_sharp, (const lego_point*)(B.f_sharp + (size_t)s * V * P.cap_sharp), cnt[CNT_SHARP]);
+  rc |= d2h(b->h_sharp_ind, B.f_sharp_ind + (size_t)s * V * P.cap_sharp, cnt[CNT_SHARP]);
+  rc |= d2h(b->h_lsharp, (const lego_point*)(B.f_lsharp + (size_t)s * V * P.cap_lsharp), cnt[CNT_LSHARP]);
+  rc |= d2h(b->h_lsharp_ind, B.f_lsharp_ind + (size_t)s * V * P.cap_lsharp, cnt[CNT_LSHARP]);
+  rc |= d2h(b->h_flat, (const lego_point*)(B.f_flat + (size_t)s * V * P.cap_flat), cnt[CNT_FLAT]);
+  rc |= d2h(b->h_flat_ind, B.f_flat_ind + (size_t)s * V * P.cap_flat, cnt[CNT_FLAT]);
+  rc |= d2h(b->h_lflat, (const lego_point*)(B.f_lflat + s * VH), cnt[CNT_LFLAT]);
+  const size_t cls = V * P.cap_lsharp;
+  rc |= d2h(b->h_clast, (const lego_point*)(B.corner_last + (size_t)s * 2 * cls + (size_t)S.last_buf * cls), S.n_corner_last);
+  rc |= d2h(b->h_slast, (const lego_point*)(B.surf_last + (size_t)s * 2 * VH + (size_t)S.last_buf * VH), S.n_surf_last);
+  rc |= d2h(b->h_olast, (const lego_point*)(B.outlier_fa + s * VH), cnt[CNT_OUTLIER]);
+  if (rc) return LEGO_EDEVICE;
+  o->status = S.status;
+  o->n_sharp = cnt[CNT_SHARP];
+  o->n_less_sharp = cnt[CNT_LSHARP];
+  o->n_flat = cnt[CNT_FLAT];
+  o->n_less_flat = cnt[CNT_LFLAT];
+  o->corner_points_sharp = b->h_sharp.data();
+  o->corner_points_less_sharp = b->h_lsharp.data();
+  o->surf_points_flat = b->h_flat.data();
+  o->surf_points_less_flat = b->h_lflat.data();
+  o->sharp_ind = b->h_sharp_ind.data();
+  o->less_sharp_ind = b->h_lsharp_ind.data();
+  o->flat_ind = b->h_flat_ind.data();
+  for (int i = 0; i < 6; ++i) {
+    o->transform_cur[i] = S.cur[i];
+    o->transform_sum[i] = S.sum[i];
+  }
+  for (int i = 0; i < 4; ++i) o->odom_orientation[i] = S.quat[i];
+  for (int i = 0; i < 3; ++i) o->odom_position[i] = S.pos[i];
+  o->lm_iter_surf = S.iters_surf;
+  o->lm_iter_corner = S.iters_corner;
+  o->n_corner_last = S.n_corner_last;
+  o->n_surf_last = S.n_surf_last;
+  o->n_outlier_last = cnt[CNT_OUTLIER];
+  o->cloud_corner_last = b->h_clast.data();
+  o->cloud_surf_last = b->h_slast.data();
+  o->cloud_outlier_last = b->h_olast.data();
+  return LEGO_OK;
+}
+
+int lego_batch_read(lego_batch* b, int32_t s, lego_projection_out* proj, lego_association_out* assoc) {
+  if (!b || s < 0 || s >= b->S) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  if (proj) {
+    int rc = read_proj(b, s, proj);
+    if (rc) return rc;
+  }
+  if (assoc) {
+    int rc = read_assoc(b, s, assoc);
+    if (rc) return rc;
+  }
+  return LEGO_OK;
+}
+
+int lego_batch_read_poses(lego_batch* b, float* out, int32_t* status) {
+  if (!b) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  std::vector<LgState> S(b->S);
+  if (hipMemcpy(S.data(), b->B.state, S.size() * sizeof(LgState), hipMemcpyDeviceToHost) != hipSuccess)
+    return LEGO_EDEVICE;
+  for (int s = 0; s < b->S; ++s) {
+    if (out)
+      for (int k = 0; k < 6; ++k) {
+        out[s * 12 + k] = S[s].cur[k];
+        out[s * 12 + 6 + k] = S[s].sum[k];
+      }
+    if (status) status[s] = S[s].status;
+  }
+  return LEGO_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// single-sequence drop-in
+// ---------------------------------------------------------------------------------------------
+int lego_ctx_create(const lego_params* p, int32_t device, lego_ctx** out) {
+  if (!out) return LEGO_EINVAL;
+  *out = nullptr;
+  if (!p) return LEGO_EINVAL;
+  lego_ctx* c = new (std::nothrow) lego_ctx();
+  if (!c) return LEGO_ENOMEM;
+  const int cap = p->num_vertical_scans > 0 && p->num_horizontal_scans > 0
+                      ? 4 * p->num_vertical_scans * p->num_horizontal_scans : 1;
+  int rc = lego_batch_create(p, device, 1, cap, &c->b);
+  if (rc != LEGO_OK) {
+    delete c;
+    return rc;
+  }
+  c->cap = 0;
+  if (hipMalloc((void**)&c->d_off, sizeof(int64_t)) != hipSuccess ||
+      hipMalloc((void**)&c->d_cnt, sizeof(int32_t)) != hipSuccess) {
+    delete c;
+    return LEGO_ENOMEM;
+  }
+  int64_t zero = 0;
+  hipMemcpy(c->d_off, &zero, sizeof(zero), hipMemcpyHostToDevice);
+  *out = c;
+  return LEGO_OK;
+}
+
+void lego_ctx_destroy(lego_ctx* ctx) { delete ctx; }
+
+int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step, int32_t ox, int32_t oy, int32_t oz,
+                       lego_projection_out* out) {
+  if (!c || (!points && n > 0) || n < 0 || step < 12 || ox < 0 || oy < 0 || oz < 0 || ox + 4 > step ||
+      oy + 4 > step || oz + 4 > step)
+    return LEGO_EINVAL;
+  lego_batch* b = c->b;
+  hipSetDevice(b->device);
+  // fromROSMsg: gather x,y,z from the strided PointCloud2 payload (intensity is not used by the path)
+  c->h_pts.resize(n > 0 ? n : 1);
+  const char* base = (const char*)points;
+  for (int i = 0; i < n; ++i) {
+    float4 q;
+    memcpy(&q.x, base + (size_t)i * step + ox, 4);
+    memcpy(&q.y, base + (size_t)i * step + oy, 4);
+    memcpy(&q.z, base + (size_t)i * step + oz, 4);
+    q.w = 0.f;
+    c->h_pts[i] = q;
+  }
+  if (n > c->cap) {
+    if (c->d_pts) hipFree(c->d_pts);
+    c->d_pts = nullptr;
+    if (hipMalloc((void**)&c->d_pts, (size_t)n * sizeof(float4)) != hipSuccess) return LEGO_ENOMEM;
+    c->cap = n;
+  }
+  if (n > 0 && hipMemcpy(c->d_pts, c->h_pts.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess)
+    return LEGO_EDEVICE;
+  if (hipMemcpy(c->d_cnt, &n, sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) return LEGO_EDEVICE;
+  int rc = run_projection(b, c->d_pts ? c->d_pts : (const float4*)c->d_off, c->d_off, c->d_cnt, nullptr);
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  LgState S;
+  if (hipMemcpy(&S, b->B.state, sizeof(S), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
+  if (S.proj_status != LEGO_OK) return S.proj_status;
+  if (out) return read_proj(b, 0, out);
+  return LEGO_OK;
+}
+
+int lego_feature_association(lego_ctx* c, lego_association_out* out) {
+  if (!c) return LEGO_EINVAL;
+  lego_batch* b = c->b;
+  hipSetDevice(b->device);
+  int rc = run_association(b, nullptr);
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  if (out) return read_assoc(b, 0, out);
+  return LEGO_OK;
+}
+
+int lego_feature_association_from(lego_ctx* c, const lego_projection_out* in, lego_association_out* out) {
+  if (!c || !in) return LEGO_EINVAL;
+  lego_batch* b = c->b;
+  const LgParams& P = b->P;
+  const LgBufs& B = b->B;
+  const int M = in->n_segmented;
+  if (M < 0 || M > P.VH || in->n_outlier < 0 || in->n_outlier > P.VH) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  // the reference's Channel<ProjectionOut>::receive (fa.cpp:1389-1397): upload the message
+  bool ok = true;
+  auto up = [&](void* d, const void* h, size_t bytes) {
+    if (bytes && hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) != hipSuccess) ok = false;
+  };
+  up(B.seg_pts, in->segmented_cloud, (size_t)M * sizeof(float4));
+  up(B.seg_range, in->segmented_cloud_range, (size_t)M * sizeof(float));
+  up(B.seg_col, in->segmented_cloud_col_ind, (size_t)M * sizeof(uint32_t));
+  up(B.seg_ground, in->segmented_cloud_ground_flag, (size_t)M);
+  up(B.ring_start, in->start_ring_index, (size_t)P.V * sizeof(int32_t));
+  up(B.ring_end, in->end_ring_index, (size_t)P.V * sizeof(int32_t));
+  up(B.outlier, in->outlier_cloud, (size_t)in->n_outlier * sizeof(float4));
+  float ori[4] = {in->start_orientation, in->end_orientation, in->orientation_diff, 1.f};
+  up(B.orient, ori, sizeof(ori));
+  int32_t cnt[CNT_N] = {M, in->n_outlier, 0, 0, 0, 0, 0, 0};
+  up(B.counts, cnt, sizeof(cnt));
+  if (!ok) return LEGO_EDEVICE;
+  return lego_feature_association(c, out);
+}
+
+}  // extern "C"

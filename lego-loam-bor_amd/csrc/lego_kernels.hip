@@ -1,0 +1,1502 @@
+// lego_kernels.hip — gfx950 kernels for LeGO-LOAM-BOR's per-scan front end + two-step LM.
+//
+// One launch per stage for ALL streams (sequences) of a batch; the stage -> kernel map:
+//   k_project     ImageProjection::resetParameters/findStartEndAngle/projectPointCloud/groundRemoval
+//                 (imageProjection.cpp:107-150, 234-249, 178-224, 254-346)  — workgroup per scan
+//   k_segment     cloudSegmentation + labelComponents (imageProjection.cpp:352-496) as union-find
+//                 connected components + raster-order compaction — workgroup per scan
+//   k_fa_prep     FeatureAssociation::adjustDistortion / calculateSmoothness / markOccludedPoints
+//                 (featureAssociation.cpp:161-262) + adjustOutlierCloud (:1273-1283)
+//   k_extract     extractFeatures (:265-383) incl. PCL VoxelGrid per ring — one wave per ring
+//   k_concat      ring-ordered concatenation of the per-ring feature clouds
+//   k_lm          updateTransformation (:1213-1235) with both LM loops, integrateTransformation
+//                 (:1241-1270), publishOdometry (:1286-1306), publishCloudsLast (:1329-1383)
+//                 — one persistent workgroup per scan pair
+// Compile with -ffp-contract=off (see lego_device.h).
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/lego_frontend.h"
+#include "lego_device.h"
+#include "lego_introsort.h"
+
+using namespace lg;
+
+#define DEG_TO_RAD_D (M_PI / 180.0)
+
+// ============================================================================================
+// block / wave helpers
+// ============================================================================================
+LG_DEVICE int lane_id() { return threadIdx.x & 63; }
+LG_DEVICE int wave_id() { return threadIdx.x >> 6; }
+LG_DEVICE int popc_below(unsigned long long m) {
+  return __popcll(m & ((1ull << lane_id()) - 1ull));
+}
+
+template <typename T>
+LG_DEVICE T wave_min(T v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    T u = __shfl_xor(v, o);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+template <typename T>
+LG_DEVICE T wave_max(T v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    T u = __shfl_xor(v, o);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+template <typename T>
+LG_DEVICE T wave_sum(T v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Block-wide exclusive scan of two booleans (any block size that is a multiple of 64, <= 1024).
+// scratch: >= 2*16+2 ints of LDS.
+LG_DEVICE void block_scan2(bool p1, bool p2, int* scratch, int& ex1, int& ex2, int& tot1, int& tot2) {
+  const int nw = blockDim.x >> 6;
+  unsigned long long b1 = __ballot(p1), b2 = __ballot(p2);
+  int w = wave_id();
+  if (lane_id() == 0) {
+    scratch[w] = __popcll(b1);
+    scratch[16 + w] = __popcll(b2);
+  }
+  __syncthreads();
+  int o1 = 0, o2 = 0, t1 = 0, t2 = 0;
+  for (int k = 0; k < nw; ++k) {
+    int a = scratch[k], b = scratch[16 + k];
+    if (k < w) { o1 += a; o2 += b; }
+    t1 += a; t2 += b;
+  }
+  ex1 = o1 + popc_below(b1);
+  ex2 = o2 + popc_below(b2);
+  tot1 = t1;
+  tot2 = t2;
+  __syncthreads();
+}
+
+LG_DEVICE int block_min_int(int v, int* scratch) {
+  v = wave_min(v);
+  if (lane_id() == 0) scratch[wave_id()] = v;
+  __syncthreads();
+  int r = scratch[0];
+  for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = min(r, scratch[k]);
+  __syncthreads();
+  return r;
+}
+LG_DEVICE int block_max_int(int v, int* scratch) {
+  v = wave_max(v);
+  if (lane_id() == 0) scratch[wave_id()] = v;
+  __syncthreads();
+  int r = scratch[0];
+  for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = max(r, scratch[k]);
+  __syncthreads();
+  return r;
+}
+
+// ============================================================================================
+// k_project: reset + findStartEndAngle + projectPointCloud + groundRemoval + 2-D scan candidates
+// ============================================================================================
+// The reference's scatter "later input point overwrites earlier ones in the same cell"
+// (imageProjection.cpp:214-222) is an atomicMax of the input index per cell, followed by a
+// column-parallel gather that writes every cell (so resetParameters' fill is fused in).
+template <bool kLdsWinner>
+__global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
+                                                  const int64_t* __restrict__ offs,
+                                                  const int32_t* __restrict__ cnts) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int V = P.V, H = P.H, VH = P.VH;
+  int* scratch = smem;                 // 64 ints
+  int* winner = kLdsWinner ? (smem + 64) : (B.winner + (size_t)s * VH);
+  const float4* in = pts + offs[s];
+  const int n = cnts[s];
+  for (int c = tid; c < VH; c += nt) winner[c] = -1;
+  __syncthreads();
+  int fmin = 0x7fffffff, fmax = -1;
+  for (int i = tid; i < n; i += nt) {
+    const float4 p = in[i];
+    if (!isfinite_f(p.x) || !isfinite_f(p.y) || !isfinite_f(p.z)) continue;  // removeNaNFromPointCloud
+    fmin = min(fmin, i);
+    fmax = max(fmax, i);
+    float range = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+    float verticalAngle = asinf_g(p.z / range);
+    int rowIdn = (int)((verticalAngle + P.ang_bottom) / P.ang_res_y);
+    if (rowIdn < 0 || rowIdn >= V) continue;
+    float horizonAngle = atan2f_g(p.x, p.y);
+    int columnIdn = (int)(-round(((double)horizonAngle - M_PI_2) / (double)P.ang_res_x) + H * 0.5);
+    if (columnIdn >= H) columnIdn -= H;
+    if (columnIdn < 0 || columnIdn >= H) continue;
+    if ((double)range < 0.1) continue;
+    atomicMax(&winner[rowIdn * H + columnIdn], i);
+  }
+  fmin = block_min_int(fmin, scratch);
+  fmax = block_max_int(fmax, scratch);
+  if (tid == 0) {
+    float so = 0.f, eo = 0.f, od = 0.f;
+    if (fmax >= 0) {  // findStartEndAngle (:234-249)
+      float4 a = in[fmin], b = in[fmax];
+      so = -atan2f_g(a.y, a.x);
+      eo = (float)(-(double)atan2f_g(b.y, b.x) + 2 * M_PI);
+      if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
+      else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
+      od = eo - so;
+    }
+    B.orient[s * 4 + 0] = so;
+    B.orient[s * 4 + 1] = eo;
+    B.orient[s * 4 + 2] = od;
+    B.orient[s * 4 + 3] = (float)(fmax >= 0);
+    B.state[s].proj_status = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
+  }
+  __syncthreads();
+  float* range = B.range + (size_t)s * VH;
+  float4* cloud = B.cloud + (size_t)s * VH;
+  int8_t* ground = B.ground + (size_t)s * VH;
+  const float qnan = __int_as_float(0x7fc00000);
+  for (int j = tid; j < H; j += nt) {
+    unsigned long long gmask = 0ull;
+    float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < V; ++i) {
+      const int c = i * H + j;
+      const int w = winner[c];
+      float4 q;
+      float r;
+      if (w >= 0) {
+        const float4 p = in[w];
+        r = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+        q = make_float4(p.x, p.y, p.z, (float)((double)(float)i + (double)(float)j / 10000.0));
+      } else {
+        r = FLT_MAX;
+        q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
+      }
+      range[c] = r;
+      cloud[c] = q;
+      if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
+        float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
+        float va = atan2f_g(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ));
+        if ((double)(va - P.mount) <= 10 * DEG_TO_RAD_D) gmask |= (3ull << (i - 1));
+      }
+      prev = q;
+    }
+    float min_range = 1000.f;
+    int id_min = -1;
+    for (int i = 0; i < V; ++i) {  // 2-D scan (:312-330)
+      const int c = i * H + j;
+      const int g = (int)((gmask >> i) & 1ull);
+      ground[c] = (int8_t)g;
+      const float r = range[c];
+      const float Z = cloud[c].z;
+      if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f) {
+        if (r < min_range) {
+          min_range = r;
+          id_min = c;
+        }
+      }
+    }
+    B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
+  }
+}
+
+// ============================================================================================
+// k_segment: labelComponents as connected components
+// ============================================================================================
+// BFS from every unlabelled cell in raster order (imageProjection.cpp:354-356, 412-496) labels the
+// connected components of the symmetric edge relation "tang > tan(theta)" over 4-neighbour cells
+// (vertical clamp, horizontal wrap) among cells with label 0 (not ground, valid range).  The BFS
+// seed is the component's minimum raster index, feasible components are numbered 1,2,... in seed
+// order, infeasible ones get 999999, and the line count excludes the seed's own row unless another
+// member shares it (:469).  Reproduced with lock-free union-find (hook larger root onto smaller:
+// the root is the component minimum = the seed), per-root size and non-seed row mask, and a
+// raster-order block scan over feasible roots.
+LG_DEVICE bool seg_edge(float ra, float rb, float sA, float cA, float thr) {
+  float d1 = (ra < rb) ? rb : ra;  // std::max(from, this)
+  float d2 = (rb < ra) ? rb : ra;  // std::min(from, this)
+  float tang = (d2 * sA / (d1 - d2 * cA));
+  return tang > thr;
+}
+
+template <typename PT>
+LG_DEVICE int uf_find(PT parent, int x) {
+  int p = parent[x];
+  while (p != x) {
+    x = p;
+    p = parent[x];
+  }
+  return x;
+}
+
+template <typename PT>
+LG_DEVICE void uf_unite(PT parent, int a, int b) {
+  bool done;
+  do {
+    a = uf_find(parent, a);
+    b = uf_find(parent, b);
+    if (a < b) {
+      int old = atomicMin(&parent[b], a);
+      done = (old == b);
+      b = old;
+    } else if (b < a) {
+      int old = atomicMin(&parent[a], b);
+      done = (old == a);
+      a = old;
+    } else {
+      done = true;
+    }
+  } while (!done);
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int V = P.V, H = P.H, VH = P.VH, G = P.G;
+  int* scratch = smem;  // 64 ints
+  int* parent = kLds ? (smem + 64) : (B.cc_parent + (size_t)s * VH);
+  const float* range = B.range + (size_t)s * VH;
+  const int8_t* ground = B.ground + (size_t)s * VH;
+  const float4* cloud = B.cloud + (size_t)s * VH;
+  int32_t* label = B.label + (size_t)s * VH;
+  auto eligible = [&](int c) { return ground[c] != 1 && range[c] != FLT_MAX; };  // _label_mat == 0
+
+  for (int c = tid; c < VH; c += nt) parent[c] = eligible(c) ? c : -1;
+  __syncthreads();
+  for (int c = tid; c < VH; c += nt) {
+    if (parent[c] < 0) continue;
+    const int i = c / H, j = c - i * H;
+    const float rc = range[c];
+    const int cr = (j + 1 < H) ? c + 1 : i * H;  // right neighbour, horizontal wrap
+    if (parent[cr] >= 0 && seg_edge(rc, range[cr], P.sinX, P.cosX, P.theta_thr)) uf_unite(parent, c, cr);
+    if (i + 1 < V) {
+      const int cd = c + H;
+      if (parent[cd] >= 0 && seg_edge(rc, range[cd], P.sinY, P.cosY, P.theta_thr)) uf_unite(parent, c, cd);
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < VH; c += nt)
+    if (parent[c] >= 0) parent[c] = uf_find(parent, c);
+  __syncthreads();
+
+  // ---- per-root size and row mask (rows of non-seed members) ----
+  if constexpr (kLds) {
+    // park roots in the label image, reuse LDS as packed {count:16 | rowmask:16} (V <= 16)
+    for (int c = tid; c < VH; c += nt) label[c] = parent[c];
+    __syncthreads();
+    unsigned* agg = (unsigned*)parent;
+    for (int c = tid; c < VH; c += nt) agg[c] = 0u;
+    __syncthreads();
+    for (int c = tid; c < VH; c += nt) {
+      const int r = label[c];
+      if (r < 0) continue;
+      atomicAdd(&agg[r], 1u);
+      if (r != c) atomicOr(&agg[r], 1u << (16 + c / H));
+    }
+    __syncthreads();
+    int running = 0;
+    for (int base = 0; base < VH; base += nt) {
+      const int c = base + tid;
+      bool feas = false, isroot = false;
+      if (c < VH && label[c] == c) {
+        isroot = true;
+        const unsigned a = agg[c];
+        const int cnt = (int)(a & 0xffffu);
+        const int lines = __popc(a >> 16);
+        feas = cnt >= 30 || (cnt >= P.seg_valid_pt && lines >= P.seg_valid_line);
+      }
+      int ex, ex2, tot, tot2;
+      block_scan2(feas, false, scratch, ex, ex2, tot, tot2);
+      if (isroot) agg[c] = feas ? (unsigned)(running + ex + 1) : 999999u;
+      running += tot;
+    }
+    __syncthreads();
+    for (int c = tid; c < VH; c += nt) {
+      const int r = label[c];
+      label[c] = (r < 0) ? -1 : (int)agg[r];
+    }
+  } else {
+    int32_t* cnt = B.cc_cnt + (size_t)s * VH;
+    unsigned long long* msk = B.cc_mask + (size_t)s * VH;
+    for (int c = tid; c < VH; c += nt) { cnt[c] = 0; msk[c] = 0ull; }
+    __syncthreads();
+    for (int c = tid; c < VH; c += nt) {
+      const int r = parent[c];
+      if (r < 0) continue;
+      atomicAdd(&cnt[r], 1);
+      if (r != c) atomicOr(&msk[r], 1ull << (c / H));
+    }
+    __syncthreads();
+    int running = 0;
+    for (int base = 0; base < VH; base += nt) {
+      const int c = base + tid;
+      bool feas = false, isroot = false;
+      if (c < VH && parent[c] == c) {
+        isroot = true;
+        const int n = cnt[c];
+        const int lines = __popcll(msk[c]);
+        feas = n >= 30 || (n >= P.seg_valid_pt && lines >= P.seg_valid_line);
+      }
+      int ex, ex2, tot, tot2;
+      block_scan2(feas, false, scratch, ex, ex2, tot, tot2);
+      if (isroot) cnt[c] = feas ? running + ex + 1 : 999999;
+      running += tot;
+    }
+    __syncthreads();
+    for (int c = tid; c < VH; c += nt) {
+      const int r = parent[c];
+      label[c] = (r < 0) ? -1 : cnt[r];
+    }
+  }
+  __syncthreads();
+
+  // ---- cloudSegmentation extraction (:358-396): raster-order compaction ----
+  float4* seg_pts = B.seg_pts + (size_t)s * VH;
+  float* seg_range = B.seg_range + (size_t)s * VH;
+  uint32_t* seg_col = B.seg_col + (size_t)s * VH;
+  uint8_t* seg_ground = B.seg_ground + (size_t)s * VH;
+  float4* outlier = B.outlier + (size_t)s * VH;
+  int32_t* ring_start = B.ring_start + (size_t)s * V;
+  int32_t* ring_end = B.ring_end + (size_t)s * V;
+  int nseg = 0, nout = 0;
+  for (int base = 0; base < VH; base += nt) {
+    const int c = base + tid;
+    bool pseg = false, pout = false;
+    int i = 0, j = 0, g = 0, lab = 0;
+    if (c < VH) {
+      i = c / H;
+      j = c - i * H;
+      lab = label[c];
+      g = ground[c];
+      if (lab > 0 || g == 1) {
+        if (lab == 999999) {
+          pout = (i > G && j % 5 == 0);
+        } else if (!(g == 1 && (j % 5 != 0 && j > 5 && j < H - 5))) {
+          pseg = true;
+        }
+      }
+    }
+    int e1, e2, t1, t2;
+    block_scan2(pseg, pout, scratch, e1, e2, t1, t2);
+    if (c < VH && j == 0) {
+      ring_start[i] = nseg + e1 - 1 + 5;
+      if (i > 0) ring_end[i - 1] = nseg + e1 - 1 - 5;
+    }
+    if (pseg) {
+      const int k = nseg + e1;
+      seg_pts[k] = cloud[c];
+      seg_range[k] = range[c];
+      seg_col[k] = (uint32_t)j;
+      seg_ground[k] = (uint8_t)(g == 1);
+    }
+    if (pout) outlier[nout + e2] = cloud[c];
+    nseg += t1;
+    nout += t2;
+  }
+  if (tid == 0) ring_end[V - 1] = nseg - 1 - 5;
+  // 2-D scan compaction (column order)
+  int nscan = 0;
+  const int32_t* cand = B.scan_cand + (size_t)s * H;
+  float4* scan = B.scan_msg + (size_t)s * H;
+  for (int base = 0; base < H; base += nt) {
+    const int j = base + tid;
+    const int cd = (j < H) ? cand[j] : -1;
+    int e1, e2, t1, t2;
+    block_scan2(cd >= 0, false, scratch, e1, e2, t1, t2);
+    if (cd >= 0) scan[nscan + e1] = cloud[cd];
+    nscan += t1;
+  }
+  if (tid == 0) {
+    int32_t* cnt = B.counts + (size_t)s * CNT_N;
+    cnt[CNT_M] = nseg;
+    cnt[CNT_OUTLIER] = nout;
+    cnt[CNT_SCAN] = nscan;
+  }
+}
+
+// ============================================================================================
+// k_fa_prep: adjustDistortion + calculateSmoothness + markOccludedPoints + adjustOutlierCloud
+// ============================================================================================
+LG_DEVICE float ori_branch1(float ori, float so) {
+  if ((double)ori < (double)so - M_PI / 2) ori = (float)((double)ori + 2 * M_PI);
+  else if ((double)ori > (double)so + M_PI * 3 / 2) ori = (float)((double)ori - 2 * M_PI);
+  return ori;
+}
+LG_DEVICE float ori_branch2(float ori, float eo) {
+  ori = (float)((double)ori + 2 * M_PI);
+  if ((double)ori < (double)eo - M_PI * 3 / 2) ori = (float)((double)ori + 2 * M_PI);
+  else if ((double)ori > (double)eo + M_PI / 2) ori = (float)((double)ori - 2 * M_PI);
+  return ori;
+}
+
+__global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
+  __shared__ int scratch[64];
+  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int VH = P.VH;
+  const int32_t* cnt = B.counts + (size_t)s * CNT_N;
+  const int M = cnt[CNT_M];
+  const float so = B.orient[s * 4 + 0], eo = B.orient[s * 4 + 1], od = B.orient[s * 4 + 2];
+  const float4* seg = B.seg_pts + (size_t)s * VH;
+  float4* fa = B.seg_fa + (size_t)s * VH;
+  const float* r = B.seg_range + (size_t)s * VH;
+  const uint32_t* col = B.seg_col + (size_t)s * VH;
+  float* curv = B.curv + (size_t)s * VH;
+  uint8_t* picked = B.picked + (size_t)s * VH;
+  int8_t* flabel = B.flabel + (size_t)s * VH;
+  int2* smooth = B.smooth + (size_t)s * VH;
+
+  // halfPassed switches after the first point whose branch-1 orientation passes start + pi
+  int h = 0x7fffffff;
+  for (int i = tid; i < M; i += nt) {
+    const float4 p = seg[i];
+    float ori = ori_branch1(-atan2f_g(p.y, p.x), so);
+    if ((double)(ori - so) > M_PI) h = min(h, i);
+  }
+  h = block_min_int(h, scratch);
+  for (int i = tid; i < M; i += nt) {
+    const float4 p = seg[i];
+    float ori = -atan2f_g(p.y, p.x);  // point.x = y, point.z = x
+    ori = (i <= h) ? ori_branch1(ori, so) : ori_branch2(ori, eo);
+    float relTime = (ori - so) / od;
+    float inten = (float)(int)p.w + P.scan_period * relTime;
+    fa[i] = make_float4(p.y, p.z, p.x, inten);
+  }
+  for (int i = 5 + tid; i < M - 5; i += nt) {
+    float d = r[i - 5] + r[i - 4] + r[i - 3] + r[i - 2] + r[i - 1] - r[i] * 10 + r[i + 1] + r[i + 2] +
+              r[i + 3] + r[i + 4] + r[i + 5];
+    const float cv = d * d;
+    curv[i] = cv;
+    picked[i] = 0;
+    flabel[i] = 0;
+    smooth[i] = make_int2(__float_as_int(cv), i);
+  }
+  __syncthreads();
+  for (int i = 5 + tid; i < M - 6; i += nt) {
+    const float depth1 = r[i], depth2 = r[i + 1];
+    const int columnDiff = abs((int)(col[i + 1] - col[i]));
+    if (columnDiff < 10) {
+      if ((double)(depth1 - depth2) > 0.3) {
+        for (int k = 0; k <= 5; ++k) picked[i - k] = 1;
+      } else if ((double)(depth2 - depth1) > 0.3) {
+        for (int k = 1; k <= 6; ++k) picked[i + k] = 1;
+      }
+    }
+    const float diff1 = fabsf(r[i - 1] - r[i]), diff2 = fabsf(r[i + 1] - r[i]);
+    if ((double)diff1 > 0.02 * (double)r[i] && (double)diff2 > 0.02 * (double)r[i]) picked[i] = 1;
+  }
+  const int nout = cnt[CNT_OUTLIER];
+  const float4* outl = B.outlier + (size_t)s * VH;
+  float4* outa = B.outlier_fa + (size_t)s * VH;
+  for (int k = tid; k < nout; k += nt) {
+    const float4 p = outl[k];
+    outa[k] = make_float4(p.y, p.z, p.x, p.w);
+  }
+}
+
+// ============================================================================================
+// k_extract: extractFeatures, one wave per ring
+// ============================================================================================
+#define SEG_MAX 512
+#define RING_MAX 2048
+
+struct ExtractLds {
+  float skey[SEG_MAX];
+  int sval[SEG_MAX];
+  unsigned vkey[RING_MAX];
+  int vval[RING_MAX];
+};
+
+struct ScanView {
+  int M, VH;
+  const float* curv;
+  uint8_t* picked;
+  int8_t* flabel;
+  const uint32_t* col;
+  const uint8_t* gflag;
+  const float4* fa;
+  LG_DEVICE uint32_t col_at(int k) const { return k < M ? col[k] : 0u; }         // tail is 0 (:138)
+  LG_DEVICE bool ground_at(int k) const { return k < M ? gflag[k] != 0 : false; }  // tail false (:137)
+};
+
+LG_DEVICE void suppress_neighbours(const ScanView& v, int ind) {  // :306-326
+  v.picked[ind] = 1;
+  for (int l = 1; l <= 5; l++) {
+    if ((unsigned)(ind + l) >= (unsigned)v.VH) continue;
+    int columnDiff = abs((int)(v.col_at(ind + l) - v.col_at(ind + l - 1)));
+    if (columnDiff > 10) break;
+    v.picked[ind + l] = 1;
+  }
+  for (int l = -1; l >= -5; l--) {
+    if (ind + l < 0) continue;
+    int columnDiff = abs((int)(v.col_at(ind + l) - v.col_at(ind + l + 1)));
+    if (columnDiff > 10) break;
+    v.picked[ind + l] = 1;
+  }
+}
+
+// Sort [0, n) of (key, val): all-distinct keys -> rank scatter (any correct sort gives the same
+// permutation); any tie -> exact libstdc++ introsort on one lane.
+LG_DEVICE void sort_segment(float* key, int* val, int n) {
+  const int lane = lane_id();
+  float rk[SEG_MAX / 64];
+  int rv[SEG_MAX / 64], rr[SEG_MAX / 64];
+  bool tie = false;
+#pragma unroll
+  for (int q = 0; q < SEG_MAX / 64; ++q) {
+    const int a = lane + 64 * q;
+    rr[q] = -1;
+    if (a < n) {
+      const float ka = key[a];
+      int r = 0, eq = 0;
+      for (int b = 0; b < n; ++b) {
+        const float kb = key[b];
+        r += (kb < ka);
+        eq += (kb == ka);
+      }
+      rk[q] = ka;
+      rv[q] = val[a];
+      rr[q] = r;
+      tie |= (eq > 1);
+    }
+  }
+  const bool any_tie = __ballot(tie) != 0ull;
+  __syncthreads();
+  if (!any_tie) {
+#pragma unroll
+    for (int q = 0; q < SEG_MAX / 64; ++q)
+      if (rr[q] >= 0) {
+        key[rr[q]] = rk[q];
+        val[rr[q]] = rv[q];
+      }
+  } else if (lane == 0) {
+    std_sort<float>(key, val, n);
+  }
+  __syncthreads();
+}
+
+struct RingOut {
+  float4* sharp; int32_t* sharp_ind;
+  float4* lsharp; int32_t* lsharp_ind;
+  float4* flat; int32_t* flat_ind;
+  float4* lflat;
+  int nS, nLS, nF, nLF;
+  int status;
+};
+
+LG_DEVICE float4 seg_point(const ScanView& v, int ind, int& status) {  // segmentedCloud->points[ind]
+  if (ind >= 0 && ind < v.M) return v.fa[ind];
+  status |= LEGO_ST_STALE_IND_OOB;
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// PCL VoxelGrid<PointXYZI> (leaf 0.2) over the ring's lessFlat points (positions in L.vval[0..n)).
+LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, RingOut& o) {
+  const int lane = lane_id();
+  o.nLF = 0;
+  if (n == 0) return;
+  const float leaf = 0.2f;
+  const float inv = 1.0f / leaf;
+  float mnx = FLT_MAX, mny = FLT_MAX, mnz = FLT_MAX, mxx = -FLT_MAX, mxy = -FLT_MAX, mxz = -FLT_MAX;
+  for (int t = lane; t < n; t += 64) {
+    const float4 p = v.fa[L.vval[t]];
+    mnx = (p.x < mnx) ? p.x : mnx; mny = (p.y < mny) ? p.y : mny; mnz = (p.z < mnz) ? p.z : mnz;
+    mxx = (p.x > mxx) ? p.x : mxx; mxy = (p.y > mxy) ? p.y : mxy; mxz = (p.z > mxz) ? p.z : mxz;
+  }
+  mnx = wave_min(mnx); mny = wave_min(mny); mnz = wave_min(mnz);
+  mxx = wave_max(mxx); mxy = wave_max(mxy); mxz = wave_max(mxz);
+  const long long dx = (long long)((mxx - mnx) * inv) + 1;
+  const long long dy = (long long)((mxy - mny) * inv) + 1;
+  const long long dz = (long long)((mxz - mnz) * inv) + 1;
+  if (dx * dy * dz > 2147483647ll) {  // PCL: "Integer indices would overflow" -> output = input
+    for (int t = lane; t < n; t += 64) o.lflat[t] = v.fa[L.vval[t]];
+    o.nLF = n;
+    o.status |= LEGO_ST_VOXEL_OVERFLOW;
+    return;
+  }
+  const int minbx = (int)floorf(mnx * inv), minby = (int)floorf(mny * inv), minbz = (int)floorf(mnz * inv);
+  const int maxbx = (int)floorf(mxx * inv), maxby = (int)floorf(mxy * inv);
+  const int divx = maxbx - minbx + 1, divy = maxby - minby + 1;
+  const int mul1 = divx, mul2 = divx * divy;
+  for (int t = lane; t < n; t += 64) {
+    const float4 p = v.fa[L.vval[t]];
+    const int i0 = (int)(floorf(p.x * inv) - (float)minbx);
+    const int i1 = (int)(floorf(p.y * inv) - (float)minby);
+    const int i2 = (int)(floorf(p.z * inv) - (float)minbz);
+    L.vkey[t] = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+  }
+  __syncthreads();
+  if (lane == 0) std_sort<unsigned>(L.vkey, L.vval, n);
+  __syncthreads();
+  int running = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int t = base + lane;
+    const bool start = t < n && (t == 0 || L.vkey[t] != L.vkey[t - 1]);
+    const unsigned long long m = __ballot(start);
+    if (start) {
+      const unsigned k = L.vkey[t];
+      float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+      int u = t;
+      for (; u < n && L.vkey[u] == k; ++u) {
+        const float4 p = v.fa[L.vval[u]];
+        sx += p.x; sy += p.y; sz += p.z; si += p.w;
+      }
+      const float cntf = (float)(u - t);
+      o.lflat[running + popc_below(m)] = make_float4(sx / cntf, sy / cntf, sz / cntf, si / cntf);
+    }
+    running += __popcll(m);
+  }
+  o.nLF = running;
+}
+
+LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, int st, int en,
+                            ExtractLds& L, RingOut& o) {
+  const int lane = lane_id();
+  int nlist = 0;
+  for (int j = 0; j < 6; j++) {
+    const int sp = (st * (6 - j) + en * j) / 6;
+    const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
+    if (sp >= ep) continue;
+    const int n = ep - sp;  // sorted range [sp, ep); ep itself is visited unsorted
+    for (int t = lane; t <= n; t += 64) {
+      const int2 e = smooth[sp + t];
+      L.skey[t] = __int_as_float(e.x);
+      L.sval[t] = e.y;
+    }
+    __syncthreads();
+    sort_segment(L.skey, L.sval, n);
+    for (int t = lane; t < n; t += 64) smooth[sp + t] = make_int2(__float_as_int(L.skey[t]), L.sval[t]);
+
+    // sharp: k = ep .. sp (descending curvature), first 2 eligible -> sharp, up to 20 -> less sharp
+    int largest = 0;
+    bool stop = false;
+    for (int base = n; base >= 0 && !stop; base -= 64) {
+      const int t = base - lane;
+      const bool valid = t >= 0;
+      const int ind = valid ? L.sval[t] : 0;
+      bool alive = valid;
+      while (true) {
+        const bool elig = alive && v.picked[ind] == 0 && v.curv[ind] > P.edge_thr && !v.ground_at(ind);
+        const unsigned long long m = __ballot(elig);
+        if (m == 0ull) break;
+        const int f = __ffsll((long long)m) - 1;
+        const int aind = __shfl(ind, f);
+        largest++;
+        if (largest > 20) { stop = true; break; }
+        if (lane == 0) {
+          const float4 pt = seg_point(v, aind, o.status);
+          if (largest <= 2) {
+            v.flabel[aind] = 2;
+            o.sharp[o.nS] = pt;
+            o.sharp_ind[o.nS] = aind;
+          } else {
+            v.flabel[aind] = 1;
+          }
+          o.lsharp[o.nLS] = pt;
+          o.lsharp_ind[o.nLS] = aind;
+          suppress_neighbours(v, aind);
+        }
+        if (largest <= 2) o.nS++;
+        o.nLS++;
+        alive = alive && lane > f;
+        __syncthreads();
+      }
+    }
+    // flat: k = sp .. ep, ground points with curvature < surf threshold, at most 4
+    int smallest = 0;
+    stop = false;
+    for (int base = 0; base <= n && !stop; base += 64) {
+      const int t = base + lane;
+      const bool valid = t <= n;
+      const int ind = valid ? L.sval[t] : 0;
+      bool alive = valid;
+      while (true) {
+        const bool elig = alive && v.picked[ind] == 0 && v.curv[ind] < P.surf_thr && v.ground_at(ind);
+        const unsigned long long m = __ballot(elig);
+        if (m == 0ull) break;
+        const int f = __ffsll((long long)m) - 1;
+        const int aind = __shfl(ind, f);
+        smallest++;
+        if (lane == 0) {
+          v.flabel[aind] = -1;
+          o.flat[o.nF] = seg_point(v, aind, o.status);
+          o.flat_ind[o.nF] = aind;
+          if (smallest < 4) suppress_neighbours(v, aind);
+        }
+        o.nF++;
+        if (smallest >= 4) { stop = true; break; }
+        alive = alive && lane > f;
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+    // lessFlat: positions k in [sp, ep] whose label <= 0 (position, not sorted index: :370-374)
+    for (int base = 0; base <= n; base += 64) {
+      const int t = base + lane;
+      const int k = sp + t;
+      const bool pr = t <= n && v.flabel[k] <= 0;
+      const unsigned long long m = __ballot(pr);
+      if (pr) L.vval[nlist + popc_below(m)] = k;
+      nlist += __popcll(m);
+    }
+    __syncthreads();
+  }
+  voxel_ring(v, L, nlist, o);
+}
+
+__global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_pass) {
+  __shared__ ExtractLds L;
+  const int V = P.V, VH = P.VH;
+  const int s = first_pass ? blockIdx.x : blockIdx.x / V;
+  const int ring = first_pass ? 0 : blockIdx.x % V;
+  const int32_t* rs = B.ring_start + (size_t)s * V;
+  const int32_t* re = B.ring_end + (size_t)s * V;
+  ScanView v;
+  v.M = B.counts[(size_t)s * CNT_N + CNT_M];
+  v.VH = VH;
+  v.curv = B.curv + (size_t)s * VH;
+  v.picked = B.picked + (size_t)s * VH;
+  v.flabel = B.flabel + (size_t)s * VH;
+  v.col = B.seg_col + (size_t)s * VH;
+  v.gflag = B.seg_ground + (size_t)s * VH;
+  v.fa = B.seg_fa + (size_t)s * VH;
+  int2* smooth = B.smooth + (size_t)s * VH;
+  // Rings whose range starts at position 4 (the leading rings) read the stale slot 4 of the
+  // persistent smoothness array, whose index may point into any ring: they run first, in order,
+  // on one wave.  Every other ring only reads/writes its own position range (+-5), so the rest
+  // run one wave per ring in parallel.
+  const int r0 = first_pass ? 0 : ring, r1 = first_pass ? V : ring + 1;
+  for (int r = r0; r < r1; ++r) {
+    const bool leading = rs[r] == 4;
+    if (first_pass ? !leading : leading) {
+      if (first_pass) break;
+      return;
+    }
+    RingOut o;
+    const size_t rb = (size_t)s * V + r;
+    o.sharp = B.r_sharp + rb * P.cap_sharp; o.sharp_ind = B.r_sharp_ind + rb * P.cap_sharp;
+    o.lsharp = B.r_lsharp + rb * P.cap_lsharp; o.lsharp_ind = B.r_lsharp_ind + rb * P.cap_lsharp;
+    o.flat = B.r_flat + rb * P.cap_flat; o.flat_ind = B.r_flat_ind + rb * P.cap_flat;
+    o.lflat = B.r_lflat + rb * P.H;
+    o.nS = o.nLS = o.nF = o.nLF = 0;
+    o.status = 0;
+    extract_ring(P, v, smooth, rs[r], re[r], L, o);
+    if (lane_id() == 0) {
+      int32_t* rc = B.r_counts + rb * 4;
+      rc[0] = o.nS; rc[1] = o.nLS; rc[2] = o.nF; rc[3] = o.nLF;
+      B.r_status[rb] = o.status;
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================================================
+// k_concat: ring-ordered concatenation (cornerPointsSharp etc. are appended ring by ring)
+// ============================================================================================
+__global__ __launch_bounds__(256) void k_concat(LgParams P, LgBufs B) {
+  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int V = P.V;
+  __shared__ int off[4][65];
+  __shared__ int st;
+  if (tid == 0) {
+    int a[4] = {0, 0, 0, 0};
+    int status = 0;
+    for (int r = 0; r < V; ++r) {
+      const int32_t* rc = B.r_counts + ((size_t)s * V + r) * 4;
+      for (int k = 0; k < 4; ++k) { off[k][r] = a[k]; a[k] += rc[k]; }
+      status |= B.r_status[(size_t)s * V + r];
+    }
+    for (int k = 0; k < 4; ++k) off[k][V] = a[k];
+    st = status;
+    int32_t* cnt = B.counts + (size_t)s * CNT_N;
+    cnt[CNT_SHARP] = a[0]; cnt[CNT_LSHARP] = a[1]; cnt[CNT_FLAT] = a[2]; cnt[CNT_LFLAT] = a[3];
+    cnt[CNT_STATUS] = status;
+  }
+  __syncthreads();
+  for (int r = 0; r < V; ++r) {
+    const size_t rb = (size_t)s * V + r;
+    const int32_t* rc = B.r_counts + rb * 4;
+    for (int t = tid; t < rc[0]; t += nt) {
+      B.f_sharp[(size_t)s * V * P.cap_sharp + off[0][r] + t] = B.r_sharp[rb * P.cap_sharp + t];
+      B.f_sharp_ind[(size_t)s * V * P.cap_sharp + off[0][r] + t] = B.r_sharp_ind[rb * P.cap_sharp + t];
+    }
+    for (int t = tid; t < rc[1]; t += nt) {
+      B.f_lsharp[(size_t)s * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp[rb * P.cap_lsharp + t];
+      B.f_lsharp_ind[(size_t)s * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp_ind[rb * P.cap_lsharp + t];
+    }
+    for (int t = tid; t < rc[2]; t += nt) {
+      B.f_flat[(size_t)s * V * P.cap_flat + off[2][r] + t] = B.r_flat[rb * P.cap_flat + t];
+      B.f_flat_ind[(size_t)s * V * P.cap_flat + off[2][r] + t] = B.r_flat_ind[rb * P.cap_flat + t];
+    }
+    for (int t = tid; t < rc[3]; t += nt)
+      B.f_lflat[(size_t)s * P.VH + off[3][r] + t] = B.r_lflat[rb * P.H + t];
+  }
+}
+
+// ============================================================================================
+// k_lm: updateTransformation + integrateTransformation + publishOdometry + publishCloudsLast
+// ============================================================================================
+#define LM_THREADS 256
+#define LM_MAXQ 1536  // 24 * 64 rings
+
+LG_DEVICE float4 transform_to_start(const float4 pi, const float* cur) {  // :388-418
+  float s = 10 * (pi.w - (float)(int)pi.w);
+  float ry = s * cur[1];
+  float rx = s * cur[0];
+  float rz = s * cur[2];
+  float tx = s * cur[3];
+  float ty = s * cur[4];
+  float tz = s * cur[5];
+  const float crz = cosf_g(rz), srz = sinf_g(rz), crx = cosf_g(rx), srx = sinf_g(rx), cry = cosf_g(ry),
+              sry = sinf_g(ry);
+  float x1 = crz * (pi.x - tx) + srz * (pi.y - ty);
+  float y1 = -srz * (pi.x - tx) + crz * (pi.y - ty);
+  float z1 = (pi.z - tz);
+  float x2 = x1;
+  float y2 = crx * y1 + srx * z1;
+  float z2 = -srx * y1 + crx * z1;
+  return make_float4(cry * x2 - sry * z2, y2, sry * x2 + cry * z2, pi.w);
+}
+
+LG_DEVICE float4 transform_to_end(const float4 pi, const float* cur) {  // :422-471
+  float s = 10 * (pi.w - (float)(int)pi.w);
+  float rx = s * cur[0];
+  float ry = s * cur[1];
+  float rz = s * cur[2];
+  float tx = s * cur[3];
+  float ty = s * cur[4];
+  float tz = s * cur[5];
+  float c, sn;
+  c = cosf_g(rz); sn = sinf_g(rz);
+  float x1 = c * (pi.x - tx) + sn * (pi.y - ty);
+  float y1 = -sn * (pi.x - tx) + c * (pi.y - ty);
+  float z1 = (pi.z - tz);
+  c = cosf_g(rx); sn = sinf_g(rx);
+  float x2 = x1;
+  float y2 = c * y1 + sn * z1;
+  float z2 = -sn * y1 + c * z1;
+  c = cosf_g(ry); sn = sinf_g(ry);
+  float x3 = c * x2 - sn * z2;
+  float y3 = y2;
+  float z3 = sn * x2 + c * z2;
+  rx = cur[0]; ry = cur[1]; rz = cur[2];
+  tx = cur[3]; ty = cur[4]; tz = cur[5];
+  c = cosf_g(ry); sn = sinf_g(ry);
+  float x4 = c * x3 + sn * z3;
+  float y4 = y3;
+  float z4 = -sn * x3 + c * z3;
+  c = cosf_g(rx); sn = sinf_g(rx);
+  float x5 = x4;
+  float y5 = c * y4 - sn * z4;
+  float z5 = sn * y4 + c * z4;
+  c = cosf_g(rz); sn = sinf_g(rz);
+  float x6 = c * x5 - sn * y5 + tx;
+  float y6 = sn * x5 + c * y5 + ty;
+  float z6 = z5 + tz;
+  return make_float4(x6, y6, z6, (float)(int)pi.w);
+}
+
+// Eigen boundary model, identical to the oracle's: ColPivHouseholderQR<Matrix3f>::solve in float.
+LG_DEVICE void qr_solve3(const float* A_in, const float* b_in, float* x) {
+  float A[9];
+  for (int i = 0; i < 9; ++i) A[i] = A_in[i];
+  const float eps = FLT_EPSILON;
+  float nu[3], nd[3], hc[3];
+  int perm[3] = {0, 1, 2};
+  for (int k = 0; k < 3; ++k) {
+    float s = 0.f;
+    for (int r = 0; r < 3; ++r) s += A[r * 3 + k] * A[r * 3 + k];
+    nu[k] = nd[k] = sqrtf(s);
+  }
+  float maxn = fmaxf(nu[0], fmaxf(nu[1], nu[2]));
+  float th_help = (maxn * eps) * (maxn * eps) / 3.0f;
+  float ndt = sqrtf(eps);
+  int nzp = 3;
+  for (int k = 0; k < 3; ++k) {
+    int bc = k;
+    for (int j = k + 1; j < 3; ++j)
+      if (nu[j] > nu[bc]) bc = j;
+    float bsq = nu[bc] * nu[bc];
+    if (nzp == 3 && bsq < th_help * float(3 - k)) nzp = k;
+    if (bc != k) {
+      for (int r = 0; r < 3; ++r) { float t = A[r * 3 + k]; A[r * 3 + k] = A[r * 3 + bc]; A[r * 3 + bc] = t; }
+      float t = nu[k]; nu[k] = nu[bc]; nu[bc] = t;
+      t = nd[k]; nd[k] = nd[bc]; nd[bc] = t;
+      int ti = perm[k]; perm[k] = perm[bc]; perm[bc] = ti;
+    }
+    float tail = 0.f;
+    for (int r = k + 1; r < 3; ++r) tail += A[r * 3 + k] * A[r * 3 + k];
+    float c0 = A[k * 3 + k], tau, beta;
+    if (tail <= FLT_MIN) {
+      tau = 0.f; beta = c0;
+      for (int r = k + 1; r < 3; ++r) A[r * 3 + k] = 0.f;
+    } else {
+      beta = sqrtf(c0 * c0 + tail);
+      if (c0 >= 0.f) beta = -beta;
+      for (int r = k + 1; r < 3; ++r) A[r * 3 + k] = A[r * 3 + k] / (c0 - beta);
+      tau = (beta - c0) / beta;
+    }
+    hc[k] = tau;
+    A[k * 3 + k] = beta;
+    if (tau != 0.f) {
+      for (int j = k + 1; j < 3; ++j) {
+        float t = A[k * 3 + j];
+        for (int r = k + 1; r < 3; ++r) t += A[r * 3 + k] * A[r * 3 + j];
+        A[k * 3 + j] -= tau * t;
+        for (int r = k + 1; r < 3; ++r) A[r * 3 + j] -= tau * A[r * 3 + k] * t;
+      }
+    }
+    for (int j = k + 1; j < 3; ++j) {
+      if (nu[j] != 0.f) {
+        float t = fabsf(A[k * 3 + j]) / nu[j];
+        t = (1.f + t) * (1.f - t);
+        if (t < 0.f) t = 0.f;
+        float q = nu[j] / nd[j];
+        float t2 = t * q * q;
+        if (t2 <= ndt) {
+          float s = 0.f;
+          for (int r = k + 1; r < 3; ++r) s += A[r * 3 + j] * A[r * 3 + j];
+          nd[j] = sqrtf(s);
+          nu[j] = nd[j];
+        } else {
+          nu[j] *= sqrtf(t);
+        }
+      }
+    }
+  }
+  float c[3] = {b_in[0], b_in[1], b_in[2]};
+  for (int k = 0; k < nzp; ++k) {
+    if (hc[k] == 0.f) continue;
+    float t = c[k];
+    for (int r = k + 1; r < 3; ++r) t += A[r * 3 + k] * c[r];
+    c[k] -= hc[k] * t;
+    for (int r = k + 1; r < 3; ++r) c[r] -= hc[k] * A[r * 3 + k] * t;
+  }
+  float y[3] = {0.f, 0.f, 0.f};
+  for (int i = nzp - 1; i >= 0; --i) {
+    float t = c[i];
+    for (int j = i + 1; j < nzp; ++j) t -= A[i * 3 + j] * y[j];
+    y[i] = t / A[i * 3 + i];
+  }
+  for (int i = 0; i < 3; ++i) x[perm[i]] = y[i];
+}
+
+LG_DEVICE double eig_max_sym3(const float* Af) {
+  double a[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) a[i][j] = Af[i * 3 + j];
+  for (int sweep = 0; sweep < 32; ++sweep) {
+    double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+    if (off == 0.0) break;
+    for (int p = 0; p < 2; ++p)
+      for (int q = p + 1; q < 3; ++q) {
+        if (a[p][q] == 0.0) continue;
+        double theta = (a[q][q] - a[p][p]) / (2.0 * a[p][q]);
+        double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < 3; ++k) {
+          double akp = a[k][p], akq = a[k][q];
+          a[k][p] = c * akp - s * akq;
+          a[k][q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < 3; ++k) {
+          double apk = a[p][k], aqk = a[q][k];
+          a[p][k] = c * apk - s * aqk;
+          a[q][k] = s * apk + c * aqk;
+        }
+      }
+  }
+  return fmax(a[0][0], fmax(a[1][1], a[2][2]));
+}
+
+struct LmLds {
+  float4 sel[LM_MAXQ];
+  int ind1[LM_MAXQ], ind2[LM_MAXQ], ind3[LM_MAXQ];
+  double red[LM_THREADS / 64][10];
+  float cur[6];
+  int flag;      // 1 = keep iterating
+  int status;
+  int skip;
+};
+
+// candidate key compare: (dist, rank) lexicographic = sequential strict-< scan order
+LG_DEVICE bool key_lt(float d1, int r1, float d2, int r2) { return d1 < d2 || (d1 == d2 && r1 < r2); }
+LG_DEVICE void wave_argmin(float& d, int& r, int& idx) {
+  for (int o = 32; o > 0; o >>= 1) {
+    float d2 = __shfl_xor(d, o);
+    int r2 = __shfl_xor(r, o), i2 = __shfl_xor(idx, o);
+    if (key_lt(d2, r2, d, r)) { d = d2; r = r2; idx = i2; }
+  }
+}
+
+// One wave: kd-tree 1-NN (brute force, lowest index among exact ties, nanoflann_pcl.h:141-152) and
+// the reference's ring-limited linear scans for the 2nd (and 3rd) correspondence (fa.cpp:503-564,
+// 640-713).  surf = 3-point plane search, else 2-point line search.
+LG_DEVICE void search_one(const LgParams& P, const float4* __restrict__ last, int nl, float4 sel, int fwd_bound,
+                          bool surf, int& o1, int& o2, int& o3, int& status) {
+  const int lane = lane_id();
+  float bd = FLT_MAX;
+  int bi = 0x7fffffff, tc = 0;
+  for (int j = lane; j < nl; j += 64) {
+    const float4 p = last[j];
+    const float dx = sel.x - p.x, dy = sel.y - p.y, dz = sel.z - p.z;
+    const float d = dx * dx + dy * dy + dz * dz;
+    if (d < bd) { bd = d; bi = j; tc = 0; }
+    else if (d == bd) tc++;
+  }
+  float gd = bd;
+  int gr = bi, gi = bi;
+  wave_argmin(gd, gr, gi);
+  const int ties = wave_sum((bd == gd && bi != 0x7fffffff) ? tc + 1 : 0) - 1;
+  if (ties > 0 && nl > 0) status |= LEGO_ST_NN_TIE;
+  o1 = -1; o2 = -1; o3 = -1;
+  if (!(gd < P.nn_dist_sqr) || nl == 0) return;
+  const int closest = gi;
+  o1 = closest;
+  const int ring0 = (int)last[closest].w;
+  float b2d = P.nn_dist_sqr, b3d = P.nn_dist_sqr;
+  int b2r = 0x7fffffff, b3r = 0x7fffffff, b2i = -1, b3i = -1;
+  int bound = fwd_bound;  // reference bug: bounded by the current feature count (:522, :661)
+  if (bound > nl) {
+    if (closest + 1 < bound) status |= LEGO_ST_FWD_OOB;
+    bound = nl;
+  }
+  // forward j = closest+1 ..
+  for (int base = closest + 1; base < bound; base += 64) {
+    const int j = base + lane;
+    const bool valid = j < bound;
+    int rj = valid ? (int)last[j].w : 0;
+    const bool brk = valid && (double)rj > (double)ring0 + 2.5;
+    const unsigned long long bm = __ballot(brk);
+    const int fb = bm ? __ffsll((long long)bm) - 1 : 64;
+    if (valid && lane < fb) {
+      const float4 p = last[j];
+      const float d = (p.x - sel.x) * (p.x - sel.x) + (p.y - sel.y) * (p.y - sel.y) + (p.z - sel.z) * (p.z - sel.z);
+      const int rank = j - closest;
+      if (surf) {
+        if (rj <= ring0) { if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; } }
+        else { if (key_lt(d, rank, b3d, b3r)) { b3d = d; b3r = rank; b3i = j; } }
+      } else if (rj > ring0) {
+        if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; }
+      }
+    }
+    if (bm) break;
+  }
+  // backward j = closest-1 .. 0
+  for (int top = closest - 1; top >= 0; top -= 64) {
+    const int j = top - lane;
+    const bool valid = j >= 0;
+    int rj = valid ? (int)last[j].w : 0;
+    const bool brk = valid && (double)rj < (double)ring0 - 2.5;
+    const unsigned long long bm = __ballot(brk);
+    const int fb = bm ? __ffsll((long long)bm) - 1 : 64;
+    if (valid && lane < fb) {
+      const float4 p = last[j];
+      const float d = (p.x - sel.x) * (p.x - sel.x) + (p.y - sel.y) * (p.y - sel.y) + (p.z - sel.z) * (p.z - sel.z);
+      const int rank = (1 << 24) + (closest - j);
+      if (surf) {
+        if (rj >= ring0) { if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; } }
+        else { if (key_lt(d, rank, b3d, b3r)) { b3d = d; b3r = rank; b3i = j; } }
+      } else if (rj < ring0) {
+        if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; }
+      }
+    }
+    if (bm) break;
+  }
+  wave_argmin(b2d, b2r, b2i);
+  o2 = b2i;
+  if (surf) {
+    wave_argmin(b3d, b3r, b3i);
+    o3 = b3i;
+  }
+}
+
+// block reduce of 9 doubles + count; result valid on thread 0
+LG_DEVICE void block_reduce10(LmLds& L, double* v) {
+  for (int k = 0; k < 10; ++k) {
+    double x = v[k];
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o);
+    v[k] = x;
+  }
+  if (lane_id() == 0)
+    for (int k = 0; k < 10; ++k) L.red[wave_id()][k] = v[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 10; ++k) {
+      double t = 0.0;
+      for (int w = 0; w < LM_THREADS / 64; ++w) t += L.red[w][k];
+      v[k] = t;
+    }
+  }
+}
+
+// thread 0: AtA/AtB -> solve -> degeneracy -> update; returns keep-iterating
+LG_DEVICE bool lm_solve(LmLds& L, LgState& S, const double* red, int iter, bool surf) {
+  float AtA[9], AtB[3], x[3];
+  AtA[0] = (float)red[0]; AtA[1] = (float)red[1]; AtA[2] = (float)red[2];
+  AtA[3] = AtA[1]; AtA[4] = (float)red[3]; AtA[5] = (float)red[4];
+  AtA[6] = AtA[2]; AtA[7] = AtA[5]; AtA[8] = (float)red[5];
+  AtB[0] = (float)red[6]; AtB[1] = (float)red[7]; AtB[2] = (float)red[8];
+  qr_solve3(AtA, AtB, x);
+  if (iter == 0) {
+    S.is_degenerate = eig_max_sym3(AtA) < 10.0;
+  } else if (S.is_degenerate) {
+    L.status |= LEGO_ST_DEGEN_UB;
+  }
+  if (S.is_degenerate) {
+    L.status |= LEGO_ST_DEGENERATE;
+    x[0] = x[1] = x[2] = 0.f;
+  }
+  const float RAD2DEG = (float)(180.0 / M_PI);
+  float deltaR, deltaT;
+  if (surf) {
+    L.cur[0] += x[0]; L.cur[2] += x[1]; L.cur[4] += x[2];
+  } else {
+    L.cur[1] += x[0]; L.cur[3] += x[1]; L.cur[5] += x[2];
+  }
+  for (int i = 0; i < 6; i++)
+    if (isnan(L.cur[i])) L.cur[i] = 0;
+  if (surf) {
+    double a = (double)(RAD2DEG * x[0]), b = (double)(RAD2DEG * x[1]);
+    deltaR = (float)sqrt(a * a + b * b);
+    double c = (double)(x[2] * 100);
+    deltaT = (float)sqrt(c * c);
+  } else {
+    double a = (double)(RAD2DEG * x[0]);
+    deltaR = (float)sqrt(a * a);
+    double b = (double)(x[1] * 100), c = (double)(x[2] * 100);
+    deltaT = (float)sqrt(b * b + c * c);
+  }
+  return !((double)deltaR < 0.1 && (double)deltaT < 0.1);
+}
+
+LG_DEVICE void accumulate_surf_row(const float* cur, const float4 po, const float4 cf, double* acc) {
+  // calculateTransformationSurf :797-857 (per-row Jacobian)
+  float srx = sinf_g(cur[0]), crx = cosf_g(cur[0]), sry = sinf_g(cur[1]), cry = cosf_g(cur[1]);
+  float srz = sinf_g(cur[2]), crz = cosf_g(cur[2]);
+  float tx = cur[3], ty = cur[4], tz = cur[5];
+  float a1 = crx * sry * srz;
+  float a2 = crx * crz * sry;
+  float a3 = srx * sry;
+  float a4 = tx * a1 - ty * a2 - tz * a3;
+  float a5 = srx * srz;
+  float a6 = crz * srx;
+  float a7 = ty * a6 - tz * crx - tx * a5;
+  float a8 = crx * cry * srz;
+  float a9 = crx * cry * crz;
+  float a10 = cry * srx;
+  float a11 = tz * a10 + ty * a9 - tx * a8;
+  float b1 = -crz * sry - cry * srx * srz;
+  float b2 = cry * crz * srx - sry * srz;
+  float b5 = cry * crz - srx * sry * srz;
+  float b6 = cry * srz + crz * srx * sry;
+  float c1 = -b6;
+  float c2 = b5;
+  float c3 = tx * b6 - ty * b5;
+  float c4 = -crx * crz;
+  float c5 = crx * srz;
+  float c6 = ty * c5 + tx * -c4;
+  float c7 = b2;
+  float c8 = -b1;
+  float c9 = tx * -b2 - ty * -b1;
+  float arx = (-a1 * po.x + a2 * po.y + a3 * po.z + a4) * cf.x + (a5 * po.x - a6 * po.y + crx * po.z + a7) * cf.y +
+              (a8 * po.x - a9 * po.y - a10 * po.z + a11) * cf.z;
+  float arz = (c1 * po.x + c2 * po.y + c3) * cf.x + (c4 * po.x - c5 * po.y + c6) * cf.y + (c7 * po.x + c8 * po.y + c9) * cf.z;
+  float aty = -b6 * cf.x + c4 * cf.y + b2 * cf.z;
+  float bb = (float)(-0.05 * (double)cf.w);
+  const float a[3] = {arx, arz, aty};
+  acc[0] += (double)(a[0] * a[0]); acc[1] += (double)(a[0] * a[1]); acc[2] += (double)(a[0] * a[2]);
+  acc[3] += (double)(a[1] * a[1]); acc[4] += (double)(a[1] * a[2]); acc[5] += (double)(a[2] * a[2]);
+  acc[6] += (double)(a[0] * bb); acc[7] += (double)(a[1] * bb); acc[8] += (double)(a[2] * bb);
+  acc[9] += 1.0;
+}
+
+LG_DEVICE void accumulate_corner_row(const float* cur, const float4 po, const float4 cf, double* acc) {
+  // calculateTransformationCorner :939-977
+  float srx = sinf_g(cur[0]), crx = cosf_g(cur[0]), sry = sinf_g(cur[1]), cry = cosf_g(cur[1]);
+  float srz = sinf_g(cur[2]), crz = cosf_g(cur[2]);
+  float tx = cur[3], ty = cur[4], tz = cur[5];
+  float b1 = -crz * sry - cry * srx * srz;
+  float b2 = cry * crz * srx - sry * srz;
+  float b3 = crx * cry;
+  float b4 = tx * -b1 + ty * -b2 + tz * b3;
+  float b5 = cry * crz - srx * sry * srz;
+  float b6 = cry * srz + crz * srx * sry;
+  float b7 = crx * sry;
+  float b8 = tz * b7 - ty * b6 - tx * b5;
+  float c5 = crx * srz;
+  float ary = (b1 * po.x + b2 * po.y - b3 * po.z + b4) * cf.x + (b5 * po.x + b6 * po.y - b7 * po.z + b8) * cf.z;
+  float atx = -b5 * cf.x + c5 * cf.y + b1 * cf.z;
+  float atz = b7 * cf.x - srx * cf.y - b3 * cf.z;
+  float bb = (float)(-0.05 * (double)cf.w);
+  const float a[3] = {ary, atx, atz};
+  acc[0] += (double)(a[0] * a[0]); acc[1] += (double)(a[0] * a[1]); acc[2] += (double)(a[0] * a[2]);
+  acc[3] += (double)(a[1] * a[1]); acc[4] += (double)(a[1] * a[2]); acc[5] += (double)(a[2] * a[2]);
+  acc[6] += (double)(a[0] * bb); acc[7] += (double)(a[1] * bb); acc[8] += (double)(a[2] * bb);
+  acc[9] += 1.0;
+}
+
+// coefficient of one correspondence (surf: plane :721-776, corner: line :571-635); returns accepted
+LG_DEVICE bool surf_coeff(const float4* last, int i1, int i2, int i3, float4 sel, int iter, float4& cf) {
+  if (!(i2 >= 0 && i3 >= 0)) return false;
+  const float4 t1 = last[i1], t2 = last[i2], t3 = last[i3];
+  float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
+  float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
+  float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
+  float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
+  float ps = sqrtf(pa * pa + pb * pb + pc * pc);
+  pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+  float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+  float s = 1;
+  if (iter >= 5)
+    s = (float)(1 - 1.8 * (double)fabsf(pd2) / (double)sqrtf(sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
+  if ((double)s > 0.1 && pd2 != 0) {
+    cf = make_float4(s * pa, s * pb, s * pc, s * pd2);
+    return true;
+  }
+  return false;
+}
+
+LG_DEVICE bool corner_coeff(const float4* last, int i1, int i2, float4 sel, int iter, float4& cf) {
+  if (!(i2 >= 0)) return false;
+  const float4 tp1 = last[i1], tp2 = last[i2];
+  float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+  float x1 = tp1.x, y1 = tp1.y, z1 = tp1.z;
+  float x2 = tp2.x, y2 = tp2.y, z2 = tp2.z;
+  float m11 = ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1));
+  float m22 = ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1));
+  float m33 = ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1));
+  float a012 = sqrtf(m11 * m11 + m22 * m22 + m33 * m33);
+  float l12 = sqrtf((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+  float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+  float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+  float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+  float ld2 = a012 / l12;
+  float s = 1;
+  if (iter >= 5) s = (float)(1 - 1.8 * (double)fabsf(ld2));
+  if ((double)s > 0.1 && ld2 != 0) {
+    cf = make_float4(s * la, s * lb, s * lc, s * ld2);
+    return true;
+  }
+  return false;
+}
+
+// one LM loop (surf or corner), <= 25 iterations
+LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __restrict__ feat, int nq,
+                       const float4* __restrict__ last, int nl, bool surf, int& iters) {
+  const int tid = threadIdx.x;
+  const int nw = LM_THREADS / 64;
+  for (int iter = 0; iter < 25; iter++) {
+    float cur[6];
+    for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
+    for (int q = tid; q < nq; q += LM_THREADS) L.sel[q] = transform_to_start(feat[q], cur);
+    __syncthreads();
+    if (iter % 5 == 0) {
+      int st = 0;
+      for (int q = wave_id(); q < nq; q += nw) {
+        int o1, o2, o3;
+        search_one(P, last, nl, L.sel[q], nq, surf, o1, o2, o3, st);
+        if (lane_id() == 0) { L.ind1[q] = o1; L.ind2[q] = o2; L.ind3[q] = o3; }
+      }
+      if (lane_id() == 0 && st) atomicOr(&L.status, st);
+      __syncthreads();
+    }
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int q = tid; q < nq; q += LM_THREADS) {
+      float4 cf;
+      const bool ok = surf ? surf_coeff(last, L.ind1[q], L.ind2[q], L.ind3[q], L.sel[q], iter, cf)
+                           : corner_coeff(last, L.ind1[q], L.ind2[q], L.sel[q], iter, cf);
+      if (ok) {
+        if (surf) accumulate_surf_row(cur, feat[q], cf, acc);
+        else accumulate_corner_row(cur, feat[q], cf, acc);
+      }
+    }
+    block_reduce10(L, acc);
+    if (tid == 0) {
+      iters = iter + 1;
+      if (acc[9] < 10.0) L.flag = 1;  // too few correspondences: `continue`
+      else L.flag = lm_solve(L, S, acc, iter, surf) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!L.flag) break;
+  }
+}
+
+__global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
+  __shared__ LmLds L;
+  __shared__ LgState S;
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const int V = P.V, VH = P.VH;
+  const int32_t* cnt = B.counts + (size_t)s * CNT_N;
+  const int n_sharp = cnt[CNT_SHARP], n_lsharp = cnt[CNT_LSHARP], n_flat = cnt[CNT_FLAT], n_lflat = cnt[CNT_LFLAT];
+  const float4* f_sharp = B.f_sharp + (size_t)s * V * P.cap_sharp;
+  const float4* f_lsharp = B.f_lsharp + (size_t)s * V * P.cap_lsharp;
+  const float4* f_flat = B.f_flat + (size_t)s * V * P.cap_flat;
+  const float4* f_lflat = B.f_lflat + (size_t)s * VH;
+  if (tid == 0) {
+    S = B.state[s];
+    L.status = cnt[CNT_STATUS];
+    for (int k = 0; k < 6; ++k) L.cur[k] = S.cur[k];
+  }
+  __syncthreads();
+  const size_t cl_stride = (size_t)V * P.cap_lsharp, sl_stride = (size_t)VH;
+  float4* corner_base = B.corner_last + (size_t)s * 2 * cl_stride;
+  float4* surf_base = B.surf_last + (size_t)s * 2 * sl_stride;
+  if (!S.initialized) {  // checkSystemInitialization (:1181-1209): Last = current, untransformed
+    float4* cl = corner_base + (size_t)S.last_buf * cl_stride;
+    float4* sl = surf_base + (size_t)S.last_buf * sl_stride;
+    for (int k = tid; k < n_lsharp; k += LM_THREADS) cl[k] = f_lsharp[k];
+    for (int k = tid; k < n_lflat; k += LM_THREADS) sl[k] = f_lflat[k];
+    if (tid == 0) {
+      S.initialized = 1;
+      S.n_corner_last = n_lsharp;
+      S.n_surf_last = n_lflat;
+      S.tree_stale = 0;
+      S.status = L.status | LEGO_ST_INIT;
+      S.iters_surf = S.iters_corner = 0;
+      B.state[s] = S;
+    }
+    return;
+  }
+  const float4* clast = corner_base + (size_t)S.last_buf * cl_stride;
+  const float4* slast = surf_base + (size_t)S.last_buf * sl_stride;
+  int it_s = 0, it_c = 0;
+  // updateTransformation (:1213-1235)
+  if (S.n_corner_last < 10 || S.n_surf_last < 100) {
+    if (tid == 0) L.status |= LEGO_ST_LM_SKIPPED;
+  } else {
+    if (tid == 0 && S.tree_stale) L.status |= LEGO_ST_STALE_TREE;
+    lm_loop(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, it_s);
+    lm_loop(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, it_c);
+  }
+  __syncthreads();
+  // integrateTransformation (:1241-1270) + publishOdometry (:1286-1298)
+  if (tid == 0) {
+    const float* cur = L.cur;
+    float* sum = S.sum;
+    float cx = sum[0], cy = sum[1], cz = sum[2], lx = -cur[0], ly = -cur[1], lz = -cur[2];
+    float clx = cosf_g(lx), slx = sinf_g(lx), cly = cosf_g(ly), sly = sinf_g(ly), clz = cosf_g(lz), slz = sinf_g(lz);
+    float ccx = cosf_g(cx), scx = sinf_g(cx), ccy = cosf_g(cy), scy = sinf_g(cy), ccz = cosf_g(cz), scz = sinf_g(cz);
+    float srx = clx * ccx * sly * scz - ccx * ccz * slx - clx * cly * scx;
+    float ox = -asinf_g(srx);
+    float srycrx = slx * (ccy * scz - ccz * scx * scy) + clx * sly * (ccy * ccz + scx * scy * scz) + clx * cly * ccx * scy;
+    float crycrx = clx * cly * ccx * ccy - clx * sly * (ccz * scy - ccy * scx * scz) - slx * (scy * scz + ccy * ccz * scx);
+    float cox = cosf_g(ox);
+    float oy = atan2f_g(srycrx / cox, crycrx / cox);
+    float srzcrx = scx * (clz * sly - cly * slx * slz) + ccx * scz * (cly * clz + slx * sly * slz) + clx * ccx * ccz * slz;
+    float crzcrx = clx * clz * ccx * ccz - ccx * scz * (cly * slz - clz * slx * sly) - scx * (sly * slz + cly * clz * slx);
+    float oz = atan2f_g(srzcrx / cox, crzcrx / cox);
+    float rx = ox, ry = oy, rz = oz;
+    float crz_ = cosf_g(rz), srz_ = sinf_g(rz), crx_ = cosf_g(rx), srx_ = sinf_g(rx), cry_ = cosf_g(ry), sry_ = sinf_g(ry);
+    float x1 = crz_ * (cur[3]) - srz_ * (cur[4]);
+    float y1 = srz_ * (cur[3]) + crz_ * (cur[4]);
+    float z1 = cur[5];
+    float x2 = x1;
+    float y2 = crx_ * y1 - srx_ * z1;
+    float z2 = srx_ * y1 + crx_ * z1;
+    float tx = sum[3] - (cry_ * x2 + sry_ * z2);
+    float ty = sum[4] - y2;
+    float tz = sum[5] - (-sry_ * x2 + cry_ * z2);
+    sum[0] = rx; sum[1] = ry; sum[2] = rz; sum[3] = tx; sum[4] = ty; sum[5] = tz;
+    for (int k = 0; k < 6; ++k) S.cur[k] = L.cur[k];
+    double roll = sum[2], pitch = -(double)sum[0], yaw = -(double)sum[1];
+    double hy = yaw * 0.5, hp = pitch * 0.5, hr = roll * 0.5;
+    double cyw = cos(hy), syw = sin(hy), cp = cos(hp), sp = sin(hp), cr = cos(hr), sr = sin(hr);
+    double qx = sr * cp * cyw - cr * sp * syw;
+    double qy = cr * sp * cyw + sr * cp * syw;
+    double qz = cr * cp * syw - sr * sp * cyw;
+    double qw = cr * cp * cyw + sr * sp * syw;
+    S.quat[0] = -qy; S.quat[1] = -qz; S.quat[2] = qx; S.quat[3] = qw;
+    S.pos[0] = sum[3]; S.pos[1] = sum[4]; S.pos[2] = sum[5];
+    S.iters_surf = it_s;
+    S.iters_corner = it_c;
+  }
+  __syncthreads();
+  // publishCloudsLast (:1329-1383): TransformToEnd into the other half of the Last double buffer
+  {
+    float cur[6];
+    for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
+    const int nb = S.last_buf ^ 1;
+    float4* cl = corner_base + (size_t)nb * cl_stride;
+    float4* sl = surf_base + (size_t)nb * sl_stride;
+    for (int k = tid; k < n_lsharp; k += LM_THREADS) cl[k] = transform_to_end(f_lsharp[k], cur);
+    for (int k = tid; k < n_lflat; k += LM_THREADS) sl[k] = transform_to_end(f_lflat[k], cur);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    S.last_buf ^= 1;
+    S.n_corner_last = n_lsharp;
+    S.n_surf_last = n_lflat;
+    S.tree_stale = !(n_lsharp > 10 && n_lflat > 100);
+    S.cycle++;
+    if (S.cycle == P.map_div) {
+      S.cycle = 0;
+      L.status |= LEGO_ST_EMITTED;
+    }
+    S.status = L.status;
+    B.state[s] = S;
+  }
+}
+
+// ============================================================================================
+// launchers
+// ============================================================================================
+#define LG_CHECK_LAUNCH()                                  \
+  do {                                                     \
+    hipError_t e_ = hipGetLastError();                     \
+    if (e_ != hipSuccess) return LEGO_EDEVICE;             \
+  } while (0)
+
+bool lg_lds_projection(const LgParams& P) { return (size_t)(P.VH + 64) * 4 <= 160 * 1024; }
+bool lg_lds_segment(const LgParams& P) { return P.V <= 16 && (size_t)(P.VH + 64) * 4 <= 160 * 1024; }
+
+int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
+                      const int32_t* cnts, hipStream_t st) {
+  if (lg_lds_projection(P)) {
+    size_t sm = (size_t)(P.VH + 64) * 4;
+    hipLaunchKernelGGL((k_project<true>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
+  } else {
+    hipLaunchKernelGGL((k_project<false>), dim3(S), dim3(1024), 64 * 4, st, P, B, pts, offs, cnts);
+  }
+  LG_CHECK_LAUNCH();
+  return LEGO_OK;
+}
+
+int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
+  if (lg_lds_segment(P)) {
+    size_t sm = (size_t)(P.VH + 64) * 4;
+    hipLaunchKernelGGL((k_segment<true>), dim3(S), dim3(1024), sm, st, P, B);
+  } else {
+    hipLaunchKernelGGL((k_segment<false>), dim3(S), dim3(1024), 64 * 4, st, P, B);
+  }
+  LG_CHECK_LAUNCH();
+  return LEGO_OK;
+}
+
+int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
+  hipLaunchKernelGGL(k_fa_prep, dim3(S), dim3(1024), 0, st, P, B);
+  LG_CHECK_LAUNCH();
+  return LEGO_OK;
+}
+
+int lg_launch_extract(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
+  hipLaunchKernelGGL(k_extract, dim3(S), dim3(64), 0, st, P, B, 1);
+  LG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_extract, dim3(S * P.V), dim3(64), 0, st, P, B, 0);
+  LG_CHECK_LAUNCH();
+  return LEGO_OK;
+}
+
+int lg_launch_concat(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
+  hipLaunchKernelGGL(k_concat, dim3(S), dim3(256), 0, st, P, B);
+  LG_CHECK_LAUNCH();
+  return LEGO_OK;
+}
+
+int lg_launch_lm(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
+  hipLaunchKernelGGL(k_lm, dim3(S), dim3(LM_THREADS), 0, st, P, B);
+  LG_CHECK_LAUNCH();
+  return LEGO_OK;
+}

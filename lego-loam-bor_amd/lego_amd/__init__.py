@@ -1,0 +1,175 @@
+"""lego_amd — Python view of the MI355X LeGO-LOAM-BOR front end (C-ABI in include/lego_frontend.h).
+
+The product is liblego_frontend.so (HIP kernels for gfx950).  This module only binds it with ctypes;
+there is no Python or CPU fallback: if the library is missing, or no HIP device is present, the
+constructors raise.
+
+  Frontend  — one sequence: cloud_handler() (ImageProjection::cloudHandler) and
+              feature_association() (one FeatureAssociation::runFeatureAssociation iteration).
+  Batch     — S independent sequences advanced one scan per step on device-resident input.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi as A
+from ._abi import (LegoAssociationOut, LegoParams, LegoPoint, LegoProjectionOut, association_to_dict,  # noqa: F401
+                   projection_from_dict, projection_to_dict)
+
+P = C.POINTER
+_lib = None
+
+
+class LegoError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load liblego_frontend.so from this package directory (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(A.LIB_FRONTEND):
+            raise LegoError("liblego_frontend.so not built: run python lego-loam-bor_amd/build.py")
+        L = C.CDLL(A.LIB_FRONTEND)
+        L.lego_abi_version.restype = C.c_int32
+        L.lego_params_vlp16.argtypes = [P(LegoParams)]
+        L.lego_params_hdl64.argtypes = [P(LegoParams)]
+        L.lego_params_validate.argtypes = [P(LegoParams)]
+        L.lego_device_count.restype = C.c_int32
+        L.lego_ctx_create.argtypes = [P(LegoParams), C.c_int32, P(C.c_void_p)]
+        L.lego_ctx_destroy.argtypes = [C.c_void_p]
+        L.lego_cloud_handler.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                         C.c_int32, P(LegoProjectionOut)]
+        L.lego_feature_association.argtypes = [C.c_void_p, P(LegoAssociationOut)]
+        L.lego_feature_association_from.argtypes = [C.c_void_p, P(LegoProjectionOut), P(LegoAssociationOut)]
+        L.lego_batch_create.argtypes = [P(LegoParams), C.c_int32, C.c_int32, C.c_int32, P(C.c_void_p)]
+        L.lego_batch_destroy.argtypes = [C.c_void_p]
+        L.lego_batch_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.lego_batch_sync.argtypes = [C.c_void_p]
+        L.lego_batch_read.argtypes = [C.c_void_p, C.c_int32, P(LegoProjectionOut), P(LegoAssociationOut)]
+        L.lego_batch_read_poses.argtypes = [C.c_void_p, P(C.c_float), P(C.c_int32)]
+        L.lego_batch_reset.argtypes = [C.c_void_p]
+        L.lego_batch_stage_times.argtypes = [C.c_void_p, P(C.c_float)]
+        L.lego_batch_set_timing.argtypes = [C.c_void_p, C.c_int32]
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise LegoError("%s failed: rc=%d" % (what, rc))
+
+
+def params_vlp16(**over):
+    p = LegoParams()
+    lib().lego_params_vlp16(C.byref(p))
+    for k, v in over.items():
+        setattr(p, k, v)
+    return p
+
+
+def params_hdl64(**over):
+    p = LegoParams()
+    lib().lego_params_hdl64(C.byref(p))
+    for k, v in over.items():
+        setattr(p, k, v)
+    return p
+
+
+def device_count():
+    return int(lib().lego_device_count())
+
+
+class Frontend:
+    """One sequence on one GPU: the drop-in for the reference's ImageProjection + FeatureAssociation."""
+
+    def __init__(self, params=None, device=0):
+        self.params = params if params is not None else params_vlp16()
+        self.V = self.params.num_vertical_scans
+        self.H = self.params.num_horizontal_scans
+        h = C.c_void_p()
+        _check(lib().lego_ctx_create(C.byref(self.params), int(device), C.byref(h)), "lego_ctx_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().lego_ctx_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def cloud_handler(self, pts, point_step=16, off=(0, 4, 8)):
+        """ImageProjection::cloudHandler on an (N, 4) float32 x,y,z,intensity array (or raw bytes)."""
+        if isinstance(pts, np.ndarray):
+            pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 4)
+            n, ptr = pts.shape[0], pts.ctypes.data
+        else:
+            raise TypeError("pts must be a numpy array")
+        out = LegoProjectionOut()
+        _check(lib().lego_cloud_handler(self.h, ptr, n, point_step, off[0], off[1], off[2], C.byref(out)),
+               "lego_cloud_handler")
+        return projection_to_dict(out, self.V, self.H)
+
+    def feature_association(self, proj=None):
+        out = LegoAssociationOut()
+        if proj is None:
+            _check(lib().lego_feature_association(self.h, C.byref(out)), "lego_feature_association")
+        else:
+            keep = []
+            pin = projection_from_dict(proj, keep)
+            _check(lib().lego_feature_association_from(self.h, C.byref(pin), C.byref(out)),
+                   "lego_feature_association_from")
+        return association_to_dict(out)
+
+
+class Batch:
+    """S independent sequences advanced one scan per step (device-resident input)."""
+
+    def __init__(self, params, n_streams, max_points, device=0):
+        self.params = params
+        self.S = int(n_streams)
+        self.V = params.num_vertical_scans
+        self.H = params.num_horizontal_scans
+        h = C.c_void_p()
+        _check(lib().lego_batch_create(C.byref(params), int(device), self.S, int(max_points), C.byref(h)),
+               "lego_batch_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().lego_batch_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def step(self, d_points, d_offsets, d_counts, stream=0):
+        """Device pointers (ints): lego_point array, int64 offsets[S], int32 counts[S]; async on `stream`."""
+        _check(lib().lego_batch_step(self.h, C.c_void_p(d_points), C.c_void_p(d_offsets), C.c_void_p(d_counts),
+                                     C.c_void_p(stream)), "lego_batch_step")
+
+    def sync(self):
+        _check(lib().lego_batch_sync(self.h), "lego_batch_sync")
+
+    def reset(self):
+        _check(lib().lego_batch_reset(self.h), "lego_batch_reset")
+
+    def set_timing(self, on=True):
+        _check(lib().lego_batch_set_timing(self.h, 1 if on else 0), "lego_batch_set_timing")
+
+    def stage_times(self):
+        ms = (C.c_float * 6)()
+        _check(lib().lego_batch_stage_times(self.h, ms), "lego_batch_stage_times")
+        return list(ms)
+
+    def read(self, s):
+        po, ao = LegoProjectionOut(), LegoAssociationOut()
+        _check(lib().lego_batch_read(self.h, int(s), C.byref(po), C.byref(ao)), "lego_batch_read")
+        return projection_to_dict(po, self.V, self.H), association_to_dict(ao)
+
+    def poses(self):
+        out = np.zeros((self.S, 12), dtype=np.float32)
+        st = np.zeros(self.S, dtype=np.int32)
+        _check(lib().lego_batch_read_poses(self.h, out.ctypes.data_as(P(C.c_float)), st.ctypes.data_as(P(C.c_int32))),
+               "lego_batch_read_poses")
+        return out, st
