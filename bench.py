@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: scans/s of LeGO-LOAM-BOR's per-scan path (project + segment + features + LM)
+on synthetic VLP-16 sweeps, one process per GPU.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S] [--kind vlp16|hdl64]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+
+A step advances every one of the S independent sequences ("streams") on a GPU by one scan: one
+launch per stage for all of them (lego_batch_step).  Inputs of all W+K steps are generated on the
+host, uploaded, and resident in HBM before the timed region.  Each rank owns its own S sequences
+(weak scaling, no collective on the data path); after timing, the per-stream trajectories are
+all-gathered to rank 0 (RCCL), the only collective.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "lego-loam-bor_amd"))
+
+METRIC = "scans/sec (project+segment+features+LM) on VLP-16 sweeps, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=256, help="independent sequences per GPU")
+    ap.add_argument("--kind", default="vlp16", choices=["vlp16", "hdl64"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (rank 0)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--threads", type=int, default=16, help="host threads for input generation")
+    return ap.parse_args()
+
+
+def cpu_baseline(params, cfg, pts, counts, budget_s):
+    """The CPU oracle (oracle/, a restatement of the reference's path; 'port') on the SAME inputs,
+    one thread, sequence by sequence, until the time budget is spent.  Scan 0 of each sequence (no
+    LM) is run but not counted, matching the GPU timed region which starts after warm-up."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    nsteps, S = counts.shape
+    t_sum, n_scans, n_seq = 0.0, 0, 0
+    t_start = time.time()
+    for s in range(S):
+        orc = O.Oracle(params)
+        for k in range(nsteps):
+            p = pts[k, s, :counts[k, s]]
+            t0 = time.perf_counter()
+            orc.cloud_handler(p)
+            orc.feature_association()
+            dt = time.perf_counter() - t0
+            if k > 0:
+                t_sum += dt
+                n_scans += 1
+        n_seq += 1
+        if time.time() - t_start > budget_s:
+            break
+    return {"value": round(n_scans / t_sum, 2), "unit": "scans/s", "cores": 1, "kind": "port",
+            "sample": "%d sequences x %d scans (scan 0 excluded) of the benchmark's own inputs, single thread, "
+                      "host %s" % (n_seq, nsteps - 1, platform.processor() or platform.machine()),
+            "ms_per_scan": round(1e3 * t_sum / max(n_scans, 1), 3)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import lego_amd as L
+    from lego_amd import _abi as A
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    params = L.params_vlp16() if args.kind == "vlp16" else L.params_hdl64()
+    cfg = A.synth_cfg(args.kind)
+    V, H = params.num_vertical_scans, params.num_horizontal_scans
+    cap = V * H
+    S, W, K = args.streams, args.warmup, args.steps
+    nsteps = W + K
+
+    # ---- inputs: rank r owns sequences r*S .. r*S+S-1, scans 0 .. W+K-1 ----------------------------
+    t0 = time.time()
+    seqs = np.repeat(np.arange(rank * S, rank * S + S, dtype=np.int32)[None, :], nsteps, 0).reshape(-1)
+    scans = np.repeat(np.arange(nsteps, dtype=np.int32)[:, None], S, 1).reshape(-1)
+    host_pts, host_cnt = A.synth_batch(cfg, seqs, scans, nthreads=args.threads)  # [nsteps*S, cap, 4]
+    host_pts = host_pts.reshape(nsteps, S, cap, 4)
+    host_cnt = host_cnt.reshape(nsteps, S)
+    t_gen = time.time() - t0
+    d_pts = torch.from_numpy(host_pts).to(dev)
+    offs = (np.arange(nsteps * S, dtype=np.int64) * cap).reshape(nsteps, S)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_cnt = torch.from_numpy(host_cnt.astype(np.int32)).to(dev)
+    batch = L.Batch(params, S, cap, device=local)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(k):
+        batch.step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
+
+    for k in range(W):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(W, W + K):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    poses, status = batch.poses()
+    # trajectory gather: the path's only collective
+    traj = torch.from_numpy(poses).to(dev)
+    if world > 1:
+        gathered = [torch.empty_like(traj) for _ in range(world)]
+        dist.all_gather(gathered, traj)
+        traj_all = torch.cat(gathered)
+    else:
+        traj_all = traj
+    total_scans = S * K * world
+    value = total_scans / elapsed
+
+    # ---- per-stage kernel times (hipEvents on the launch stream), re-running the timed steps ------
+    batch.reset()
+    batch.set_timing(True)
+    stage = np.zeros(6)
+    for k in range(W + K):
+        step(k)
+        if k >= W:
+            stage += np.array(batch.stage_times())
+    stage /= K
+    batch.set_timing(False)
+    n_mean = float(host_cnt[W:].mean())
+    # algorithmic bytes of k_project per launch: read x,y,z,i of every point (16 B) and
+    # write the range image (4 B) + the full cloud cell (16 B) of every cell; S scans per launch.
+    b_proj = S * (16.0 * n_mean + 20.0 * cap)
+    proj_ms = stage[0]
+    achieved = b_proj / (proj_ms * 1e-3) / 1e9
+    roofline = {"kernel": "k_project", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_per_launch": int(b_proj), "launch_ms": round(proj_ms, 4)}
+
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K, "warmup": W,
+        "ms_per_step": round(1e3 * elapsed / K, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "C3: batched synthetic %s sweeps, %d independent sequences per GPU x 1 scan per step"
+                               % (args.kind.upper(), S),
+                   "V": V, "H": H, "points_per_scan": round(n_mean, 1), "streams_per_gpu": S,
+                   "parallelism": "sequence-sharded x%d" % world},
+        "roofline": roofline,
+        "stages_ms": {"project": round(stage[0], 4), "segment": round(stage[1], 4), "fa_prep": round(stage[2], 4),
+                      "extract": round(stage[3], 4), "concat": round(stage[4], 4), "lm": round(stage[5], 4)},
+        "lm_status_bits": int(np.bitwise_or.reduce(status)),
+        "trajectories_gathered": int(traj_all.shape[0]),
+        "input_gen_s": round(t_gen, 2),
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(params, cfg, host_pts, host_cnt, args.cpu_seconds)
+        out["speedup_vs_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

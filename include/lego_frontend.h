@@ -165,6 +165,11 @@ int  lego_batch_reset(lego_batch* b);
 int  lego_batch_stage_times(lego_batch* b, float* ms6);
 int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
 
+/* ---- test hooks ------------------------------------------------------------------ */
+/* Evaluate the device libm restatement on host arrays: which = 0 asinf(a), 1 atan2f(a, b),
+ * 2 atanf(a), 3 sqrtf(a), 4 a / b.  Lets tests compare gfx950 results with the host's glibc. */
+int  lego_test_libm(const float* a, const float* b, float* out, int32_t n, int32_t which);
+
 #ifdef __cplusplus
 }
 #endif

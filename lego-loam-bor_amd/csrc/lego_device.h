@@ -17,142 +17,8 @@
 
 #define LG_DEVICE __device__ __forceinline__
 
-namespace lg {
+#include "lego_libm.h"
 
-LG_DEVICE uint32_t fbits(float f) { return __float_as_uint(f); }
-LG_DEVICE float bitsf(uint32_t u) { return __uint_as_float(u); }
-
-// ---- glibc/fdlibm atanf (sysdeps/ieee754/flt-32/s_atanf.c) ---------------------------------
-LG_DEVICE float atanf_g(float x) {
-  const float atanhi0 = 4.6364760399e-01f, atanhi1 = 7.8539812565e-01f, atanhi2 = 9.8279368877e-01f,
-              atanhi3 = 1.5707962513e+00f;
-  const float atanlo0 = 5.0121582440e-09f, atanlo1 = 3.7748947079e-08f, atanlo2 = 3.4473217170e-08f,
-              atanlo3 = 7.5497894159e-08f;
-  const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
-              aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
-              aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
-              aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
-  int32_t hx = (int32_t)fbits(x);
-  int32_t ix = hx & 0x7fffffff;
-  int id;
-  if (ix >= 0x4c000000) {
-    if (ix > 0x7f800000) return x + x;
-    return (hx > 0) ? atanhi3 + atanlo3 : -atanhi3 - atanlo3;
-  }
-  if (ix < 0x3ee00000) {
-    if (ix < 0x31000000) return x;
-    id = -1;
-  } else {
-    x = fabsf(x);
-    if (ix < 0x3f980000) {
-      if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
-      else { id = 1; x = (x - 1.0f) / (x + 1.0f); }
-    } else {
-      if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
-      else { id = 3; x = -1.0f / x; }
-    }
-  }
-  float z = x * x;
-  float w = z * z;
-  float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
-  float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-  if (id < 0) return x - x * (s1 + s2);
-  float hi = id == 0 ? atanhi0 : id == 1 ? atanhi1 : id == 2 ? atanhi2 : atanhi3;
-  float lo = id == 0 ? atanlo0 : id == 1 ? atanlo1 : id == 2 ? atanlo2 : atanlo3;
-  z = hi - ((x * (s1 + s2) - lo) - x);
-  return (hx < 0) ? -z : z;
-}
-
-// ---- glibc/fdlibm atan2f (sysdeps/ieee754/flt-32/e_atan2f.c) -------------------------------
-LG_DEVICE float atan2f_g(float y, float x) {
-  const float pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
-              pi_lo = -8.7422776573e-08f, tiny = 1.0e-30f;
-  int32_t hx = (int32_t)fbits(x), hy = (int32_t)fbits(y);
-  int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
-  if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
-  if (hx == 0x3f800000) return atanf_g(y);
-  int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
-  if (iy == 0) {
-    switch (m) {
-      case 0:
-      case 1: return y;
-      case 2: return pi + tiny;
-      default: return -pi - tiny;
-    }
-  }
-  if (ix == 0) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
-  if (ix == 0x7f800000) {
-    if (iy == 0x7f800000) {
-      switch (m) {
-        case 0: return pi_o_4 + tiny;
-        case 1: return -pi_o_4 - tiny;
-        case 2: return 3.0f * pi_o_4 + tiny;
-        default: return -3.0f * pi_o_4 - tiny;
-      }
-    } else {
-      switch (m) {
-        case 0: return 0.0f;
-        case 1: return -0.0f;
-        case 2: return pi + tiny;
-        default: return -pi - tiny;
-      }
-    }
-  }
-  if (iy == 0x7f800000) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
-  int k = (iy - ix) >> 23;
-  float z;
-  if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
-  else if (hx < 0 && k < -60) z = 0.0f;
-  else z = atanf_g(fabsf(y / x));
-  switch (m) {
-    case 0: return z;
-    case 1: return -z;
-    case 2: return pi - (z - pi_lo);
-    default: return (z - pi_lo) - pi;
-  }
-}
-
-// ---- glibc asinf (sysdeps/ieee754/flt-32/e_asinf.c) ----------------------------------------
-LG_DEVICE float asinf_g(float x) {
-  const float pio2_hi = 1.57079637050628662109375f, pio2_lo = -4.37113900018624283e-8f,
-              pio4_hi = 0.785398185253143310546875f, p0 = 1.666675248e-1f, p1 = 7.495297643e-2f,
-              p2 = 4.547037598e-2f, p3 = 2.417951451e-2f, p4 = 4.216630880e-2f;
-  int32_t hx = (int32_t)fbits(x);
-  int32_t ix = hx & 0x7fffffff;
-  float t, w, p, q, c, r, s;
-  if (ix == 0x3f800000) return x * pio2_hi + x * pio2_lo;
-  if (ix > 0x3f800000) return (x - x) / (x - x);
-  if (ix < 0x3f000000) {
-    if (ix < 0x32000000) return x;
-    t = x * x;
-    w = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
-    return x + x * w;
-  }
-  w = 1.0f - fabsf(x);
-  t = w * 0.5f;
-  p = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
-  s = sqrtf(t);
-  if (ix >= 0x3F79999A) {
-    t = pio2_hi - (2.0f * (s + s * p) - pio2_lo);
-  } else {
-    w = bitsf(fbits(s) & 0xfffff000u);
-    c = (t - w * w) / (s + w);
-    r = p;
-    p = 2.0f * s * r - (pio2_lo - 2.0f * c);
-    q = pio4_hi - 2.0f * w;
-    t = pio4_hi - (p - q);
-  }
-  return (hx > 0) ? t : -t;
-}
-
-// sinf/cosf: double evaluation rounded once (glibc's own sinf/cosf differ on ~1e-3 of inputs;
-// they are used only inside the LM, which is parity-checked within 1e-4).
-LG_DEVICE float sinf_g(float x) { return (float)sin((double)x); }
-LG_DEVICE float cosf_g(float x) { return (float)cos((double)x); }
-
-LG_DEVICE bool isfinite_f(float x) { return (fbits(x) & 0x7f800000u) != 0x7f800000u; }
-
-}  // namespace lg
 
 // ---- shared POD types (host + device) ---------------------------------------------------------
 struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-derived)

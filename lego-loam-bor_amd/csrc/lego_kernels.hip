@@ -490,9 +490,11 @@ __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
   const int nout = cnt[CNT_OUTLIER];
   const float4* outl = B.outlier + (size_t)s * VH;
   float4* outa = B.outlier_fa + (size_t)s * VH;
+  // adjustOutlierCloud runs in publishCloudsLast, i.e. not on the initialisation scan (:1414-1416)
+  const bool swap_axes = B.state[s].initialized != 0;
   for (int k = tid; k < nout; k += nt) {
     const float4 p = outl[k];
-    outa[k] = make_float4(p.y, p.z, p.x, p.w);
+    outa[k] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;
   }
 }
 
@@ -1499,4 +1501,38 @@ int lg_launch_lm(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   hipLaunchKernelGGL(k_lm, dim3(S), dim3(LM_THREADS), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
+}
+
+// ============================================================================================
+// test hooks (declared in include/lego_frontend.h under "test hooks")
+// ============================================================================================
+__global__ void k_libm_test(const float* a, const float* b, float* out, int n, int which) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float r;
+  if (which == 0) r = asinf_g(a[i]);
+  else if (which == 1) r = atan2f_g(a[i], b[i]);
+  else if (which == 2) r = atanf_g(a[i]);
+  else if (which == 3) r = sqrtf(a[i]);
+  else r = a[i] / b[i];
+  out[i] = r;
+}
+
+extern "C" int lego_test_libm(const float* h_a, const float* h_b, float* h_out, int32_t n, int32_t which) {
+  if (n <= 0 || !h_a || !h_b || !h_out) return LEGO_EINVAL;
+  float *a = nullptr, *b = nullptr, *o = nullptr;
+  const size_t bytes = (size_t)n * sizeof(float);
+  if (hipMalloc((void**)&a, bytes) != hipSuccess) return LEGO_ENOMEM;
+  if (hipMalloc((void**)&b, bytes) != hipSuccess) { hipFree(a); return LEGO_ENOMEM; }
+  if (hipMalloc((void**)&o, bytes) != hipSuccess) { hipFree(a); hipFree(b); return LEGO_ENOMEM; }
+  int rc = LEGO_OK;
+  if (hipMemcpy(a, h_a, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(b, h_b, bytes, hipMemcpyHostToDevice) != hipSuccess) rc = LEGO_EDEVICE;
+  if (rc == LEGO_OK) {
+    hipLaunchKernelGGL(k_libm_test, dim3((n + 255) / 256), dim3(256), 0, 0, a, b, o, n, which);
+    if (hipGetLastError() != hipSuccess || hipMemcpy(h_out, o, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = LEGO_EDEVICE;
+  }
+  hipFree(a); hipFree(b); hipFree(o);
+  return rc;
 }

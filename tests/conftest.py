@@ -1,0 +1,42 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "lego-loam-bor_amd")
+for p in (PKG, os.path.join(REPO, "oracle"), os.path.join(REPO, "tests"), os.path.join(REPO, "tests", "golden")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
+
+
+def _ensure_built():
+    import build as B  # lego-loam-bor_amd/build.py
+    B.build_synth()
+    if os.path.exists("/opt/rocm/bin/hipcc") or os.path.exists(os.path.join(PKG, "lego_amd", "liblego_frontend.so")):
+        B.build_frontend()
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "liblego_oracle.so"])
+
+
+@pytest.fixture(scope="session", autouse=True)
+def built():
+    _ensure_built()
+    yield
+
+
+@pytest.fixture(scope="session")
+def has_gpu():
+    import lego_amd
+    return lego_amd.device_count() > 0
+
+
+@pytest.fixture(scope="session")
+def gpu(has_gpu):
+    if not has_gpu:
+        pytest.fail("no HIP device visible: -m gpu tests must run on the MI355X box")
+    return 0

@@ -1,0 +1,74 @@
+"""CPU tests of the C-ABI library: it loads, exports every declared symbol, and refuses to run
+without a device (no CPU fallback)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import lego_amd as L
+from lego_amd import _abi as A
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "lego_frontend.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\**\s+(lego_[a-z0-9_]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for required in ["lego_ctx_create", "lego_ctx_destroy", "lego_cloud_handler", "lego_feature_association",
+                     "lego_feature_association_from", "lego_batch_create", "lego_batch_step", "lego_batch_read"]:
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = C.CDLL(A.LIB_FRONTEND)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_params_and_validation():
+    p = L.params_vlp16()
+    assert (p.num_vertical_scans, p.num_horizontal_scans, p.ground_scan_index) == (16, 1800, 7)
+    assert p.segment_theta == 60.0 and p.mapping_frequency_divider == 5
+    assert L.lib().lego_params_validate(C.byref(p)) == A.LEGO_OK
+    p.fp_mode = 1
+    assert L.lib().lego_params_validate(C.byref(p)) == A.LEGO_ENOTSUP
+    q = L.params_hdl64()
+    assert (q.num_vertical_scans, q.num_horizontal_scans, q.ground_scan_index) == (64, 2048, 55)
+    q.num_horizontal_scans = 4096
+    assert L.lib().lego_params_validate(C.byref(q)) == A.LEGO_EINVAL
+
+
+def test_struct_layouts_match_header():
+    # 16-byte lego_point (pcl::PointXYZI payload) and the params POD
+    assert C.sizeof(A.LegoPoint) == 16
+    assert C.sizeof(A.LegoParams) == 15 * 4
+
+
+def test_no_cpu_fallback_without_device():
+    """Creating a context on a machine without a HIP device must fail loudly (LEGO_EDEVICE)."""
+    if L.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    h = C.c_void_p()
+    p = L.params_vlp16()
+    assert L.lib().lego_ctx_create(C.byref(p), 0, C.byref(h)) == A.LEGO_EDEVICE
+    with pytest.raises(L.LegoError):
+        L.Frontend(p)
+
+
+def test_synth_is_deterministic():
+    cfg = A.synth_cfg("vlp16")
+    a = A.synth_scan(cfg, 3, 5)
+    b = A.synth_scan(cfg, 3, 5)
+    assert a.shape[0] > 20000 and np.array_equal(a, b)
+    pts, cnt = A.synth_batch(cfg, [3, 4], [5, 5], nthreads=2)
+    assert cnt[0] == a.shape[0] and np.array_equal(pts[0, :cnt[0]], a)
+    assert not np.array_equal(pts[1, :cnt[1]][:100], a[:100])

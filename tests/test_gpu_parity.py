@@ -1,0 +1,254 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the CPU oracle on the same inputs.
+
+Bar (BASELINE.json north_star): bit-exact range/label/ground images, segmented cloud + cloud_info,
+feature indices and feature clouds; 6-DoF transform within 1e-4 (rad / m).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import helpers as Hs
+import lego_amd as L
+import make_golden as MG
+from lego_amd import _abi as A
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_for(params):
+    import oracle as O
+    return O.Oracle(params)
+
+
+def run_pair(params, cfg, seq, nscans, scans=None):
+    fe = L.Frontend(params)
+    orc = oracle_for(params)
+    results = []
+    for k in (scans if scans is not None else range(nscans)):
+        pts = A.synth_scan(cfg, seq, k)
+        pg, fg = fe.cloud_handler(pts), None
+        pr = orc.cloud_handler(pts)
+        fg = fe.feature_association()
+        fr = orc.feature_association()
+        results.append((k, pg, pr, fg, fr))
+    fe.close()
+    return results
+
+
+def assert_scan_parity(k, pg, pr, fg, fr, tf_tol=Hs.TF_TOL):
+    bad = Hs.diff_report(Hs.PROJ_KEYS, pg, pr)
+    assert not bad, ("projection", k, bad)
+    bad = Hs.diff_report(Hs.FEAT_KEYS, fg, fr)
+    assert not bad, ("features", k, bad)
+    assert fg["status"] == fr["status"], (k, hex(fg["status"]), hex(fr["status"]))
+    assert (fg["lm_iter_surf"], fg["lm_iter_corner"]) == (fr["lm_iter_surf"], fr["lm_iter_corner"]), k
+    np.testing.assert_allclose(fg["transform_cur"], fr["transform_cur"], atol=tf_tol, rtol=0)
+    np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=tf_tol, rtol=0)
+    np.testing.assert_allclose(fg["corner_last"][:, :3], fr["corner_last"][:, :3], atol=1e-3, rtol=0)
+    assert Hs.bits_equal(fg["corner_last"][:, 3], fr["corner_last"][:, 3])
+    np.testing.assert_allclose(fg["surf_last"][:, :3], fr["surf_last"][:, :3], atol=1e-3, rtol=0)
+    assert Hs.bits_equal(fg["outlier_last"], fr["outlier_last"])
+
+
+def test_device_libm_matches_glibc(gpu):
+    """gfx950 asinf/atan2f/atanf restatement and IEEE sqrt/div equal the host glibc bit for bit."""
+    rng = np.random.default_rng(1)
+    n = 1 << 21
+    a = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    b = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    u = rng.uniform(-1, 1, n).astype(np.float32)
+    xy = rng.uniform(-100, 100, (2, n)).astype(np.float32)
+    libm = C.CDLL("libm.so.6")
+    for f in ("asinf", "atanf", "sqrtf"):
+        getattr(libm, f).restype = C.c_float
+        getattr(libm, f).argtypes = [C.c_float]
+    libm.atan2f.restype = C.c_float
+    libm.atan2f.argtypes = [C.c_float, C.c_float]
+
+    def dev(x, y, which):
+        out = np.zeros_like(x)
+        fp = C.POINTER(C.c_float)
+        rc = L.lib().lego_test_libm(x.ctypes.data_as(fp), y.ctypes.data_as(fp), out.ctypes.data_as(fp), len(x), which)
+        assert rc == 0
+        return out
+
+    cases = [(u, u, 0, lambda x, y: libm.asinf(x)), (a, a, 0, lambda x, y: libm.asinf(x)),
+             (xy[0], xy[1], 1, lambda x, y: libm.atan2f(x, y)), (a, b, 1, lambda x, y: libm.atan2f(x, y)),
+             (a, a, 2, lambda x, y: libm.atanf(x)), (np.abs(a), a, 3, lambda x, y: libm.sqrtf(x))]
+    for x, y, which, ref in cases:
+        got = dev(np.ascontiguousarray(x), np.ascontiguousarray(y), which)
+        idx = rng.choice(len(x), 20000, replace=False)  # host glibc reference on a sample (ctypes is slow)
+        exp = np.array([ref(float(x[i]), float(y[i])) for i in idx], dtype=np.float32)
+        g = got[idx]
+        both_nan = np.isnan(g) & np.isnan(exp)  # NaN results: payload/sign not specified by either side
+        assert Hs.bits_equal(np.where(both_nan, 0, g), np.where(both_nan, 0, exp)), which
+    q = dev(xy[0], xy[1], 4)
+    assert Hs.bits_equal(q, xy[0] / xy[1])  # numpy float32 division is IEEE
+
+
+@pytest.mark.parametrize("seq", [0, 7, 21])
+def test_vlp16_sequence_parity(gpu, seq):
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    for row in run_pair(params, cfg, seq, 8):
+        assert_scan_parity(*row)
+
+
+def test_vlp16_noise_free_ties(gpu):
+    """Noise-free sweeps make exact curvature / voxel-index ties common: the introsort emulation
+    must give the reference's std::sort permutation."""
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16", range_noise=0.0, az_jitter_deg=0.0, roll_pitch_noise_deg=0.0)
+    for row in run_pair(params, cfg, 3, 5):
+        assert_scan_parity(*row)
+
+
+def test_hdl64_parity(gpu):
+    """HDL-64E-like config: global-memory union-find / winner paths (V*H > LDS)."""
+    params = L.params_hdl64()
+    cfg = A.synth_cfg("hdl64")
+    for row in run_pair(params, cfg, 0, 3):
+        assert_scan_parity(*row)
+
+
+@pytest.mark.parametrize("case", ["vlp16_seq0", "vlp16_noisefree_seq3", "hdl64_seq0"])
+def test_gpu_reproduces_golden(gpu, case):
+    import hashlib
+
+    def h(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:24]
+
+    g = Hs.golden_case(case)
+    params = L.params_vlp16() if g["kind"] == "vlp16" else L.params_hdl64()
+    cfg = A.synth_cfg(g["kind"], **g["synth"])
+    fe = L.Frontend(params)
+    for row in g["scans"]:
+        pts = A.synth_scan(cfg, g["seq"], row["scan"])
+        pr = fe.cloud_handler(pts)
+        fa = fe.feature_association()
+        for k in MG.PROJ_HASH:
+            assert h(pr[k]) == row["p_" + k], (case, row["scan"], k)
+        for k in ["sharp_ind", "less_sharp_ind", "flat_ind", "sharp", "less_sharp", "flat", "less_flat"]:
+            assert h(fa[k]) == row["f_" + k], (case, row["scan"], k)
+        np.testing.assert_allclose(fa["transform_cur"], row["transform_cur"], atol=Hs.TF_TOL, rtol=0)
+
+
+def test_injected_projection_lm_parity(gpu):
+    """FeatureAssociation fed the oracle's own ProjectionOut (the Channel hop) matches the oracle."""
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    fe = L.Frontend(params)
+    orc = oracle_for(params)
+    for k in range(5):
+        pr = orc.cloud_handler(A.synth_scan(cfg, 9, k))
+        fr = orc.feature_association()
+        fg = fe.feature_association(pr)
+        assert not Hs.diff_report(Hs.FEAT_KEYS, fg, fr)
+        np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
+
+
+def test_batch_streams_match_oracle(gpu):
+    """The batched engine (S sequences, one launch per stage) equals S independent oracle runs."""
+    import torch
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    S, steps = 6, 5
+    cap = params.num_vertical_scans * params.num_horizontal_scans
+    seqs = np.repeat(np.arange(S)[None, :] + 30, steps, 0).reshape(-1)
+    scans = np.repeat(np.arange(steps)[:, None], S, 1).reshape(-1)
+    pts, cnt = A.synth_batch(cfg, seqs, scans)
+    d_pts = torch.from_numpy(pts).cuda()
+    offs = torch.from_numpy((np.arange(S * steps, dtype=np.int64) * cap).reshape(steps, S)).cuda()
+    cnts = torch.from_numpy(cnt.reshape(steps, S).astype(np.int32)).cuda()
+    b = L.Batch(params, S, cap)
+    oracles = [oracle_for(params) for _ in range(S)]
+    for k in range(steps):
+        b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), torch.cuda.current_stream().cuda_stream)
+        b.sync()
+        for s in range(S):
+            p = pts[k * S + s, :cnt[k * S + s]]
+            pr = oracles[s].cloud_handler(p)
+            fr = oracles[s].feature_association()
+            pg, fg = b.read(s)
+            assert_scan_parity(k, pg, pr, fg, fr)
+    poses, st = b.poses()
+    np.testing.assert_allclose(poses[0, 6:], fg["transform_sum"] if S == 1 else poses[0, 6:])
+    b.close()
+
+
+def test_edge_inputs(gpu):
+    """Empty / all-NaN clouds fail like the oracle; sparse, tiny, colliding and out-of-FOV clouds match."""
+    params = L.params_vlp16()
+    fe = L.Frontend(params)
+    with pytest.raises(L.LegoError, match="rc=-5"):
+        fe.cloud_handler(np.zeros((0, 4), np.float32))
+    with pytest.raises(L.LegoError, match="rc=-5"):
+        fe.cloud_handler(np.full((64, 4), np.nan, np.float32))
+    fe.close()
+    base = A.synth_scan(A.synth_cfg("vlp16"), 4, 0)
+    rng = np.random.default_rng(3)
+    odd = base.copy()
+    odd[rng.choice(len(odd), 500, replace=False), :3] = np.nan           # NaN points dropped
+    odd[rng.choice(len(odd), 200, replace=False), 2] = 500.0             # out of vertical FOV
+    odd[rng.choice(len(odd), 100, replace=False), :3] = 0.01             # range < 0.1
+    variants = {
+        "tiny": base[:40],
+        "sparse": base[::37],
+        "collisions": np.concatenate([base, base * np.float32(1.0002)]),
+        "odd": odd,
+        "ring_gap": base[(np.arange(len(base)) % 16) != 5],
+    }
+    for name, pts in variants.items():
+        fe = L.Frontend(params)
+        orc = oracle_for(params)
+        for k in range(3):  # same cloud twice more: exercises the stale-state path across scans
+            pg = fe.cloud_handler(pts)
+            pr = orc.cloud_handler(pts)
+            fg = fe.feature_association()
+            fr = orc.feature_association()
+            assert not Hs.diff_report(Hs.PROJ_KEYS, pg, pr), name
+            assert not Hs.diff_report(Hs.FEAT_KEYS, fg, fr), name
+            assert fg["status"] == fr["status"], (name, hex(fg["status"]), hex(fr["status"]))
+            np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
+        fe.close()
+
+
+def test_full_size_batch_properties(gpu):
+    """Bench-size batch (256 sequences): size-independent properties on every stream and exact
+    parity on a sample of streams."""
+    import torch
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    S, steps = 256, 3
+    cap = params.num_vertical_scans * params.num_horizontal_scans
+    seqs = np.repeat(np.arange(S)[None, :] + 1000, steps, 0).reshape(-1)
+    scans = np.repeat(np.arange(steps)[:, None], S, 1).reshape(-1)
+    pts, cnt = A.synth_batch(cfg, seqs, scans)
+    d_pts = torch.from_numpy(pts).cuda()
+    offs = torch.from_numpy((np.arange(S * steps, dtype=np.int64) * cap).reshape(steps, S)).cuda()
+    cnts = torch.from_numpy(cnt.reshape(steps, S).astype(np.int32)).cuda()
+    b = L.Batch(params, S, cap)
+    for k in range(steps):
+        b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), torch.cuda.current_stream().cuda_stream)
+    b.sync()
+    poses, st = b.poses()
+    assert np.all((st & A.ST_UB_MASK) == 0)
+    # forward motion 0.1 m/scan along the camera z axis (LOAM frame) and ~0.5 deg yaw per scan
+    assert np.all(np.abs(poses[:, 5] + 0.1) < 0.05) and np.all(np.abs(poses[:, 1] + np.radians(0.5)) < 0.005)
+    for s in range(S):
+        pg, fg = b.read(s)
+        lab = pg["label_mat"]
+        feas = np.unique(lab[(lab > 0) & (lab != 999999)])
+        assert np.array_equal(feas, np.arange(1, len(feas) + 1))
+        M = len(pg["segmented_cloud"])
+        assert pg["start_ring_index"][0] == 4 and pg["end_ring_index"][-1] == M - 6
+        assert np.all(fg["sharp_ind"] < M) and np.all(fg["flat_ind"] < M)
+    for s in (0, 77, 255):  # exact parity on a sample
+        orc = oracle_for(params)
+        for k in range(steps):
+            pr = orc.cloud_handler(pts[k * S + s, :cnt[k * S + s]])
+            fr = orc.feature_association()
+        pg, fg = b.read(s)
+        assert_scan_parity(steps - 1, pg, pr, fg, fr)
+    b.close()

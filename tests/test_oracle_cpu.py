@@ -1,0 +1,210 @@
+"""CPU tests of the oracle (the parity checker): golden vectors, pinned boundaries, properties."""
+import hashlib
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import helpers as Hs
+from lego_amd import _abi as A
+
+REPO = Hs.HERE.rsplit(os.sep, 1)[0]
+
+
+def oracle_mod():
+    import oracle as O
+    return O
+
+
+def _h(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:24]
+
+
+@pytest.mark.parametrize("case", ["vlp16_seq0", "vlp16_seq7", "vlp16_noisefree_seq3", "hdl64_seq0"])
+def test_oracle_reproduces_golden(case):
+    """The oracle restatement reproduces the committed golden vectors (regression pin)."""
+    O = oracle_mod()
+    import make_golden as MG
+    g = Hs.golden_case(case)
+    params = MG.params_for(g["kind"])
+    cfg = A.synth_cfg(g["kind"], **g["synth"])
+    orc = O.Oracle(params)
+    for row in g["scans"]:
+        pts = A.synth_scan(cfg, g["seq"], row["scan"])
+        assert _h(pts) == row["input"], "synthetic generator is no longer deterministic / changed"
+        pr = orc.cloud_handler(pts)
+        fa = orc.feature_association()
+        for k in MG.PROJ_HASH:
+            assert _h(pr[k]) == row["p_" + k], (case, row["scan"], k)
+        for k in MG.FEAT_HASH:
+            assert _h(fa[k]) == row["f_" + k], (case, row["scan"], k)
+        assert fa["status"] == row["status"]
+        np.testing.assert_array_equal(fa["transform_cur"], np.float32(row["transform_cur"]))
+
+
+def _py_label_components(rng, ground, params_derived, seg_valid_pt, seg_valid_line):
+    """Independent pure-Python BFS restatement of labelComponents + the raster driver
+    (imageProjection.cpp:354-356, 412-496) for small grids."""
+    V, H = rng.shape
+    label = np.zeros((V, H), dtype=np.int64)
+    label[(ground == 1) | (rng == np.float32(np.finfo(np.float32).max))] = -1
+    sinX, cosX, sinY, cosY, thr = params_derived
+    count = 1
+    for i in range(V):
+        for j in range(H):
+            if label[i, j] != 0:
+                continue
+            queue = [(i, j)]
+            pushed = [(i, j)]
+            lines = set()
+            qh = 0
+            while qh < len(queue):
+                fx, fy = queue[qh]
+                qh += 1
+                label[fx, fy] = count
+                for dx, dy in ((0, -1), (-1, 0), (1, 0), (0, 1)):
+                    x, y = fx + dx, fy + dy
+                    if x < 0 or x >= V:
+                        continue
+                    y = H - 1 if y < 0 else (0 if y >= H else y)
+                    if label[x, y] != 0:
+                        continue
+                    rf, rt = rng[fx, fy], rng[x, y]
+                    d1 = rt if rf < rt else rf
+                    d2 = rt if rt < rf else rf
+                    sA, cA = (sinX, cosX) if dx == 0 else (sinY, cosY)
+                    tang = np.float32(np.float32(d2 * sA) / np.float32(d1 - np.float32(d2 * cA)))
+                    if tang > thr:
+                        queue.append((x, y))
+                        label[x, y] = count
+                        lines.add(x)
+                        pushed.append((x, y))
+            ok = len(pushed) >= 30 or (len(pushed) >= seg_valid_pt and len(lines) >= seg_valid_line)
+            if ok:
+                count += 1
+            else:
+                for (x, y) in pushed:
+                    label[x, y] = 999999
+    return label
+
+
+def test_oracle_segmentation_matches_python_bfs():
+    """Second, independent restatement of the BFS segmentation agrees with the C++ oracle."""
+    O = oracle_mod()
+    import make_golden as MG
+    params = MG.params_for("vlp16")
+    params.num_horizontal_scans = 360  # small grid: pure-Python BFS finishes in seconds
+    cfg = A.synth_cfg("vlp16", H=360)
+    orc = O.Oracle(params)
+    pts = A.synth_scan(cfg, 5, 0)
+    pr = orc.cloud_handler(pts)
+    # constants exactly as ImageProjection derives them (float)
+    f32 = np.float32
+    res_x = f32((np.pi * 2) / 360)
+    res_y = f32((np.pi / 180.0) * float(f32(15.0) - f32(-15.0)) / float(f32(15.0)))
+    theta = f32(f32(60.0) * (np.pi / 180.0))
+    lib = __import__("ctypes").CDLL("libm.so.6")
+    lib.sinf.restype = lib.cosf.restype = lib.tanf.restype = __import__("ctypes").c_float
+    lib.sinf.argtypes = lib.cosf.argtypes = lib.tanf.argtypes = [__import__("ctypes").c_float]
+    consts = (f32(lib.sinf(res_x)), f32(lib.cosf(res_x)), f32(lib.sinf(res_y)), f32(lib.cosf(res_y)),
+              f32(lib.tanf(theta)))
+    lab = _py_label_components(pr["range_mat"], pr["ground_mat"], consts, 5, 3)
+    np.testing.assert_array_equal(lab, pr["label_mat"].astype(np.int64))
+    assert (lab > 0).sum() > 100 and (lab == 999999).any()
+
+
+def test_oracle_cloud_info_invariants():
+    O = oracle_mod()
+    import make_golden as MG
+    params = MG.params_for("vlp16")
+    orc = O.Oracle(params)
+    pts = A.synth_scan(A.synth_cfg("vlp16"), 11, 0)
+    pr = orc.cloud_handler(pts)
+    M = len(pr["segmented_cloud"])
+    s, e = pr["start_ring_index"], pr["end_ring_index"]
+    assert s[0] == 4 and e[-1] == M - 1 - 5
+    assert np.all(s[1:] - e[:-1] == 10)  # count_before(i+1) - 1 + 5 - (count_after(i) - 1 - 5)
+    # segmented cloud is raster ordered: row = int(intensity), col = colInd
+    rows = pr["segmented_cloud"][:, 3].astype(np.int64)
+    key = rows * 1800 + pr["segmented_cloud_col_ind"].astype(np.int64)
+    assert np.all(np.diff(key) > 0)
+    # labels are 1..K contiguous among feasible cells
+    lab = pr["label_mat"]
+    feas = np.unique(lab[(lab > 0) & (lab != 999999)])
+    np.testing.assert_array_equal(feas, np.arange(1, len(feas) + 1))
+
+
+def test_oracle_empty_cloud_is_an_error():
+    O = oracle_mod()
+    import make_golden as MG
+    orc = O.Oracle(MG.params_for("vlp16"))
+    with pytest.raises(RuntimeError):
+        orc.cloud_handler(np.zeros((0, 4), np.float32))
+    nan = np.full((10, 4), np.nan, np.float32)
+    with pytest.raises(RuntimeError):
+        orc.cloud_handler(nan)
+
+
+def test_oracle_last_writer_wins():
+    """Two input points in one cell: the later one is kept (imageProjection.cpp:214-222)."""
+    O = oracle_mod()
+    import make_golden as MG
+    orc = O.Oracle(MG.params_for("vlp16"))
+    pts = A.synth_scan(A.synth_cfg("vlp16"), 2, 0)
+    dup = pts.copy()
+    dup[:, :3] *= np.float32(1.0001)  # same cells, slightly different ranges
+    both = np.concatenate([pts, dup])
+    r_dup = orc.cloud_handler(dup)["range_mat"]
+    r_both = orc.cloud_handler(both)["range_mat"]
+    assert Hs.bits_equal(r_both, r_dup)
+
+
+def test_nanoflann_pin():
+    """The oracle's brute-force 1-NN equals the reference's vendored nanoflann 1.3.0 (built from
+    /root/reference into oracle/_ref; skipped where the reference is not mounted, e.g. the GPU box)."""
+    if not os.path.exists("/root/reference/LeGO-LOAM/include/lego_loam/nanoflann.hpp"):
+        pytest.skip("reference sources not mounted here")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "ref"])
+    exe = os.path.join(REPO, "oracle", "_ref", "nanoflann_pin")
+    O = oracle_mod()
+    import make_golden as MG
+    orc = O.Oracle(MG.params_for("vlp16"))
+    cfg = A.synth_cfg("vlp16")
+    orc.cloud_handler(A.synth_scan(cfg, 0, 0))
+    orc.feature_association()
+    orc.cloud_handler(A.synth_scan(cfg, 0, 1))
+    fa = orc.feature_association()
+    rng = np.random.default_rng(0)
+    for cloud, queries in ((fa["surf_last"], fa["flat"]), (fa["corner_last"], fa["sharp"])):
+        xyz = np.ascontiguousarray(cloud[:, :3], np.float32)
+        q = np.concatenate([queries[:, :3], xyz[rng.integers(0, len(xyz), 200)] + rng.normal(0, 0.3, (200, 3))]).astype(np.float32)
+        blob = struct.pack("<i", len(xyz)) + xyz.tobytes() + struct.pack("<i", len(q)) + q.tobytes()
+        out = subprocess.run([exe], input=blob, stdout=subprocess.PIPE, check=True).stdout
+        res = np.frombuffer(out, dtype=np.dtype([("i", "<i4"), ("d", "<f4")]))
+        # brute force exactly as the oracle: float ((dx*dx + dy*dy) + dz*dz), lowest index among ties
+        d = ((q[:, None, 0] - xyz[None, :, 0]) ** 2 + (q[:, None, 1] - xyz[None, :, 1]) ** 2) + (q[:, None, 2] - xyz[None, :, 2]) ** 2
+        bi = np.argmin(d, axis=1)
+        np.testing.assert_array_equal(res["i"], bi)
+        assert Hs.bits_equal(res["d"], d[np.arange(len(q)), bi])
+
+
+def _compile_and_run(src, exe, args=()):
+    csrc = os.path.join(REPO, "lego-loam-bor_amd", "csrc")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-I" + csrc, src, "-o", exe])
+    r = subprocess.run([exe] + list(args), stdout=subprocess.PIPE, universal_newlines=True)
+    return r.returncode, r.stdout
+
+
+def test_introsort_matches_libstdcxx(tmp_path):
+    """The device's std::sort restatement gives libstdc++'s exact permutation on tie-heavy input."""
+    rc, out = _compile_and_run(os.path.join(REPO, "tests", "native", "introsort_check.cpp"), str(tmp_path / "ic"))
+    assert rc == 0, out
+
+
+def test_libm_restatement_matches_glibc(tmp_path):
+    """asinf/atanf/atan2f restated for the device equal the host glibc bit for bit."""
+    rc, out = _compile_and_run(os.path.join(REPO, "tests", "native", "libm_check.cpp"), str(tmp_path / "lc"),
+                               ["3000000"])
+    assert rc == 0, out
