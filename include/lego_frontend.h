@@ -169,6 +169,12 @@ int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
 /* Evaluate the device libm restatement on host arrays: which = 0 asinf(a), 1 atan2f(a, b),
  * 2 atanf(a), 3 sqrtf(a), 4 a / b.  Lets tests compare gfx950 results with the host's glibc. */
 int  lego_test_libm(const float* a, const float* b, float* out, int32_t n, int32_t which);
+/* Sort (key, val) pairs by key with the device's wave-parallel std::sort emulation (n <= 2048);
+ * keys are float bit patterns when is_float != 0, else uint32. */
+int  lego_test_sort(uint32_t* keys, int32_t* vals, int32_t n, int32_t is_float);
+/* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
+ * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */
+int  lego_debug_prof(uint64_t* out32, int32_t reset);
 
 #ifdef __cplusplus
 }

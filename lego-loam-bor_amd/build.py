@@ -31,11 +31,12 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_frontend(force=False):
-    target = os.path.join(OUT, "liblego_frontend.so")
+def build_frontend(force=False, profile=False):
+    target = os.path.join(OUT, "liblego_frontend_prof.so" if profile else "liblego_frontend.so")
     deps = [os.path.join(CSRC, f) for f in FRONTEND_DEPS] + [os.path.join(REPO, "include", "lego_frontend.h")]
     if force or _stale(target, deps):
-        cmd = [HIPCC] + HIP_FLAGS + [os.path.join(CSRC, f) for f in FRONTEND_SRC] + ["-o", target]
+        cmd = [HIPCC] + HIP_FLAGS + (["-DLG_PROFILE"] if profile else []) + \
+            [os.path.join(CSRC, f) for f in FRONTEND_SRC] + ["-o", target]
         print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
     return target
@@ -58,3 +59,5 @@ def build_all(force=False):
 
 if __name__ == "__main__":
     build_all(force="--force" in sys.argv)
+    if "--profile" in sys.argv:
+        build_frontend(force=True, profile=True)

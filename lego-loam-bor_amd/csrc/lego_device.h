@@ -97,5 +97,6 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   // Last clouds, double-buffered
   float4* corner_last;   // [S][2][V*cap_lsharp]
   float4* surf_last;     // [S][2][VH]
+  float4* grid_pts;      // [S][VH]  LM scratch: Last cloud bucketed by grid cell (xyz, index bits)
   LgState* state;        // [S]
 };

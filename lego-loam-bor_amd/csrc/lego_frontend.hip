@@ -217,7 +217,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   A(f_lsharp, S * V * P.cap_lsharp); A(f_lsharp_ind, S * V * P.cap_lsharp);
   A(f_flat, S * V * P.cap_flat); A(f_flat_ind, S * V * P.cap_flat);
   A(f_lflat, S * VH);
-  A(corner_last, S * 2 * V * P.cap_lsharp); A(surf_last, S * 2 * VH);
+  A(corner_last, S * 2 * V * P.cap_lsharp); A(surf_last, S * 2 * VH); A(grid_pts, S * VH);
   A(state, S);
 #undef A
   if (rc != LEGO_OK) {

@@ -26,6 +26,17 @@ using namespace lg;
 
 #define DEG_TO_RAD_D (M_PI / 180.0)
 
+// ---- diagnostic phase timers (build with -DLG_PROFILE; never in the shipped library) -----------
+#ifdef LG_PROFILE
+__device__ unsigned long long g_prof[32];
+#define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(slot, t0) \
+  do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof[slot], __builtin_amdgcn_s_memtime() - (t0)); } while (0)
+#else
+#define PROF_T(v) do {} while (0)
+#define PROF_ADD(slot, t0) do {} while (0)
+#endif
+
 // ============================================================================================
 // block / wave helpers
 // ============================================================================================
@@ -49,6 +60,10 @@ LG_DEVICE T wave_max(T v) {
     T u = __shfl_xor(v, o);
     v = u > v ? u : v;
   }
+  return v;
+}
+LG_DEVICE int wave_or(int v) {
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
   return v;
 }
 template <typename T>
@@ -504,12 +519,226 @@ __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
 #define SEG_MAX 512
 #define RING_MAX 2048
 
+#define SORT_SMALL 64
+#define SMALL_MAX 160
+
 struct ExtractLds {
-  float skey[SEG_MAX];
-  int sval[SEG_MAX];
-  unsigned vkey[RING_MAX];
-  int vval[RING_MAX];
+  union {
+    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;   // segment sort (extract phase)
+    struct { int posL[RING_MAX]; int posR[RING_MAX]; } part;  // partition scratch (voxel phase)
+  } u;
+  unsigned vkey[RING_MAX];  // voxel keys; doubles as partition scratch during the segment phase
+  int vval[RING_MAX];       // lessFlat positions of the ring, sorted with vkey
+  unsigned blk[RING_MAX / 32];  // final-block start bits of the introsort emulation
+  int stk[3 * 64];
+  int small[3 * SMALL_MAX];     // ranges of 17..64 elements handed to single lanes
+  int nsmall;
 };
+
+// __introsort_loop on one small range by one lane (depth carried over from the parent range);
+// marks the start of every final block in blk.
+template <typename K>
+LG_DEVICE void lane_introsort_range(const SortView<K>& a, int first0, int last0, int depth0, unsigned* blk) {
+  int fs[24], ls[24], ds[24];  // pending frames have strictly decreasing depth: <= 2*log2(2048)+1
+  int sp = 0;
+  fs[0] = first0; ls[0] = last0; ds[0] = depth0;
+  sp = 1;
+  while (sp > 0) {
+    --sp;
+    int first = fs[sp], last = ls[sp], depth = ds[sp];
+    while (last - first > 16) {
+      if (depth == 0) {
+        heap_sort(a, first, last);
+        break;
+      }
+      --depth;
+      const int cut = unguarded_partition_pivot(a, first, last);
+      fs[sp] = cut; ls[sp] = last; ds[sp] = depth;
+      ++sp;
+      last = cut;
+    }
+    atomicOr(&blk[first >> 5], 1u << (first & 31));
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// wave_std_sort: libstdc++ std::sort (lego_introsort.h) executed by one wave64, same permutation.
+//  * __introsort_loop's ranges are processed one at a time by the whole wave; the median-of-3 move
+//    is serial, the __unguarded_partition is computed in parallel: with Lk = k-th position (from
+//    first+1 up) whose key is !(key < pivot) and Rk = k-th position (from last-1 down) whose key is
+//    !(pivot < key), the sequential scans swap (Lk, Rk) for every k with Lk < Rk and return
+//    min(L[K], R[K-1]) (R[-1] = last), K = number of swaps.
+//  * Partitioning leaves blocks (<= 16 elements, or heap-sorted ranges) whose elements are >= all
+//    earlier blocks and <= all later ones, so __final_insertion_sort (stable, strict <) never moves
+//    an element across a block boundary: it runs as independent insertion sorts, one lane per block.
+// --------------------------------------------------------------------------------------------
+// __unguarded_partition_pivot on a range of 17..64 elements held one per lane; returns the cut.
+// tab: >= 128 ints of LDS scratch.
+template <typename K>
+LG_DEVICE int wave_partition_small(const SortView<K>& a, int first, int last, int* tab) {
+  const int lane = lane_id();
+  const int m = last - first;
+  const bool in = lane < m;
+  K k = in ? a.key[first + lane] : K(0);
+  int v = in ? a.val[first + lane] : 0;
+  // __move_median_to_first(first, first+1, mid, last-1)
+  const int im = m / 2, il = m - 1;
+  const K kx = __shfl(k, 1), ky = __shfl(k, im), kz = __shfl(k, il);
+  int sel;
+  if (kx < ky) {
+    if (ky < kz) sel = im;
+    else if (kx < kz) sel = il;
+    else sel = 1;
+  } else if (kx < kz) sel = 1;
+  else if (ky < kz) sel = il;
+  else sel = im;
+  {
+    const K k0 = __shfl(k, 0), ks = __shfl(k, sel);
+    const int v0 = __shfl(v, 0), vs = __shfl(v, sel);
+    if (lane == 0) { k = ks; v = vs; }
+    else if (lane == sel) { k = k0; v = v0; }
+  }
+  const K pv = __shfl(k, 0);
+  const bool lf = in && lane >= 1 && !(k < pv);
+  const bool rf = in && lane >= 1 && !(pv < k);
+  const unsigned long long bl = __ballot(lf), br = __ballot(rf);
+  const int nL = __popcll(bl), nR = __popcll(br);
+  const int lrank = popc_below(bl);                                   // k-th left stop, from first+1 up
+  const int rrank = __popcll(br & ~((2ull << lane) - 1ull));          // k-th right stop, from last-1 down
+  if (lf) tab[lrank] = lane;
+  if (rf) tab[64 + rrank] = lane;
+  __syncthreads();
+  int partner = -1;
+  bool left_swap = false;  // a pivot-equal lane is both kinds of stop: count only its left role
+  if (lf && lrank < nR) {
+    const int q = tab[64 + lrank];
+    if (lane < q) { partner = q; left_swap = true; }
+  }
+  if (rf && rrank < nL) {
+    const int q = tab[rrank];
+    if (q < lane) partner = q;
+  }
+  const K kp = __shfl(k, partner < 0 ? lane : partner);
+  const int vp = __shfl(v, partner < 0 ? lane : partner);
+  const unsigned long long sw = __ballot(left_swap);
+  const int nsw = __popcll(sw);
+  if (partner >= 0) { k = kp; v = vp; }
+  // cut = min(L[nsw], R[nsw-1]) (R[-1] = last)
+  const unsigned long long lk = __ballot(lf && lrank == nsw);
+  const unsigned long long rk = __ballot(rf && rrank == nsw - 1);
+  const int cl = lk ? __ffsll((long long)lk) - 1 : m;
+  const int cr = (nsw > 0 && rk) ? __ffsll((long long)rk) - 1 : m;
+  if (in) { a.key[first + lane] = k; a.val[first + lane] = v; }
+  __syncthreads();
+  return first + min(cl, cr);
+}
+
+template <typename K>
+LG_DEVICE void wave_std_sort(K* key, int* val, int n, int* posL, int* posR, unsigned* blk, int* stk,
+                             int* small, int* nsmall) {
+  const int lane = lane_id();
+  if (n <= 1) return;
+  for (int w = lane; w < (n + 31) / 32; w += 64) blk[w] = 0u;
+  __syncthreads();
+  SortView<K> a{key, val};
+  int sp = 0;
+  PROF_T(t_part0);
+  if (lane == 0) { stk[0] = 0; stk[1] = n; stk[2] = 2 * floor_log2(n); *nsmall = 0; }
+  sp = 1;
+  __syncthreads();
+  while (sp > 0) {
+    --sp;
+    int first = stk[3 * sp], last = stk[3 * sp + 1], depth = stk[3 * sp + 2];
+    __syncthreads();
+    while (last - first > 16) {
+      if (depth == 0) {
+        if (lane == 0) heap_sort(a, first, last);
+        break;
+      }
+      --depth;
+      if (last - first <= 64) {  // one chunk: partition in registers
+        const int cut = wave_partition_small(a, first, last, small);
+        if (lane == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = last; stk[3 * sp + 2] = depth; }
+        ++sp;
+        last = cut;
+        __syncthreads();
+        continue;
+      }
+      if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
+      __syncthreads();
+      const K pv = key[first];
+      // pass 1: rank the stops, record positions
+      int nL = 0, nR = 0;
+      for (int base = first + 1; base < last; base += 64) {
+        const int p = base + lane;
+        const bool in = p < last;
+        const K kp = in ? key[p] : pv;
+        const bool lf = in && !(kp < pv), rf = in && !(pv < kp);
+        const unsigned long long bl = __ballot(lf), br = __ballot(rf);
+        if (lf) posL[nL + popc_below(bl)] = p;
+        if (rf) posR[nR + popc_below(br)] = p;  // ascending for now
+        nL += __popcll(bl);
+        nR += __popcll(br);
+      }
+      __syncthreads();
+      // pass 2: k-th left stop vs k-th right stop from the right (posR[nR-1-k]); swap while Lk < Rk
+      int nsw = 0;
+      const int kmax = min(nL, nR);
+      for (int base = 0; base < kmax; base += 64) {
+        const int k = base + lane;
+        const bool sw = k < kmax && posL[k] < posR[nR - 1 - k];
+        const unsigned long long m = __ballot(sw);
+        if (sw) a.swap(posL[k], posR[nR - 1 - k]);
+        nsw += __popcll(m);
+        if (m != ~0ull) break;  // monotone: once a pair crosses, all later pairs do
+      }
+      __syncthreads();
+      const int lk = (nsw < nL) ? posL[nsw] : last;
+      const int rk = (nsw > 0) ? posR[nR - nsw] : last;
+      const int cut = min(lk, rk);
+      __syncthreads();
+      if (lane == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = last; stk[3 * sp + 2] = depth; }
+      ++sp;
+      last = cut;
+      __syncthreads();
+    }
+    if (lane == 0) blk[first >> 5] |= 1u << (first & 31);  // a final block starts here
+    __syncthreads();
+  }
+  PROF_ADD(6, t_part0);
+  PROF_T(t_fin0);
+  // __final_insertion_sort as independent per-block insertion sorts: compact the block starts,
+  // then every lane sorts its own blocks (all 64 lanes busy at once).
+  int nblk = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int p = base + lane;
+    const bool st = p < n && ((blk[p >> 5] >> (p & 31)) & 1u);
+    const unsigned long long m = __ballot(st);
+    if (st) posL[nblk + popc_below(m)] = p;
+    nblk += __popcll(m);
+  }
+  __syncthreads();
+  for (int bi = lane; bi < nblk; bi += 64) {
+    const int p = posL[bi];
+    const int e = (bi + 1 < nblk) ? posL[bi + 1] : n;
+    {
+      for (int i = p + 1; i < e; ++i) {
+        K vk = key[i];
+        int vv = val[i];
+        int j = i;
+        while (j > p && vk < key[j - 1]) {
+          key[j] = key[j - 1];
+          val[j] = val[j - 1];
+          --j;
+        }
+        key[j] = vk;
+        val[j] = vv;
+      }
+    }
+  }
+  __syncthreads();
+  PROF_ADD(11, t_fin0);
+}
 
 struct ScanView {
   int M, VH;
@@ -539,30 +768,62 @@ LG_DEVICE void suppress_neighbours(const ScanView& v, int ind) {  // :306-326
   }
 }
 
+// rank of every element = #keys strictly smaller; eq = #equal keys (itself included)
+template <int NQ>
+LG_DEVICE void rank_pass(const float* key, int n, const float* rk, int* rr, int* eqc) {
+  int b = 0;
+  for (; b + 4 <= n; b += 4) {
+    const float k0 = key[b], k1 = key[b + 1], k2 = key[b + 2], k3 = key[b + 3];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      rr[q] += (k0 < rk[q]) + (k1 < rk[q]) + (k2 < rk[q]) + (k3 < rk[q]);
+      eqc[q] += (k0 == rk[q]) + (k1 == rk[q]) + (k2 == rk[q]) + (k3 == rk[q]);
+    }
+  }
+  for (; b < n; ++b) {
+    const float kb = key[b];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      rr[q] += (kb < rk[q]);
+      eqc[q] += (kb == rk[q]);
+    }
+  }
+}
+
 // Sort [0, n) of (key, val): all-distinct keys -> rank scatter (any correct sort gives the same
 // permutation); any tie -> exact libstdc++ introsort on one lane.
-LG_DEVICE void sort_segment(float* key, int* val, int n) {
+LG_DEVICE void sort_segment(ExtractLds& L, int n) {
+  float* key = L.u.seg.skey;
+  int* val = L.u.seg.sval;
   const int lane = lane_id();
   float rk[SEG_MAX / 64];
   int rv[SEG_MAX / 64], rr[SEG_MAX / 64];
   bool tie = false;
+  int eqc[SEG_MAX / 64];
 #pragma unroll
   for (int q = 0; q < SEG_MAX / 64; ++q) {
     const int a = lane + 64 * q;
-    rr[q] = -1;
-    if (a < n) {
-      const float ka = key[a];
-      int r = 0, eq = 0;
-      for (int b = 0; b < n; ++b) {
-        const float kb = key[b];
-        r += (kb < ka);
-        eq += (kb == ka);
-      }
-      rk[q] = ka;
-      rv[q] = val[a];
-      rr[q] = r;
-      tie |= (eq > 1);
-    }
+    rk[q] = (a < n) ? key[a] : 0.f;
+    rv[q] = (a < n) ? val[a] : 0;
+    rr[q] = 0;
+    eqc[q] = 0;
+  }
+  const int nq = (n + 63) >> 6;  // active slots (wave-uniform)
+  switch (nq) {
+    case 1: rank_pass<1>(key, n, rk, rr, eqc); break;
+    case 2: rank_pass<2>(key, n, rk, rr, eqc); break;
+    case 3: rank_pass<3>(key, n, rk, rr, eqc); break;
+    case 4: rank_pass<4>(key, n, rk, rr, eqc); break;
+    case 5: rank_pass<5>(key, n, rk, rr, eqc); break;
+    case 6: rank_pass<6>(key, n, rk, rr, eqc); break;
+    case 7: rank_pass<7>(key, n, rk, rr, eqc); break;
+    default: rank_pass<8>(key, n, rk, rr, eqc); break;
+  }
+#pragma unroll
+  for (int q = 0; q < SEG_MAX / 64; ++q) {
+    const int a = lane + 64 * q;
+    if (a < n) tie |= (eqc[q] > 1);
+    else rr[q] = -1;
   }
   const bool any_tie = __ballot(tie) != 0ull;
   __syncthreads();
@@ -573,10 +834,14 @@ LG_DEVICE void sort_segment(float* key, int* val, int n) {
         key[rr[q]] = rk[q];
         val[rr[q]] = rv[q];
       }
-  } else if (lane == 0) {
-    std_sort<float>(key, val, n);
+    __syncthreads();
+  } else {
+#ifdef LG_PROFILE
+    if (lane == 0) atomicAdd(&g_prof[14], 1ull);
+#endif
+    int* scratch = (int*)L.vkey;  // free during the segment phase
+    wave_std_sort<float>(key, val, n, scratch, scratch + SEG_MAX, L.blk, L.stk, L.small, &L.nsmall);
   }
-  __syncthreads();
 }
 
 struct RingOut {
@@ -630,8 +895,9 @@ LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, RingOut& o) {
     L.vkey[t] = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
   }
   __syncthreads();
-  if (lane == 0) std_sort<unsigned>(L.vkey, L.vval, n);
-  __syncthreads();
+  PROF_T(t_vs0);
+  wave_std_sort<unsigned>(L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.small, &L.nsmall);
+  PROF_ADD(5, t_vs0);
   int running = 0;
   for (int base = 0; base < n; base += 64) {
     const int t = base + lane;
@@ -662,22 +928,28 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
     const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
     if (sp >= ep) continue;
     const int n = ep - sp;  // sorted range [sp, ep); ep itself is visited unsorted
+    PROF_T(t_seg0);
     for (int t = lane; t <= n; t += 64) {
       const int2 e = smooth[sp + t];
-      L.skey[t] = __int_as_float(e.x);
-      L.sval[t] = e.y;
+      L.u.seg.skey[t] = __int_as_float(e.x);
+      L.u.seg.sval[t] = e.y;
     }
     __syncthreads();
-    sort_segment(L.skey, L.sval, n);
-    for (int t = lane; t < n; t += 64) smooth[sp + t] = make_int2(__float_as_int(L.skey[t]), L.sval[t]);
+    PROF_ADD(12, t_seg0);
+    PROF_T(t_rs0);
+    sort_segment(L, n);
+    PROF_ADD(13, t_rs0);
+    for (int t = lane; t < n; t += 64) smooth[sp + t] = make_int2(__float_as_int(L.u.seg.skey[t]), L.u.seg.sval[t]);
 
+    PROF_ADD(0, t_seg0);
+    PROF_T(t_sharp0);
     // sharp: k = ep .. sp (descending curvature), first 2 eligible -> sharp, up to 20 -> less sharp
     int largest = 0;
     bool stop = false;
     for (int base = n; base >= 0 && !stop; base -= 64) {
       const int t = base - lane;
       const bool valid = t >= 0;
-      const int ind = valid ? L.sval[t] : 0;
+      const int ind = valid ? L.u.seg.sval[t] : 0;
       bool alive = valid;
       while (true) {
         const bool elig = alive && v.picked[ind] == 0 && v.curv[ind] > P.edge_thr && !v.ground_at(ind);
@@ -706,13 +978,15 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
         __syncthreads();
       }
     }
+    PROF_ADD(1, t_sharp0);
+    PROF_T(t_flat0);
     // flat: k = sp .. ep, ground points with curvature < surf threshold, at most 4
     int smallest = 0;
     stop = false;
     for (int base = 0; base <= n && !stop; base += 64) {
       const int t = base + lane;
       const bool valid = t <= n;
-      const int ind = valid ? L.sval[t] : 0;
+      const int ind = valid ? L.u.seg.sval[t] : 0;
       bool alive = valid;
       while (true) {
         const bool elig = alive && v.picked[ind] == 0 && v.curv[ind] < P.surf_thr && v.ground_at(ind);
@@ -734,6 +1008,8 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
       }
     }
     __syncthreads();
+    PROF_ADD(2, t_flat0);
+    PROF_T(t_lf0);
     // lessFlat: positions k in [sp, ep] whose label <= 0 (position, not sorted index: :370-374)
     for (int base = 0; base <= n; base += 64) {
       const int t = base + lane;
@@ -744,8 +1020,11 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
       nlist += __popcll(m);
     }
     __syncthreads();
+    PROF_ADD(3, t_lf0);
   }
+  PROF_T(t_vox0);
   voxel_ring(v, L, nlist, o);
+  PROF_ADD(4, t_vox0);
 }
 
 __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_pass) {
@@ -840,7 +1119,8 @@ __global__ __launch_bounds__(256) void k_concat(LgParams P, LgBufs B) {
 // ============================================================================================
 // k_lm: updateTransformation + integrateTransformation + publishOdometry + publishCloudsLast
 // ============================================================================================
-#define LM_THREADS 256
+#define LM_THREADS 512
+#define GRID_MAX 4096
 #define LM_MAXQ 1536  // 24 * 64 rings
 
 LG_DEVICE float4 transform_to_start(const float4 pi, const float* cur) {  // :388-418
@@ -1017,6 +1297,11 @@ struct LmLds {
   float4 sel[LM_MAXQ];
   int ind1[LM_MAXQ], ind2[LM_MAXQ], ind3[LM_MAXQ];
   double red[LM_THREADS / 64][10];
+  int gcell[GRID_MAX + 1];  // uniform grid over the Last cloud: end offset of every cell
+  float gmin[3], gcs;
+  int gdim[3];
+  float fred[6][LM_THREADS / 64];
+  int iscan[LM_THREADS / 64];
   float cur[6];
   int flag;      // 1 = keep iterating
   int status;
@@ -1033,30 +1318,139 @@ LG_DEVICE void wave_argmin(float& d, int& r, int& idx) {
   }
 }
 
-// One wave: kd-tree 1-NN (brute force, lowest index among exact ties, nanoflann_pcl.h:141-152) and
-// the reference's ring-limited linear scans for the 2nd (and 3rd) correspondence (fa.cpp:503-564,
-// 640-713).  surf = 3-point plane search, else 2-point line search.
-LG_DEVICE void search_one(const LgParams& P, const float4* __restrict__ last, int nl, float4 sel, int fwd_bound,
-                          bool surf, int& o1, int& o2, int& o3, int& status) {
-  const int lane = lane_id();
+// ---- kd-tree 1-NN (nanoflann_pcl.h:141-152) as an exact uniform-grid search --------------------
+// The reference only uses the nearest neighbour when its squared distance is < 25
+// (nearest_feature_search_distance^2, fa.cpp:516,654).  With cells >= 1.1 x that radius, every
+// point closer than the radius lies in the query's 3x3x3 cell neighbourhood, so the grid returns
+// the brute-force result -- the lowest index among exact distance ties (pinned against nanoflann by
+// tests/test_oracle_cpu.py) -- whenever it is accepted, and "not accepted" otherwise.
+LG_DEVICE int block_excl_scan_int(LmLds& L, int v, int& total) {
+  const int lane = lane_id(), w = wave_id();
+  int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) L.iscan[w] = x;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int k = 0; k < LM_THREADS / 64; ++k) {
+    if (k < w) off += L.iscan[k];
+    tot += L.iscan[k];
+  }
+  total = tot;
+  __syncthreads();
+  return off + x - v;
+}
+
+LG_DEVICE int grid_coord(float v, float mn, float cs, int dim) {
+  float f = floorf((v - mn) / cs);
+  f = fminf(fmaxf(f, -2.f), (float)dim + 1.f);
+  return (int)f;
+}
+
+LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, float4* gp, float cs0) {
+  const int tid = threadIdx.x;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int j = tid; j < nl; j += LM_THREADS) {
+    const float4 p = last[j];
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  for (int d = 0; d < 3; ++d) {
+    const float a = wave_min(mn[d]), b = wave_max(mx[d]);
+    if (lane_id() == 0) { L.fred[d][wave_id()] = a; L.fred[3 + d][wave_id()] = b; }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float lo[3], hi[3];
+    for (int d = 0; d < 3; ++d) {
+      lo[d] = L.fred[d][0]; hi[d] = L.fred[3 + d][0];
+      for (int w = 1; w < LM_THREADS / 64; ++w) { lo[d] = fminf(lo[d], L.fred[d][w]); hi[d] = fmaxf(hi[d], L.fred[3 + d][w]); }
+      if (nl == 0) { lo[d] = 0.f; hi[d] = 0.f; }
+    }
+    float cs = cs0;
+    int dim[3];
+    while (true) {
+      long long tot = 1;
+      for (int d = 0; d < 3; ++d) { dim[d] = (int)((hi[d] - lo[d]) / cs) + 1; tot *= dim[d]; }
+      if (tot <= GRID_MAX) break;
+      cs *= 2.f;
+    }
+    for (int d = 0; d < 3; ++d) { L.gmin[d] = lo[d]; L.gdim[d] = dim[d]; }
+    L.gcs = cs;
+  }
+  __syncthreads();
+  const int ncell = L.gdim[0] * L.gdim[1] * L.gdim[2];
+  for (int c = tid; c <= ncell; c += LM_THREADS) L.gcell[c] = 0;
+  __syncthreads();
+  for (int j = tid; j < nl; j += LM_THREADS) {
+    const float4 p = last[j];
+    const int cx = min(max(grid_coord(p.x, L.gmin[0], L.gcs, L.gdim[0]), 0), L.gdim[0] - 1);
+    const int cy = min(max(grid_coord(p.y, L.gmin[1], L.gcs, L.gdim[1]), 0), L.gdim[1] - 1);
+    const int cz = min(max(grid_coord(p.z, L.gmin[2], L.gcs, L.gdim[2]), 0), L.gdim[2] - 1);
+    atomicAdd(&L.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
+  }
+  __syncthreads();
+  // exclusive scan of the counts -> cell start offsets (each thread a contiguous chunk)
+  const int per = (ncell + LM_THREADS - 1) / LM_THREADS;
+  const int c0 = min(tid * per, ncell), c1 = min(c0 + per, ncell);
+  int local = 0;
+  for (int c = c0; c < c1; ++c) local += L.gcell[c];
+  int tot;
+  int run = block_excl_scan_int(L, local, tot);
+  for (int c = c0; c < c1; ++c) {
+    const int n = L.gcell[c];
+    L.gcell[c] = run;
+    run += n;
+  }
+  __syncthreads();
+  // scatter; afterwards gcell[c] = end of cell c = start of cell c+1
+  for (int j = tid; j < nl; j += LM_THREADS) {
+    const float4 p = last[j];
+    const int cx = min(max(grid_coord(p.x, L.gmin[0], L.gcs, L.gdim[0]), 0), L.gdim[0] - 1);
+    const int cy = min(max(grid_coord(p.y, L.gmin[1], L.gcs, L.gdim[1]), 0), L.gdim[1] - 1);
+    const int cz = min(max(grid_coord(p.z, L.gmin[2], L.gcs, L.gdim[2]), 0), L.gdim[2] - 1);
+    const int slot = atomicAdd(&L.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
+    gp[slot] = make_float4(p.x, p.y, p.z, __int_as_float(j));
+  }
+  __syncthreads();
+}
+
+// one thread: nearest neighbour of q; returns index (or -1 if none closer than the radius) and ties
+LG_DEVICE int grid_nn(const LmLds& L, const float4* __restrict__ gp, float4 q, float r2, bool& tie) {
+  const int qx = grid_coord(q.x, L.gmin[0], L.gcs, L.gdim[0]);
+  const int qy = grid_coord(q.y, L.gmin[1], L.gcs, L.gdim[1]);
+  const int qz = grid_coord(q.z, L.gmin[2], L.gcs, L.gdim[2]);
   float bd = FLT_MAX;
   int bi = 0x7fffffff, tc = 0;
-  for (int j = lane; j < nl; j += 64) {
-    const float4 p = last[j];
-    const float dx = sel.x - p.x, dy = sel.y - p.y, dz = sel.z - p.z;
-    const float d = dx * dx + dy * dy + dz * dz;
-    if (d < bd) { bd = d; bi = j; tc = 0; }
-    else if (d == bd) tc++;
-  }
-  float gd = bd;
-  int gr = bi, gi = bi;
-  wave_argmin(gd, gr, gi);
-  const int ties = wave_sum((bd == gd && bi != 0x7fffffff) ? tc + 1 : 0) - 1;
-  if (ties > 0 && nl > 0) status |= LEGO_ST_NN_TIE;
-  o1 = -1; o2 = -1; o3 = -1;
-  if (!(gd < P.nn_dist_sqr) || nl == 0) return;
-  const int closest = gi;
-  o1 = closest;
+  for (int cz = max(qz - 1, 0); cz <= min(qz + 1, L.gdim[2] - 1); ++cz)
+    for (int cy = max(qy - 1, 0); cy <= min(qy + 1, L.gdim[1] - 1); ++cy) {
+      const int row = (cz * L.gdim[1] + cy) * L.gdim[0];
+      const int x0 = max(qx - 1, 0), x1 = min(qx + 1, L.gdim[0] - 1);
+      if (x0 > x1) continue;
+      const int b = (row + x0 == 0) ? 0 : L.gcell[row + x0 - 1];
+      const int e = L.gcell[row + x1];  // cells x0..x1 of a row are contiguous
+      for (int k = b; k < e; ++k) {
+        const float4 p = gp[k];
+        const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+        const float d = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
+        const int idx = __float_as_int(p.w);
+        if (d < bd) { bd = d; bi = idx; tc = 0; }
+        else if (d == bd) { tc++; bi = min(bi, idx); }
+      }
+    }
+  tie = (bd < r2) && tc > 0;
+  return (bd < r2) ? bi : -1;
+}
+
+// One wave: the reference's ring-limited linear scans for the 2nd (and 3rd) correspondence around
+// the accepted nearest neighbour `closest` (fa.cpp:514-564, 652-713).  surf = plane (3 points),
+// else line (2 points).
+LG_DEVICE void ring_scans(const LgParams& P, const float4* __restrict__ last, int nl, float4 sel, int fwd_bound,
+                          bool surf, int closest, int& o2, int& o3, int& status) {
+  const int lane = lane_id();
+  o2 = -1; o3 = -1;
   const int ring0 = (int)last[closest].w;
   float b2d = P.nn_dist_sqr, b3d = P.nn_dist_sqr;
   int b2r = 0x7fffffff, b3r = 0x7fffffff, b2i = -1, b3i = -1;
@@ -1287,24 +1681,38 @@ LG_DEVICE bool corner_coeff(const float4* last, int i1, int i2, float4 sel, int 
 
 // one LM loop (surf or corner), <= 25 iterations
 LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __restrict__ feat, int nq,
-                       const float4* __restrict__ last, int nl, bool surf, int& iters) {
+                       const float4* __restrict__ last, int nl, bool surf, float4* gp, int& iters) {
   const int tid = threadIdx.x;
   const int nw = LM_THREADS / 64;
+  build_grid(L, last, nl, gp, 1.1f * sqrtf(P.nn_dist_sqr) + 0.05f);
   for (int iter = 0; iter < 25; iter++) {
     float cur[6];
     for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
+    PROF_T(t_sel0);
     for (int q = tid; q < nq; q += LM_THREADS) L.sel[q] = transform_to_start(feat[q], cur);
     __syncthreads();
+    PROF_ADD(8, t_sel0);
+    PROF_T(t_srch0);
     if (iter % 5 == 0) {
       int st = 0;
-      for (int q = wave_id(); q < nq; q += nw) {
-        int o1, o2, o3;
-        search_one(P, last, nl, L.sel[q], nq, surf, o1, o2, o3, st);
-        if (lane_id() == 0) { L.ind1[q] = o1; L.ind2[q] = o2; L.ind3[q] = o3; }
+      for (int q = tid; q < nq; q += LM_THREADS) {
+        bool tie = false;
+        L.ind1[q] = grid_nn(L, gp, L.sel[q], P.nn_dist_sqr, tie);
+        if (tie) st |= LEGO_ST_NN_TIE;
       }
+      __syncthreads();
+      for (int q = wave_id(); q < nq; q += nw) {
+        const int c = L.ind1[q];
+        int o2 = -1, o3 = -1;
+        if (c >= 0) ring_scans(P, last, nl, L.sel[q], nq, surf, c, o2, o3, st);
+        if (lane_id() == 0) { L.ind2[q] = o2; L.ind3[q] = o3; }
+      }
+      st = wave_or(st);
       if (lane_id() == 0 && st) atomicOr(&L.status, st);
       __syncthreads();
     }
+    PROF_ADD(9, t_srch0);
+    PROF_T(t_acc0);
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int q = tid; q < nq; q += LM_THREADS) {
       float4 cf;
@@ -1316,6 +1724,7 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
       }
     }
     block_reduce10(L, acc);
+    PROF_ADD(10, t_acc0);
     if (tid == 0) {
       iters = iter + 1;
       if (acc[9] < 10.0) L.flag = 1;  // too few correspondences: `continue`
@@ -1370,8 +1779,9 @@ __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
     if (tid == 0) L.status |= LEGO_ST_LM_SKIPPED;
   } else {
     if (tid == 0 && S.tree_stale) L.status |= LEGO_ST_STALE_TREE;
-    lm_loop(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, it_s);
-    lm_loop(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, it_c);
+    float4* gp = B.grid_pts + (size_t)s * VH;
+    lm_loop(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, gp, it_s);
+    lm_loop(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, gp, it_c);
   }
   __syncthreads();
   // integrateTransformation (:1241-1270) + publishOdometry (:1286-1298)
@@ -1535,4 +1945,50 @@ extern "C" int lego_test_libm(const float* h_a, const float* h_b, float* h_out, 
   }
   hipFree(a); hipFree(b); hipFree(o);
   return rc;
+}
+
+__global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int n, int is_float) {
+  __shared__ ExtractLds L;
+  const int lane = lane_id();
+  for (int i = lane; i < n; i += 64) { L.vkey[i] = keys[i]; L.vval[i] = vals[i]; }
+  __syncthreads();
+  if (is_float) {
+    wave_std_sort<float>((float*)L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.small, &L.nsmall);
+  } else {
+    wave_std_sort<unsigned>(L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.small, &L.nsmall);
+  }
+  for (int i = lane; i < n; i += 64) { keys[i] = L.vkey[i]; vals[i] = L.vval[i]; }
+}
+
+extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int32_t is_float) {
+  if (n < 0 || n > RING_MAX || !h_keys || !h_vals) return LEGO_EINVAL;
+  if (n == 0) return LEGO_OK;
+  unsigned* k = nullptr;
+  int* v = nullptr;
+  if (hipMalloc((void**)&k, n * 4) != hipSuccess) return LEGO_ENOMEM;
+  if (hipMalloc((void**)&v, n * 4) != hipSuccess) { hipFree(k); return LEGO_ENOMEM; }
+  int rc = LEGO_OK;
+  if (hipMemcpy(k, h_keys, n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(v, h_vals, n * 4, hipMemcpyHostToDevice) != hipSuccess) rc = LEGO_EDEVICE;
+  if (rc == LEGO_OK) {
+    hipLaunchKernelGGL(k_sort_test, dim3(1), dim3(64), 0, 0, k, v, n, is_float);
+    if (hipGetLastError() != hipSuccess || hipMemcpy(h_keys, k, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(h_vals, v, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = LEGO_EDEVICE;
+  }
+  hipFree(k); hipFree(v);
+  return rc;
+}
+
+extern "C" int lego_debug_prof(uint64_t* out32, int32_t reset) {
+#ifdef LG_PROFILE
+  if (out32 && hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(uint64_t) * 32) != hipSuccess) return LEGO_EDEVICE;
+  if (reset) {
+    uint64_t z[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return LEGO_EDEVICE;
+  }
+  return LEGO_OK;
+#else
+  (void)out32; (void)reset;
+  return LEGO_ENOTSUP;
+#endif
 }

@@ -52,6 +52,8 @@ def lib():
         L.lego_batch_reset.argtypes = [C.c_void_p]
         L.lego_batch_stage_times.argtypes = [C.c_void_p, P(C.c_float)]
         L.lego_batch_set_timing.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_test_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int32, C.c_int32]
+        L.lego_test_libm.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_int32, C.c_int32]
         _lib = L
     return _lib
 

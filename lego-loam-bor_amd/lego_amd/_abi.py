@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_FRONTEND = os.path.join(PKG_DIR, "liblego_frontend.so")
+LIB_FRONTEND = os.environ.get("LEGO_FRONTEND_LIB", os.path.join(PKG_DIR, "liblego_frontend.so"))
 LIB_SYNTH = os.path.join(PKG_DIR, "liblego_synth.so")
 
 LEGO_OK, LEGO_EINVAL, LEGO_ENOMEM, LEGO_EDEVICE, LEGO_ENOTSUP, LEGO_EEMPTY = 0, -1, -2, -3, -4, -5

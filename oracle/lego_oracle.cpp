@@ -755,7 +755,7 @@ struct FeatureAssociation {
       if (d < bd) { bd = d; best = j; ties = 0; }
       else if (d == bd) ++ties;
     }
-    if (ties) status |= LEGO_ST_NN_TIE;
+    if (ties && bd < nn_dist_sqr) status |= LEGO_ST_NN_TIE;  // tie-break only matters when accepted
     *d_out = bd;
     return best;
   }
@@ -1257,6 +1257,22 @@ int oracle_smoothness(oracle_ctx* c, int k, float* value, int64_t* ind) {
   *value = c->fa.cloudSmoothness[k].value;
   *ind = (int64_t)c->fa.cloudSmoothness[k].ind;
   return LEGO_OK;
+}
+
+// Test hook: libstdc++ std::sort of (key, val) pairs by key only (the reference's sort semantics).
+int oracle_std_sort(uint32_t* keys, int32_t* vals, int n, int is_float) {
+  if (is_float) {
+    std::vector<smoothness_t> v(n);
+    for (int i = 0; i < n; ++i) { std::memcpy(&v[i].value, &keys[i], 4); v[i].ind = (size_t)vals[i]; }
+    std::sort(v.begin(), v.end(), by_value());
+    for (int i = 0; i < n; ++i) { std::memcpy(&keys[i], &v[i].value, 4); vals[i] = (int32_t)v[i].ind; }
+  } else {
+    std::vector<cloud_point_index_idx> v(n);
+    for (int i = 0; i < n; ++i) { v[i].idx = keys[i]; v[i].cloud_point_index = (unsigned)vals[i]; }
+    std::sort(v.begin(), v.end(), std::less<cloud_point_index_idx>());
+    for (int i = 0; i < n; ++i) { keys[i] = v[i].idx; vals[i] = (int32_t)v[i].cloud_point_index; }
+  }
+  return 0;
 }
 
 // Test hooks for the libm restatement: glibc's float functions as the reference calls them.

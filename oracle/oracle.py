@@ -37,6 +37,7 @@ def lib():
         L.oracle_feature_association.argtypes = [C.c_void_p, P(A.LegoAssociationOut)]
         L.oracle_feature_association_from.argtypes = [C.c_void_p, P(A.LegoProjectionOut), P(A.LegoAssociationOut)]
         L.oracle_smoothness.argtypes = [C.c_void_p, C.c_int, P(C.c_float), P(C.c_int64)]
+        L.oracle_std_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int, C.c_int]
         L.oracle_atan2f.argtypes = [C.c_float, C.c_float]
         L.oracle_atan2f.restype = C.c_float
         L.oracle_asinf.argtypes = [C.c_float]
@@ -87,3 +88,12 @@ class Oracle:
         i = C.c_int64()
         lib().oracle_smoothness(self.h, k, C.byref(v), C.byref(i))
         return v.value, i.value
+
+
+def std_sort(keys, vals, is_float):
+    """libstdc++ std::sort of (key, val) by key only; keys as uint32 bit patterns."""
+    import numpy as np
+    k = np.ascontiguousarray(keys, dtype=np.uint32).copy()
+    v = np.ascontiguousarray(vals, dtype=np.int32).copy()
+    lib().oracle_std_sort(k.ctypes.data_as(P(C.c_uint32)), v.ctypes.data_as(P(C.c_int32)), len(k), int(is_float))
+    return k, v

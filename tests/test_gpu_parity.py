@@ -87,6 +87,27 @@ def test_device_libm_matches_glibc(gpu):
     assert Hs.bits_equal(q, xy[0] / xy[1])  # numpy float32 division is IEEE
 
 
+def test_device_sort_matches_libstdcxx(gpu):
+    """The wave-parallel introsort (segment + voxel sorts) gives libstdc++ std::sort's permutation."""
+    import oracle as O
+    rng = np.random.default_rng(7)
+    fp = C.POINTER
+    for n in [0, 1, 2, 15, 16, 17, 40, 64, 65, 100, 300, 511, 512, 1000, 1800, 2048]:
+        for distinct in [1, 2, 5, 40, 10 ** 6]:
+            for is_float in (0, 1):
+                if is_float:
+                    keys = (rng.integers(0, distinct, n) * 0.37).astype(np.float32).view(np.uint32)
+                else:
+                    keys = rng.integers(0, distinct, n).astype(np.uint32)
+                vals = np.arange(n, dtype=np.int32)
+                ek, ev = O.std_sort(keys, vals, is_float)
+                gk, gv = keys.copy(), vals.copy()
+                rc = L.lib().lego_test_sort(gk.ctypes.data_as(fp(C.c_uint32)), gv.ctypes.data_as(fp(C.c_int32)), n,
+                                            is_float)
+                assert rc == 0
+                assert np.array_equal(gv, ev) and np.array_equal(gk, ek), (n, distinct, is_float)
+
+
 @pytest.mark.parametrize("seq", [0, 7, 21])
 def test_vlp16_sequence_parity(gpu, seq):
     params = L.params_vlp16()
