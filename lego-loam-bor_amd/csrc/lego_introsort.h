@@ -20,14 +20,14 @@
 
 namespace lg {
 
-template <typename K>
+template <typename K, typename V = int>
 struct SortView {
   K* key;
-  int* val;
+  V* val;
   LG_HD bool lt(int a, int b) const { return key[a] < key[b]; }
   LG_HD void swap(int a, int b) const {
     K tk = key[a]; key[a] = key[b]; key[b] = tk;
-    int tv = val[a]; val[a] = val[b]; val[b] = tv;
+    V tv = val[a]; val[a] = val[b]; val[b] = tv;
   }
   LG_HD void move(int dst, int src) const { key[dst] = key[src]; val[dst] = val[src]; }
 };
@@ -38,8 +38,8 @@ LG_HD int floor_log2(int n) {
   return r;
 }
 
-template <typename K>
-LG_HD void adjust_heap(const SortView<K>& a, int first, int hole, int len, K vk, int vv) {
+template <typename K, typename V>
+LG_HD void adjust_heap(const SortView<K, V>& a, int first, int hole, int len, K vk, V vv) {
   const int top = hole;
   int second = hole;
   while (second < (len - 1) / 2) {
@@ -64,14 +64,14 @@ LG_HD void adjust_heap(const SortView<K>& a, int first, int hole, int len, K vk,
   a.val[first + hole] = vv;
 }
 
-template <typename K>
-LG_HD void heap_sort(const SortView<K>& a, int first, int last) {  // __partial_sort(first, last, last)
+template <typename K, typename V>
+LG_HD void heap_sort(const SortView<K, V>& a, int first, int last) {  // __partial_sort(first, last, last)
   const int len = last - first;
   if (len >= 2) {  // __make_heap
     int parent = (len - 2) / 2;
     while (true) {
       K vk = a.key[first + parent];
-      int vv = a.val[first + parent];
+      V vv = a.val[first + parent];
       adjust_heap(a, first, parent, len, vk, vv);
       if (parent == 0) break;
       parent--;
@@ -80,14 +80,14 @@ LG_HD void heap_sort(const SortView<K>& a, int first, int last) {  // __partial_
   while (last - first > 1) {  // __sort_heap / __pop_heap
     --last;
     K vk = a.key[last];
-    int vv = a.val[last];
+    V vv = a.val[last];
     a.move(last, first);
     adjust_heap(a, first, 0, last - first, vk, vv);
   }
 }
 
-template <typename K>
-LG_HD void move_median_to_first(const SortView<K>& a, int result, int x, int y, int z) {
+template <typename K, typename V>
+LG_HD void move_median_to_first(const SortView<K, V>& a, int result, int x, int y, int z) {
   if (a.lt(x, y)) {
     if (a.lt(y, z)) a.swap(result, y);
     else if (a.lt(x, z)) a.swap(result, z);
@@ -97,8 +97,8 @@ LG_HD void move_median_to_first(const SortView<K>& a, int result, int x, int y, 
   else a.swap(result, y);
 }
 
-template <typename K>
-LG_HD int unguarded_partition_pivot(const SortView<K>& a, int first, int last) {
+template <typename K, typename V>
+LG_HD int unguarded_partition_pivot(const SortView<K, V>& a, int first, int last) {
   const int mid = first + (last - first) / 2;
   move_median_to_first(a, first, first + 1, mid, last - 1);
   int lo = first + 1, hi = last;
@@ -113,10 +113,10 @@ LG_HD int unguarded_partition_pivot(const SortView<K>& a, int first, int last) {
   }
 }
 
-template <typename K>
-LG_HD void unguarded_linear_insert(const SortView<K>& a, int last) {
+template <typename K, typename V>
+LG_HD void unguarded_linear_insert(const SortView<K, V>& a, int last) {
   K vk = a.key[last];
-  int vv = a.val[last];
+  V vv = a.val[last];
   int next = last - 1;
   while (vk < a.key[next]) {
     a.move(last, next);
@@ -127,13 +127,13 @@ LG_HD void unguarded_linear_insert(const SortView<K>& a, int last) {
   a.val[last] = vv;
 }
 
-template <typename K>
-LG_HD void insertion_sort(const SortView<K>& a, int first, int last) {
+template <typename K, typename V>
+LG_HD void insertion_sort(const SortView<K, V>& a, int first, int last) {
   if (first == last) return;
   for (int i = first + 1; i != last; ++i) {
     if (a.lt(i, first)) {
       K vk = a.key[i];
-      int vv = a.val[i];
+      V vv = a.val[i];
       for (int k = i; k > first; --k) a.move(k, k - 1);  // move_backward
       a.key[first] = vk;
       a.val[first] = vv;
@@ -144,10 +144,10 @@ LG_HD void insertion_sort(const SortView<K>& a, int first, int last) {
 }
 
 // std::sort(key, key + n) carrying val; comparator key[a] < key[b].
-template <typename K>
-LG_HD void std_sort(K* key, int* val, int n) {
+template <typename K, typename V = int>
+LG_HD void std_sort(K* key, V* val, int n) {
   if (n <= 1) return;
-  SortView<K> a{key, val};
+  SortView<K, V> a{key, val};
   struct Frame { int first, last, depth; };
   Frame stack[64];
   int sp = 0;

@@ -522,65 +522,27 @@ __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
 #define SORT_SMALL 64
 #define SMALL_MAX 160
 
-struct ExtractLds {
+struct ExtractLds {  // 21.5 KB per wave -> 7 waves per CU
   union {
-    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;   // segment sort (extract phase)
-    struct { int posL[RING_MAX]; int posR[RING_MAX]; } part;  // partition scratch (voxel phase)
+    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;             // segment sort (extract phase)
+    struct { uint16_t posL[RING_MAX]; uint16_t posR[RING_MAX]; } part;  // partition scratch (voxel phase)
   } u;
-  unsigned vkey[RING_MAX];  // voxel keys; doubles as partition scratch during the segment phase
-  int vval[RING_MAX];       // lessFlat positions of the ring, sorted with vkey
+  unsigned vkey[RING_MAX];      // voxel keys; doubles as partition scratch during the segment phase
+  uint16_t vval[RING_MAX];      // lessFlat positions of the ring (relative to the ring start), sorted with vkey
   unsigned blk[RING_MAX / 32];  // final-block start bits of the introsort emulation
   int stk[3 * 64];
-  int small[3 * SMALL_MAX];     // ranges of 17..64 elements handed to single lanes
-  int nsmall;
+  int tab[128];                 // lane-pairing table of the in-register partition
 };
 
-// __introsort_loop on one small range by one lane (depth carried over from the parent range);
-// marks the start of every final block in blk.
-template <typename K>
-LG_DEVICE void lane_introsort_range(const SortView<K>& a, int first0, int last0, int depth0, unsigned* blk) {
-  int fs[24], ls[24], ds[24];  // pending frames have strictly decreasing depth: <= 2*log2(2048)+1
-  int sp = 0;
-  fs[0] = first0; ls[0] = last0; ds[0] = depth0;
-  sp = 1;
-  while (sp > 0) {
-    --sp;
-    int first = fs[sp], last = ls[sp], depth = ds[sp];
-    while (last - first > 16) {
-      if (depth == 0) {
-        heap_sort(a, first, last);
-        break;
-      }
-      --depth;
-      const int cut = unguarded_partition_pivot(a, first, last);
-      fs[sp] = cut; ls[sp] = last; ds[sp] = depth;
-      ++sp;
-      last = cut;
-    }
-    atomicOr(&blk[first >> 5], 1u << (first & 31));
-  }
-}
-
-// --------------------------------------------------------------------------------------------
-// wave_std_sort: libstdc++ std::sort (lego_introsort.h) executed by one wave64, same permutation.
-//  * __introsort_loop's ranges are processed one at a time by the whole wave; the median-of-3 move
-//    is serial, the __unguarded_partition is computed in parallel: with Lk = k-th position (from
-//    first+1 up) whose key is !(key < pivot) and Rk = k-th position (from last-1 down) whose key is
-//    !(pivot < key), the sequential scans swap (Lk, Rk) for every k with Lk < Rk and return
-//    min(L[K], R[K-1]) (R[-1] = last), K = number of swaps.
-//  * Partitioning leaves blocks (<= 16 elements, or heap-sorted ranges) whose elements are >= all
-//    earlier blocks and <= all later ones, so __final_insertion_sort (stable, strict <) never moves
-//    an element across a block boundary: it runs as independent insertion sorts, one lane per block.
-// --------------------------------------------------------------------------------------------
 // __unguarded_partition_pivot on a range of 17..64 elements held one per lane; returns the cut.
 // tab: >= 128 ints of LDS scratch.
-template <typename K>
-LG_DEVICE int wave_partition_small(const SortView<K>& a, int first, int last, int* tab) {
+template <typename K, typename V>
+LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last, int* tab) {
   const int lane = lane_id();
   const int m = last - first;
   const bool in = lane < m;
   K k = in ? a.key[first + lane] : K(0);
-  int v = in ? a.val[first + lane] : 0;
+  int v = in ? (int)a.val[first + lane] : 0;
   // __move_median_to_first(first, first+1, mid, last-1)
   const int im = m / 2, il = m - 1;
   const K kx = __shfl(k, 1), ky = __shfl(k, im), kz = __shfl(k, il);
@@ -628,22 +590,22 @@ LG_DEVICE int wave_partition_small(const SortView<K>& a, int first, int last, in
   const unsigned long long rk = __ballot(rf && rrank == nsw - 1);
   const int cl = lk ? __ffsll((long long)lk) - 1 : m;
   const int cr = (nsw > 0 && rk) ? __ffsll((long long)rk) - 1 : m;
-  if (in) { a.key[first + lane] = k; a.val[first + lane] = v; }
+  if (in) { a.key[first + lane] = k; a.val[first + lane] = (V)v; }
   __syncthreads();
   return first + min(cl, cr);
 }
 
-template <typename K>
-LG_DEVICE void wave_std_sort(K* key, int* val, int n, int* posL, int* posR, unsigned* blk, int* stk,
-                             int* small, int* nsmall) {
+template <typename K, typename V>
+LG_DEVICE void wave_std_sort(K* key, V* val, int n, uint16_t* posL, uint16_t* posR, unsigned* blk, int* stk,
+                             int* tab) {
   const int lane = lane_id();
   if (n <= 1) return;
   for (int w = lane; w < (n + 31) / 32; w += 64) blk[w] = 0u;
   __syncthreads();
-  SortView<K> a{key, val};
+  SortView<K, V> a{key, val};
   int sp = 0;
   PROF_T(t_part0);
-  if (lane == 0) { stk[0] = 0; stk[1] = n; stk[2] = 2 * floor_log2(n); *nsmall = 0; }
+  if (lane == 0) { stk[0] = 0; stk[1] = n; stk[2] = 2 * floor_log2(n); }
   sp = 1;
   __syncthreads();
   while (sp > 0) {
@@ -657,7 +619,7 @@ LG_DEVICE void wave_std_sort(K* key, int* val, int n, int* posL, int* posR, unsi
       }
       --depth;
       if (last - first <= 64) {  // one chunk: partition in registers
-        const int cut = wave_partition_small(a, first, last, small);
+        const int cut = wave_partition_small(a, first, last, tab);
         if (lane == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = last; stk[3 * sp + 2] = depth; }
         ++sp;
         last = cut;
@@ -675,8 +637,8 @@ LG_DEVICE void wave_std_sort(K* key, int* val, int n, int* posL, int* posR, unsi
         const K kp = in ? key[p] : pv;
         const bool lf = in && !(kp < pv), rf = in && !(pv < kp);
         const unsigned long long bl = __ballot(lf), br = __ballot(rf);
-        if (lf) posL[nL + popc_below(bl)] = p;
-        if (rf) posR[nR + popc_below(br)] = p;  // ascending for now
+        if (lf) posL[nL + popc_below(bl)] = (uint16_t)p;
+        if (rf) posR[nR + popc_below(br)] = (uint16_t)p;  // ascending for now
         nL += __popcll(bl);
         nR += __popcll(br);
       }
@@ -714,7 +676,7 @@ LG_DEVICE void wave_std_sort(K* key, int* val, int n, int* posL, int* posR, unsi
     const int p = base + lane;
     const bool st = p < n && ((blk[p >> 5] >> (p & 31)) & 1u);
     const unsigned long long m = __ballot(st);
-    if (st) posL[nblk + popc_below(m)] = p;
+    if (st) posL[nblk + popc_below(m)] = (uint16_t)p;
     nblk += __popcll(m);
   }
   __syncthreads();
@@ -724,7 +686,7 @@ LG_DEVICE void wave_std_sort(K* key, int* val, int n, int* posL, int* posR, unsi
     {
       for (int i = p + 1; i < e; ++i) {
         K vk = key[i];
-        int vv = val[i];
+        V vv = val[i];
         int j = i;
         while (j > p && vk < key[j - 1]) {
           key[j] = key[j - 1];
@@ -751,6 +713,28 @@ struct ScanView {
   LG_DEVICE uint32_t col_at(int k) const { return k < M ? col[k] : 0u; }         // tail is 0 (:138)
   LG_DEVICE bool ground_at(int k) const { return k < M ? gflag[k] != 0 : false; }  // tail false (:137)
 };
+
+// The +-5 neighbour suppression with one wave: lanes 0..4 take l = 1..5, lanes 8..12 take
+// l = -1..-5; each direction stops at its first column jump > 10 (the reference's `break`) and skips
+// out-of-range l (`continue`), exactly as the sequential loops (all writes set picked to 1).
+LG_DEVICE void suppress_wave(const ScanView& v, int ind) {
+  const int lane = lane_id();
+  const int l = (lane < 5) ? lane + 1 : (lane >= 8 && lane < 13) ? -(lane - 7) : 0;
+  bool valid = false, brk = false;
+  if (l > 0) {
+    valid = (unsigned)(ind + l) < (unsigned)v.VH;
+    if (valid) brk = abs((int)(v.col_at(ind + l) - v.col_at(ind + l - 1))) > 10;
+  } else if (l < 0) {
+    valid = ind + l >= 0;
+    if (valid) brk = abs((int)(v.col_at(ind + l) - v.col_at(ind + l + 1))) > 10;
+  }
+  const unsigned long long bm = __ballot(brk);
+  const unsigned fwd = (unsigned)(bm & 0x1full), bwd = (unsigned)((bm >> 8) & 0x1full);
+  const int ff = fwd ? __ffs(fwd) - 1 : 5, fb = bwd ? __ffs(bwd) - 1 : 5;  // index of the breaking l
+  if (l > 0 && valid && (l - 1) < ff) v.picked[ind + l] = 1;
+  if (l < 0 && valid && (-l - 1) < fb) v.picked[ind + l] = 1;
+  if (lane == 0) v.picked[ind] = 1;
+}
 
 LG_DEVICE void suppress_neighbours(const ScanView& v, int ind) {  // :306-326
   v.picked[ind] = 1;
@@ -839,8 +823,8 @@ LG_DEVICE void sort_segment(ExtractLds& L, int n) {
 #ifdef LG_PROFILE
     if (lane == 0) atomicAdd(&g_prof[14], 1ull);
 #endif
-    int* scratch = (int*)L.vkey;  // free during the segment phase
-    wave_std_sort<float>(key, val, n, scratch, scratch + SEG_MAX, L.blk, L.stk, L.small, &L.nsmall);
+    uint16_t* scratch = (uint16_t*)L.vkey;  // free during the segment phase
+    wave_std_sort<float, int>(key, val, n, scratch, scratch + SEG_MAX, L.blk, L.stk, L.tab);
   }
 }
 
@@ -860,7 +844,8 @@ LG_DEVICE float4 seg_point(const ScanView& v, int ind, int& status) {  // segmen
 }
 
 // PCL VoxelGrid<PointXYZI> (leaf 0.2) over the ring's lessFlat points (positions in L.vval[0..n)).
-LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, RingOut& o) {
+LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, int base_pos, RingOut& o) {
+  const float4* fa = v.fa + base_pos;  // L.vval holds positions relative to the ring start
   const int lane = lane_id();
   o.nLF = 0;
   if (n == 0) return;
@@ -868,7 +853,7 @@ LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, RingOut& o) {
   const float inv = 1.0f / leaf;
   float mnx = FLT_MAX, mny = FLT_MAX, mnz = FLT_MAX, mxx = -FLT_MAX, mxy = -FLT_MAX, mxz = -FLT_MAX;
   for (int t = lane; t < n; t += 64) {
-    const float4 p = v.fa[L.vval[t]];
+    const float4 p = fa[L.vval[t]];
     mnx = (p.x < mnx) ? p.x : mnx; mny = (p.y < mny) ? p.y : mny; mnz = (p.z < mnz) ? p.z : mnz;
     mxx = (p.x > mxx) ? p.x : mxx; mxy = (p.y > mxy) ? p.y : mxy; mxz = (p.z > mxz) ? p.z : mxz;
   }
@@ -878,7 +863,7 @@ LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, RingOut& o) {
   const long long dy = (long long)((mxy - mny) * inv) + 1;
   const long long dz = (long long)((mxz - mnz) * inv) + 1;
   if (dx * dy * dz > 2147483647ll) {  // PCL: "Integer indices would overflow" -> output = input
-    for (int t = lane; t < n; t += 64) o.lflat[t] = v.fa[L.vval[t]];
+    for (int t = lane; t < n; t += 64) o.lflat[t] = fa[L.vval[t]];
     o.nLF = n;
     o.status |= LEGO_ST_VOXEL_OVERFLOW;
     return;
@@ -888,7 +873,7 @@ LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, RingOut& o) {
   const int divx = maxbx - minbx + 1, divy = maxby - minby + 1;
   const int mul1 = divx, mul2 = divx * divy;
   for (int t = lane; t < n; t += 64) {
-    const float4 p = v.fa[L.vval[t]];
+    const float4 p = fa[L.vval[t]];
     const int i0 = (int)(floorf(p.x * inv) - (float)minbx);
     const int i1 = (int)(floorf(p.y * inv) - (float)minby);
     const int i2 = (int)(floorf(p.z * inv) - (float)minbz);
@@ -896,7 +881,7 @@ LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, RingOut& o) {
   }
   __syncthreads();
   PROF_T(t_vs0);
-  wave_std_sort<unsigned>(L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.small, &L.nsmall);
+  wave_std_sort<unsigned, uint16_t>(L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.tab);
   PROF_ADD(5, t_vs0);
   int running = 0;
   for (int base = 0; base < n; base += 64) {
@@ -908,7 +893,7 @@ LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, RingOut& o) {
       float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
       int u = t;
       for (; u < n && L.vkey[u] == k; ++u) {
-        const float4 p = v.fa[L.vval[u]];
+        const float4 p = fa[L.vval[u]];
         sx += p.x; sy += p.y; sz += p.z; si += p.w;
       }
       const float cntf = (float)(u - t);
@@ -970,8 +955,8 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
           }
           o.lsharp[o.nLS] = pt;
           o.lsharp_ind[o.nLS] = aind;
-          suppress_neighbours(v, aind);
         }
+        suppress_wave(v, aind);
         if (largest <= 2) o.nS++;
         o.nLS++;
         alive = alive && lane > f;
@@ -999,8 +984,8 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
           v.flabel[aind] = -1;
           o.flat[o.nF] = seg_point(v, aind, o.status);
           o.flat_ind[o.nF] = aind;
-          if (smallest < 4) suppress_neighbours(v, aind);
         }
+        if (smallest < 4) suppress_wave(v, aind);
         o.nF++;
         if (smallest >= 4) { stop = true; break; }
         alive = alive && lane > f;
@@ -1016,14 +1001,14 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
       const int k = sp + t;
       const bool pr = t <= n && v.flabel[k] <= 0;
       const unsigned long long m = __ballot(pr);
-      if (pr) L.vval[nlist + popc_below(m)] = k;
+      if (pr) L.vval[nlist + popc_below(m)] = (uint16_t)(k - st);
       nlist += __popcll(m);
     }
     __syncthreads();
     PROF_ADD(3, t_lf0);
   }
   PROF_T(t_vox0);
-  voxel_ring(v, L, nlist, o);
+  voxel_ring(v, L, nlist, st, o);
   PROF_ADD(4, t_vox0);
 }
 
@@ -1950,12 +1935,12 @@ extern "C" int lego_test_libm(const float* h_a, const float* h_b, float* h_out, 
 __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int n, int is_float) {
   __shared__ ExtractLds L;
   const int lane = lane_id();
-  for (int i = lane; i < n; i += 64) { L.vkey[i] = keys[i]; L.vval[i] = vals[i]; }
+  for (int i = lane; i < n; i += 64) { L.vkey[i] = keys[i]; L.vval[i] = (uint16_t)vals[i]; }
   __syncthreads();
   if (is_float) {
-    wave_std_sort<float>((float*)L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.small, &L.nsmall);
+    wave_std_sort<float, uint16_t>((float*)L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.tab);
   } else {
-    wave_std_sort<unsigned>(L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.small, &L.nsmall);
+    wave_std_sort<unsigned, uint16_t>(L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.tab);
   }
   for (int i = lane; i < n; i += 64) { keys[i] = L.vkey[i]; vals[i] = L.vval[i]; }
 }
