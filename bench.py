@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (rank 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threads", type=int, default=16, help="host threads for input generation")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (test rehearsal)")
     return ap.parse_args()
 
 
@@ -81,9 +82,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group(args.dist_backend)
+    ndev = torch.cuda.device_count()
+    local_dev = local % max(ndev, 1)  # == local on a full node; lets a 1-GPU box rehearse N>1 with gloo
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     params = L.params_vlp16() if args.kind == "vlp16" else L.params_hdl64()
     cfg = A.synth_cfg(args.kind)
@@ -104,7 +108,7 @@ def main():
     offs = (np.arange(nsteps * S, dtype=np.int64) * cap).reshape(nsteps, S)
     d_off = torch.from_numpy(offs).to(dev)
     d_cnt = torch.from_numpy(host_cnt.astype(np.int32)).to(dev)
-    batch = L.Batch(params, S, cap, device=local)
+    batch = L.Batch(params, S, cap, device=local_dev)
     stream = torch.cuda.current_stream(dev)
 
     def step(k):
@@ -125,12 +129,12 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     poses, status = batch.poses()
     # trajectory gather: the path's only collective
-    traj = torch.from_numpy(poses).to(dev)
+    traj = torch.from_numpy(poses).to(coll_dev)
     if world > 1:
         gathered = [torch.empty_like(traj) for _ in range(world)]
         dist.all_gather(gathered, traj)

@@ -1,0 +1,66 @@
+// replay_pipeline.cpp — the reference's main.cpp topology (LeGO-LOAM/src/main.cpp:37-47,72-95)
+// without ROS: ImageProjection on the caller thread, FeatureAssociation on its own thread, joined by
+// a blocking Channel<ProjectionOut>; AssociationOut goes to a non-blocking channel (live mode).
+//
+//   replay_pipeline <scans.bin> [device]
+// scans.bin: int32 nscans, then per scan: int32 n, n x (float x, y, z, intensity).
+// Prints one line per run: "cycles <n> status <bits> position x y z orientation x y z w".
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "lego_loam_amd.hpp"
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s scans.bin [device]\n", argv[0]);
+    return 2;
+  }
+  const int device = argc > 2 ? std::atoi(argv[2]) : 0;
+  FILE* f = std::fopen(argv[1], "rb");
+  if (!f) return 2;
+  int32_t nscans = 0;
+  if (std::fread(&nscans, 4, 1, f) != 1) return 2;
+  std::vector<std::vector<float>> scans(nscans);
+  for (int i = 0; i < nscans; ++i) {
+    int32_t n = 0;
+    if (std::fread(&n, 4, 1, f) != 1) return 2;
+    scans[i].resize((size_t)n * 4);
+    if (n && std::fread(scans[i].data(), 16, n, f) != (size_t)n) return 2;
+  }
+  std::fclose(f);
+
+  using namespace lego_amd;
+  lego_params params = vlp16_params();
+  Channel<ProjectionOut> projection_out_channel(true);
+  Channel<AssociationOut> association_out_channel(false);
+  Odometry odom;
+  int status = 0, cycles = 0;
+  try {
+    ImageProjection IP(params, projection_out_channel, device);
+    FeatureAssociation FA(params, projection_out_channel, association_out_channel, device);
+    for (int i = 0; i < nscans; ++i) {  // rosbag replay loop (main.cpp:72-95)
+      PointCloud2View msg;
+      msg.stamp = 0.1 * i;
+      msg.data = scans[i].data();
+      msg.width = (int32_t)(scans[i].size() / 4);
+      IP.cloudHandler(msg);
+    }
+    // hand the worker a sentinel after the last scan and wait for it (the dtor does the same)
+    while (FA.cycles() < nscans && FA.error().empty()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    if (!FA.error().empty()) {
+      std::fprintf(stderr, "%s\n", FA.error().c_str());
+      return 1;
+    }
+    odom = FA.last_odometry();
+    status = FA.last_status();
+    cycles = FA.cycles();
+  } catch (const Error& e) {
+    std::fprintf(stderr, "error: %s\n", e.what());
+    return 1;
+  }
+  std::printf("cycles %d status %d position %.9g %.9g %.9g orientation %.9g %.9g %.9g %.9g\n", cycles, status,
+              odom.position[0], odom.position[1], odom.position[2], odom.orientation[0], odom.orientation[1],
+              odom.orientation[2], odom.orientation[3]);
+  return 0;
+}
