@@ -121,7 +121,9 @@ LG_DEVICE int block_max_int(int v, int* scratch) {
 // The reference's scatter "later input point overwrites earlier ones in the same cell"
 // (imageProjection.cpp:214-222) is an atomicMax of the input index per cell, followed by a
 // column-parallel gather that writes every cell (so resetParameters' fill is fused in).
-template <bool kLdsWinner>
+// kRows > 0: the column pass keeps its (at most kRows) cells in registers, so the 2-D scan does not
+// re-read the range/cloud images it has just written (PMC: that re-read was 40% of FETCH_SIZE).
+template <bool kLdsWinner, int kRows>
 __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                   const int64_t* __restrict__ offs,
                                                   const int32_t* __restrict__ cnts) {
@@ -132,25 +134,42 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   int* winner = kLdsWinner ? (smem + 64) : (B.winner + (size_t)s * VH);
   const float4* in = pts + offs[s];
   const int n = cnts[s];
+  PROF_T(t_p0);
   for (int c = tid; c < VH; c += nt) winner[c] = -1;
   __syncthreads();
+  PROF_ADD(20, t_p0);
+  PROF_T(t_p1);
   int fmin = 0x7fffffff, fmax = -1;
-  for (int i = tid; i < n; i += nt) {
-    const float4 p = in[i];
-    if (!isfinite_f(p.x) || !isfinite_f(p.y) || !isfinite_f(p.z)) continue;  // removeNaNFromPointCloud
-    fmin = min(fmin, i);
-    fmax = max(fmax, i);
-    float range = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-    float verticalAngle = asinf_g(p.z / range);
-    int rowIdn = (int)((verticalAngle + P.ang_bottom) / P.ang_res_y);
-    if (rowIdn < 0 || rowIdn >= V) continue;
-    float horizonAngle = atan2f_g(p.x, p.y);
-    int columnIdn = (int)(-round(((double)horizonAngle - M_PI_2) / (double)P.ang_res_x) + H * 0.5);
-    if (columnIdn >= H) columnIdn -= H;
-    if (columnIdn < 0 || columnIdn >= H) continue;
-    if ((double)range < 0.1) continue;
-    atomicMax(&winner[rowIdn * H + columnIdn], i);
+  constexpr int kUnroll = 4;  // four independent point loads in flight per lane
+  for (int i0 = tid; i0 < n; i0 += nt * kUnroll) {
+    float4 pk[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int i = i0 + u * nt;
+      pk[u] = (i < n) ? in[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int i = i0 + u * nt;
+      const float4 p = pk[u];
+      if (i >= n) break;
+      if (!isfinite_f(p.x) || !isfinite_f(p.y) || !isfinite_f(p.z)) continue;  // removeNaNFromPointCloud
+      fmin = min(fmin, i);
+      fmax = max(fmax, i);
+      float range = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+      float verticalAngle = asinf_g(p.z / range);
+      int rowIdn = (int)((verticalAngle + P.ang_bottom) / P.ang_res_y);
+      if (rowIdn < 0 || rowIdn >= V) continue;
+      float horizonAngle = atan2f_g(p.x, p.y);
+      int columnIdn = (int)(-round(((double)horizonAngle - M_PI_2) / (double)P.ang_res_x) + H * 0.5);
+      if (columnIdn >= H) columnIdn -= H;
+      if (columnIdn < 0 || columnIdn >= H) continue;
+      if ((double)range < 0.1) continue;
+      atomicMax(&winner[rowIdn * H + columnIdn], i);
+    }
   }
+  PROF_ADD(21, t_p1);
+  PROF_T(t_p2);
   fmin = block_min_int(fmin, scratch);
   fmax = block_max_int(fmax, scratch);
   if (tid == 0) {
@@ -170,6 +189,8 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
     B.state[s].proj_status = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
   }
   __syncthreads();
+  PROF_ADD(22, t_p2);
+  PROF_T(t_p3);
   float* range = B.range + (size_t)s * VH;
   float4* cloud = B.cloud + (size_t)s * VH;
   int8_t* ground = B.ground + (size_t)s * VH;
@@ -177,7 +198,8 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   for (int j = tid; j < H; j += nt) {
     unsigned long long gmask = 0ull;
     float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = 0; i < V; ++i) {
+    float rr[kRows > 0 ? kRows : 1], zz[kRows > 0 ? kRows : 1];
+    auto cell = [&](int i) {
       const int c = i * H + j;
       const int w = winner[c];
       float4 q;
@@ -198,24 +220,41 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
         if ((double)(va - P.mount) <= 10 * DEG_TO_RAD_D) gmask |= (3ull << (i - 1));
       }
       prev = q;
+      if constexpr (kRows > 0) {
+        rr[i] = r;
+        zz[i] = q.z;
+      }
+    };
+    if constexpr (kRows > 0) {
+#pragma unroll
+      for (int i = 0; i < kRows; ++i)
+        if (i < V) cell(i);
+    } else {
+      for (int i = 0; i < V; ++i) cell(i);
     }
     float min_range = 1000.f;
     int id_min = -1;
-    for (int i = 0; i < V; ++i) {  // 2-D scan (:312-330)
+    auto scan = [&](int i, float r, float Z) {  // 2-D scan (:312-330)
       const int c = i * H + j;
       const int g = (int)((gmask >> i) & 1ull);
       ground[c] = (int8_t)g;
-      const float r = range[c];
-      const float Z = cloud[c].z;
       if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f) {
         if (r < min_range) {
           min_range = r;
           id_min = c;
         }
       }
+    };
+    if constexpr (kRows > 0) {
+#pragma unroll
+      for (int i = 0; i < kRows; ++i)
+        if (i < V) scan(i, rr[i], zz[i]);
+    } else {
+      for (int i = 0; i < V; ++i) scan(i, range[i * H + j], cloud[i * H + j].z);
     }
     B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
   }
+  PROF_ADD(23, t_p3);
 }
 
 // ============================================================================================
@@ -1669,7 +1708,9 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
                        const float4* __restrict__ last, int nl, bool surf, float4* gp, int& iters) {
   const int tid = threadIdx.x;
   const int nw = LM_THREADS / 64;
+  PROF_T(t_bg0);
   build_grid(L, last, nl, gp, 1.1f * sqrtf(P.nn_dist_sqr) + 0.05f);
+  PROF_ADD(16, t_bg0);
   for (int iter = 0; iter < 25; iter++) {
     float cur[6];
     for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
@@ -1710,12 +1751,14 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
     }
     block_reduce10(L, acc);
     PROF_ADD(10, t_acc0);
+    PROF_T(t_sol0);
     if (tid == 0) {
       iters = iter + 1;
       if (acc[9] < 10.0) L.flag = 1;  // too few correspondences: `continue`
       else L.flag = lm_solve(L, S, acc, iter, surf) ? 1 : 0;
     }
     __syncthreads();
+    PROF_ADD(15, t_sol0);
     if (!L.flag) break;
   }
 }
@@ -1765,8 +1808,12 @@ __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
   } else {
     if (tid == 0 && S.tree_stale) L.status |= LEGO_ST_STALE_TREE;
     float4* gp = B.grid_pts + (size_t)s * VH;
+    PROF_T(t_ls0);
     lm_loop(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, gp, it_s);
+    PROF_ADD(17, t_ls0);
+    PROF_T(t_lc0);
     lm_loop(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, gp, it_c);
+    PROF_ADD(18, t_lc0);
   }
   __syncthreads();
   // integrateTransformation (:1241-1270) + publishOdometry (:1286-1298)
@@ -1853,9 +1900,12 @@ int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* p
                       const int32_t* cnts, hipStream_t st) {
   if (lg_lds_projection(P)) {
     size_t sm = (size_t)(P.VH + 64) * 4;
-    hipLaunchKernelGGL((k_project<true>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
+    if (P.V <= 16)
+      hipLaunchKernelGGL((k_project<true, 16>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
+    else
+      hipLaunchKernelGGL((k_project<true, 0>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
   } else {
-    hipLaunchKernelGGL((k_project<false>), dim3(S), dim3(1024), 64 * 4, st, P, B, pts, offs, cnts);
+    hipLaunchKernelGGL((k_project<false, 0>), dim3(S), dim3(1024), 64 * 4, st, P, B, pts, offs, cnts);
   }
   LG_CHECK_LAUNCH();
   return LEGO_OK;

@@ -19,7 +19,9 @@ from lego_amd import _abi as A  # noqa: E402
 
 NAMES = {0: "x:load+sort seg", 1: "x:sharp greedy", 2: "x:flat greedy", 3: "x:lessflat list", 4: "x:voxel total",
          5: "x:voxel sort", 6: "  sort:wave partitions", 7: "  sort:small lanes", 11: "  sort:final insertion",
-         12: "  seg: global load", 13: "  seg: sort", 8: "lm:transform sel", 9: "lm:search", 10: "lm:coeff+reduce"}
+         12: "  seg: global load", 13: "  seg: sort", 8: "lm:transform sel", 9: "lm:search", 10: "lm:coeff+reduce",
+         15: "lm:solve (thread 0)", 16: "lm:build grid", 17: "lm:surf loop", 18: "lm:corner loop",
+         20: "p:init winner", 21: "p:scatter", 22: "p:reduce+orient", 23: "p:columns"}
 
 
 def main():
@@ -46,7 +48,7 @@ def main():
     b.sync()
     rc = lib.lego_debug_prof(prof, 0)
     assert rc == 0, rc
-    tot = sum(prof[i] for i in NAMES)
+    tot = sum(prof[i] for i in NAMES if i < 17 or i >= 20)
     nsteps = steps - 1
     print("segments sorted via the tie path: %d per step (of %d segments)" % (prof[14] / nsteps, S * 16 * 6))
     for i, nm in NAMES.items():
