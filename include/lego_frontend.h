@@ -174,7 +174,7 @@ int  lego_test_libm(const float* a, const float* b, float* out, int32_t n, int32
 int  lego_test_sort(uint32_t* keys, int32_t* vals, int32_t n, int32_t is_float);
 /* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
  * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */
-int  lego_debug_prof(uint64_t* out32, int32_t reset);
+int  lego_debug_prof(uint64_t* out256, int32_t reset);
 
 #ifdef __cplusplus
 }

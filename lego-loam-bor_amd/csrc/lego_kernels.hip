@@ -28,10 +28,16 @@ using namespace lg;
 
 // ---- diagnostic phase timers (build with -DLG_PROFILE; never in the shipped library) -----------
 #ifdef LG_PROFILE
-__device__ unsigned long long g_prof[32];
+__device__ unsigned long long g_prof[256];  // [0,32) phases; [64+r] / [128+r] per-ring sum / max
 #define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
-#define PROF_ADD(slot, t0) \
-  do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof[slot], __builtin_amdgcn_s_memtime() - (t0)); } while (0)
+#define PROF_ADD(slot, t0)                                           \
+  do {                                                               \
+    if ((threadIdx.x & 63) == 0) {                                   \
+      const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - (t0); \
+      atomicAdd(&g_prof[slot], dt_);                                 \
+      atomicMax(&g_prof[192 + (slot)], dt_);                         \
+    }                                                                \
+  } while (0)
 #else
 #define PROF_T(v) do {} while (0)
 #define PROF_ADD(slot, t0) do {} while (0)
@@ -558,20 +564,88 @@ __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
 #define SEG_MAX 512
 #define RING_MAX 2048
 
-#define SORT_SMALL 64
-#define SMALL_MAX 160
-
-struct ExtractLds {  // 21.5 KB per wave -> 7 waves per CU
+struct ExtractLds {  // 13.5 KB per wave -> 11 waves per CU
   union {
-    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;             // segment sort (extract phase)
-    struct { uint16_t posL[RING_MAX]; uint16_t posR[RING_MAX]; } part;  // partition scratch (voxel phase)
+    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;  // segment sort (extract phase)
+    unsigned vkey[RING_MAX];                                 // voxel keys (voxel phase)
   } u;
-  unsigned vkey[RING_MAX];      // voxel keys; doubles as partition scratch during the segment phase
   uint16_t vval[RING_MAX];      // lessFlat positions of the ring (relative to the ring start), sorted with vkey
   unsigned blk[RING_MAX / 32];  // final-block start bits of the introsort emulation
   int stk[3 * 64];
-  int tab[128];                 // lane-pairing table of the in-register partition
+  int tab[128];                 // lane-pairing / stop-queue scratch of the partitions
 };
+
+// libstdc++ __adjust_heap (lego_introsort.h) on one lane; each level's two children are loaded
+// (key and value) before the choice, so a level of the sift-down costs one LDS round trip.
+template <typename K, typename V>
+LG_DEVICE void adjust_heap_pf(const SortView<K, V>& a, int first, int hole, int len, K vk, V vv) {
+  K* key = a.key + first;
+  V* val = a.val + first;
+  const int top = hole;
+  int second = hole;
+  const int lim = (len - 1) / 2;
+  if (second < lim) {
+    int c = 2 * (second + 1);
+    K kr = key[c], kl = key[c - 1];
+    V vr = val[c], vl = val[c - 1];
+    while (true) {
+      second = c;
+      K ks = kr;
+      V vs = vr;
+      if (kr < kl) { second = c - 1; ks = kl; vs = vl; }
+      key[hole] = ks;
+      val[hole] = vs;
+      hole = second;
+      if (!(second < lim)) break;
+      c = 2 * (second + 1);
+      kr = key[c]; kl = key[c - 1];
+      vr = val[c]; vl = val[c - 1];
+    }
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    key[hole] = key[second - 1];
+    val[hole] = val[second - 1];
+    hole = second - 1;
+  }
+  int parent = (hole - 1) / 2;  // __push_heap
+  while (hole > top && key[parent] < vk) {
+    key[hole] = key[parent];
+    val[hole] = val[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  key[hole] = vk;
+  val[hole] = vv;
+}
+
+// __partial_sort(first, last, last) = __make_heap + __sort_heap.  __make_heap sifts the parents
+// from (len-2)/2 down to 0; parents on one heap level have disjoint subtrees (and __push_heap stops
+// at `top`), so each level runs in parallel, deepest level first.  __sort_heap's pops are a chain.
+template <typename K, typename V>
+LG_DEVICE void heap_sort_wave(const SortView<K, V>& a, int first, int last) {
+  const int lane = lane_id();
+  const int len = last - first;
+  if (len >= 2) {
+    const int plast = (len - 2) / 2;
+    for (int lev = floor_log2(plast + 1); lev >= 0; --lev) {
+      const int lo = (1 << lev) - 1, hi = min((2 << lev) - 2, plast);
+      for (int p = hi - lane; p >= lo; p -= 64) adjust_heap_pf(a, first, p, len, a.key[first + p], a.val[first + p]);
+      __syncthreads();
+    }
+  }
+  if (lane == 0) {
+    int l = last;
+    while (l - first > 1) {
+      --l;
+      const K vk = a.key[l];
+      const V vv = a.val[l];
+      a.move(l, first);
+      adjust_heap_pf(a, first, 0, l - first, vk, vv);
+    }
+  }
+  __syncthreads();
+}
 
 // __unguarded_partition_pivot on a range of 17..64 elements held one per lane; returns the cut.
 // tab: >= 128 ints of LDS scratch.
@@ -634,12 +708,67 @@ LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last,
   return first + min(cl, cr);
 }
 
+// __unguarded_partition_pivot on [first, last) with the pivot already at first, > 64 elements.
+// Hoare's loop pairs the k-th left stop L_k (!(key < pivot), scanning up from first+1) with the
+// k-th right stop R_k (!(pivot < key), scanning down from last-1), swaps while L_k < R_k, and
+// returns min(L_K, R_{K-1}) for the first crossing pair K (R_{-1} = last).  Here both scans advance
+// 64 positions at a time and the stops found are queued one per lane; a pair is only formed when
+// both of its stops are known.  Positions swapped by pair j (L_j, R_j) lie outside the span
+// (L_k, R_k) of every later valid pair k, so stops read in a chunk before or after such a swap are
+// the same up to the crossing, and the min() covers a left scan that has run into swapped
+// territory.  Every position is read at most once.
 template <typename K, typename V>
-LG_DEVICE void wave_std_sort(K* key, V* val, int n, uint16_t* posL, uint16_t* posR, unsigned* blk, int* stk,
-                             int* tab) {
+LG_DEVICE int wave_partition_stream(const SortView<K, V>& a, int first, int last, int* tab) {
+  const int lane = lane_id();
+  const K pv = a.key[first];
+  int lo = first + 1, hi = last - 1;
+  int qL = 0, qR = 0, nqL = 0, nqR = 0;
+  int lastR = last;
+  while (true) {
+    const bool scanL = nqL == 0, scanR = nqR == 0;
+    if (scanL && lo >= last) {  // unreachable for a median-of-3 pivot; mirrors the unguarded end
+      __syncthreads();
+      return min(last, lastR);
+    }
+    bool stL = false, stR = false;
+    const int pL = lo + lane, pR = hi - lane;
+    if (scanL && pL < last) stL = !(a.key[pL] < pv);
+    if (scanR && pR >= first) stR = !(pv < a.key[pR]);
+    const unsigned long long mL = __ballot(stL), mR = __ballot(stR);
+    if (stL) tab[popc_below(mL)] = pL;
+    if (stR) tab[64 + popc_below(mR)] = pR;
+    __syncthreads();
+    if (scanL) { qL = tab[lane]; nqL = __popcll(mL); lo += 64; }
+    if (scanR) { qR = tab[64 + lane]; nqR = __popcll(mR); hi -= 64; }
+    __syncthreads();
+    const int np = min(nqL, nqR);
+    const bool valid = lane < np && qL < qR;
+    const int nv = __popcll(__ballot(valid));  // valid pairs form a prefix (L increasing, R decreasing)
+    if (valid) a.swap(qL, qR);
+    if (nv < np) {
+      const int Lk = __shfl(qL, nv);
+      const int Rk1 = nv > 0 ? __shfl(qR, nv - 1) : lastR;
+      __syncthreads();
+      return min(Lk, Rk1);
+    }
+    if (np > 0) {
+      lastR = __shfl(qR, np - 1);
+      const int src = min(lane + np, 63);
+      qL = __shfl(qL, src);
+      qR = __shfl(qR, src);
+      nqL -= np;
+      nqR -= np;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename K, typename V>
+LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int* tab) {
   const int lane = lane_id();
   if (n <= 1) return;
-  for (int w = lane; w < (n + 31) / 32; w += 64) blk[w] = 0u;
+  const int nwords = (n + 31) >> 5;
+  for (int w = lane; w < nwords; w += 64) blk[w] = 0u;
   __syncthreads();
   SortView<K, V> a{key, val};
   int sp = 0;
@@ -653,51 +782,29 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, uint16_t* posL, uint16_t* po
     __syncthreads();
     while (last - first > 16) {
       if (depth == 0) {
-        if (lane == 0) heap_sort(a, first, last);
+        PROF_T(t_hs0);
+        heap_sort_wave(a, first, last);
+        PROF_ADD(7, t_hs0);
+#ifdef LG_PROFILE
+        if (lane == 0) atomicAdd(&g_prof[24], 1ull);
+#endif
         break;
       }
       --depth;
+      int cut;
       if (last - first <= 64) {  // one chunk: partition in registers
-        const int cut = wave_partition_small(a, first, last, tab);
-        if (lane == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = last; stk[3 * sp + 2] = depth; }
-        ++sp;
-        last = cut;
+#ifdef LG_PROFILE
+        if (lane == 0) atomicAdd(&g_prof[26], 1ull);
+#endif
+        cut = wave_partition_small(a, first, last, tab);
+      } else {
+#ifdef LG_PROFILE
+        if (lane == 0) { atomicAdd(&g_prof[25], 1ull); atomicAdd(&g_prof[27], (unsigned long long)(last - first)); }
+#endif
+        if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
         __syncthreads();
-        continue;
+        cut = wave_partition_stream(a, first, last, tab);
       }
-      if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
-      __syncthreads();
-      const K pv = key[first];
-      // pass 1: rank the stops, record positions
-      int nL = 0, nR = 0;
-      for (int base = first + 1; base < last; base += 64) {
-        const int p = base + lane;
-        const bool in = p < last;
-        const K kp = in ? key[p] : pv;
-        const bool lf = in && !(kp < pv), rf = in && !(pv < kp);
-        const unsigned long long bl = __ballot(lf), br = __ballot(rf);
-        if (lf) posL[nL + popc_below(bl)] = (uint16_t)p;
-        if (rf) posR[nR + popc_below(br)] = (uint16_t)p;  // ascending for now
-        nL += __popcll(bl);
-        nR += __popcll(br);
-      }
-      __syncthreads();
-      // pass 2: k-th left stop vs k-th right stop from the right (posR[nR-1-k]); swap while Lk < Rk
-      int nsw = 0;
-      const int kmax = min(nL, nR);
-      for (int base = 0; base < kmax; base += 64) {
-        const int k = base + lane;
-        const bool sw = k < kmax && posL[k] < posR[nR - 1 - k];
-        const unsigned long long m = __ballot(sw);
-        if (sw) a.swap(posL[k], posR[nR - 1 - k]);
-        nsw += __popcll(m);
-        if (m != ~0ull) break;  // monotone: once a pair crosses, all later pairs do
-      }
-      __syncthreads();
-      const int lk = (nsw < nL) ? posL[nsw] : last;
-      const int rk = (nsw > 0) ? posR[nR - nsw] : last;
-      const int cut = min(lk, rk);
-      __syncthreads();
       if (lane == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = last; stk[3 * sp + 2] = depth; }
       ++sp;
       last = cut;
@@ -708,21 +815,28 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, uint16_t* posL, uint16_t* po
   }
   PROF_ADD(6, t_part0);
   PROF_T(t_fin0);
-  // __final_insertion_sort as independent per-block insertion sorts: compact the block starts,
-  // then every lane sorts its own blocks (all 64 lanes busy at once).
-  int nblk = 0;
-  for (int base = 0; base < n; base += 64) {
-    const int p = base + lane;
-    const bool st = p < n && ((blk[p >> 5] >> (p & 31)) & 1u);
-    const unsigned long long m = __ballot(st);
-    if (st) posL[nblk + popc_below(m)] = (uint16_t)p;
-    nblk += __popcll(m);
-  }
-  __syncthreads();
-  for (int bi = lane; bi < nblk; bi += 64) {
-    const int p = posL[bi];
-    const int e = (bi + 1 < nblk) ? posL[bi + 1] : n;
-    {
+  // __final_insertion_sort as independent per-block insertion sorts: lane h sorts the blocks that
+  // start in positions [16h, 16h + 16).
+  const int nhalf = (n + 15) >> 4;
+  for (int h = lane; h < nhalf; h += 64) {
+    unsigned bits = (blk[h >> 1] >> ((h & 1) * 16)) & 0xffffu;
+    while (bits) {
+      const int p = 16 * h + __ffs(bits) - 1;
+      bits &= bits - 1u;
+      int e = n;
+      if (bits) {
+        e = 16 * h + __ffs(bits) - 1;
+      } else {
+        const unsigned rest = blk[h >> 1] & ~((2u << ((h & 1) * 16 + 15)) - 1u);  // later bits of this word
+        if ((h & 1) == 0 && rest) {
+          e = 32 * (h >> 1) + __ffs(rest) - 1;
+        } else {
+          for (int ww = (h >> 1) + 1; ww < nwords; ++ww) {
+            const unsigned nb = blk[ww];
+            if (nb) { e = 32 * ww + __ffs(nb) - 1; break; }
+          }
+        }
+      }
       for (int i = p + 1; i < e; ++i) {
         K vk = key[i];
         V vv = val[i];
@@ -773,6 +887,33 @@ LG_DEVICE void suppress_wave(const ScanView& v, int ind) {
   if (l > 0 && valid && (l - 1) < ff) v.picked[ind + l] = 1;
   if (l < 0 && valid && (-l - 1) < fb) v.picked[ind + l] = 1;
   if (lane == 0) v.picked[ind] = 1;
+}
+
+// The extent of suppress_neighbours(ind): it sets picked[ind - fb .. ind + ff] (both <= 5).  Depends
+// only on colInd, so a candidate can compute it before it is picked.
+LG_DEVICE void supp_extent(const ScanView& v, int ind, int& ff, int& fb) {
+  uint32_t c[11];
+#pragma unroll
+  for (int j = 0; j < 11; ++j) {
+    const int k = ind - 5 + j;
+    c[j] = (k >= 0 && k < v.M) ? v.col[k] : 0u;  // col_at
+  }
+  ff = 0;
+#pragma unroll
+  for (int l = 1; l <= 5; ++l) {
+    if (ff != l - 1) break;
+    if ((unsigned)(ind + l) >= (unsigned)v.VH) break;  // `continue` for this and every later l
+    if (abs((int)(c[5 + l] - c[4 + l])) > 10) break;
+    ff = l;
+  }
+  fb = 0;
+#pragma unroll
+  for (int l = 1; l <= 5; ++l) {
+    if (fb != l - 1) break;
+    if (ind - l < 0) break;
+    if (abs((int)(c[5 - l] - c[6 - l])) > 10) break;
+    fb = l;
+  }
 }
 
 LG_DEVICE void suppress_neighbours(const ScanView& v, int ind) {  // :306-326
@@ -862,8 +1003,7 @@ LG_DEVICE void sort_segment(ExtractLds& L, int n) {
 #ifdef LG_PROFILE
     if (lane == 0) atomicAdd(&g_prof[14], 1ull);
 #endif
-    uint16_t* scratch = (uint16_t*)L.vkey;  // free during the segment phase
-    wave_std_sort<float, int>(key, val, n, scratch, scratch + SEG_MAX, L.blk, L.stk, L.tab);
+    wave_std_sort<float, int>(key, val, n, L.blk, L.stk, L.tab);
   }
 }
 
@@ -916,22 +1056,22 @@ LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, int base_pos,
     const int i0 = (int)(floorf(p.x * inv) - (float)minbx);
     const int i1 = (int)(floorf(p.y * inv) - (float)minby);
     const int i2 = (int)(floorf(p.z * inv) - (float)minbz);
-    L.vkey[t] = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+    L.u.vkey[t] = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
   }
   __syncthreads();
   PROF_T(t_vs0);
-  wave_std_sort<unsigned, uint16_t>(L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.tab);
+  wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
   PROF_ADD(5, t_vs0);
   int running = 0;
   for (int base = 0; base < n; base += 64) {
     const int t = base + lane;
-    const bool start = t < n && (t == 0 || L.vkey[t] != L.vkey[t - 1]);
+    const bool start = t < n && (t == 0 || L.u.vkey[t] != L.u.vkey[t - 1]);
     const unsigned long long m = __ballot(start);
     if (start) {
-      const unsigned k = L.vkey[t];
+      const unsigned k = L.u.vkey[t];
       float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
       int u = t;
-      for (; u < n && L.vkey[u] == k; ++u) {
+      for (; u < n && L.u.vkey[u] == k; ++u) {
         const float4 p = fa[L.vval[u]];
         sx += p.x; sy += p.y; sz += p.z; si += p.w;
       }
@@ -967,20 +1107,24 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
 
     PROF_ADD(0, t_seg0);
     PROF_T(t_sharp0);
-    // sharp: k = ep .. sp (descending curvature), first 2 eligible -> sharp, up to 20 -> less sharp
+    // sharp: k = ep .. sp (descending curvature), first 2 eligible -> sharp, up to 20 -> less sharp.
+    // picked[] is read once per chunk; a pick then kills the chunk's lanes inside its suppression
+    // extent in registers (the same writes still go to picked[] for later chunks and passes).
     int largest = 0;
     bool stop = false;
     for (int base = n; base >= 0 && !stop; base -= 64) {
       const int t = base - lane;
       const bool valid = t >= 0;
       const int ind = valid ? L.u.seg.sval[t] : 0;
-      bool alive = valid;
+      bool cand = valid && v.picked[ind] == 0 && v.curv[ind] > P.edge_thr && !v.ground_at(ind);
+      if (__ballot(cand) == 0ull) continue;
+      int ff = 0, fb = 0;
+      if (cand) supp_extent(v, ind, ff, fb);
       while (true) {
-        const bool elig = alive && v.picked[ind] == 0 && v.curv[ind] > P.edge_thr && !v.ground_at(ind);
-        const unsigned long long m = __ballot(elig);
+        const unsigned long long m = __ballot(cand);
         if (m == 0ull) break;
         const int f = __ffsll((long long)m) - 1;
-        const int aind = __shfl(ind, f);
+        const int aind = __shfl(ind, f), aff = __shfl(ff, f), afb = __shfl(fb, f);
         largest++;
         if (largest > 20) { stop = true; break; }
         if (lane == 0) {
@@ -995,12 +1139,12 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
           o.lsharp[o.nLS] = pt;
           o.lsharp_ind[o.nLS] = aind;
         }
-        suppress_wave(v, aind);
+        if (lane <= aff + afb) v.picked[aind - afb + lane] = 1;
         if (largest <= 2) o.nS++;
         o.nLS++;
-        alive = alive && lane > f;
-        __syncthreads();
+        cand = cand && lane > f && !(ind >= aind - afb && ind <= aind + aff);
       }
+      __syncthreads();  // picked[] writes land before the next chunk reads them
     }
     PROF_ADD(1, t_sharp0);
     PROF_T(t_flat0);
@@ -1011,25 +1155,27 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
       const int t = base + lane;
       const bool valid = t <= n;
       const int ind = valid ? L.u.seg.sval[t] : 0;
-      bool alive = valid;
+      bool cand = valid && v.picked[ind] == 0 && v.curv[ind] < P.surf_thr && v.ground_at(ind);
+      if (__ballot(cand) == 0ull) continue;
+      int ff = 0, fb = 0;
+      if (cand) supp_extent(v, ind, ff, fb);
       while (true) {
-        const bool elig = alive && v.picked[ind] == 0 && v.curv[ind] < P.surf_thr && v.ground_at(ind);
-        const unsigned long long m = __ballot(elig);
+        const unsigned long long m = __ballot(cand);
         if (m == 0ull) break;
         const int f = __ffsll((long long)m) - 1;
-        const int aind = __shfl(ind, f);
+        const int aind = __shfl(ind, f), aff = __shfl(ff, f), afb = __shfl(fb, f);
         smallest++;
         if (lane == 0) {
           v.flabel[aind] = -1;
           o.flat[o.nF] = seg_point(v, aind, o.status);
           o.flat_ind[o.nF] = aind;
         }
-        if (smallest < 4) suppress_wave(v, aind);
         o.nF++;
-        if (smallest >= 4) { stop = true; break; }
-        alive = alive && lane > f;
-        __syncthreads();
+        if (smallest >= 4) { stop = true; break; }  // the 4th breaks before its suppression
+        if (lane <= aff + afb) v.picked[aind - afb + lane] = 1;
+        cand = cand && lane > f && !(ind >= aind - afb && ind <= aind + aff);
       }
+      __syncthreads();
     }
     __syncthreads();
     PROF_ADD(2, t_flat0);
@@ -1087,7 +1233,15 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_
     o.lflat = B.r_lflat + rb * P.H;
     o.nS = o.nLS = o.nF = o.nLF = 0;
     o.status = 0;
+    PROF_T(t_ring0);
     extract_ring(P, v, smooth, rs[r], re[r], L, o);
+#ifdef LG_PROFILE
+    if (lane_id() == 0) {
+      const unsigned long long dt = __builtin_amdgcn_s_memtime() - t_ring0;
+      atomicAdd(&g_prof[64 + (first_pass ? 63 : r)], dt);
+      atomicMax(&g_prof[128 + (first_pass ? 63 : r)], dt);
+    }
+#endif
     if (lane_id() == 0) {
       int32_t* rc = B.r_counts + rb * 4;
       rc[0] = o.nS; rc[1] = o.nLS; rc[2] = o.nF; rc[3] = o.nLF;
@@ -1985,14 +2139,14 @@ extern "C" int lego_test_libm(const float* h_a, const float* h_b, float* h_out, 
 __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int n, int is_float) {
   __shared__ ExtractLds L;
   const int lane = lane_id();
-  for (int i = lane; i < n; i += 64) { L.vkey[i] = keys[i]; L.vval[i] = (uint16_t)vals[i]; }
+  for (int i = lane; i < n; i += 64) { L.u.vkey[i] = keys[i]; L.vval[i] = (uint16_t)vals[i]; }
   __syncthreads();
   if (is_float) {
-    wave_std_sort<float, uint16_t>((float*)L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.tab);
+    wave_std_sort<float, uint16_t>((float*)L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
   } else {
-    wave_std_sort<unsigned, uint16_t>(L.vkey, L.vval, n, L.u.part.posL, L.u.part.posR, L.blk, L.stk, L.tab);
+    wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
   }
-  for (int i = lane; i < n; i += 64) { keys[i] = L.vkey[i]; vals[i] = L.vval[i]; }
+  for (int i = lane; i < n; i += 64) { keys[i] = L.u.vkey[i]; vals[i] = L.vval[i]; }
 }
 
 extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int32_t is_float) {
@@ -2016,9 +2170,9 @@ extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int3
 
 extern "C" int lego_debug_prof(uint64_t* out32, int32_t reset) {
 #ifdef LG_PROFILE
-  if (out32 && hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(uint64_t) * 32) != hipSuccess) return LEGO_EDEVICE;
+  if (out32 && hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(uint64_t) * 256) != hipSuccess) return LEGO_EDEVICE;
   if (reset) {
-    uint64_t z[32] = {0};
+    uint64_t z[256] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return LEGO_EDEVICE;
   }
   return LEGO_OK;

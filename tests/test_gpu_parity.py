@@ -4,6 +4,7 @@ Bar (BASELINE.json north_star): bit-exact range/label/ground images, segmented c
 feature indices and feature clouds; 6-DoF transform within 1e-4 (rad / m).
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -14,6 +15,7 @@ import make_golden as MG
 from lego_amd import _abi as A
 
 pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def oracle_for(params):
@@ -106,6 +108,36 @@ def test_device_sort_matches_libstdcxx(gpu):
                                             is_float)
                 assert rc == 0
                 assert np.array_equal(gv, ev) and np.array_equal(gk, ek), (n, distinct, is_float)
+    # structured inputs: long stop-free runs on one side, organ pipes, runs of equal keys
+    for n in [65, 129, 700, 2048]:
+        i = np.arange(n)
+        for name, keys in [("sorted", i), ("reverse", n - i), ("organ", np.minimum(i, n - i)),
+                           ("saw", i % 37), ("runs", i // 9), ("two", (i > n // 3).astype(np.int64)),
+                           ("spike", np.where(i == n // 2, 10 ** 6, 5))]:
+            keys = keys.astype(np.uint32)
+            vals = np.arange(n, dtype=np.int32)
+            ek, ev = O.std_sort(keys, vals, 0)
+            gk, gv = keys.copy(), vals.copy()
+            assert L.lib().lego_test_sort(gk.ctypes.data_as(fp(C.c_uint32)), gv.ctypes.data_as(fp(C.c_int32)), n,
+                                          0) == 0
+            assert np.array_equal(gv, ev) and np.array_equal(gk, ek), (n, name)
+    # inputs that hit the introsort depth limit (heap-sort fallback), with ties
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "ia")
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-I" + os.path.join(REPO, "lego-loam-bor_amd", "csrc"),
+                               os.path.join(REPO, "tests", "native", "introsort_adversary.cpp"), "-o", exe])
+        for n in [100, 700, 2048]:
+            for c in [1, 2]:
+                out = subprocess.run([exe, str(n), str(c)], stdout=subprocess.PIPE, universal_newlines=True, check=True)
+                keys = np.array(out.stdout.split(), dtype=np.uint32)
+                vals = np.arange(n, dtype=np.int32)
+                ek, ev = O.std_sort(keys, vals, 0)
+                gk, gv = keys.copy(), vals.copy()
+                assert L.lib().lego_test_sort(gk.ctypes.data_as(fp(C.c_uint32)), gv.ctypes.data_as(fp(C.c_int32)),
+                                              n, 0) == 0
+                assert np.array_equal(gv, ev) and np.array_equal(gk, ek), ("adversary", n, c)
 
 
 @pytest.mark.parametrize("seq", [0, 7, 21])

@@ -203,6 +203,14 @@ def test_introsort_matches_libstdcxx(tmp_path):
     assert rc == 0, out
 
 
+def test_introsort_depth_limit_inputs(tmp_path):
+    """McIlroy-adversary inputs (with ties) drive the restated introsort into its heap-sort fallback,
+    and it still gives libstdc++'s permutation."""
+    rc, out = _compile_and_run(os.path.join(REPO, "tests", "native", "introsort_adversary.cpp"), str(tmp_path / "ia"),
+                               ["--check"])
+    assert rc == 0, out
+
+
 def test_libm_restatement_matches_glibc(tmp_path):
     """asinf/atanf/atan2f restated for the device equal the host glibc bit for bit."""
     rc, out = _compile_and_run(os.path.join(REPO, "tests", "native", "libm_check.cpp"), str(tmp_path / "lc"),

@@ -18,7 +18,7 @@ import lego_amd as L  # noqa: E402
 from lego_amd import _abi as A  # noqa: E402
 
 NAMES = {0: "x:load+sort seg", 1: "x:sharp greedy", 2: "x:flat greedy", 3: "x:lessflat list", 4: "x:voxel total",
-         5: "x:voxel sort", 6: "  sort:wave partitions", 7: "  sort:small lanes", 11: "  sort:final insertion",
+         5: "x:voxel sort", 6: "  sort:wave partitions", 7: "  sort:heap fallback", 11: "  sort:final insertion",
          12: "  seg: global load", 13: "  seg: sort", 8: "lm:transform sel", 9: "lm:search", 10: "lm:coeff+reduce",
          15: "lm:solve (thread 0)", 16: "lm:build grid", 17: "lm:surf loop", 18: "lm:corner loop",
          20: "p:init winner", 21: "p:scatter", 22: "p:reduce+orient", 23: "p:columns"}
@@ -37,7 +37,7 @@ def main():
     offs = torch.from_numpy((np.arange(S * steps, dtype=np.int64) * cap).reshape(steps, S)).cuda()
     cnts = torch.from_numpy(cnt.reshape(steps, S).astype(np.int32)).cuda()
     b = L.Batch(params, S, cap)
-    prof = (C.c_uint64 * 32)()
+    prof = (C.c_uint64 * 256)()
     lib = L.lib()
     lib.lego_debug_prof.argtypes = [C.POINTER(C.c_uint64), C.c_int32]
     for k in range(steps):
@@ -52,8 +52,18 @@ def main():
     nsteps = steps - 1
     print("segments sorted via the tie path: %d per step (of %d segments)" % (prof[14] / nsteps, S * 16 * 6))
     for i, nm in NAMES.items():
-        print("%-20s %14.0f cycles/step  (%5.1f%%)  per ring-wave %.0f  per stream %.0f" % (
-            nm, prof[i] / nsteps, 100.0 * prof[i] / max(tot, 1), prof[i] / nsteps / (S * 16), prof[i] / nsteps / S))
+        print("%-20s %14.0f cycles/step  (%5.1f%%)  per ring-wave %.0f  per stream %.0f  max one %.0f" % (
+            nm, prof[i] / nsteps, 100.0 * prof[i] / max(tot, 1), prof[i] / nsteps / (S * 16), prof[i] / nsteps / S,
+            prof[192 + i]))
+
+
+    print("heap sorts %d, stream partitions %d (mean length %.0f), register partitions %d  per step" % (
+        prof[24] / nsteps, prof[25] / nsteps, prof[27] / max(prof[25], 1), prof[26] / nsteps))
+    V = 16
+    print("per-ring extract wave cycles (mean / max over streams), ring 63 = first pass:")
+    for r in list(range(V)) + [63]:
+        if prof[128 + r]:
+            print("  ring %2d  mean %9.0f  max %9.0f" % (r, prof[64 + r] / nsteps / S, prof[128 + r]))
 
 
 if __name__ == "__main__":
