@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (test rehearsal)")
+    ap.add_argument("--groups", type=int, default=2, help="stream slices launched on separate HIP streams")
     return ap.parse_args()
 
 
@@ -109,6 +110,7 @@ def main():
     d_off = torch.from_numpy(offs).to(dev)
     d_cnt = torch.from_numpy(host_cnt.astype(np.int32)).to(dev)
     batch = L.Batch(params, S, cap, device=local_dev)
+    batch.set_groups(args.groups)
     stream = torch.cuda.current_stream(dev)
 
     def step(k):
@@ -171,7 +173,7 @@ def main():
         "config": {"workload": "C3: batched synthetic %s sweeps, %d independent sequences per GPU x 1 scan per step"
                                % (args.kind.upper(), S),
                    "V": V, "H": H, "points_per_scan": round(n_mean, 1), "streams_per_gpu": S,
-                   "parallelism": "sequence-sharded x%d" % world},
+                   "parallelism": "sequence-sharded x%d" % world, "stream_groups": args.groups},
         "roofline": roofline,
         "stages_ms": {"project": round(stage[0], 4), "segment": round(stage[1], 4), "fa_prep": round(stage[2], 4),
                       "extract": round(stage[3], 4), "concat": round(stage[4], 4), "lm": round(stage[5], 4)},

@@ -163,7 +163,13 @@ int  lego_batch_reset(lego_batch* b);
 /* Kernel timing of the last step (ms, measured with hipEvents on the step's stream):
  * [0] project, [1] segment, [2] distortion+smoothness+occlusion, [3] features, [4] concat, [5] LM. */
 int  lego_batch_stage_times(lego_batch* b, float* ms6);
+/* While timing is enabled, steps run as one slice on the caller's stream. */
 int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
+/* Split the streams into `groups` (1..LEGO_MAX_GROUPS) slices, each launched on its own internal HIP
+ * stream (forked from and joined back into the step's stream), so one slice's long-tail kernels
+ * overlap the others'.  Results do not depend on the grouping. */
+#define LEGO_MAX_GROUPS 4
+int  lego_batch_set_groups(lego_batch* b, int32_t groups);
 
 /* ---- test hooks ------------------------------------------------------------------ */
 /* Evaluate the device libm restatement on host arrays: which = 0 asinf(a), 1 atan2f(a, b),

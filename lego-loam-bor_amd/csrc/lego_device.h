@@ -29,6 +29,7 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   float scan_period, edge_thr, surf_thr, nn_dist_sqr;
   int map_div;
   int cap_sharp, cap_lsharp, cap_flat;  // per-ring caps: 12, 120, 24
+  int s0;                               // first stream of the launch (stream groups; 0 otherwise)
 };
 
 struct LgState {  // FeatureAssociation members that persist across scans (featureAssociation.h)

@@ -94,6 +94,11 @@ struct lego_batch {
   hipEvent_t ev[8];
   bool timing = false;
   bool events = false;
+  // stream groups: the S sequences split into `groups` slices, each launched on its own HIP stream
+  // so one slice's long-tail kernels overlap the next slice's (fork/join on the caller's stream)
+  int groups = 1;
+  hipStream_t gs[LEGO_MAX_GROUPS] = {};
+  hipEvent_t fork = nullptr, join[LEGO_MAX_GROUPS] = {};
   hipStream_t last_stream = nullptr;
   // host mirrors for lego_batch_read
   std::vector<lego_point> h_seg, h_out, h_scan, h_sharp, h_lsharp, h_flat, h_lflat, h_clast, h_slast, h_olast;
@@ -107,6 +112,11 @@ struct lego_batch {
     for (void* p : owned) hipFree(p);
     if (events)
       for (int i = 0; i < 8; ++i) hipEventDestroy(ev[i]);
+    for (int g = 0; g < LEGO_MAX_GROUPS; ++g) {
+      if (gs[g]) hipStreamDestroy(gs[g]);
+      if (join[g]) hipEventDestroy(join[g]);
+    }
+    if (fork) hipEventDestroy(fork);
   }
 };
 
@@ -263,29 +273,48 @@ int lego_batch_set_timing(lego_batch* b, int32_t enabled) {
   return LEGO_OK;
 }
 
-static int run_projection(lego_batch* b, const float4* pts, const int64_t* offs, const int32_t* cnts, hipStream_t st) {
-  int rc = lg_launch_project(b->P, b->B, b->S, pts, offs, cnts, st);
+// Streams [s0, s0 + n) of the batch.  Stage events are recorded only for the whole batch (timing).
+static int run_projection(lego_batch* b, const float4* pts, const int64_t* offs, const int32_t* cnts, hipStream_t st,
+                          int s0, int n) {
+  LgParams P = b->P;
+  P.s0 = s0;
+  int rc = lg_launch_project(P, b->B, n, pts, offs, cnts, st);
   if (rc) return rc;
   if (b->timing) hipEventRecord(b->ev[1], st);
-  rc = lg_launch_segment(b->P, b->B, b->S, st);
+  rc = lg_launch_segment(P, b->B, n, st);
   if (rc) return rc;
   if (b->timing) hipEventRecord(b->ev[2], st);
   return LEGO_OK;
 }
 
-static int run_association(lego_batch* b, hipStream_t st) {
-  int rc = lg_launch_fa_prep(b->P, b->B, b->S, st);
+static int run_association(lego_batch* b, hipStream_t st, int s0, int n) {
+  LgParams P = b->P;
+  P.s0 = s0;
+  int rc = lg_launch_fa_prep(P, b->B, n, st);
   if (rc) return rc;
   if (b->timing) hipEventRecord(b->ev[3], st);
-  rc = lg_launch_extract(b->P, b->B, b->S, st);
+  rc = lg_launch_extract(P, b->B, n, st);
   if (rc) return rc;
   if (b->timing) hipEventRecord(b->ev[4], st);
-  rc = lg_launch_concat(b->P, b->B, b->S, st);
+  rc = lg_launch_concat(P, b->B, n, st);
   if (rc) return rc;
   if (b->timing) hipEventRecord(b->ev[5], st);
-  rc = lg_launch_lm(b->P, b->B, b->S, st);
+  rc = lg_launch_lm(P, b->B, n, st);
   if (rc) return rc;
   if (b->timing) hipEventRecord(b->ev[6], st);
+  return LEGO_OK;
+}
+
+int lego_batch_set_groups(lego_batch* b, int32_t groups) {
+  if (!b || groups < 1 || groups > LEGO_MAX_GROUPS) return LEGO_EINVAL;
+  if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
+  groups = groups > b->S ? b->S : groups;
+  if (!b->fork && hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
+  for (int g = 0; g < groups; ++g) {
+    if (!b->gs[g] && hipStreamCreateWithFlags(&b->gs[g], hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
+    if (!b->join[g] && hipEventCreateWithFlags(&b->join[g], hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
+  }
+  b->groups = groups;
   return LEGO_OK;
 }
 
@@ -295,10 +324,25 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   hipStream_t st = (hipStream_t)hip_stream;
   b->last_stream = st;
-  if (b->timing) hipEventRecord(b->ev[0], st);
-  int rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st);
-  if (rc) return rc;
-  return run_association(b, st);
+  if (b->timing || b->groups <= 1) {  // one stream (per-stage timing needs the stages in order)
+    if (b->timing) hipEventRecord(b->ev[0], st);
+    int rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+    if (rc) return rc;
+    return run_association(b, st, 0, b->S);
+  }
+  if (hipEventRecord(b->fork, st) != hipSuccess) return LEGO_EDEVICE;
+  const int G = b->groups;
+  for (int g = 0; g < G; ++g) {
+    const int s0 = (int)((long long)b->S * g / G), s1 = (int)((long long)b->S * (g + 1) / G);
+    if (hipStreamWaitEvent(b->gs[g], b->fork, 0) != hipSuccess) return LEGO_EDEVICE;
+    int rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, b->gs[g], s0, s1 - s0);
+    if (rc) return rc;
+    rc = run_association(b, b->gs[g], s0, s1 - s0);
+    if (rc) return rc;
+    if (hipEventRecord(b->join[g], b->gs[g]) != hipSuccess) return LEGO_EDEVICE;
+    if (hipStreamWaitEvent(st, b->join[g], 0) != hipSuccess) return LEGO_EDEVICE;
+  }
+  return LEGO_OK;
 }
 
 int lego_batch_sync(lego_batch* b) {
@@ -501,7 +545,7 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
   if (n > 0 && hipMemcpy(c->d_pts, c->h_pts.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess)
     return LEGO_EDEVICE;
   if (hipMemcpy(c->d_cnt, &n, sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) return LEGO_EDEVICE;
-  int rc = run_projection(b, c->d_pts ? c->d_pts : (const float4*)c->d_off, c->d_off, c->d_cnt, nullptr);
+  int rc = run_projection(b, c->d_pts ? c->d_pts : (const float4*)c->d_off, c->d_off, c->d_cnt, nullptr, 0, 1);
   if (rc) return rc;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
   LgState S;
@@ -515,7 +559,7 @@ int lego_feature_association(lego_ctx* c, lego_association_out* out) {
   if (!c) return LEGO_EINVAL;
   lego_batch* b = c->b;
   hipSetDevice(b->device);
-  int rc = run_association(b, nullptr);
+  int rc = run_association(b, nullptr, 0, 1);
   if (rc) return rc;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
   if (out) return read_assoc(b, 0, out);

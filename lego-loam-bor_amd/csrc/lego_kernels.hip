@@ -134,7 +134,7 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
                                                   const int64_t* __restrict__ offs,
                                                   const int32_t* __restrict__ cnts) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
-  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, H = P.H, VH = P.VH;
   int* scratch = smem;                 // 64 ints
   int* winner = kLdsWinner ? (smem + 64) : (B.winner + (size_t)s * VH);
@@ -314,7 +314,7 @@ LG_DEVICE void uf_unite(PT parent, int a, int b) {
 template <bool kLds>
 __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
-  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, H = P.H, VH = P.VH, G = P.G;
   int* scratch = smem;  // 64 ints
   int* parent = kLds ? (smem + 64) : (B.cc_parent + (size_t)s * VH);
@@ -494,7 +494,7 @@ LG_DEVICE float ori_branch2(float ori, float eo) {
 
 __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
   __shared__ int scratch[64];
-  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int VH = P.VH;
   const int32_t* cnt = B.counts + (size_t)s * CNT_N;
   const int M = cnt[CNT_M];
@@ -793,14 +793,9 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
       --depth;
       int cut;
       if (last - first <= 64) {  // one chunk: partition in registers
-#ifdef LG_PROFILE
-        if (lane == 0) atomicAdd(&g_prof[26], 1ull);
-#endif
         cut = wave_partition_small(a, first, last, tab);
       } else {
-#ifdef LG_PROFILE
-        if (lane == 0) { atomicAdd(&g_prof[25], 1ull); atomicAdd(&g_prof[27], (unsigned long long)(last - first)); }
-#endif
+
         if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
         __syncthreads();
         cut = wave_partition_stream(a, first, last, tab);
@@ -1200,7 +1195,7 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
 __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_pass) {
   __shared__ ExtractLds L;
   const int V = P.V, VH = P.VH;
-  const int s = first_pass ? blockIdx.x : blockIdx.x / V;
+  const int s = P.s0 + (first_pass ? blockIdx.x : blockIdx.x / V);
   const int ring = first_pass ? 0 : blockIdx.x % V;
   const int32_t* rs = B.ring_start + (size_t)s * V;
   const int32_t* re = B.ring_end + (size_t)s * V;
@@ -1255,7 +1250,7 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_
 // k_concat: ring-ordered concatenation (cornerPointsSharp etc. are appended ring by ring)
 // ============================================================================================
 __global__ __launch_bounds__(256) void k_concat(LgParams P, LgBufs B) {
-  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V;
   __shared__ int off[4][65];
   __shared__ int st;
@@ -1609,14 +1604,23 @@ LG_DEVICE int grid_nn(const LmLds& L, const float4* __restrict__ gp, float4 q, f
       if (x0 > x1) continue;
       const int b = (row + x0 == 0) ? 0 : L.gcell[row + x0 - 1];
       const int e = L.gcell[row + x1];  // cells x0..x1 of a row are contiguous
-      for (int k = b; k < e; ++k) {
-        const float4 p = gp[k];
+      // the (d, idx) minimum and tie count do not depend on the visiting order: 8 loads in flight
+      auto visit = [&](const float4 p) {
         const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
         const float d = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
         const int idx = __float_as_int(p.w);
         if (d < bd) { bd = d; bi = idx; tc = 0; }
         else if (d == bd) { tc++; bi = min(bi, idx); }
+      };
+      int k = b;
+      for (; k + 8 <= e; k += 8) {
+        float4 p8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p8[u] = gp[k + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) visit(p8[u]);
       }
+      for (; k < e; ++k) visit(gp[k]);
     }
   tie = (bd < r2) && tc > 0;
   return (bd < r2) ? bi : -1;
@@ -1637,47 +1641,60 @@ LG_DEVICE void ring_scans(const LgParams& P, const float4* __restrict__ last, in
     if (closest + 1 < bound) status |= LEGO_ST_FWD_OOB;
     bound = nl;
   }
-  // forward j = closest+1 ..
-  for (int base = closest + 1; base < bound; base += 64) {
-    const int j = base + lane;
-    const bool valid = j < bound;
-    int rj = valid ? (int)last[j].w : 0;
-    const bool brk = valid && (double)rj > (double)ring0 + 2.5;
-    const unsigned long long bm = __ballot(brk);
-    const int fb = bm ? __ffsll((long long)bm) - 1 : 64;
-    if (valid && lane < fb) {
-      const float4 p = last[j];
-      const float d = (p.x - sel.x) * (p.x - sel.x) + (p.y - sel.y) * (p.y - sel.y) + (p.z - sel.z) * (p.z - sel.z);
-      const int rank = j - closest;
-      if (surf) {
-        if (rj <= ring0) { if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; } }
-        else { if (key_lt(d, rank, b3d, b3r)) { b3d = d; b3r = rank; b3i = j; } }
-      } else if (rj > ring0) {
-        if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; }
-      }
+  auto consider = [&](int j, int rj, const float4 p, int rank, bool fwd) {
+    const float d = (p.x - sel.x) * (p.x - sel.x) + (p.y - sel.y) * (p.y - sel.y) + (p.z - sel.z) * (p.z - sel.z);
+    if (surf) {
+      if (fwd ? rj <= ring0 : rj >= ring0) { if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; } }
+      else { if (key_lt(d, rank, b3d, b3r)) { b3d = d; b3r = rank; b3i = j; } }
+    } else if (fwd ? rj > ring0 : rj < ring0) {
+      if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; }
     }
-    if (bm) break;
+  };
+  // forward j = closest+1 .. (bound), 4 chunks of 64 loaded at once; stop at the first ring break
+  for (int base = closest + 1; base < bound; base += 256) {
+    float4 p4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = base + 64 * u + lane;
+      p4[u] = (j < bound) ? last[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    bool stop = false;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (stop) break;
+      const int j = base + 64 * u + lane;
+      const bool valid = j < bound;
+      const int rj = valid ? (int)p4[u].w : 0;
+      const bool brk = valid && (double)rj > (double)ring0 + 2.5;
+      const unsigned long long bm = __ballot(brk);
+      const int fb = bm ? __ffsll((long long)bm) - 1 : 64;
+      if (valid && lane < fb) consider(j, rj, p4[u], j - closest, true);
+      if (bm || base + 64 * (u + 1) >= bound) stop = true;
+    }
+    if (stop) break;
   }
   // backward j = closest-1 .. 0
-  for (int top = closest - 1; top >= 0; top -= 64) {
-    const int j = top - lane;
-    const bool valid = j >= 0;
-    int rj = valid ? (int)last[j].w : 0;
-    const bool brk = valid && (double)rj < (double)ring0 - 2.5;
-    const unsigned long long bm = __ballot(brk);
-    const int fb = bm ? __ffsll((long long)bm) - 1 : 64;
-    if (valid && lane < fb) {
-      const float4 p = last[j];
-      const float d = (p.x - sel.x) * (p.x - sel.x) + (p.y - sel.y) * (p.y - sel.y) + (p.z - sel.z) * (p.z - sel.z);
-      const int rank = (1 << 24) + (closest - j);
-      if (surf) {
-        if (rj >= ring0) { if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; } }
-        else { if (key_lt(d, rank, b3d, b3r)) { b3d = d; b3r = rank; b3i = j; } }
-      } else if (rj < ring0) {
-        if (key_lt(d, rank, b2d, b2r)) { b2d = d; b2r = rank; b2i = j; }
-      }
+  for (int top = closest - 1; top >= 0; top -= 256) {
+    float4 p4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = top - 64 * u - lane;
+      p4[u] = (j >= 0) ? last[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if (bm) break;
+    bool stop = false;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (stop) break;
+      const int j = top - 64 * u - lane;
+      const bool valid = j >= 0;
+      const int rj = valid ? (int)p4[u].w : 0;
+      const bool brk = valid && (double)rj < (double)ring0 - 2.5;
+      const unsigned long long bm = __ballot(brk);
+      const int fb = bm ? __ffsll((long long)bm) - 1 : 64;
+      if (valid && lane < fb) consider(j, rj, p4[u], (1 << 24) + (closest - j), false);
+      if (bm || top - 64 * (u + 1) < 0) stop = true;
+    }
+    if (stop) break;
   }
   wave_argmin(b2d, b2r, b2i);
   o2 = b2i;
@@ -1920,7 +1937,7 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
 __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
   __shared__ LmLds L;
   __shared__ LgState S;
-  const int s = blockIdx.x, tid = threadIdx.x;
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x;
   const int V = P.V, VH = P.VH;
   const int32_t* cnt = B.counts + (size_t)s * CNT_N;
   const int n_sharp = cnt[CNT_SHARP], n_lsharp = cnt[CNT_LSHARP], n_flat = cnt[CNT_FLAT], n_lflat = cnt[CNT_LFLAT];

@@ -52,6 +52,7 @@ def lib():
         L.lego_batch_reset.argtypes = [C.c_void_p]
         L.lego_batch_stage_times.argtypes = [C.c_void_p, P(C.c_float)]
         L.lego_batch_set_timing.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_batch_set_groups.argtypes = [C.c_void_p, C.c_int32]
         L.lego_test_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int32, C.c_int32]
         L.lego_test_libm.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_int32, C.c_int32]
         _lib = L
@@ -158,6 +159,10 @@ class Batch:
 
     def set_timing(self, on=True):
         _check(lib().lego_batch_set_timing(self.h, 1 if on else 0), "lego_batch_set_timing")
+
+    def set_groups(self, groups):
+        """Launch the streams as `groups` slices on separate HIP streams (overlapping kernel tails)."""
+        _check(lib().lego_batch_set_groups(self.h, int(groups)), "lego_batch_set_groups")
 
     def stage_times(self):
         ms = (C.c_float * 6)()

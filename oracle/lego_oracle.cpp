@@ -29,6 +29,8 @@
 #include <cstdint>
 #include <cstring>
 #include <functional>
+#include <cstdlib>
+#include <cstdio>
 #include <limits>
 #include <vector>
 
@@ -337,6 +339,14 @@ int voxel_grid(const std::vector<Pt>& in, float leaf, std::vector<Pt>& out) {
     e.idx = static_cast<unsigned int>(idx);
     e.cloud_point_index = (unsigned int)i;
     iv.push_back(e);
+  }
+  if (const char* dump = std::getenv("LEGO_ORACLE_DUMP_VOXEL_KEYS")) {  // diagnostics: raw keys per call
+    if (FILE* f = std::fopen(dump, "ab")) {
+      const uint32_t n = (uint32_t)iv.size();
+      std::fwrite(&n, 4, 1, f);
+      for (const auto& e : iv) std::fwrite(&e.idx, 4, 1, f);
+      std::fclose(f);
+    }
   }
   std::sort(iv.begin(), iv.end(), std::less<cloud_point_index_idx>());
   unsigned int index = 0;

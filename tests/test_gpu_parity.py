@@ -201,8 +201,10 @@ def test_injected_projection_lm_parity(gpu):
         np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
 
 
-def test_batch_streams_match_oracle(gpu):
-    """The batched engine (S sequences, one launch per stage) equals S independent oracle runs."""
+@pytest.mark.parametrize("groups", [1, 3])
+def test_batch_streams_match_oracle(gpu, groups):
+    """The batched engine (S sequences, one launch per stage, optionally as `groups` slices on their
+    own HIP streams) equals S independent oracle runs."""
     import torch
     params = L.params_vlp16()
     cfg = A.synth_cfg("vlp16")
@@ -215,6 +217,8 @@ def test_batch_streams_match_oracle(gpu):
     offs = torch.from_numpy((np.arange(S * steps, dtype=np.int64) * cap).reshape(steps, S)).cuda()
     cnts = torch.from_numpy(cnt.reshape(steps, S).astype(np.int32)).cuda()
     b = L.Batch(params, S, cap)
+    if groups > 1:
+        b.set_groups(groups)
     oracles = [oracle_for(params) for _ in range(S)]
     for k in range(steps):
         b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), torch.cuda.current_stream().cuda_stream)

@@ -57,8 +57,7 @@ def main():
             prof[192 + i]))
 
 
-    print("heap sorts %d, stream partitions %d (mean length %.0f), register partitions %d  per step" % (
-        prof[24] / nsteps, prof[25] / nsteps, prof[27] / max(prof[25], 1), prof[26] / nsteps))
+    print("heap-sort fallbacks %d per step" % (prof[24] / nsteps))
     V = 16
     print("per-ring extract wave cycles (mean / max over streams), ring 63 = first pass:")
     for r in list(range(V)) + [63]:
