@@ -181,6 +181,8 @@ int  lego_test_sort(uint32_t* keys, int32_t* vals, int32_t n, int32_t is_float);
 /* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
  * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */
 int  lego_debug_prof(uint64_t* out256, int32_t reset);
+/* Kernel time of `blocks` concurrent one-wave copies of the device sort of h_keys (profile build). */
+int  lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, float* ms);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,9 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "../../include/lego_frontend.h"
 #include "lego_device.h"
 #include "lego_introsort.h"
@@ -28,14 +31,17 @@ using namespace lg;
 
 // ---- diagnostic phase timers (build with -DLG_PROFILE; never in the shipped library) -----------
 #ifdef LG_PROFILE
-__device__ unsigned long long g_prof[256];  // [0,32) phases; [64+r] / [128+r] per-ring sum / max
+// 256 logical slots ([0,32) phases, [64+r] / [128+r] per-ring sum / max, [192+i] phase max), each in
+// 64 copies picked by block index so that the timer atomics do not serialise on one address.
+__device__ unsigned long long g_prof[256 * 64];
+#define PROF_SLOT(i) g_prof[(size_t)(i) * 64 + (blockIdx.x & 63)]
 #define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(slot, t0)                                           \
   do {                                                               \
     if ((threadIdx.x & 63) == 0) {                                   \
       const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - (t0); \
-      atomicAdd(&g_prof[slot], dt_);                                 \
-      atomicMax(&g_prof[192 + (slot)], dt_);                         \
+      atomicAdd(&PROF_SLOT(slot), dt_);                              \
+      atomicMax(&PROF_SLOT(192 + (slot)), dt_);                      \
     }                                                                \
   } while (0)
 #else
@@ -621,7 +627,8 @@ LG_DEVICE void adjust_heap_pf(const SortView<K, V>& a, int first, int hole, int 
 
 // __partial_sort(first, last, last) = __make_heap + __sort_heap.  __make_heap sifts the parents
 // from (len-2)/2 down to 0; parents on one heap level have disjoint subtrees (and __push_heap stops
-// at `top`), so each level runs in parallel, deepest level first.  __sort_heap's pops are a chain.
+// at `top`), so each level runs in parallel, deepest level first.  __sort_heap's pops are a chain
+// (one lane; tools/sort_bench.py measured whole-wave and register-resident variants slower).
 template <typename K, typename V>
 LG_DEVICE void heap_sort_wave(const SortView<K, V>& a, int first, int last) {
   const int lane = lane_id();
@@ -634,7 +641,7 @@ LG_DEVICE void heap_sort_wave(const SortView<K, V>& a, int first, int last) {
       __syncthreads();
     }
   }
-  if (lane == 0) {
+  if (lane == 0) {  // __sort_heap
     int l = last;
     while (l - first > 1) {
       --l;
@@ -786,7 +793,7 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
         heap_sort_wave(a, first, last);
         PROF_ADD(7, t_hs0);
 #ifdef LG_PROFILE
-        if (lane == 0) atomicAdd(&g_prof[24], 1ull);
+        if (lane == 0) atomicAdd(&PROF_SLOT(24), 1ull);
 #endif
         break;
       }
@@ -996,7 +1003,7 @@ LG_DEVICE void sort_segment(ExtractLds& L, int n) {
     __syncthreads();
   } else {
 #ifdef LG_PROFILE
-    if (lane == 0) atomicAdd(&g_prof[14], 1ull);
+    if (lane == 0) atomicAdd(&PROF_SLOT(14), 1ull);
 #endif
     wave_std_sort<float, int>(key, val, n, L.blk, L.stk, L.tab);
   }
@@ -1233,8 +1240,8 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_
 #ifdef LG_PROFILE
     if (lane_id() == 0) {
       const unsigned long long dt = __builtin_amdgcn_s_memtime() - t_ring0;
-      atomicAdd(&g_prof[64 + (first_pass ? 63 : r)], dt);
-      atomicMax(&g_prof[128 + (first_pass ? 63 : r)], dt);
+      atomicAdd(&PROF_SLOT(64 + (first_pass ? 63 : r)), dt);
+      atomicMax(&PROF_SLOT(128 + (first_pass ? 63 : r)), dt);
     }
 #endif
     if (lane_id() == 0) {
@@ -2185,12 +2192,60 @@ extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int3
   return rc;
 }
 
+#ifdef LG_PROFILE
+__global__ __launch_bounds__(64) void k_sort_bench(const unsigned* keys, int n, unsigned* out) {
+  __shared__ ExtractLds L;
+  const int lane = lane_id();
+  for (int i = lane; i < n; i += 64) { L.u.vkey[i] = keys[i]; L.vval[i] = (uint16_t)i; }
+  __syncthreads();
+  wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
+  if (lane == 0) out[blockIdx.x] = L.vval[n / 2];
+}
+#endif
+
+// Diagnostics (profile build only): time `blocks` concurrent copies of one device sort.
+extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, float* ms) {
+#ifdef LG_PROFILE
+  unsigned *k = nullptr, *o = nullptr;
+  if (n < 1 || n > RING_MAX || blocks < 1) return LEGO_EINVAL;
+  hipMalloc((void**)&k, n * 4);
+  hipMalloc((void**)&o, blocks * 4);
+  hipMemcpy(k, h_keys, n * 4, hipMemcpyHostToDevice);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
+  hipEventRecord(a, 0);
+  hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
+  hipEventRecord(b, 0);
+  hipEventSynchronize(b);
+  hipEventElapsedTime(ms, a, b);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  hipFree(k);
+  hipFree(o);
+  return LEGO_OK;
+#else
+  (void)h_keys; (void)n; (void)blocks; (void)ms;
+  return LEGO_ENOTSUP;
+#endif
+}
+
 extern "C" int lego_debug_prof(uint64_t* out32, int32_t reset) {
 #ifdef LG_PROFILE
-  if (out32 && hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(uint64_t) * 256) != hipSuccess) return LEGO_EDEVICE;
+  std::vector<uint64_t> h(256 * 64, 0);
+  if (out32) {
+    if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_prof), sizeof(uint64_t) * h.size()) != hipSuccess) return LEGO_EDEVICE;
+    for (int i = 0; i < 256; ++i) {
+      const bool is_max = (i >= 128 && i < 192) || i >= 192;
+      uint64_t r = 0;
+      for (int c = 0; c < 64; ++c) r = is_max ? std::max(r, h[(size_t)i * 64 + c]) : r + h[(size_t)i * 64 + c];
+      out32[i] = r;
+    }
+  }
   if (reset) {
-    uint64_t z[256] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return LEGO_EDEVICE;
+    std::fill(h.begin(), h.end(), 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), h.data(), sizeof(uint64_t) * h.size()) != hipSuccess) return LEGO_EDEVICE;
   }
   return LEGO_OK;
 #else

@@ -143,9 +143,43 @@ LG_LIBM float asinf_g(float x) {
 }
 
 // sinf/cosf: double evaluation rounded once (glibc's own sinf/cosf differ on ~1e-3 of inputs;
-// they are used only inside the LM, which is parity-checked within 1e-4).
-LG_LIBM float sinf_g(float x) { return (float)sin((double)x); }
-LG_LIBM float cosf_g(float x) { return (float)cos((double)x); }
+// they are used only inside the LM, which is parity-checked within 1e-4).  For |x| <= pi/4 (every
+// LM angle in practice) a Taylor polynomial in double: truncation < 1e-19 relative, a few double
+// ulps of rounding, so the float result is the rounded true value except within ~1e-15 of a float
+// rounding boundary; larger |x| goes to the library's double sin/cos.
+LG_LIBM double sin_poly_d(double x) {
+  const double x2 = x * x;
+  double p = 1.0 / 355687428096000.0;
+  p = __builtin_fma(p, x2, -1.0 / 1307674368000.0);
+  p = __builtin_fma(p, x2, 1.0 / 6227020800.0);
+  p = __builtin_fma(p, x2, -1.0 / 39916800.0);
+  p = __builtin_fma(p, x2, 1.0 / 362880.0);
+  p = __builtin_fma(p, x2, -1.0 / 5040.0);
+  p = __builtin_fma(p, x2, 1.0 / 120.0);
+  p = __builtin_fma(p, x2, -1.0 / 6.0);
+  return __builtin_fma(x * x2, p, x);
+}
+LG_LIBM double cos_poly_d(double x) {
+  const double x2 = x * x;
+  double p = -1.0 / 6402373705728000.0;
+  p = __builtin_fma(p, x2, 1.0 / 20922789888000.0);
+  p = __builtin_fma(p, x2, -1.0 / 87178291200.0);
+  p = __builtin_fma(p, x2, 1.0 / 479001600.0);
+  p = __builtin_fma(p, x2, -1.0 / 3628800.0);
+  p = __builtin_fma(p, x2, 1.0 / 40320.0);
+  p = __builtin_fma(p, x2, -1.0 / 720.0);
+  p = __builtin_fma(p, x2, 1.0 / 24.0);
+  p = __builtin_fma(p, x2, -0.5);
+  return __builtin_fma(x2, p, 1.0);
+}
+LG_LIBM float sinf_g(float x) {
+  const double d = (double)x;
+  return (float)(__builtin_fabs(d) <= 0.78539816 ? sin_poly_d(d) : sin(d));
+}
+LG_LIBM float cosf_g(float x) {
+  const double d = (double)x;
+  return (float)(__builtin_fabs(d) <= 0.78539816 ? cos_poly_d(d) : cos(d));
+}
 
 LG_LIBM bool isfinite_f(float x) { return (fbits(x) & 0x7f800000u) != 0x7f800000u; }
 

@@ -211,6 +211,12 @@ def test_introsort_depth_limit_inputs(tmp_path):
     assert rc == 0, out
 
 
+def test_lm_trig_polynomial(tmp_path):
+    """The LM's sinf/cosf fast path equals float(sin(double x)) except in double-rounding corner cases."""
+    rc, out = _compile_and_run(os.path.join(REPO, "tests", "native", "trig_check.cpp"), str(tmp_path / "tc"), ["101"])
+    assert rc == 0, out
+
+
 def test_libm_restatement_matches_glibc(tmp_path):
     """asinf/atanf/atan2f restated for the device equal the host glibc bit for bit."""
     rc, out = _compile_and_run(os.path.join(REPO, "tests", "native", "libm_check.cpp"), str(tmp_path / "lc"),

@@ -1,0 +1,35 @@
+"""Diagnostic: kernel time of the device std::sort emulation on recorded voxel-key sets.
+
+  LEGO_FRONTEND_LIB=lego-loam-bor_amd/lego_amd/liblego_frontend_prof.so python tools/sort_bench.py
+
+tools/data/voxel_keys_heavy.npz holds VoxelGrid key sequences of single rings recorded from the CPU
+oracle on synthetic VLP-16 scans (c110 drives libstdc++'s introsort into a 1309-element heap-sort
+fallback; c10 is an ordinary ring).  Each set is sorted by 1 block (latency) and by 256*11 blocks
+(one per wave slot of the chip, throughput).
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "lego-loam-bor_amd"))
+import lego_amd as L  # noqa: E402
+
+
+def main():
+    lib = L.lib()
+    lib.lego_debug_sort_bench.argtypes = [C.POINTER(C.c_uint32), C.c_int32, C.c_int32, C.POINTER(C.c_float)]
+    d = np.load(os.path.join(REPO, "tools", "data", "voxel_keys_heavy.npz"))
+    for name in d.files:
+        k = np.ascontiguousarray(d[name].astype(np.uint32))
+        for blocks in (1, 256 * 11):
+            ms = C.c_float()
+            rc = lib.lego_debug_sort_bench(k.ctypes.data_as(C.POINTER(C.c_uint32)), len(k), blocks, C.byref(ms))
+            assert rc == 0, rc
+            print("%-5s n=%5d blocks=%5d  %.3f ms" % (name, len(k), blocks, ms.value))
+
+
+if __name__ == "__main__":
+    main()
