@@ -72,6 +72,25 @@ def cpu_baseline(params, cfg, pts, counts, budget_s):
             "ms_per_scan": round(1e3 * t_sum / max(n_scans, 1), 3)}
 
 
+def pmc_traffic(args, S, kernels):
+    """HBM bytes per launch of `kernels` from the committed rocprofv3 PMC summary of this workload
+    (profiles/*_pmc.json, written by tools/pmc_summarize.py from separate FETCH_SIZE / WRITE_SIZE
+    passes); None when no summary matches the workload."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        by_base = {k.split("<")[0]: v for k, v in d.get("kernels", {}).items()}  # k_project<true, 16> -> k_project
+        if d.get("streams") == S and d.get("workload") == args.kind and all(k in by_base for k in kernels):
+            best = (f, by_base)
+    if best is None:
+        return None, None
+    return int(sum(best[1][k]["hbm_bytes"] for k in kernels)), os.path.relpath(best[0], REPO)
+
+
 def main():
     args = parse()
     import torch
@@ -154,17 +173,30 @@ def main():
         step(k)
         if k >= W:
             stage += np.array(batch.stage_times())
+        if k == W + K - 1:
+            m_last = batch.counts()[:, 0].astype(np.float64)  # segmented-cloud sizes M of the last step
     stage /= K
     batch.set_timing(False)
     n_mean = float(host_cnt[W:].mean())
-    # algorithmic bytes of k_project per launch: read x,y,z,i of every point (16 B) and
-    # write the range image (4 B) + the full cloud cell (16 B) of every cell; S scans per launch.
+    # Algorithmic bytes, per launch of S scans:
+    #   projection  B_proj = 16 N + 20 V H  (read x,y,z,i of every point; write range + cloud cell of every cell)
+    #   smoothness  B_smooth = 22 M         (read range + colInd; write curvature, picked, label, sort key/index)
     b_proj = S * (16.0 * n_mean + 20.0 * cap)
-    proj_ms = stage[0]
-    achieved = b_proj / (proj_ms * 1e-3) / 1e9
-    roofline = {"kernel": "k_project", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "bytes_per_launch": int(b_proj), "launch_ms": round(proj_ms, 4)}
+    b_smooth = 22.0 * float(m_last.sum())
+    t_ms = stage[0] + stage[2]  # k_project + k_fa_prep
+    achieved = (b_proj + b_smooth) / (t_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args, S, ("k_project", "k_fa_prep"))
+    roofline = {"kernel": "k_project+k_fa_prep (projection+smoothness)", "bound": "hbm",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "bytes_per_launch": int(b_proj + b_smooth), "launch_ms": round(t_ms, 4),
+                "per_kernel": {"k_project": {"bytes": int(b_proj), "ms": round(stage[0], 4),
+                                             "GBps": round(b_proj / (stage[0] * 1e-3) / 1e9, 1)},
+                               "k_fa_prep": {"bytes": int(b_smooth), "ms": round(stage[2], 4),
+                                             "GBps": round(b_smooth / (stage[2] * 1e-3) / 1e9, 1)}},
+                "traffic_source": traffic_src,
+                "note": "%d scans per launch: working set below the 256 MiB Infinity Cache (cache-assisted)" % S
+                        if S < 2048 else "working set above the Infinity Cache"}
 
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K, "warmup": W,

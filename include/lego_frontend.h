@@ -158,6 +158,9 @@ int  lego_batch_sync(lego_batch* b);
 int  lego_batch_read(lego_batch* b, int32_t s, lego_projection_out* proj, lego_association_out* assoc);
 /* Poses of all streams: out[s*12 + 0..5] = transformCur, [6..11] = transformSum; status[s]. */
 int  lego_batch_read_poses(lego_batch* b, float* out, int32_t* status);
+/* Sizes of the last step per stream: out[s*7 + 0..6] = segmented, outlier, scan_msg, sharp,
+ * less sharp, flat, less flat point counts. */
+int  lego_batch_read_counts(lego_batch* b, int32_t* out);
 /* Reset every stream to the freshly constructed state (systemInitedLM = false, transforms 0). */
 int  lego_batch_reset(lego_batch* b);
 /* Kernel timing of the last step (ms, measured with hipEvents on the step's stream):

@@ -488,6 +488,22 @@ int lego_batch_read_poses(lego_batch* b, float* out, int32_t* status) {
   return LEGO_OK;
 }
 
+int lego_batch_read_counts(lego_batch* b, int32_t* out) {
+  if (!b || !out) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  std::vector<int32_t> c((size_t)b->S * CNT_N);
+  if (hipMemcpy(c.data(), b->B.counts, c.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return LEGO_EDEVICE;
+  for (int s = 0; s < b->S; ++s) {
+    const int32_t* k = &c[(size_t)s * CNT_N];
+    int32_t* o = out + (size_t)s * 7;
+    o[0] = k[CNT_M]; o[1] = k[CNT_OUTLIER]; o[2] = k[CNT_SCAN]; o[3] = k[CNT_SHARP];
+    o[4] = k[CNT_LSHARP]; o[5] = k[CNT_FLAT]; o[6] = k[CNT_LFLAT];
+  }
+  return LEGO_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // single-sequence drop-in
 // ---------------------------------------------------------------------------------------------

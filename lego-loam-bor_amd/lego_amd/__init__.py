@@ -53,6 +53,7 @@ def lib():
         L.lego_batch_stage_times.argtypes = [C.c_void_p, P(C.c_float)]
         L.lego_batch_set_timing.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_groups.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_batch_read_counts.argtypes = [C.c_void_p, P(C.c_int32)]
         L.lego_test_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int32, C.c_int32]
         L.lego_test_libm.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_int32, C.c_int32]
         _lib = L
@@ -163,6 +164,12 @@ class Batch:
     def set_groups(self, groups):
         """Launch the streams as `groups` slices on separate HIP streams (overlapping kernel tails)."""
         _check(lib().lego_batch_set_groups(self.h, int(groups)), "lego_batch_set_groups")
+
+    def counts(self):
+        """[S, 7] int32: segmented, outlier, scan_msg, sharp, less sharp, flat, less flat counts."""
+        out = np.zeros((self.S, 7), dtype=np.int32)
+        _check(lib().lego_batch_read_counts(self.h, out.ctypes.data_as(P(C.c_int32))), "lego_batch_read_counts")
+        return out
 
     def stage_times(self):
         ms = (C.c_float * 6)()
