@@ -200,6 +200,9 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   if (!b) return LEGO_ENOMEM;
   b->params = *p;
   b->P = derive(*p);
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
+  b->P.ncu = ncu;
   b->S = n_streams;
   b->max_points = max_points;
   b->device = device;

@@ -581,15 +581,42 @@ struct ExtractLds {  // 13.5 KB per wave -> 11 waves per CU
   int tab[128];                 // lane-pairing / stop-queue scratch of the partitions
 };
 
-// libstdc++ __adjust_heap (lego_introsort.h) on one lane; each level's two children are loaded
-// (key and value) before the choice, so a level of the sift-down costs one LDS round trip.
+// libstdc++ __adjust_heap (lego_introsort.h) on one lane.  LG_HEAP_LOOKAHEAD: the sift-down reads
+// both children and all four grandchildren (keys and values) in one go and takes two levels per LDS
+// round trip; otherwise one level (children prefetched).  The push-up is as in libstdc++.
 template <typename K, typename V>
 LG_DEVICE void adjust_heap_pf(const SortView<K, V>& a, int first, int hole, int len, K vk, V vv) {
   K* key = a.key + first;
   V* val = a.val + first;
   const int top = hole;
   int second = hole;
-  const int lim = (len - 1) / 2;
+  const int lim = (len - 1) / 2;  // nodes below lim have two children
+#ifdef LG_HEAP_LOOKAHEAD
+  while (second < lim) {
+    const int c = 2 * (second + 1);  // right child (left: c - 1)
+    const K kr = key[c], kl = key[c - 1];
+    const V vr = val[c], vl = val[c - 1];
+    const int gl = 2 * c, gr = 2 * (c + 1);
+    K kll = kl, klr = kl, krl = kr, krr = kr;
+    V vll = vl, vlr = vl, vrl = vr, vrr = vr;
+    if (c - 1 < lim) { klr = key[gl]; kll = key[gl - 1]; vlr = val[gl]; vll = val[gl - 1]; }
+    if (c < lim) { krr = key[gr]; krl = key[gr - 1]; vrr = val[gr]; vrl = val[gr - 1]; }
+    const bool left = kr < kl;
+    second = left ? c - 1 : c;
+    key[hole] = left ? kl : kr;
+    val[hole] = left ? vl : vr;
+    hole = second;
+    if (!(second < lim)) break;
+    const int c2 = 2 * (second + 1);
+    const K k2r = left ? klr : krr, k2l = left ? kll : krl;
+    const V v2r = left ? vlr : vrr, v2l = left ? vll : vrl;
+    const bool left2 = k2r < k2l;
+    second = left2 ? c2 - 1 : c2;
+    key[hole] = left2 ? k2l : k2r;
+    val[hole] = left2 ? v2l : v2r;
+    hole = second;
+  }
+#else
   if (second < lim) {
     int c = 2 * (second + 1);
     K kr = key[c], kl = key[c - 1];
@@ -608,6 +635,7 @@ LG_DEVICE void adjust_heap_pf(const SortView<K, V>& a, int first, int hole, int 
       vr = val[c]; vl = val[c - 1];
     }
   }
+#endif
   if ((len & 1) == 0 && second == (len - 2) / 2) {
     second = 2 * (second + 1);
     key[hole] = key[second - 1];
@@ -1202,8 +1230,13 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
 __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_pass) {
   __shared__ ExtractLds L;
   const int V = P.V, VH = P.VH;
-  const int s = P.s0 + (first_pass ? blockIdx.x : blockIdx.x / V);
-  const int ring = first_pass ? 0 : blockIdx.x % V;
+  // Workgroups reach the CUs round-robin, so with ring = blockIdx % V a CU would only ever see one
+  // ring index (the upper, non-ground rings are the heavy ones).  Rotating the ring by the stream
+  // block (s / (ncu / V)) gives every CU every ring index; the map stays a bijection per stream.
+  const int sl = first_pass ? blockIdx.x : blockIdx.x / V;
+  const int s = P.s0 + sl;
+  const int rot = sl / max(P.ncu / V, 1);
+  const int ring = first_pass ? 0 : (int)((blockIdx.x % V + rot) % V);
   const int32_t* rs = B.ring_start + (size_t)s * V;
   const int32_t* re = B.ring_end + (size_t)s * V;
   ScanView v;
