@@ -11,6 +11,12 @@ launch per stage for all of them (lego_batch_step).  Inputs of all W+K steps are
 host, uploaded, and resident in HBM before the timed region.  Each rank owns its own S sequences
 (weak scaling, no collective on the data path); after timing, the per-stream trajectories are
 all-gathered to rank 0 (RCCL), the only collective.  Rank 0 prints one JSON line.
+
+The measured path runs PCL VoxelGrid with voxel_tie_order = 1 (each voxel's points summed in point
+order) unless --voxel-tie-order 0 is given; order 0 reproduces the GCC/libstdc++-built reference bit
+for bit (its introsort tie order), and at N = 1 it is measured on the same inputs and reported as
+"other_voxel_tie_order".  Labels, feature indices and the 6-DoF transform meet the north_star bar in
+both orders (tests/test_gpu_parity.py).
 """
 import argparse
 import json
@@ -39,7 +45,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (test rehearsal)")
-    ap.add_argument("--groups", type=int, default=2, help="stream slices launched on separate HIP streams")
+    ap.add_argument("--groups", type=int, default=1, help="stream slices launched on separate HIP streams")
+    ap.add_argument("--voxel-tie-order", type=int, default=1, choices=[0, 1],
+                    help="lego_params.voxel_tie_order of the measured path: 1 = VoxelGrid sums each voxel in "
+                         "point order (stable); 0 = libstdc++ std::sort order, bit-identical to the GCC-built "
+                         "reference. At N=1 the other order is measured too and reported beside the value.")
+    ap.add_argument("--no-alt-order", action="store_true", help="skip measuring the other voxel_tie_order")
     return ap.parse_args()
 
 
@@ -109,7 +120,7 @@ def main():
     dev = torch.device("cuda", local_dev)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
-    params = L.params_vlp16() if args.kind == "vlp16" else L.params_hdl64()
+    params = (L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64)(voxel_tie_order=args.voxel_tie_order)
     cfg = A.synth_cfg(args.kind)
     V, H = params.num_vertical_scans, params.num_horizontal_scans
     cap = V * H
@@ -132,27 +143,32 @@ def main():
     batch.set_groups(args.groups)
     stream = torch.cuda.current_stream(dev)
 
-    def step(k):
-        batch.step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
+    def step(k, b=None):
+        (b or batch).step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
 
-    for k in range(W):
-        step(k)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(W, W + K):
-        step(k)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(b):
+        """W untimed warm-up steps, then exactly K timed steps between barrier + sync; max over ranks."""
+        for k in range(W):
+            step(k, b)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(W, W + K):
+            step(k, b)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    elapsed = timed(batch)
     poses, status = batch.poses()
     # trajectory gather: the path's only collective (SURVEY §8(e))
     traj = torch.from_numpy(poses).to(coll_dev)
@@ -164,6 +180,16 @@ def main():
         traj_all = traj
     total_scans = S * K * world
     value = total_scans / elapsed
+    alt = None
+    if world == 1 and not args.no_alt_order:  # the other VoxelGrid tie order, same inputs
+        alt_order = 1 - args.voxel_tie_order
+        params_alt = (L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64)(voxel_tie_order=alt_order)
+        batch_alt = L.Batch(params_alt, S, cap, device=local_dev)
+        batch_alt.set_groups(args.groups)
+        el_alt = timed(batch_alt)
+        batch_alt.close()
+        alt = {"voxel_tie_order": alt_order, "value": round(total_scans / el_alt, 1),
+               "ms_per_step": round(1e3 * el_alt / K, 3)}
 
     # ---- per-stage kernel times (hipEvents on the launch stream), re-running the timed steps ------
     batch.reset()
@@ -205,16 +231,19 @@ def main():
         "config": {"workload": "C3: batched synthetic %s sweeps, %d independent sequences per GPU x 1 scan per step"
                                % (args.kind.upper(), S),
                    "V": V, "H": H, "points_per_scan": round(n_mean, 1), "streams_per_gpu": S,
-                   "parallelism": "sequence-sharded x%d" % world, "stream_groups": args.groups},
+                   "parallelism": "sequence-sharded x%d" % world, "stream_groups": args.groups,
+                   "voxel_tie_order": args.voxel_tie_order},
         "roofline": roofline,
         "stages_ms": {"project": round(stage[0], 4), "segment": round(stage[1], 4), "fa_prep": round(stage[2], 4),
                       "extract": round(stage[3], 4), "concat": round(stage[4], 4), "lm": round(stage[5], 4)},
+        "other_voxel_tie_order": alt,
         "lm_status_bits": int(np.bitwise_or.reduce(status)),
         "trajectories_gathered": int(traj_all.shape[0]),
         "input_gen_s": round(t_gen, 2),
     }
-    if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(params, cfg, host_pts, host_cnt, args.cpu_seconds)
+    if rank == 0 and not args.no_cpu_baseline:  # the reference's own VoxelGrid order (std::sort)
+        params_ref = (L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64)(voxel_tie_order=0)
+        out["cpu_baseline"] = cpu_baseline(params_ref, cfg, host_pts, host_cnt, args.cpu_seconds)
         out["speedup_vs_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)

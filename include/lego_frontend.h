@@ -67,6 +67,14 @@ typedef struct lego_params {
   int32_t fp_mode;                         /* libm overload model: 0 = float
                                               overloads of unqualified sin/cos/atan2 (only mode
                                               implemented), 1 = double promotion (LEGO_ENOTSUP)  */
+  int32_t voxel_tie_order;                 /* order in which PCL VoxelGrid sums the points of one
+                                              voxel (featureAssociation.cpp:377-379): PCL sorts
+                                              (voxel, point) pairs with std::sort by voxel only, so
+                                              the order is the C++ library's.  0 = libstdc++'s
+                                              introsort, emulated exactly (the reference as built
+                                              with GCC); 1 = ascending point order (std::stable_sort;
+                                              faster: no introsort emulation).  Centroids can differ
+                                              in the last bits; voxel set, count and order do not. */
 } lego_params;
 
 /* pcl::PointXYZI payload (utility.h:46); 16 B, the device layout of every cloud. */

@@ -31,6 +31,7 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int cap_sharp, cap_lsharp, cap_flat;  // per-ring caps: 12, 120, 24
   int s0;                               // first stream of the launch (stream groups; 0 otherwise)
   int ncu;                              // compute units of the device (k_extract's ring rotation)
+  int voxel_stable;                     // lego_params.voxel_tie_order == 1
 };
 
 struct LgState {  // FeatureAssociation members that persist across scans (featureAssociation.h)

@@ -60,6 +60,7 @@ LgParams derive(const lego_params& p) {
   float nd = p.nearest_feature_search_distance;
   P.nn_dist_sqr = nd * nd;
   P.map_div = p.mapping_frequency_divider;
+  P.voxel_stable = p.voxel_tie_order == 1;
   P.cap_sharp = 12;   // 2 per segment x 6 (fa.cpp:295)
   P.cap_lsharp = 120; // 20 per segment x 6 (fa.cpp:299)
   P.cap_flat = 24;    // 4 per segment x 6 (fa.cpp:340)
@@ -158,6 +159,7 @@ void lego_params_vlp16(lego_params* p) {  // LeGO-LOAM/config/loam_config.yaml
   p->nearest_feature_search_distance = 5.f;
   p->mapping_frequency_divider = 5;
   p->fp_mode = 0;
+  p->voxel_tie_order = 0;
 }
 
 void lego_params_hdl64(lego_params* p) {
@@ -172,6 +174,7 @@ void lego_params_hdl64(lego_params* p) {
 int lego_params_validate(const lego_params* p) {
   if (!p) return LEGO_EINVAL;
   if (p->fp_mode != 0) return LEGO_ENOTSUP;
+  if (p->voxel_tie_order != 0 && p->voxel_tie_order != 1) return LEGO_EINVAL;
   if (p->num_vertical_scans < 2 || p->num_vertical_scans > 64) return LEGO_EINVAL;
   if (p->num_horizontal_scans < 16 || p->num_horizontal_scans > 2048) return LEGO_EINVAL;
   if (p->ground_scan_index < 0 || p->ground_scan_index >= p->num_vertical_scans) return LEGO_EINVAL;

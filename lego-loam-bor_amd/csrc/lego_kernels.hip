@@ -317,6 +317,46 @@ LG_DEVICE void uf_unite(PT parent, int a, int b) {
   } while (!done);
 }
 
+// Raster-order compaction without block-wide scans: wave w owns the contiguous cells
+// [w*L, w*L + L) (L a multiple of 64; one ring per wave for VLP-16), counts its two predicates with
+// ballots, publishes the totals in wt[] (2 * waves ints of LDS), and after one barrier knows its
+// exclusive offsets.  pred(c, p1, p2) is evaluated twice (count pass, then emit pass);
+// emit(c, p1, p2, k1, k2) gets the raster-order output positions.  Returns the two totals.
+template <typename Pred, typename Emit>
+LG_DEVICE int2 wave_raster_compact(int n, int* wt, Pred pred, Emit emit) {
+  const int lane = lane_id(), w = wave_id(), nw = (int)(blockDim.x >> 6);
+  const int L = ((n + nw - 1) / nw + 63) & ~63;
+  const int lo = min(w * L, n), hi = min(lo + L, n);
+  int c1 = 0, c2 = 0;
+  for (int base = lo; base < hi; base += 64) {
+    const int c = base + lane;
+    bool p1 = false, p2 = false;
+    if (c < hi) pred(c, p1, p2);
+    c1 += __popcll(__ballot(p1));
+    c2 += __popcll(__ballot(p2));
+  }
+  if (lane == 0) { wt[w] = c1; wt[nw + w] = c2; }
+  __syncthreads();
+  int o1 = 0, o2 = 0, t1 = 0, t2 = 0;
+  for (int k = 0; k < nw; ++k) {
+    const int a = wt[k], b = wt[nw + k];
+    if (k < w) { o1 += a; o2 += b; }
+    t1 += a;
+    t2 += b;
+  }
+  for (int base = lo; base < hi; base += 64) {
+    const int c = base + lane;
+    bool p1 = false, p2 = false;
+    if (c < hi) pred(c, p1, p2);
+    const unsigned long long m1 = __ballot(p1), m2 = __ballot(p2);
+    if (c < hi) emit(c, p1, p2, o1 + popc_below(m1), o2 + popc_below(m2));
+    o1 += __popcll(m1);
+    o2 += __popcll(m2);
+  }
+  __syncthreads();  // wt[] reusable, emits visible block-wide
+  return make_int2(t1, t2);
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
@@ -330,8 +370,11 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
   int32_t* label = B.label + (size_t)s * VH;
   auto eligible = [&](int c) { return ground[c] != 1 && range[c] != FLT_MAX; };  // _label_mat == 0
 
+  PROF_T(t_s0);
   for (int c = tid; c < VH; c += nt) parent[c] = eligible(c) ? c : -1;
   __syncthreads();
+  PROF_ADD(25, t_s0);
+  PROF_T(t_s1);
   for (int c = tid; c < VH; c += nt) {
     if (parent[c] < 0) continue;
     const int i = c / H, j = c - i * H;
@@ -344,9 +387,13 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
     }
   }
   __syncthreads();
+  PROF_ADD(26, t_s1);
+  PROF_T(t_s2);
   for (int c = tid; c < VH; c += nt)
     if (parent[c] >= 0) parent[c] = uf_find(parent, c);
   __syncthreads();
+  PROF_ADD(27, t_s2);
+  PROF_T(t_s3);
 
   // ---- per-root size and row mask (rows of non-seed members) ----
   if constexpr (kLds) {
@@ -363,23 +410,21 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
       if (r != c) atomicOr(&agg[r], 1u << (16 + c / H));
     }
     __syncthreads();
-    int running = 0;
-    for (int base = 0; base < VH; base += nt) {
-      const int c = base + tid;
-      bool feas = false, isroot = false;
-      if (c < VH && label[c] == c) {
-        isroot = true;
-        const unsigned a = agg[c];
-        const int cnt = (int)(a & 0xffffu);
-        const int lines = __popc(a >> 16);
-        feas = cnt >= 30 || (cnt >= P.seg_valid_pt && lines >= P.seg_valid_line);
-      }
-      int ex, ex2, tot, tot2;
-      block_scan2(feas, false, scratch, ex, ex2, tot, tot2);
-      if (isroot) agg[c] = feas ? (unsigned)(running + ex + 1) : 999999u;
-      running += tot;
-    }
-    __syncthreads();
+    // feasible roots numbered in raster order of their seed (= the BFS's _label_count++)
+    wave_raster_compact(
+        VH, scratch,
+        [&](int c, bool& feas, bool& isroot) {
+          isroot = label[c] == c;
+          if (isroot) {
+            const unsigned a = agg[c];
+            const int cnt = (int)(a & 0xffffu);
+            const int lines = __popc(a >> 16);
+            feas = cnt >= 30 || (cnt >= P.seg_valid_pt && lines >= P.seg_valid_line);
+          }
+        },
+        [&](int c, bool feas, bool isroot, int k, int) {
+          if (isroot) agg[c] = feas ? (unsigned)(k + 1) : 999999u;
+        });
     for (int c = tid; c < VH; c += nt) {
       const int r = label[c];
       label[c] = (r < 0) ? -1 : (int)agg[r];
@@ -396,28 +441,27 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
       if (r != c) atomicOr(&msk[r], 1ull << (c / H));
     }
     __syncthreads();
-    int running = 0;
-    for (int base = 0; base < VH; base += nt) {
-      const int c = base + tid;
-      bool feas = false, isroot = false;
-      if (c < VH && parent[c] == c) {
-        isroot = true;
-        const int n = cnt[c];
-        const int lines = __popcll(msk[c]);
-        feas = n >= 30 || (n >= P.seg_valid_pt && lines >= P.seg_valid_line);
-      }
-      int ex, ex2, tot, tot2;
-      block_scan2(feas, false, scratch, ex, ex2, tot, tot2);
-      if (isroot) cnt[c] = feas ? running + ex + 1 : 999999;
-      running += tot;
-    }
-    __syncthreads();
+    wave_raster_compact(
+        VH, scratch,
+        [&](int c, bool& feas, bool& isroot) {
+          isroot = parent[c] == c;
+          if (isroot) {
+            const int n = cnt[c];
+            const int lines = __popcll(msk[c]);
+            feas = n >= 30 || (n >= P.seg_valid_pt && lines >= P.seg_valid_line);
+          }
+        },
+        [&](int c, bool feas, bool isroot, int k, int) {
+          if (isroot) cnt[c] = feas ? k + 1 : 999999;
+        });
     for (int c = tid; c < VH; c += nt) {
       const int r = parent[c];
       label[c] = (r < 0) ? -1 : cnt[r];
     }
   }
   __syncthreads();
+  PROF_ADD(28, t_s3);
+  PROF_T(t_s4);
 
   // ---- cloudSegmentation extraction (:358-396): raster-order compaction ----
   float4* seg_pts = B.seg_pts + (size_t)s * VH;
@@ -427,54 +471,36 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
   float4* outlier = B.outlier + (size_t)s * VH;
   int32_t* ring_start = B.ring_start + (size_t)s * V;
   int32_t* ring_end = B.ring_end + (size_t)s * V;
-  int nseg = 0, nout = 0;
-  for (int base = 0; base < VH; base += nt) {
-    const int c = base + tid;
-    bool pseg = false, pout = false;
-    int i = 0, j = 0, g = 0, lab = 0;
-    if (c < VH) {
-      i = c / H;
-      j = c - i * H;
-      lab = label[c];
-      g = ground[c];
-      if (lab > 0 || g == 1) {
-        if (lab == 999999) {
-          pout = (i > G && j % 5 == 0);
-        } else if (!(g == 1 && (j % 5 != 0 && j > 5 && j < H - 5))) {
-          pseg = true;
-        }
-      }
+  auto cls = [&](int c, bool& pseg, bool& pout) {
+    const int i = c / H, j = c - i * H;
+    const int lab = label[c], g = ground[c];
+    if (lab > 0 || g == 1) {
+      if (lab == 999999) pout = (i > G && j % 5 == 0);
+      else if (!(g == 1 && (j % 5 != 0 && j > 5 && j < H - 5))) pseg = true;
     }
-    int e1, e2, t1, t2;
-    block_scan2(pseg, pout, scratch, e1, e2, t1, t2);
-    if (c < VH && j == 0) {
-      ring_start[i] = nseg + e1 - 1 + 5;
-      if (i > 0) ring_end[i - 1] = nseg + e1 - 1 - 5;
+  };
+  const int2 tot = wave_raster_compact(VH, scratch, cls, [&](int c, bool pseg, bool pout, int k1, int k2) {
+    const int i = c / H, j = c - i * H;
+    if (j == 0) {  // k1 = segmented points before this ring
+      ring_start[i] = k1 - 1 + 5;
+      if (i > 0) ring_end[i - 1] = k1 - 1 - 5;
     }
     if (pseg) {
-      const int k = nseg + e1;
-      seg_pts[k] = cloud[c];
-      seg_range[k] = range[c];
-      seg_col[k] = (uint32_t)j;
-      seg_ground[k] = (uint8_t)(g == 1);
+      seg_pts[k1] = cloud[c];
+      seg_range[k1] = range[c];
+      seg_col[k1] = (uint32_t)j;
+      seg_ground[k1] = (uint8_t)(ground[c] == 1);
     }
-    if (pout) outlier[nout + e2] = cloud[c];
-    nseg += t1;
-    nout += t2;
-  }
+    if (pout) outlier[k2] = cloud[c];
+  });
+  const int nseg = tot.x, nout = tot.y;
   if (tid == 0) ring_end[V - 1] = nseg - 1 - 5;
   // 2-D scan compaction (column order)
-  int nscan = 0;
   const int32_t* cand = B.scan_cand + (size_t)s * H;
   float4* scan = B.scan_msg + (size_t)s * H;
-  for (int base = 0; base < H; base += nt) {
-    const int j = base + tid;
-    const int cd = (j < H) ? cand[j] : -1;
-    int e1, e2, t1, t2;
-    block_scan2(cd >= 0, false, scratch, e1, e2, t1, t2);
-    if (cd >= 0) scan[nscan + e1] = cloud[cd];
-    nscan += t1;
-  }
+  const int nscan = wave_raster_compact(H, scratch, [&](int j, bool& p, bool&) { p = cand[j] >= 0; },
+                                        [&](int j, bool p, bool, int k, int) { if (p) scan[k] = cloud[cand[j]]; }).x;
+  PROF_ADD(29, t_s4);
   if (tid == 0) {
     int32_t* cnt = B.counts + (size_t)s * CNT_N;
     cnt[CNT_M] = nseg;
@@ -581,9 +607,9 @@ struct ExtractLds {  // 13.5 KB per wave -> 11 waves per CU
   int tab[128];                 // lane-pairing / stop-queue scratch of the partitions
 };
 
-// libstdc++ __adjust_heap (lego_introsort.h) on one lane.  LG_HEAP_LOOKAHEAD: the sift-down reads
-// both children and all four grandchildren (keys and values) in one go and takes two levels per LDS
-// round trip; otherwise one level (children prefetched).  The push-up is as in libstdc++.
+// libstdc++ __adjust_heap (lego_introsort.h) on one lane, each level's two children (key and value)
+// loaded before the choice.  (Reading the grandchildren too, two levels per round trip, measured
+// 1.4x slower in tools/sort_bench.py: the extra LDS reads cost more than the latency they hide.)
 template <typename K, typename V>
 LG_DEVICE void adjust_heap_pf(const SortView<K, V>& a, int first, int hole, int len, K vk, V vv) {
   K* key = a.key + first;
@@ -591,32 +617,6 @@ LG_DEVICE void adjust_heap_pf(const SortView<K, V>& a, int first, int hole, int 
   const int top = hole;
   int second = hole;
   const int lim = (len - 1) / 2;  // nodes below lim have two children
-#ifdef LG_HEAP_LOOKAHEAD
-  while (second < lim) {
-    const int c = 2 * (second + 1);  // right child (left: c - 1)
-    const K kr = key[c], kl = key[c - 1];
-    const V vr = val[c], vl = val[c - 1];
-    const int gl = 2 * c, gr = 2 * (c + 1);
-    K kll = kl, klr = kl, krl = kr, krr = kr;
-    V vll = vl, vlr = vl, vrl = vr, vrr = vr;
-    if (c - 1 < lim) { klr = key[gl]; kll = key[gl - 1]; vlr = val[gl]; vll = val[gl - 1]; }
-    if (c < lim) { krr = key[gr]; krl = key[gr - 1]; vrr = val[gr]; vrl = val[gr - 1]; }
-    const bool left = kr < kl;
-    second = left ? c - 1 : c;
-    key[hole] = left ? kl : kr;
-    val[hole] = left ? vl : vr;
-    hole = second;
-    if (!(second < lim)) break;
-    const int c2 = 2 * (second + 1);
-    const K k2r = left ? klr : krr, k2l = left ? kll : krl;
-    const V v2r = left ? vlr : vrr, v2l = left ? vll : vrl;
-    const bool left2 = k2r < k2l;
-    second = left2 ? c2 - 1 : c2;
-    key[hole] = left2 ? k2l : k2r;
-    val[hole] = left2 ? v2l : v2r;
-    hole = second;
-  }
-#else
   if (second < lim) {
     int c = 2 * (second + 1);
     K kr = key[c], kl = key[c - 1];
@@ -635,7 +635,6 @@ LG_DEVICE void adjust_heap_pf(const SortView<K, V>& a, int first, int hole, int 
       vr = val[c]; vl = val[c - 1];
     }
   }
-#endif
   if ((len & 1) == 0 && second == (len - 2) / 2) {
     second = 2 * (second + 1);
     key[hole] = key[second - 1];
@@ -1053,7 +1052,35 @@ LG_DEVICE float4 seg_point(const ScanView& v, int ind, int& status) {  // segmen
 }
 
 // PCL VoxelGrid<PointXYZI> (leaf 0.2) over the ring's lessFlat points (positions in L.vval[0..n)).
-LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, int base_pos, RingOut& o) {
+// Ascending sort of n <= RING_MAX (key, val) pairs by (key, val), one wave, bitonic network in LDS.
+// vals are distinct ring positions appended in point order, so this is the order std::stable_sort
+// gives by key alone (lego_params.voxel_tie_order == 1).
+LG_DEVICE void wave_bitonic_kv(unsigned* key, uint16_t* val, int n) {
+  const int lane = lane_id();
+  int N = 1;
+  while (N < n) N <<= 1;
+  for (int i = n + lane; i < N; i += 64) { key[i] = 0xffffffffu; val[i] = 0xffffu; }  // sort last
+  __syncthreads();
+  for (int k = 2; k <= N; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int lj = __ffs(j) - 1;
+      for (int p = lane; p < (N >> 1); p += 64) {
+        const int i = ((p >> lj) << (lj + 1)) | (p & (j - 1));
+        const int l = i | j;
+        const unsigned ki = key[i], kl = key[l];
+        const uint16_t vi = val[i], vl = val[l];
+        const bool gt = ki > kl || (ki == kl && vi > vl);
+        if (gt == ((i & k) == 0)) {
+          key[i] = kl; key[l] = ki;
+          val[i] = vl; val[l] = vi;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, int n, int base_pos, RingOut& o) {
   const float4* fa = v.fa + base_pos;  // L.vval holds positions relative to the ring start
   const int lane = lane_id();
   o.nLF = 0;
@@ -1090,7 +1117,8 @@ LG_DEVICE void voxel_ring(const ScanView& v, ExtractLds& L, int n, int base_pos,
   }
   __syncthreads();
   PROF_T(t_vs0);
-  wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
+  if (P.voxel_stable) wave_bitonic_kv(L.u.vkey, L.vval, n);
+  else wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
   PROF_ADD(5, t_vs0);
   int running = 0;
   for (int base = 0; base < n; base += 64) {
@@ -1223,7 +1251,7 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
     PROF_ADD(3, t_lf0);
   }
   PROF_T(t_vox0);
-  voxel_ring(v, L, nlist, st, o);
+  voxel_ring(P, v, L, nlist, st, o);
   PROF_ADD(4, t_vox0);
 }
 

@@ -45,6 +45,7 @@ class LegoParams(C.Structure):
         ("nearest_feature_search_distance", C.c_float),
         ("mapping_frequency_divider", C.c_int32),
         ("fp_mode", C.c_int32),
+        ("voxel_tie_order", C.c_int32),
     ]
 
 

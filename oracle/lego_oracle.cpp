@@ -301,7 +301,7 @@ struct cloud_point_index_idx {
   bool operator<(const cloud_point_index_idx& p) const { return (idx < p.idx); }
 };
 
-int voxel_grid(const std::vector<Pt>& in, float leaf, std::vector<Pt>& out) {
+int voxel_grid(const std::vector<Pt>& in, float leaf, std::vector<Pt>& out, bool stable) {
   out.clear();
   const float inv = 1.0f / leaf;  // inverse_leaf_size_ = Array4f::Ones() / leaf_size_
   // getMinMax3D (dense path): min/max of x,y,z
@@ -348,7 +348,10 @@ int voxel_grid(const std::vector<Pt>& in, float leaf, std::vector<Pt>& out) {
       std::fclose(f);
     }
   }
-  std::sort(iv.begin(), iv.end(), std::less<cloud_point_index_idx>());
+  if (stable)  // lego_params.voxel_tie_order == 1
+    std::stable_sort(iv.begin(), iv.end(), std::less<cloud_point_index_idx>());
+  else
+    std::sort(iv.begin(), iv.end(), std::less<cloud_point_index_idx>());
   unsigned int index = 0;
   while (index < iv.size()) {
     unsigned int i = index + 1;
@@ -521,6 +524,8 @@ struct FeatureAssociation {
   int iters_surf = 0, iters_corner = 0;
   double quat[4] = {0, 0, 0, 1}, pos[3] = {0, 0, 0};
 
+  bool voxel_stable = false;  // lego_params.voxel_tie_order == 1 (std::stable_sort in VoxelGrid)
+
   explicit FeatureAssociation(const lego_params& p) {  // ctor :69-84 + initializationValue :96-157
     V = p.num_vertical_scans;
     H = p.num_horizontal_scans;
@@ -528,6 +533,7 @@ struct FeatureAssociation {
     edge_thr = p.edge_threshold;
     surf_thr = p.surf_threshold;
     map_div = p.mapping_frequency_divider;
+    voxel_stable = p.voxel_tie_order == 1;
     float nearest_dist = p.nearest_feature_search_distance;
     nn_dist_sqr = nearest_dist * nearest_dist;
     const size_t n = (size_t)V * H;
@@ -668,7 +674,7 @@ struct FeatureAssociation {
         for (int k = sp; k <= ep; k++)
           if (cloudLabel[k] <= 0) less_flat_scan.push_back(seg_point(k));
       }
-      status |= voxel_grid(less_flat_scan, 0.2f, less_flat_scan_ds);
+      status |= voxel_grid(less_flat_scan, 0.2f, less_flat_scan_ds, voxel_stable);
       less_flat.insert(less_flat.end(), less_flat_scan_ds.begin(), less_flat_scan_ds.end());
     }
   }

@@ -47,10 +47,19 @@ def test_params_and_validation():
     assert L.lib().lego_params_validate(C.byref(q)) == A.LEGO_EINVAL
 
 
-def test_struct_layouts_match_header():
-    # 16-byte lego_point (pcl::PointXYZI payload) and the params POD
-    assert C.sizeof(A.LegoPoint) == 16
-    assert C.sizeof(A.LegoParams) == 15 * 4
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors have the C header's sizes (compiled with the host C compiler)."""
+    import subprocess
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "lego_frontend.h"\nint main(void){printf("%zu %zu %zu %zu",'
+                   'sizeof(lego_params), sizeof(lego_point), sizeof(lego_projection_out), sizeof(lego_association_out));'
+                   'return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I" + os.path.join(REPO, "include"), str(src), "-o", str(exe)])
+    sizes = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert sizes == [C.sizeof(A.LegoParams), C.sizeof(A.LegoPoint), C.sizeof(A.LegoProjectionOut),
+                     C.sizeof(A.LegoAssociationOut)]
+    assert sizes[1] == 16  # pcl::PointXYZI payload
 
 
 def test_no_cpu_fallback_without_device():

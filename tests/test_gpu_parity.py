@@ -148,6 +148,36 @@ def test_vlp16_sequence_parity(gpu, seq):
         assert_scan_parity(*row)
 
 
+@pytest.mark.parametrize("seq", [0, 21])
+def test_voxel_stable_order_parity(gpu, seq):
+    """voxel_tie_order = 1 (VoxelGrid sums each voxel in point order, std::stable_sort) equals the oracle
+    in the same mode bit for bit."""
+    params = L.params_vlp16(voxel_tie_order=1)
+    cfg = A.synth_cfg("vlp16")
+    for row in run_pair(params, cfg, seq, 8):
+        assert_scan_parity(*row)
+
+
+def test_voxel_stable_order_meets_north_star_bar(gpu):
+    """voxel_tie_order = 1 against the reference's own tie order (oracle, libstdc++ std::sort): labels
+    and feature indices bit-exact, 6-DoF transform within 1e-4 (north_star); less-flat centroids may
+    differ in the last bits only (float sums of one voxel in another order)."""
+    cfg = A.synth_cfg("vlp16", range_noise=0.0, az_jitter_deg=0.0, roll_pitch_noise_deg=0.0)
+    fe = L.Frontend(L.params_vlp16(voxel_tie_order=1))
+    orc = oracle_for(L.params_vlp16())
+    for k in range(8):
+        pts = A.synth_scan(cfg, 3, k)
+        pg, pr = fe.cloud_handler(pts), orc.cloud_handler(pts)
+        fg, fr = fe.feature_association(), orc.feature_association()
+        assert not Hs.diff_report(Hs.PROJ_KEYS, pg, pr), k
+        assert not Hs.diff_report(["sharp_ind", "less_sharp_ind", "flat_ind", "sharp", "less_sharp", "flat"], fg, fr), k
+        assert fg["less_flat"].shape == fr["less_flat"].shape, k
+        np.testing.assert_allclose(fg["less_flat"], fr["less_flat"], rtol=1e-6, atol=1e-5)
+        np.testing.assert_allclose(fg["transform_cur"], fr["transform_cur"], atol=Hs.TF_TOL, rtol=0)
+        np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
+    fe.close()
+
+
 def test_vlp16_noise_free_ties(gpu):
     """Noise-free sweeps make exact curvature / voxel-index ties common: the introsort emulation
     must give the reference's std::sort permutation."""

@@ -21,7 +21,8 @@ NAMES = {0: "x:load+sort seg", 1: "x:sharp greedy", 2: "x:flat greedy", 3: "x:le
          5: "x:voxel sort", 6: "  sort:wave partitions", 7: "  sort:heap fallback", 11: "  sort:final insertion",
          12: "  seg: global load", 13: "  seg: sort", 8: "lm:transform sel", 9: "lm:search", 10: "lm:coeff+reduce",
          15: "lm:solve (thread 0)", 16: "lm:build grid", 17: "lm:surf loop", 18: "lm:corner loop",
-         20: "p:init winner", 21: "p:scatter", 22: "p:reduce+orient", 23: "p:columns"}
+         20: "p:init winner", 21: "p:scatter", 22: "p:reduce+orient", 23: "p:columns",
+         25: "s:init parents", 26: "s:edges+unite", 27: "s:find roots", 28: "s:sizes+rank+label", 29: "s:compaction"}
 
 
 def main():
