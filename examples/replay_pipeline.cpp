@@ -2,33 +2,43 @@
 // without ROS: ImageProjection on the caller thread, FeatureAssociation on its own thread, joined by
 // a blocking Channel<ProjectionOut>; AssociationOut goes to a non-blocking channel (live mode).
 //
-//   replay_pipeline <scans.bin> [device]
+//   replay_pipeline <scans.bin | file.bag> [device] [topic]
 // scans.bin: int32 nscans, then per scan: int32 n, n x (float x, y, z, intensity).
+// file.bag: a ROS bag v2.0; every sensor_msgs/PointCloud2 on `topic` (default /velodyne_points,
+// the reference's pointCloudTopic, utility.h:28) is decoded zero-copy (lego_rosbag.hpp) and replayed
+// in file order, as main.cpp:62-76 does with rosbag::View.
 // Prints one line per run: "cycles <n> status <bits> position x y z orientation x y z w".
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "lego_loam_amd.hpp"
+#include "lego_rosbag.hpp"
 
 int main(int argc, char** argv) {
   if (argc < 2) {
-    std::fprintf(stderr, "usage: %s scans.bin [device]\n", argv[0]);
+    std::fprintf(stderr, "usage: %s scans.bin|file.bag [device] [topic]\n", argv[0]);
     return 2;
   }
   const int device = argc > 2 ? std::atoi(argv[2]) : 0;
-  FILE* f = std::fopen(argv[1], "rb");
-  if (!f) return 2;
-  int32_t nscans = 0;
-  if (std::fread(&nscans, 4, 1, f) != 1) return 2;
-  std::vector<std::vector<float>> scans(nscans);
-  for (int i = 0; i < nscans; ++i) {
-    int32_t n = 0;
-    if (std::fread(&n, 4, 1, f) != 1) return 2;
-    scans[i].resize((size_t)n * 4);
-    if (n && std::fread(scans[i].data(), 16, n, f) != (size_t)n) return 2;
+  const std::string path = argv[1], topic = argc > 3 ? argv[3] : "/velodyne_points";
+  const bool is_bag = path.size() > 4 && path.compare(path.size() - 4, 4, ".bag") == 0;
+  std::vector<std::vector<float>> scans;
+  if (!is_bag) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return 2;
+    int32_t nscans = 0;
+    if (std::fread(&nscans, 4, 1, f) != 1) return 2;
+    scans.resize(nscans);
+    for (int i = 0; i < nscans; ++i) {
+      int32_t n = 0;
+      if (std::fread(&n, 4, 1, f) != 1) return 2;
+      scans[i].resize((size_t)n * 4);
+      if (n && std::fread(scans[i].data(), 16, n, f) != (size_t)n) return 2;
+    }
+    std::fclose(f);
   }
-  std::fclose(f);
 
   using namespace lego_amd;
   lego_params params = vlp16_params();
@@ -39,12 +49,23 @@ int main(int argc, char** argv) {
   try {
     ImageProjection IP(params, projection_out_channel, device);
     FeatureAssociation FA(params, projection_out_channel, association_out_channel, device);
-    for (int i = 0; i < nscans; ++i) {  // rosbag replay loop (main.cpp:72-95)
-      PointCloud2View msg;
-      msg.stamp = 0.1 * i;
-      msg.data = scans[i].data();
-      msg.width = (int32_t)(scans[i].size() / 4);
-      IP.cloudHandler(msg);
+    int nscans = 0;
+    if (is_bag) {  // rosbag replay loop (main.cpp:62-76)
+      BagReader bag(path);
+      bag.for_each(topic, [&](const BagMessage& m) {
+        if (m.type != "sensor_msgs/PointCloud2") return;
+        IP.cloudHandler(decode_pointcloud2(m));
+        ++nscans;
+      });
+    } else {
+      nscans = (int)scans.size();
+      for (int i = 0; i < nscans; ++i) {
+        PointCloud2View msg;
+        msg.stamp = 0.1 * i;
+        msg.data = scans[i].data();
+        msg.width = (int32_t)(scans[i].size() / 4);
+        IP.cloudHandler(msg);
+      }
     }
     // hand the worker a sentinel after the last scan and wait for it (the dtor does the same)
     while (FA.cycles() < nscans && FA.error().empty()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
@@ -58,6 +79,9 @@ int main(int argc, char** argv) {
   } catch (const Error& e) {
     std::fprintf(stderr, "error: %s\n", e.what());
     return 1;
+  } catch (const BagError& e) {
+    std::fprintf(stderr, "error: %s\n", e.what());
+    return 2;
   }
   std::printf("cycles %d status %d position %.9g %.9g %.9g orientation %.9g %.9g %.9g %.9g\n", cycles, status,
               odom.position[0], odom.position[1], odom.position[2], odom.orientation[0], odom.orientation[1],

@@ -1659,38 +1659,51 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
 }
 
 // one thread: nearest neighbour of q; returns index (or -1 if none closer than the radius) and ties
-LG_DEVICE int grid_nn(const LmLds& L, const float4* __restrict__ gp, float4 q, float r2, bool& tie) {
+// tpq adjacent lanes (1, 2, 4 or 8; a power of two, so a group never straddles a wave) share one
+// query: lane `sub` of the group visits every tpq-th candidate of each run, and the group merges
+// (d, lowest idx among equal d, points at that d) with xor shuffles.  Inactive lanes (act = false)
+// only join the shuffles.
+LG_DEVICE int grid_nn(const LmLds& L, const float4* __restrict__ gp, float4 q, float r2, bool& tie, int sub,
+                      int tpq, bool act) {
   const int qx = grid_coord(q.x, L.gmin[0], L.gcs, L.gdim[0]);
   const int qy = grid_coord(q.y, L.gmin[1], L.gcs, L.gdim[1]);
   const int qz = grid_coord(q.z, L.gmin[2], L.gcs, L.gdim[2]);
   float bd = FLT_MAX;
-  int bi = 0x7fffffff, tc = 0;
-  for (int cz = max(qz - 1, 0); cz <= min(qz + 1, L.gdim[2] - 1); ++cz)
-    for (int cy = max(qy - 1, 0); cy <= min(qy + 1, L.gdim[1] - 1); ++cy) {
-      const int row = (cz * L.gdim[1] + cy) * L.gdim[0];
-      const int x0 = max(qx - 1, 0), x1 = min(qx + 1, L.gdim[0] - 1);
-      if (x0 > x1) continue;
-      const int b = (row + x0 == 0) ? 0 : L.gcell[row + x0 - 1];
-      const int e = L.gcell[row + x1];  // cells x0..x1 of a row are contiguous
-      // the (d, idx) minimum and tie count do not depend on the visiting order: 8 loads in flight
-      auto visit = [&](const float4 p) {
-        const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
-        const float d = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
-        const int idx = __float_as_int(p.w);
-        if (d < bd) { bd = d; bi = idx; tc = 0; }
-        else if (d == bd) { tc++; bi = min(bi, idx); }
-      };
-      int k = b;
-      for (; k + 8 <= e; k += 8) {
-        float4 p8[8];
+  int bi = 0x7fffffff, bc = 0;
+  if (act) {
+    for (int cz = max(qz - 1, 0); cz <= min(qz + 1, L.gdim[2] - 1); ++cz)
+      for (int cy = max(qy - 1, 0); cy <= min(qy + 1, L.gdim[1] - 1); ++cy) {
+        const int row = (cz * L.gdim[1] + cy) * L.gdim[0];
+        const int x0 = max(qx - 1, 0), x1 = min(qx + 1, L.gdim[0] - 1);
+        if (x0 > x1) continue;
+        const int b = (row + x0 == 0) ? 0 : L.gcell[row + x0 - 1];
+        const int e = L.gcell[row + x1];  // cells x0..x1 of a row are contiguous
+        // the (d, idx) minimum and tie count do not depend on the visiting order: 8 loads in flight
+        auto visit = [&](const float4 p) {
+          const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+          const float d = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
+          const int idx = __float_as_int(p.w);
+          if (d < bd) { bd = d; bi = idx; bc = 1; }
+          else if (d == bd) { bc++; bi = min(bi, idx); }
+        };
+        int k = b + sub;
+        for (; k + 7 * tpq < e; k += 8 * tpq) {
+          float4 p8[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) p8[u] = gp[k + u];
+          for (int u = 0; u < 8; ++u) p8[u] = gp[k + u * tpq];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) visit(p8[u]);
+          for (int u = 0; u < 8; ++u) visit(p8[u]);
+        }
+        for (; k < e; k += tpq) visit(gp[k]);
       }
-      for (; k < e; ++k) visit(gp[k]);
-    }
-  tie = (bd < r2) && tc > 0;
+  }
+  for (int o = tpq >> 1; o > 0; o >>= 1) {
+    const float d2 = __shfl_xor(bd, o);
+    const int i2 = __shfl_xor(bi, o), c2 = __shfl_xor(bc, o);
+    if (d2 < bd) { bd = d2; bi = i2; bc = c2; }
+    else if (d2 == bd) { bi = min(bi, i2); bc += c2; }
+  }
+  tie = (bd < r2) && bc > 1;
   return (bd < r2) ? bi : -1;
 }
 
@@ -1960,10 +1973,18 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
     PROF_T(t_srch0);
     if (iter % 5 == 0) {
       int st = 0;
-      for (int q = tid; q < nq; q += LM_THREADS) {
+      // as many lanes per query as the block allows (surf ~170 queries: 2; corner ~115: 4)
+      const int tpq = nq * 8 <= LM_THREADS ? 8 : nq * 4 <= LM_THREADS ? 4 : nq * 2 <= LM_THREADS ? 2 : 1;
+      for (int base = 0; base < nq * tpq; base += LM_THREADS) {
+        const int t = base + tid, q = t / tpq;
+        const bool act = q < nq;
         bool tie = false;
-        L.ind1[q] = grid_nn(L, gp, L.sel[q], P.nn_dist_sqr, tie);
-        if (tie) st |= LEGO_ST_NN_TIE;
+        const int c = grid_nn(L, gp, act ? L.sel[q] : make_float4(0.f, 0.f, 0.f, 0.f), P.nn_dist_sqr, tie, t % tpq,
+                              tpq, act);
+        if (act && t % tpq == 0) {
+          L.ind1[q] = c;
+          if (tie) st |= LEGO_ST_NN_TIE;
+        }
       }
       __syncthreads();
       for (int q = wave_id(); q < nq; q += nw) {

@@ -62,3 +62,26 @@ def test_mirror_pipeline_matches_oracle(gpu, tmp_path):
     assert cycles == len(scans)
     np.testing.assert_allclose(pos, fa["odom_position"], atol=Hs.TF_TOL, rtol=0)
     np.testing.assert_allclose(quat, fa["odom_orientation"], atol=Hs.TF_TOL, rtol=0)
+
+
+@pytest.mark.gpu
+def test_rosbag_replay_equals_direct_replay(gpu, tmp_path):
+    """The same sweeps replayed from a ROS bag (PointCloud2 decoded zero-copy, lego_rosbag.hpp) and from
+    a plain file give the identical odometry line."""
+    build()
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "bag_tool"])
+    cfg = A.synth_cfg("vlp16")
+    scans = [A.synth_scan(cfg, 5, k) for k in range(5)]
+    f = tmp_path / "s.bin"
+    write_scans(str(f), scans)
+    bag = tmp_path / "s.bag"
+    subprocess.check_call([os.path.join(REPO, "examples", "bag_tool"), "write", str(f), str(bag)],
+                          stdout=subprocess.DEVNULL)
+    outs = []
+    for src in (f, bag):
+        r = subprocess.run([EXE, str(src), "0"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           universal_newlines=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        outs.append(r.stdout.strip())
+    assert outs[0] == outs[1]
+    assert outs[0].startswith("cycles 5 ")

@@ -27,8 +27,9 @@ NAMES = {0: "x:load+sort seg", 1: "x:sharp greedy", 2: "x:flat greedy", 3: "x:le
 
 def main():
     S = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    order = int(sys.argv[2]) if len(sys.argv) > 2 else 1  # voxel_tie_order (bench default 1)
     steps = 4
-    params = L.params_vlp16()
+    params = L.params_vlp16(voxel_tie_order=order)
     cfg = A.synth_cfg("vlp16")
     cap = 16 * 1800
     seqs = np.repeat(np.arange(S)[None, :], steps, 0).reshape(-1)
