@@ -1423,13 +1423,19 @@ LG_DEVICE float4 transform_to_end(const float4 pi, const float* cur) {  // :422-
 
 // Eigen boundary model, identical to the oracle's: ColPivHouseholderQR<Matrix3f>::solve in float.
 LG_DEVICE void qr_solve3(const float* A_in, const float* b_in, float* x) {
+  // Fully unrolled with every array index a compile-time constant (pivot swaps and the rank-limited
+  // loops become guarded static accesses), so the factorisation stays in registers.  The floating-
+  // point operations and their order are unchanged.
   float A[9];
+#pragma unroll
   for (int i = 0; i < 9; ++i) A[i] = A_in[i];
   const float eps = FLT_EPSILON;
   float nu[3], nd[3], hc[3];
   int perm[3] = {0, 1, 2};
+#pragma unroll
   for (int k = 0; k < 3; ++k) {
     float s = 0.f;
+#pragma unroll
     for (int r = 0; r < 3; ++r) s += A[r * 3 + k] * A[r * 3 + k];
     nu[k] = nd[k] = sqrtf(s);
   }
@@ -1437,40 +1443,54 @@ LG_DEVICE void qr_solve3(const float* A_in, const float* b_in, float* x) {
   float th_help = (maxn * eps) * (maxn * eps) / 3.0f;
   float ndt = sqrtf(eps);
   int nzp = 3;
+#pragma unroll
   for (int k = 0; k < 3; ++k) {
     int bc = k;
+    float bv = nu[k];
+#pragma unroll
     for (int j = k + 1; j < 3; ++j)
-      if (nu[j] > nu[bc]) bc = j;
-    float bsq = nu[bc] * nu[bc];
+      if (nu[j] > bv) { bc = j; bv = nu[j]; }
+    float bsq = bv * bv;
     if (nzp == 3 && bsq < th_help * float(3 - k)) nzp = k;
-    if (bc != k) {
-      for (int r = 0; r < 3; ++r) { float t = A[r * 3 + k]; A[r * 3 + k] = A[r * 3 + bc]; A[r * 3 + bc] = t; }
-      float t = nu[k]; nu[k] = nu[bc]; nu[bc] = t;
-      t = nd[k]; nd[k] = nd[bc]; nd[bc] = t;
-      int ti = perm[k]; perm[k] = perm[bc]; perm[bc] = ti;
+#pragma unroll
+    for (int j = k + 1; j < 3; ++j) {
+      if (bc == j) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) { float t = A[r * 3 + k]; A[r * 3 + k] = A[r * 3 + j]; A[r * 3 + j] = t; }
+        float t = nu[k]; nu[k] = nu[j]; nu[j] = t;
+        t = nd[k]; nd[k] = nd[j]; nd[j] = t;
+        int ti = perm[k]; perm[k] = perm[j]; perm[j] = ti;
+      }
     }
     float tail = 0.f;
+#pragma unroll
     for (int r = k + 1; r < 3; ++r) tail += A[r * 3 + k] * A[r * 3 + k];
     float c0 = A[k * 3 + k], tau, beta;
     if (tail <= FLT_MIN) {
       tau = 0.f; beta = c0;
+#pragma unroll
       for (int r = k + 1; r < 3; ++r) A[r * 3 + k] = 0.f;
     } else {
       beta = sqrtf(c0 * c0 + tail);
       if (c0 >= 0.f) beta = -beta;
+#pragma unroll
       for (int r = k + 1; r < 3; ++r) A[r * 3 + k] = A[r * 3 + k] / (c0 - beta);
       tau = (beta - c0) / beta;
     }
     hc[k] = tau;
     A[k * 3 + k] = beta;
     if (tau != 0.f) {
+#pragma unroll
       for (int j = k + 1; j < 3; ++j) {
         float t = A[k * 3 + j];
+#pragma unroll
         for (int r = k + 1; r < 3; ++r) t += A[r * 3 + k] * A[r * 3 + j];
         A[k * 3 + j] -= tau * t;
+#pragma unroll
         for (int r = k + 1; r < 3; ++r) A[r * 3 + j] -= tau * A[r * 3 + k] * t;
       }
     }
+#pragma unroll
     for (int j = k + 1; j < 3; ++j) {
       if (nu[j] != 0.f) {
         float t = fabsf(A[k * 3 + j]) / nu[j];
@@ -1480,6 +1500,7 @@ LG_DEVICE void qr_solve3(const float* A_in, const float* b_in, float* x) {
         float t2 = t * q * q;
         if (t2 <= ndt) {
           float s = 0.f;
+#pragma unroll
           for (int r = k + 1; r < 3; ++r) s += A[r * 3 + j] * A[r * 3 + j];
           nd[j] = sqrtf(s);
           nu[j] = nd[j];
@@ -1490,20 +1511,32 @@ LG_DEVICE void qr_solve3(const float* A_in, const float* b_in, float* x) {
     }
   }
   float c[3] = {b_in[0], b_in[1], b_in[2]};
-  for (int k = 0; k < nzp; ++k) {
-    if (hc[k] == 0.f) continue;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k >= nzp || hc[k] == 0.f) continue;
     float t = c[k];
+#pragma unroll
     for (int r = k + 1; r < 3; ++r) t += A[r * 3 + k] * c[r];
     c[k] -= hc[k] * t;
+#pragma unroll
     for (int r = k + 1; r < 3; ++r) c[r] -= hc[k] * A[r * 3 + k] * t;
   }
   float y[3] = {0.f, 0.f, 0.f};
-  for (int i = nzp - 1; i >= 0; --i) {
+#pragma unroll
+  for (int i = 2; i >= 0; --i) {
+    if (i >= nzp) continue;
     float t = c[i];
-    for (int j = i + 1; j < nzp; ++j) t -= A[i * 3 + j] * y[j];
+#pragma unroll
+    for (int j = i + 1; j < 3; ++j)
+      if (j < nzp) t -= A[i * 3 + j] * y[j];
     y[i] = t / A[i * 3 + i];
   }
-  for (int i = 0; i < 3; ++i) x[perm[i]] = y[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+      if (perm[i] == m) x[m] = y[i];
+  }
 }
 
 LG_DEVICE double eig_max_sym3(const float* Af) {
@@ -1513,7 +1546,9 @@ LG_DEVICE double eig_max_sym3(const float* Af) {
   for (int sweep = 0; sweep < 32; ++sweep) {
     double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
     if (off == 0.0) break;
+#pragma unroll
     for (int p = 0; p < 2; ++p)
+#pragma unroll
       for (int q = p + 1; q < 3; ++q) {
         if (a[p][q] == 0.0) continue;
         double theta = (a[q][q] - a[p][p]) / (2.0 * a[p][q]);
