@@ -187,7 +187,8 @@ int  lego_batch_set_groups(lego_batch* b, int32_t groups);
  * 2 atanf(a), 3 sqrtf(a), 4 a / b.  Lets tests compare gfx950 results with the host's glibc. */
 int  lego_test_libm(const float* a, const float* b, float* out, int32_t n, int32_t which);
 /* Sort (key, val) pairs by key with the device's wave-parallel std::sort emulation (n <= 2048);
- * keys are float bit patterns when is_float != 0, else uint32. */
+ * keys are uint32 (is_float 0) or float bit patterns (1); is_float 2 runs k_extract's segment
+ * sort (float keys, n <= 512: register sort when keys are distinct, else the emulation). */
 int  lego_test_sort(uint32_t* keys, int32_t* vals, int32_t n, int32_t is_float);
 /* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
  * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */

@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/lego_frontend.h"
@@ -797,8 +798,14 @@ LG_DEVICE int wave_partition_stream(const SortView<K, V>& a, int first, int last
   }
 }
 
+template <int R>
+LG_DEVICE void seg_final_bitonic(float* key, int* val, int n);
+
+// final_reg: n <= 512 float keys, none negative or NaN -> __final_insertion_sort is computed as a
+// register sort by (key, position): it is stable and never moves an element across a partition
+// cut, so its result is the post-partition array stably sorted by key.
 template <typename K, typename V>
-LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int* tab) {
+LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int* tab, bool final_reg = false) {
   const int lane = lane_id();
   if (n <= 1) return;
   const int nwords = (n + 31) >> 5;
@@ -844,6 +851,16 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
   }
   PROF_ADD(6, t_part0);
   PROF_T(t_fin0);
+  if constexpr (sizeof(K) == 4 && sizeof(V) == 4 && !std::is_integral<K>::value) {
+    if (final_reg) {
+      if (n <= 64) seg_final_bitonic<1>((float*)key, (int*)val, n);
+      else if (n <= 128) seg_final_bitonic<2>((float*)key, (int*)val, n);
+      else if (n <= 256) seg_final_bitonic<4>((float*)key, (int*)val, n);
+      else seg_final_bitonic<8>((float*)key, (int*)val, n);
+      PROF_ADD(11, t_fin0);
+      return;
+    }
+  }
   // __final_insertion_sort as independent per-block insertion sorts: lane h sorts the blocks that
   // start in positions [16h, 16h + 16).
   const int nhalf = (n + 15) >> 4;
@@ -961,78 +978,124 @@ LG_DEVICE void suppress_neighbours(const ScanView& v, int ind) {  // :306-326
   }
 }
 
-// rank of every element = #keys strictly smaller; eq = #equal keys (itself included)
-template <int NQ>
-LG_DEVICE void rank_pass(const float* key, int n, const float* rk, int* rr, int* eqc) {
-  int b = 0;
-  for (; b + 4 <= n; b += 4) {
-    const float k0 = key[b], k1 = key[b + 1], k2 = key[b + 2], k3 = key[b + 3];
+// Ascending bitonic sort of R u64 values per lane (element lane*R + r), all in registers: strides
+// below R swap registers, larger strides exchange with lane ^ (j / R).
+template <int R>
+LG_DEVICE void reg_bitonic_u64(unsigned long long (&a)[R]) {
+  const int lane = lane_id();
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      rr[q] += (k0 < rk[q]) + (k1 < rk[q]) + (k2 < rk[q]) + (k3 < rk[q]);
-      eqc[q] += (k0 == rk[q]) + (k1 == rk[q]) + (k2 == rk[q]) + (k3 == rk[q]);
-    }
-  }
-  for (; b < n; ++b) {
-    const float kb = key[b];
+  for (int k = 2; k <= 64 * R; k <<= 1) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      rr[q] += (kb < rk[q]);
-      eqc[q] += (kb == rk[q]);
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j < R) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (r & j) continue;
+          const bool asc = (((lane * R + r) & k) == 0);
+          const unsigned long long x = a[r], y = a[r | j];
+          const bool sw = asc ? (x > y) : (x < y);
+          a[r] = sw ? y : x;
+          a[r | j] = sw ? x : y;
+        }
+      } else {
+        const int m = j / R;
+        const bool lower = (lane & m) == 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const bool asc = (((lane * R + r) & k) == 0);
+          const unsigned long long x = a[r];
+          const unsigned long long y = ((unsigned long long)(unsigned)__shfl_xor((int)(x >> 32), m) << 32) |
+                                       (unsigned)__shfl_xor((int)(unsigned)x, m);
+          const bool take_min = (lower == asc);
+          a[r] = take_min ? (x < y ? x : y) : (x > y ? x : y);
+        }
+      }
     }
   }
 }
 
-// Sort [0, n) of (key, val): all-distinct keys -> rank scatter (any correct sort gives the same
-// permutation); any tie -> exact libstdc++ introsort on one lane.
+// The post-partition array [0, n) sorted by (key bits, position), values gathered by position.
+template <int R>
+LG_DEVICE void seg_final_bitonic(float* key, int* val, int n) {
+  const int lane = lane_id();
+  unsigned long long a[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane * R + r;
+    a[r] = e < n ? (((unsigned long long)(unsigned)__float_as_int(key[e]) << 32) | (unsigned)e) : ~0ull;
+  }
+  reg_bitonic_u64<R>(a);
+  int vg[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) vg[r] = (lane * R + r < n) ? val[(unsigned)a[r]] : 0;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane * R + r;
+    if (e < n) {
+      key[e] = __int_as_float((int)(a[r] >> 32));
+      val[e] = vg[r];
+    }
+  }
+  __syncthreads();
+}
+
+// (curvature bits << 32 | ring index) in registers; returns false (and leaves LDS untouched) when a
+// key tie, a NaN or a sign bit makes the order depend on the sort algorithm (*anomaly: NaN / sign).
+template <int R>
+LG_DEVICE bool seg_sort_distinct(float* key, int* val, int n, bool* anomaly) {
+  const int lane = lane_id();
+  unsigned long long a[R];
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane * R + r;
+    if (e < n) {
+      const unsigned kb = (unsigned)__float_as_int(key[e]);
+      bad |= kb > 0x7f800000u;  // NaN, or negative (incl. -0.0)
+      a[r] = ((unsigned long long)kb << 32) | (unsigned)val[e];
+    } else {
+      a[r] = ~0ull;
+    }
+  }
+  *anomaly = __ballot(bad) != 0ull;
+  reg_bitonic_u64<R>(a);
+  const unsigned nxt = (unsigned)__shfl_down((int)(a[0] >> 32), 1);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane * R + r;
+    const unsigned kn = (r + 1 < R) ? (unsigned)(a[r + 1 < R ? r + 1 : r] >> 32) : nxt;
+    if (e + 1 < n && (unsigned)(a[r] >> 32) == kn) bad = true;
+  }
+  if (__ballot(bad) != 0ull) return false;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane * R + r;
+    if (e < n) {
+      key[e] = __int_as_float((int)(a[r] >> 32));
+      val[e] = (int)(unsigned)a[r];
+    }
+  }
+  __syncthreads();
+  return true;
+}
+
+// Sort [0, n) of (key, val): all-distinct keys -> register bitonic sort (any correct sort gives the
+// same permutation); any tie -> exact libstdc++ introsort emulation.
 LG_DEVICE void sort_segment(ExtractLds& L, int n) {
   float* key = L.u.seg.skey;
   int* val = L.u.seg.sval;
-  const int lane = lane_id();
-  float rk[SEG_MAX / 64];
-  int rv[SEG_MAX / 64], rr[SEG_MAX / 64];
-  bool tie = false;
-  int eqc[SEG_MAX / 64];
-#pragma unroll
-  for (int q = 0; q < SEG_MAX / 64; ++q) {
-    const int a = lane + 64 * q;
-    rk[q] = (a < n) ? key[a] : 0.f;
-    rv[q] = (a < n) ? val[a] : 0;
-    rr[q] = 0;
-    eqc[q] = 0;
-  }
-  const int nq = (n + 63) >> 6;  // active slots (wave-uniform)
-  switch (nq) {
-    case 1: rank_pass<1>(key, n, rk, rr, eqc); break;
-    case 2: rank_pass<2>(key, n, rk, rr, eqc); break;
-    case 3: rank_pass<3>(key, n, rk, rr, eqc); break;
-    case 4: rank_pass<4>(key, n, rk, rr, eqc); break;
-    case 5: rank_pass<5>(key, n, rk, rr, eqc); break;
-    case 6: rank_pass<6>(key, n, rk, rr, eqc); break;
-    case 7: rank_pass<7>(key, n, rk, rr, eqc); break;
-    default: rank_pass<8>(key, n, rk, rr, eqc); break;
-  }
-#pragma unroll
-  for (int q = 0; q < SEG_MAX / 64; ++q) {
-    const int a = lane + 64 * q;
-    if (a < n) tie |= (eqc[q] > 1);
-    else rr[q] = -1;
-  }
-  const bool any_tie = __ballot(tie) != 0ull;
-  __syncthreads();
-  if (!any_tie) {
-#pragma unroll
-    for (int q = 0; q < SEG_MAX / 64; ++q)
-      if (rr[q] >= 0) {
-        key[rr[q]] = rk[q];
-        val[rr[q]] = rv[q];
-      }
-    __syncthreads();
-  } else {
+  bool ok, anomaly = true;
+  if (n <= 64) ok = seg_sort_distinct<1>(key, val, n, &anomaly);
+  else if (n <= 128) ok = seg_sort_distinct<2>(key, val, n, &anomaly);
+  else if (n <= 256) ok = seg_sort_distinct<4>(key, val, n, &anomaly);
+  else ok = seg_sort_distinct<8>(key, val, n, &anomaly);
+  if (!ok) {
 #ifdef LG_PROFILE
-    if (lane == 0) atomicAdd(&PROF_SLOT(14), 1ull);
+    if (lane_id() == 0) atomicAdd(&PROF_SLOT(14), 1ull);
 #endif
-    wave_std_sort<float, int>(key, val, n, L.blk, L.stk, L.tab);
+    wave_std_sort<float, int>(key, val, n, L.blk, L.stk, L.tab, !anomaly && n <= SEG_MAX);
   }
 }
 
@@ -2282,7 +2345,13 @@ __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int
   const int lane = lane_id();
   for (int i = lane; i < n; i += 64) { L.u.vkey[i] = keys[i]; L.vval[i] = (uint16_t)vals[i]; }
   __syncthreads();
-  if (is_float) {
+  if (is_float == 2) {  // k_extract's segment sort (n <= SEG_MAX)
+    for (int i = lane; i < n; i += 64) { L.u.seg.skey[i] = __int_as_float((int)keys[i]); L.u.seg.sval[i] = vals[i]; }
+    __syncthreads();
+    sort_segment(L, n);
+    for (int i = lane; i < n; i += 64) { keys[i] = (unsigned)__float_as_int(L.u.seg.skey[i]); vals[i] = L.u.seg.sval[i]; }
+    return;
+  } else if (is_float) {
     wave_std_sort<float, uint16_t>((float*)L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
   } else {
     wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
@@ -2291,7 +2360,8 @@ __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int
 }
 
 extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int32_t is_float) {
-  if (n < 0 || n > RING_MAX || !h_keys || !h_vals) return LEGO_EINVAL;
+  if (n < 0 || n > RING_MAX || !h_keys || !h_vals || is_float < 0 || is_float > 2) return LEGO_EINVAL;
+  if (is_float == 2 && n > SEG_MAX) return LEGO_EINVAL;
   if (n == 0) return LEGO_OK;
   unsigned* k = nullptr;
   int* v = nullptr;
