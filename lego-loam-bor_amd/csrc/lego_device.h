@@ -32,6 +32,7 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int s0;                               // first stream of the launch (stream groups; 0 otherwise)
   int ncu;                              // compute units of the device (k_extract's ring rotation)
   int voxel_stable;                     // lego_params.voxel_tie_order == 1
+  int epoch;                            // per-launch token for k_extract's first-pass flags
 };
 
 struct LgState {  // FeatureAssociation members that persist across scans (featureAssociation.h)
@@ -83,6 +84,7 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   uint8_t* picked;       // [S][VH]
   int8_t* flabel;        // [S][VH]
   int2* smooth;          // [S][VH]  {float bits of value, ind}
+  int32_t* fp_sync;      // [S][2]   stale ind of smoothness slot 4, first-pass done epoch
   float4* seg_fa;        // [S][VH]  segmentedCloud after adjustDistortion
   float4* outlier_fa;    // [S][VH]  adjustOutlierCloud
   // per-ring staging

@@ -95,6 +95,7 @@ struct lego_batch {
   hipEvent_t ev[8];
   bool timing = false;
   bool events = false;
+  int epoch = 0;  // k_extract first-pass token (LgParams.epoch), never 0 after the first launch
   // stream groups: the S sequences split into `groups` slices, each launched on its own HIP stream
   // so one slice's long-tail kernels overlap the next slice's (fork/join on the caller's stream)
   int groups = 1;
@@ -224,7 +225,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   A(scan_cand, S * H); A(orient, S * 4);
   A(seg_pts, S * VH); A(seg_range, S * VH); A(seg_col, S * VH); A(seg_ground, S * VH);
   A(ring_start, S * V); A(ring_end, S * V); A(outlier, S * VH); A(scan_msg, S * H); A(counts, S * CNT_N);
-  A(curv, S * VH); A(picked, S * VH); A(flabel, S * VH); A(smooth, S * VH); A(seg_fa, S * VH); A(outlier_fa, S * VH);
+  A(curv, S * VH); A(picked, S * VH); A(flabel, S * VH); A(smooth, S * VH); A(fp_sync, S * 2); A(seg_fa, S * VH); A(outlier_fa, S * VH);
   A(r_sharp, S * V * P.cap_sharp); A(r_sharp_ind, S * V * P.cap_sharp);
   A(r_lsharp, S * V * P.cap_lsharp); A(r_lsharp_ind, S * V * P.cap_lsharp);
   A(r_flat, S * V * P.cap_flat); A(r_flat_ind, S * V * P.cap_flat);
@@ -261,6 +262,8 @@ int lego_batch_reset(lego_batch* b) {
   if (hipMemset(B.picked, 0, S * VH) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.flabel, 0, S * VH) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.smooth, 0, S * VH * sizeof(int2)) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemset(B.fp_sync, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
+  b->epoch = 0;
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.counts, 0, S * CNT_N * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
@@ -296,6 +299,8 @@ static int run_projection(lego_batch* b, const float4* pts, const int64_t* offs,
 static int run_association(lego_batch* b, hipStream_t st, int s0, int n) {
   LgParams P = b->P;
   P.s0 = s0;
+  b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
+  P.epoch = b->epoch;
   int rc = lg_launch_fa_prep(P, b->B, n, st);
   if (rc) return rc;
   if (b->timing) hipEventRecord(b->ev[3], st);

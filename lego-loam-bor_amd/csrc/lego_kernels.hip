@@ -557,6 +557,8 @@ __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
     float inten = (float)(int)p.w + P.scan_period * relTime;
     fa[i] = make_float4(p.y, p.z, p.x, inten);
   }
+  // k_extract's first pass may move the stale slot 4 while other rings check where it points
+  if (tid == 0) B.fp_sync[2 * s] = smooth[4].y;
   for (int i = 5 + tid; i < M - 5; i += nt) {
     float d = r[i - 5] + r[i - 4] + r[i - 3] + r[i - 2] + r[i - 1] - r[i] * 10 + r[i + 1] + r[i + 2] +
               r[i + 3] + r[i + 4] + r[i + 5];
@@ -597,15 +599,24 @@ __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
 #define SEG_MAX 512
 #define RING_MAX 2048
 
-struct ExtractLds {  // 13.5 KB per wave -> 11 waves per CU
+struct ExtractLds {  // k_voxel (and the sort test hooks): 13.5 KB per wave
   union {
-    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;  // segment sort (extract phase)
-    unsigned vkey[RING_MAX];                                 // voxel keys (voxel phase)
+    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;  // segment sort (test hook)
+    unsigned vkey[RING_MAX];                                 // voxel keys
   } u;
   uint16_t vval[RING_MAX];      // lessFlat positions of the ring (relative to the ring start), sorted with vkey
   unsigned blk[RING_MAX / 32];  // final-block start bits of the introsort emulation
   int stk[3 * 64];
   int tab[128];                 // lane-pairing / stop-queue scratch of the partitions
+};
+
+struct SegLds {  // k_extract: 5.6 KB per wave
+  union {
+    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;  // segment sort
+  } u;
+  unsigned blk[RING_MAX / 32];
+  int stk[3 * 64];
+  int tab[128];
 };
 
 // libstdc++ __adjust_heap (lego_introsort.h) on one lane, each level's two children (key and value)
@@ -979,36 +990,37 @@ LG_DEVICE void suppress_neighbours(const ScanView& v, int ind) {  // :306-326
 }
 
 // Ascending bitonic sort of R u64 values per lane (element lane*R + r), all in registers: strides
-// below R swap registers, larger strides exchange with lane ^ (j / R).
+// j >= R exchange with lane ^ (j / R), smaller strides swap registers.  The k and cross-lane j
+// loops stay rolled (code size); the in-register strides are unrolled with a uniform guard.
 template <int R>
 LG_DEVICE void reg_bitonic_u64(unsigned long long (&a)[R]) {
   const int lane = lane_id();
-#pragma unroll
+#pragma unroll 1
   for (int k = 2; k <= 64 * R; k <<= 1) {
+#pragma unroll 1
+    for (int j = k >> 1; j >= R; j >>= 1) {
+      const int m = j / R;
+      // k >= 2R here, so bit k of lane*R + r does not depend on r
+      const bool take_min = ((lane & m) == 0) == (((lane * R) & k) == 0);
 #pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j < R) {
+      for (int r = 0; r < R; ++r) {
+        const unsigned long long x = a[r];
+        const unsigned long long y = ((unsigned long long)(unsigned)__shfl_xor((int)(x >> 32), m) << 32) |
+                                     (unsigned)__shfl_xor((int)(unsigned)x, m);
+        a[r] = ((x < y) == take_min) ? x : y;
+      }
+    }
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (r & j) continue;
-          const bool asc = (((lane * R + r) & k) == 0);
-          const unsigned long long x = a[r], y = a[r | j];
-          const bool sw = asc ? (x > y) : (x < y);
-          a[r] = sw ? y : x;
-          a[r | j] = sw ? x : y;
-        }
-      } else {
-        const int m = j / R;
-        const bool lower = (lane & m) == 0;
+    for (int j = R / 2; j >= 1; j >>= 1) {
+      if (j > (k >> 1)) continue;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const bool asc = (((lane * R + r) & k) == 0);
-          const unsigned long long x = a[r];
-          const unsigned long long y = ((unsigned long long)(unsigned)__shfl_xor((int)(x >> 32), m) << 32) |
-                                       (unsigned)__shfl_xor((int)(unsigned)x, m);
-          const bool take_min = (lower == asc);
-          a[r] = take_min ? (x < y ? x : y) : (x > y ? x : y);
-        }
+      for (int r = 0; r < R; ++r) {
+        if (r & j) continue;
+        const bool asc = (((lane * R + r) & k) == 0);
+        const unsigned long long x = a[r], y = a[r | j];
+        const bool sw = (x > y) == asc;
+        a[r] = sw ? y : x;
+        a[r | j] = sw ? x : y;
       }
     }
   }
@@ -1083,7 +1095,8 @@ LG_DEVICE bool seg_sort_distinct(float* key, int* val, int n, bool* anomaly) {
 
 // Sort [0, n) of (key, val): all-distinct keys -> register bitonic sort (any correct sort gives the
 // same permutation); any tie -> exact libstdc++ introsort emulation.
-LG_DEVICE void sort_segment(ExtractLds& L, int n) {
+template <class Lds>
+LG_DEVICE void sort_segment(Lds& L, int n) {
   float* key = L.u.seg.skey;
   int* val = L.u.seg.sval;
   bool ok, anomaly = true;
@@ -1115,32 +1128,38 @@ LG_DEVICE float4 seg_point(const ScanView& v, int ind, int& status) {  // segmen
 }
 
 // PCL VoxelGrid<PointXYZI> (leaf 0.2) over the ring's lessFlat points (positions in L.vval[0..n)).
-// Ascending sort of n <= RING_MAX (key, val) pairs by (key, val), one wave, bitonic network in LDS.
-// vals are distinct ring positions appended in point order, so this is the order std::stable_sort
-// gives by key alone (lego_params.voxel_tie_order == 1).
-LG_DEVICE void wave_bitonic_kv(unsigned* key, uint16_t* val, int n) {
+// Ascending sort of n <= RING_MAX (key, val) pairs by (key, val), one wave, (key << 32 | val) in
+// registers.  vals are distinct ring positions appended in point order, so this is the order
+// std::stable_sort gives by key alone (lego_params.voxel_tie_order == 1).
+template <int R>
+LG_DEVICE void voxel_sort_reg(unsigned* key, uint16_t* val, int n) {
   const int lane = lane_id();
-  int N = 1;
-  while (N < n) N <<= 1;
-  for (int i = n + lane; i < N; i += 64) { key[i] = 0xffffffffu; val[i] = 0xffffu; }  // sort last
+  unsigned long long a[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane * R + r;
+    a[r] = e < n ? (((unsigned long long)key[e] << 32) | val[e]) : ~0ull;
+  }
+  reg_bitonic_u64<R>(a);
   __syncthreads();
-  for (int k = 2; k <= N; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int lj = __ffs(j) - 1;
-      for (int p = lane; p < (N >> 1); p += 64) {
-        const int i = ((p >> lj) << (lj + 1)) | (p & (j - 1));
-        const int l = i | j;
-        const unsigned ki = key[i], kl = key[l];
-        const uint16_t vi = val[i], vl = val[l];
-        const bool gt = ki > kl || (ki == kl && vi > vl);
-        if (gt == ((i & k) == 0)) {
-          key[i] = kl; key[l] = ki;
-          val[i] = vl; val[l] = vi;
-        }
-      }
-      __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane * R + r;
+    if (e < n) {
+      key[e] = (unsigned)(a[r] >> 32);
+      val[e] = (uint16_t)a[r];
     }
   }
+  __syncthreads();
+}
+
+LG_DEVICE void voxel_sort_stable(unsigned* key, uint16_t* val, int n) {
+  if (n <= 64) voxel_sort_reg<1>(key, val, n);
+  else if (n <= 128) voxel_sort_reg<2>(key, val, n);
+  else if (n <= 256) voxel_sort_reg<4>(key, val, n);
+  else if (n <= 512) voxel_sort_reg<8>(key, val, n);
+  else if (n <= 1024) voxel_sort_reg<16>(key, val, n);
+  else voxel_sort_reg<32>(key, val, n);
 }
 
 LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, int n, int base_pos, RingOut& o) {
@@ -1180,7 +1199,7 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
   }
   __syncthreads();
   PROF_T(t_vs0);
-  if (P.voxel_stable) wave_bitonic_kv(L.u.vkey, L.vval, n);
+  if (P.voxel_stable) voxel_sort_stable(L.u.vkey, L.vval, n);
   else wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
   PROF_ADD(5, t_vs0);
   int running = 0;
@@ -1205,9 +1224,8 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
 }
 
 LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, int st, int en,
-                            ExtractLds& L, RingOut& o) {
+                            SegLds& L, RingOut& o) {
   const int lane = lane_id();
-  int nlist = 0;
   for (int j = 0; j < 6; j++) {
     const int sp = (st * (6 - j) + en * j) / 6;
     const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
@@ -1300,36 +1318,87 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
     }
     __syncthreads();
     PROF_ADD(2, t_flat0);
-    PROF_T(t_lf0);
-    // lessFlat: positions k in [sp, ep] whose label <= 0 (position, not sorted index: :370-374)
-    for (int base = 0; base <= n; base += 64) {
-      const int t = base + lane;
-      const int k = sp + t;
-      const bool pr = t <= n && v.flabel[k] <= 0;
+  }
+}
+
+// lessFlat list of one ring: positions k in [sp, ep] of each segment whose label <= 0 (position
+// order, not sorted order: :370-374).  Labels of a segment's positions are final once k_extract
+// has processed that segment (later picks label their own segment; the stale slot-4 pick lands
+// before its ring runs), so the list is rebuilt here from cloudLabel after k_extract.
+LG_DEVICE int lessflat_list(const ScanView& v, int st, int en, uint16_t* list) {
+  const int lane = lane_id();
+  int nlist = 0;
+  for (int j = 0; j < 6; j++) {
+    const int sp = (st * (6 - j) + en * j) / 6;
+    const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
+    if (sp >= ep) continue;
+    for (int k0 = sp; k0 <= ep; k0 += 64) {
+      const int k = k0 + lane;
+      const bool pr = k <= ep && v.flabel[k] <= 0;
       const unsigned long long m = __ballot(pr);
-      if (pr) L.vval[nlist + popc_below(m)] = (uint16_t)(k - st);
+      if (pr) list[nlist + popc_below(m)] = (uint16_t)(k - st);
       nlist += __popcll(m);
     }
-    __syncthreads();
-    PROF_ADD(3, t_lf0);
   }
+  __syncthreads();
+  return nlist;
+}
+
+// ============================================================================================
+// k_voxel: surfPointsLessFlatScan -> VoxelGrid (leaf 0.2) per ring, one wave per ring.  A kernel
+// of its own so the register-resident voxel sort's VGPRs do not cut k_extract's occupancy.
+// ============================================================================================
+__global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
+  __shared__ ExtractLds L;
+  const int V = P.V, VH = P.VH;
+  const int b = blockIdx.x, sl = b / V, s = P.s0 + sl;
+  const int ring = (b % V + sl / max(P.ncu / V, 1)) % V;  // ring rotation as in k_extract
+  const int st = B.ring_start[(size_t)s * V + ring], en = B.ring_end[(size_t)s * V + ring];
+  ScanView v;
+  v.M = B.counts[(size_t)s * CNT_N + CNT_M];
+  v.VH = VH;
+  v.flabel = B.flabel + (size_t)s * VH;
+  v.fa = B.seg_fa + (size_t)s * VH;
+  PROF_T(t_lf0);
+  const int nlist = lessflat_list(v, st, en, L.vval);
+  PROF_ADD(3, t_lf0);
+  RingOut o;
+  const size_t rb = (size_t)s * V + ring;
+  o.lflat = B.r_lflat + rb * P.H;
+  o.nLF = 0;
+  o.status = 0;
   PROF_T(t_vox0);
   voxel_ring(P, v, L, nlist, st, o);
   PROF_ADD(4, t_vox0);
+  if (lane_id() == 0) {
+    B.r_counts[rb * 4 + 3] = o.nLF;
+    if (o.status) B.r_status[rb] |= o.status;
+  }
 }
 
-__global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_pass) {
-  __shared__ ExtractLds L;
+__global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
+  __shared__ SegLds L;
   const int V = P.V, VH = P.VH;
-  // Workgroups reach the CUs round-robin, so with ring = blockIdx % V a CU would only ever see one
-  // ring index (the upper, non-ground rings are the heavy ones).  Rotating the ring by the stream
-  // block (s / (ncu / V)) gives every CU every ring index; the map stays a bijection per stream.
-  const int sl = first_pass ? blockIdx.x : blockIdx.x / V;
+  // Blocks [0, n): the first pass of scan s0 + b.  Rings whose range starts at position 4 (the
+  // leading rings) read the stale slot 4 of the persistent smoothness array, whose index may point
+  // into any ring: they run first, in order, on one wave.  Blocks [n, n + n*V): one ring each.
+  // Every other ring only reads/writes its own position range (+-5), so it runs at once unless
+  // that range meets the stale index's +-5 zone; then it waits for its scan's first pass
+  // (SURVEY.md Appendix B/C).  Workgroups are dispatched in index order, so a waiting ring only
+  // ever waits on a first-pass wave that is already resident.
+  const int nS = gridDim.x / (V + 1);
+  const bool first_pass = (int)blockIdx.x < nS;
+  const int b = first_pass ? (int)blockIdx.x : (int)blockIdx.x - nS;
+  // Workgroups reach the CUs round-robin, so with ring = b % V a CU would only ever see one ring
+  // index (the upper, non-ground rings are the heavy ones).  Rotating the ring by the stream block
+  // (sl / (ncu / V)) gives every CU every ring index; the map stays a bijection per stream.
+  const int sl = first_pass ? b : b / V;
   const int s = P.s0 + sl;
   const int rot = sl / max(P.ncu / V, 1);
-  const int ring = first_pass ? 0 : (int)((blockIdx.x % V + rot) % V);
+  const int ring = first_pass ? 0 : (b % V + rot) % V;
   const int32_t* rs = B.ring_start + (size_t)s * V;
   const int32_t* re = B.ring_end + (size_t)s * V;
+  int32_t* sync = B.fp_sync + 2 * (size_t)s;
   ScanView v;
   v.M = B.counts[(size_t)s * CNT_N + CNT_M];
   v.VH = VH;
@@ -1340,17 +1409,20 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_
   v.gflag = B.seg_ground + (size_t)s * VH;
   v.fa = B.seg_fa + (size_t)s * VH;
   int2* smooth = B.smooth + (size_t)s * VH;
-  // Rings whose range starts at position 4 (the leading rings) read the stale slot 4 of the
-  // persistent smoothness array, whose index may point into any ring: they run first, in order,
-  // on one wave.  Every other ring only reads/writes its own position range (+-5), so the rest
-  // run one wave per ring in parallel.
+  if (!first_pass) {
+    if (rs[ring] == 4) return;  // a leading ring: done by the first pass
+    const int stale = sync[0];
+    if (stale + 5 >= rs[ring] - 5 && stale - 5 <= re[ring] + 5) {
+      while (__hip_atomic_load(sync + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != P.epoch)
+        __builtin_amdgcn_s_sleep(4);
+#ifdef LG_PROFILE
+      if (lane_id() == 0) atomicAdd(&PROF_SLOT(30), 1ull);
+#endif
+    }
+  }
   const int r0 = first_pass ? 0 : ring, r1 = first_pass ? V : ring + 1;
   for (int r = r0; r < r1; ++r) {
-    const bool leading = rs[r] == 4;
-    if (first_pass ? !leading : leading) {
-      if (first_pass) break;
-      return;
-    }
+    if (first_pass && rs[r] != 4) break;
     RingOut o;
     const size_t rb = (size_t)s * V + r;
     o.sharp = B.r_sharp + rb * P.cap_sharp; o.sharp_ind = B.r_sharp_ind + rb * P.cap_sharp;
@@ -1370,10 +1442,14 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B, int first_
 #endif
     if (lane_id() == 0) {
       int32_t* rc = B.r_counts + rb * 4;
-      rc[0] = o.nS; rc[1] = o.nLS; rc[2] = o.nF; rc[3] = o.nLF;
+      rc[0] = o.nS; rc[1] = o.nLS; rc[2] = o.nF;  // rc[3]: k_voxel
       B.r_status[rb] = o.status;
     }
     __syncthreads();
+  }
+  if (first_pass) {
+    __threadfence();
+    if (lane_id() == 0) __hip_atomic_store(sync + 1, P.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2287,9 +2363,9 @@ int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
 }
 
 int lg_launch_extract(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  hipLaunchKernelGGL(k_extract, dim3(S), dim3(64), 0, st, P, B, 1);
+  hipLaunchKernelGGL(k_extract, dim3(S * (P.V + 1)), dim3(64), 0, st, P, B);
   LG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_extract, dim3(S * P.V), dim3(64), 0, st, P, B, 0);
+  hipLaunchKernelGGL(k_voxel, dim3(S * P.V), dim3(64), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }

@@ -321,6 +321,50 @@ def test_edge_inputs(gpu):
         fe.close()
 
 
+def _ring0_cropped(pts, keep):
+    """Drop all but the first `keep` points of VLP-16 ring 0 (elevation -15 deg)."""
+    el = np.degrees(np.arctan2(pts[:, 2], np.hypot(pts[:, 0], pts[:, 1])))
+    r0 = np.nonzero(np.round((el + 15) / 2) == 0)[0]
+    return np.delete(pts, r0[keep:], axis=0)
+
+
+def test_stale_slot_points_into_later_ring(gpu):
+    """The stale slot 4 of the smoothness array keeps its initial {0, 0} unless a fresh zero curvature
+    ties with it.  Even scans get exactly constant ranges over ring 0's first segment (curvature 0,
+    the introsort then leaves a fresh index in slot 4); odd scans cut ring 0 to a few points, so that
+    index lands in ring 1, which must wait for its scan's first pass in k_extract.  Fed through the
+    injected-projection path (the Channel hop) to GPU and oracle alike."""
+    import oracle as O
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    src = O.Oracle(params)
+    projs = []
+    for k in range(6):
+        pts = A.synth_scan(cfg, 11, k)
+        pr = src.cloud_handler(pts if k % 2 == 0 else _ring0_cropped(pts, 40))
+        src.feature_association()
+        if k % 2 == 0:
+            r = np.array(pr["segmented_cloud_range"])
+            r[4:200] = 4.0
+            pr["segmented_cloud_range"] = r
+        projs.append(pr)
+    fe = L.Frontend(params)
+    orc = oracle_for(params)
+    foreign = 0
+    for k, pr in enumerate(projs):
+        stale = orc.smoothness(4)[1]
+        fr = orc.feature_association(pr)
+        fg = fe.feature_association(pr)
+        bad = Hs.diff_report(Hs.FEAT_KEYS, fg, fr)
+        assert not bad, (k, bad)
+        assert fg["status"] == fr["status"], (k, hex(fg["status"]), hex(fr["status"]))
+        np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
+        rs, re = np.asarray(pr["start_ring_index"]), np.asarray(pr["end_ring_index"])
+        foreign += int(any(rs[r] != 4 and stale + 5 >= rs[r] - 5 and stale - 5 <= re[r] + 5 for r in range(16)))
+    fe.close()
+    assert foreign >= 2, foreign  # the case under test actually happened
+
+
 def test_full_size_batch_properties(gpu):
     """Bench-size batch (256 sequences): size-independent properties on every stream and exact
     parity on a sample of streams."""

@@ -53,6 +53,7 @@ def main():
     tot = sum(prof[i] for i in NAMES if i < 17 or i >= 20)
     nsteps = steps - 1
     print("segments sorted via the tie path: %d per step (of %d segments)" % (prof[14] / nsteps, S * 16 * 6))
+    print("rings waiting for their scan's first pass: %d per step (of %d rings)" % (prof[30] / nsteps, S * 16))
     for i, nm in NAMES.items():
         print("%-20s %14.0f cycles/step  (%5.1f%%)  per ring-wave %.0f  per stream %.0f  max one %.0f" % (
             nm, prof[i] / nsteps, 100.0 * prof[i] / max(tot, 1), prof[i] / nsteps / (S * 16), prof[i] / nsteps / S,
