@@ -809,12 +809,13 @@ LG_DEVICE int wave_partition_stream(const SortView<K, V>& a, int first, int last
   }
 }
 
-template <int R>
-LG_DEVICE void seg_final_bitonic(float* key, int* val, int n);
+template <int R, typename K, typename V>
+LG_DEVICE void final_bitonic(K* key, V* val, int n);
 
-// final_reg: n <= 512 float keys, none negative or NaN -> __final_insertion_sort is computed as a
-// register sort by (key, position): it is stable and never moves an element across a partition
-// cut, so its result is the post-partition array stably sorted by key.
+// final_reg: __final_insertion_sort is computed as a register sort by (key, position): it is stable
+// and never moves an element across a partition cut, so its result is the post-partition array
+// stably sorted by key.  Needs key bit order == key order: unsigned keys, or float keys none
+// negative or NaN (the caller checks); n <= 2048 (unsigned) / 512 (float).
 template <typename K, typename V>
 LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int* tab, bool final_reg = false) {
   const int lane = lane_id();
@@ -862,15 +863,17 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
   }
   PROF_ADD(6, t_part0);
   PROF_T(t_fin0);
-  if constexpr (sizeof(K) == 4 && sizeof(V) == 4 && !std::is_integral<K>::value) {
-    if (final_reg) {
-      if (n <= 64) seg_final_bitonic<1>((float*)key, (int*)val, n);
-      else if (n <= 128) seg_final_bitonic<2>((float*)key, (int*)val, n);
-      else if (n <= 256) seg_final_bitonic<4>((float*)key, (int*)val, n);
-      else seg_final_bitonic<8>((float*)key, (int*)val, n);
-      PROF_ADD(11, t_fin0);
-      return;
+  if (final_reg && (n <= 512 || std::is_integral<K>::value)) {
+    if (n <= 64) final_bitonic<1>(key, val, n);
+    else if (n <= 128) final_bitonic<2>(key, val, n);
+    else if (n <= 256) final_bitonic<4>(key, val, n);
+    else if (n <= 512) final_bitonic<8>(key, val, n);
+    else if constexpr (std::is_integral<K>::value) {
+      if (n <= 1024) final_bitonic<16>(key, val, n);
+      else final_bitonic<32>(key, val, n);
     }
+    PROF_ADD(11, t_fin0);
+    return;
   }
   // __final_insertion_sort as independent per-block insertion sorts: lane h sorts the blocks that
   // start in positions [16h, 16h + 16).
@@ -1026,26 +1029,31 @@ LG_DEVICE void reg_bitonic_u64(unsigned long long (&a)[R]) {
   }
 }
 
+LG_DEVICE unsigned key_bits(float k) { return (unsigned)__float_as_int(k); }
+LG_DEVICE unsigned key_bits(unsigned k) { return k; }
+LG_DEVICE void key_from_bits(float& k, unsigned b) { k = __int_as_float((int)b); }
+LG_DEVICE void key_from_bits(unsigned& k, unsigned b) { k = b; }
+
 // The post-partition array [0, n) sorted by (key bits, position), values gathered by position.
-template <int R>
-LG_DEVICE void seg_final_bitonic(float* key, int* val, int n) {
+template <int R, typename K, typename V>
+LG_DEVICE void final_bitonic(K* key, V* val, int n) {
   const int lane = lane_id();
   unsigned long long a[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int e = lane * R + r;
-    a[r] = e < n ? (((unsigned long long)(unsigned)__float_as_int(key[e]) << 32) | (unsigned)e) : ~0ull;
+    a[r] = e < n ? (((unsigned long long)key_bits(key[e]) << 32) | (unsigned)e) : ~0ull;
   }
   reg_bitonic_u64<R>(a);
-  int vg[R];
+  V vg[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) vg[r] = (lane * R + r < n) ? val[(unsigned)a[r]] : 0;
+  for (int r = 0; r < R; ++r) vg[r] = (lane * R + r < n) ? val[(unsigned)a[r]] : V(0);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int e = lane * R + r;
     if (e < n) {
-      key[e] = __int_as_float((int)(a[r] >> 32));
+      key_from_bits(key[e], (unsigned)(a[r] >> 32));
       val[e] = vg[r];
     }
   }
@@ -1200,7 +1208,7 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
   __syncthreads();
   PROF_T(t_vs0);
   if (P.voxel_stable) voxel_sort_stable(L.u.vkey, L.vval, n);
-  else wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
+  else wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
   PROF_ADD(5, t_vs0);
   int running = 0;
   for (int base = 0; base < n; base += 64) {
@@ -2430,7 +2438,7 @@ __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int
   } else if (is_float) {
     wave_std_sort<float, uint16_t>((float*)L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
   } else {
-    wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
+    wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);  // as k_voxel
   }
   for (int i = lane; i < n; i += 64) { keys[i] = L.u.vkey[i]; vals[i] = L.vval[i]; }
 }
