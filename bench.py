@@ -235,7 +235,8 @@ def main():
                    "voxel_tie_order": args.voxel_tie_order},
         "roofline": roofline,
         "stages_ms": {"project": round(stage[0], 4), "segment": round(stage[1], 4), "fa_prep": round(stage[2], 4),
-                      "extract": round(stage[3], 4), "concat": round(stage[4], 4), "lm": round(stage[5], 4)},
+                      "extract": round(stage[3], 4), "concat_voxel": round(stage[4], 4),
+                      "lm_publish": round(stage[5], 4)},
         "other_voxel_tie_order": alt,
         "lm_status_bits": int(np.bitwise_or.reduce(status)),
         "trajectories_gathered": int(traj_all.shape[0]),

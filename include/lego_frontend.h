@@ -158,9 +158,15 @@ int  lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, 
 void lego_batch_destroy(lego_batch* b);
 /* Advance every stream by one scan.  d_points: DEVICE array of lego_point (x,y,z,intensity);
  * stream s's scan is d_points[d_offsets[s] .. d_offsets[s] + d_counts[s]).  d_offsets / d_counts are
- * DEVICE arrays (int64 / int32) of length n_streams.  Asynchronous on hip_stream (NULL = default). */
+ * DEVICE arrays (int64 / int32) of length n_streams.  Asynchronous on hip_stream (NULL = default).
+ * The step's VoxelGrid runs on an internal stream, overlapping its LM and the next step's front end;
+ * the lessFlat half of publishCloudsLast is issued by the next step (before its LM) or by
+ * lego_batch_flush / lego_batch_sync / lego_batch_read*, which all see completed scans. */
 int  lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_offsets,
                      const int32_t* d_counts, void* hip_stream);
+/* Enqueue the last step's pending work on its stream (asynchronous); then a device synchronize sees
+ * every output of that step. */
+int  lego_batch_flush(lego_batch* b);
 int  lego_batch_sync(lego_batch* b);
 /* Copy one stream's last projection / association outputs to host (blocking). */
 int  lego_batch_read(lego_batch* b, int32_t s, lego_projection_out* proj, lego_association_out* assoc);

@@ -33,6 +33,8 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int ncu;                              // compute units of the device (k_extract's ring rotation)
   int voxel_stable;                     // lego_params.voxel_tie_order == 1
   int epoch;                            // per-launch token for k_extract's first-pass flags
+  int par;                              // lessFlat staging half of this step (k_concat -> k_voxel)
+  int S;                                // streams of the batch (staging stride)
 };
 
 struct LgState {  // FeatureAssociation members that persist across scans (featureAssociation.h)
@@ -47,7 +49,7 @@ struct LgState {  // FeatureAssociation members that persist across scans (featu
   int status;            // LEGO_ST_* of the last association
   int iters_surf, iters_corner;
   int proj_status;       // 0 or LEGO_EEMPTY for the last projection
-  int pad;
+  int pub_copy;          // k_publish stores the lessFlat cloud untransformed (checkSystemInitialization)
   double quat[4];
   double pos[3];
 };
@@ -91,9 +93,12 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   float4* r_sharp; int32_t* r_sharp_ind;    // [S][V][cap_sharp]
   float4* r_lsharp; int32_t* r_lsharp_ind;  // [S][V][cap_lsharp]
   float4* r_flat; int32_t* r_flat_ind;      // [S][V][cap_flat]
-  float4* r_lflat;                          // [S][V][H]
-  int32_t* r_counts;                        // [S][V][4]
-  int32_t* r_status;                        // [S][V]
+  float4* r_lflat;                          // [S][V][H]   VoxelGrid output per ring
+  int32_t* r_counts;                        // [S][V][4]   sharp, lessSharp, flat, lessFlat (k_voxel)
+  int32_t* r_status;                        // [S][V]      k_extract status bits
+  int32_t* r_vstatus;                       // [S][V]      k_voxel status bits
+  float4* lf_stage;                         // [2][S][V][H] surfPointsLessFlatScan per ring (k_concat)
+  int32_t* lf_count;                        // [2][S][V]
   // concatenated features
   float4* f_sharp; int32_t* f_sharp_ind;    // [S][V*cap_sharp]
   float4* f_lsharp; int32_t* f_lsharp_ind;  // [S][V*cap_lsharp]

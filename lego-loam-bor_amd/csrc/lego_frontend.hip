@@ -18,10 +18,12 @@
 int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
                       const int32_t* cnts, hipStream_t st);
 int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
-int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
+int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st, bool distort);
 int lg_launch_extract(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
 int lg_launch_concat(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
 int lg_launch_lm(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
+int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
+int lg_launch_publish(const LgParams& P, const LgBufs& B, int S, hipStream_t st);
 
 namespace {
 
@@ -102,6 +104,15 @@ struct lego_batch {
   hipStream_t gs[LEGO_MAX_GROUPS] = {};
   hipEvent_t fork = nullptr, join[LEGO_MAX_GROUPS] = {};
   hipStream_t last_stream = nullptr;
+  // VoxelGrid overlap: each slice's k_voxel runs on a side stream (vs) while the slice goes on with
+  // k_lm and the next scan's front end; the lessFlat half of publishCloudsLast (k_publish) of scan k
+  // is issued just before scan k+1's k_lm, or by lego_batch_flush.
+  hipStream_t vs[LEGO_MAX_GROUPS] = {};
+  hipEvent_t ev_cat[LEGO_MAX_GROUPS] = {}, ev_vox[LEGO_MAX_GROUPS] = {};
+  bool pending = false;      // k_publish of the last step not issued yet
+  int pend_groups = 1;       // slices of that step
+  hipStream_t pend_stream = nullptr;
+  int par = 0;               // lessFlat staging half of the next step
   // host mirrors for lego_batch_read
   std::vector<lego_point> h_seg, h_out, h_scan, h_sharp, h_lsharp, h_flat, h_lflat, h_clast, h_slast, h_olast;
   std::vector<int32_t> h_rs, h_re, h_label, h_sharp_ind, h_lsharp_ind, h_flat_ind;
@@ -117,6 +128,9 @@ struct lego_batch {
     for (int g = 0; g < LEGO_MAX_GROUPS; ++g) {
       if (gs[g]) hipStreamDestroy(gs[g]);
       if (join[g]) hipEventDestroy(join[g]);
+      if (vs[g]) hipStreamDestroy(vs[g]);
+      if (ev_cat[g]) hipEventDestroy(ev_cat[g]);
+      if (ev_vox[g]) hipEventDestroy(ev_vox[g]);
     }
     if (fork) hipEventDestroy(fork);
   }
@@ -207,6 +221,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
   b->P.ncu = ncu;
+  b->P.S = n_streams;
   b->S = n_streams;
   b->max_points = max_points;
   b->device = device;
@@ -216,7 +231,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   const size_t S = n_streams, VH = P.VH, V = P.V, H = P.H;
   std::vector<void*>& o = b->owned;
   bool lds_proj = (size_t)(P.VH + 64) * 4 <= 160 * 1024;
-  bool lds_seg = P.V <= 16 && lds_proj;
+  bool lds_seg = P.V <= 16 && P.VH < 32768;  // lg_lds_segment
   rc = LEGO_OK;
 #define A(ptr, n) if (rc == LEGO_OK) rc = dalloc(&B.ptr, (n), o)
   A(range, S * VH); A(cloud, S * VH); A(ground, S * VH); A(label, S * VH);
@@ -229,7 +244,8 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   A(r_sharp, S * V * P.cap_sharp); A(r_sharp_ind, S * V * P.cap_sharp);
   A(r_lsharp, S * V * P.cap_lsharp); A(r_lsharp_ind, S * V * P.cap_lsharp);
   A(r_flat, S * V * P.cap_flat); A(r_flat_ind, S * V * P.cap_flat);
-  A(r_lflat, S * V * H); A(r_counts, S * V * 4); A(r_status, S * V);
+  A(r_lflat, S * V * H); A(r_counts, S * V * 4); A(r_status, S * V); A(r_vstatus, S * V);
+  A(lf_stage, 2 * S * V * H); A(lf_count, 2 * S * V);
   A(f_sharp, S * V * P.cap_sharp); A(f_sharp_ind, S * V * P.cap_sharp);
   A(f_lsharp, S * V * P.cap_lsharp); A(f_lsharp_ind, S * V * P.cap_lsharp);
   A(f_flat, S * V * P.cap_flat); A(f_flat_ind, S * V * P.cap_flat);
@@ -264,6 +280,8 @@ int lego_batch_reset(lego_batch* b) {
   if (hipMemset(B.smooth, 0, S * VH * sizeof(int2)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fp_sync, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   b->epoch = 0;
+  b->pending = false;
+  b->par = 0;
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.counts, 0, S * CNT_N * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
@@ -296,23 +314,77 @@ static int run_projection(lego_batch* b, const float4* pts, const int64_t* offs,
   return LEGO_OK;
 }
 
-static int run_association(lego_batch* b, hipStream_t st, int s0, int n) {
+// One slice [s0, s0 + n) of the streams through FeatureAssociation.  distort: the ProjectionOut came
+// from the host (adjustDistortion / adjustOutlierCloud run in k_fa_prep instead of k_segment).
+// overlap == false: everything in order on st, k_publish included (single context, stage timing).
+// overlap == true: k_voxel on the slice's side stream vs[g]; the previous step's k_publish (joined
+// with its k_voxel) goes in before this step's k_lm, this step's stays pending.
+static int run_association(lego_batch* b, hipStream_t st, int s0, int n, bool distort = false, bool overlap = false,
+                           int g = 0) {
   LgParams P = b->P;
   P.s0 = s0;
-  b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
   P.epoch = b->epoch;
-  int rc = lg_launch_fa_prep(P, b->B, n, st);
+  P.par = b->par;
+  int rc = lg_launch_fa_prep(P, b->B, n, st, distort);
   if (rc) return rc;
   if (b->timing) hipEventRecord(b->ev[3], st);
   rc = lg_launch_extract(P, b->B, n, st);
   if (rc) return rc;
-  if (b->timing) hipEventRecord(b->ev[4], st);
+  if (!overlap) {
+    if (b->timing) hipEventRecord(b->ev[4], st);
+    rc = lg_launch_concat(P, b->B, n, st);
+    if (!rc) rc = lg_launch_voxel(P, b->B, n, st);
+    if (rc) return rc;
+    if (b->timing) hipEventRecord(b->ev[5], st);
+    rc = lg_launch_lm(P, b->B, n, st);
+    if (!rc) rc = lg_launch_publish(P, b->B, n, st);
+    if (rc) return rc;
+    if (b->timing) hipEventRecord(b->ev[6], st);
+    return LEGO_OK;
+  }
   rc = lg_launch_concat(P, b->B, n, st);
   if (rc) return rc;
-  if (b->timing) hipEventRecord(b->ev[5], st);
-  rc = lg_launch_lm(P, b->B, n, st);
+  if (b->pending) {  // scan k-1's lessFlat publish: after its k_voxel, before this scan's k_lm
+    if (hipStreamWaitEvent(st, b->ev_vox[g], 0) != hipSuccess) return LEGO_EDEVICE;
+    rc = lg_launch_publish(P, b->B, n, st);
+    if (rc) return rc;
+  }
+  if (hipEventRecord(b->ev_cat[g], st) != hipSuccess) return LEGO_EDEVICE;
+  if (hipStreamWaitEvent(b->vs[g], b->ev_cat[g], 0) != hipSuccess) return LEGO_EDEVICE;
+  rc = lg_launch_voxel(P, b->B, n, b->vs[g]);
   if (rc) return rc;
-  if (b->timing) hipEventRecord(b->ev[6], st);
+  if (hipEventRecord(b->ev_vox[g], b->vs[g]) != hipSuccess) return LEGO_EDEVICE;
+  return lg_launch_lm(P, b->B, n, st);
+}
+
+static int ensure_streams(lego_batch* b, int groups) {
+  if (!b->fork && hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
+  for (int g = 0; g < groups; ++g) {
+    if (!b->gs[g] && hipStreamCreateWithFlags(&b->gs[g], hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
+    if (!b->join[g] && hipEventCreateWithFlags(&b->join[g], hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
+    if (!b->vs[g] && hipStreamCreateWithFlags(&b->vs[g], hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
+    if (!b->ev_cat[g] && hipEventCreateWithFlags(&b->ev_cat[g], hipEventDisableTiming) != hipSuccess)
+      return LEGO_EDEVICE;
+    if (!b->ev_vox[g] && hipEventCreateWithFlags(&b->ev_vox[g], hipEventDisableTiming) != hipSuccess)
+      return LEGO_EDEVICE;
+  }
+  return LEGO_OK;
+}
+
+// Issue the pending k_publish (joined with its k_voxel) on the stream of the step that left it.
+static int flush_pending(lego_batch* b) {
+  if (!b->pending) return LEGO_OK;
+  const int G = b->pend_groups;
+  for (int g = 0; g < G; ++g) {
+    const int s0 = (int)((long long)b->S * g / G), s1 = (int)((long long)b->S * (g + 1) / G);
+    LgParams P = b->P;
+    P.s0 = s0;
+    hipStream_t st = b->pend_stream;
+    if (hipStreamWaitEvent(st, b->ev_vox[g], 0) != hipSuccess) return LEGO_EDEVICE;
+    int rc = lg_launch_publish(P, b->B, s1 - s0, st);
+    if (rc) return rc;
+  }
+  b->pending = false;
   return LEGO_OK;
 }
 
@@ -320,11 +392,10 @@ int lego_batch_set_groups(lego_batch* b, int32_t groups) {
   if (!b || groups < 1 || groups > LEGO_MAX_GROUPS) return LEGO_EINVAL;
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   groups = groups > b->S ? b->S : groups;
-  if (!b->fork && hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
-  for (int g = 0; g < groups; ++g) {
-    if (!b->gs[g] && hipStreamCreateWithFlags(&b->gs[g], hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
-    if (!b->join[g] && hipEventCreateWithFlags(&b->join[g], hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
-  }
+  int rc = flush_pending(b);  // the pending publish belongs to the old slicing
+  if (rc) return rc;
+  rc = ensure_streams(b, groups);
+  if (rc) return rc;
   b->groups = groups;
   return LEGO_OK;
 }
@@ -334,31 +405,59 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   if (!b || !d_points || !d_offsets || !d_counts) return LEGO_EINVAL;
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   hipStream_t st = (hipStream_t)hip_stream;
-  b->last_stream = st;
-  if (b->timing || b->groups <= 1) {  // one stream (per-stage timing needs the stages in order)
-    if (b->timing) hipEventRecord(b->ev[0], st);
-    int rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+  b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
+  if (b->timing) {  // per-stage timing: one stream, stages in order, nothing left pending
+    int rc = flush_pending(b);
     if (rc) return rc;
-    return run_association(b, st, 0, b->S);
+    b->last_stream = st;
+    hipEventRecord(b->ev[0], st);
+    rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+    if (!rc) rc = run_association(b, st, 0, b->S);
+    b->par ^= 1;
+    return rc;
   }
-  if (hipEventRecord(b->fork, st) != hipSuccess) return LEGO_EDEVICE;
   const int G = b->groups;
-  for (int g = 0; g < G; ++g) {
-    const int s0 = (int)((long long)b->S * g / G), s1 = (int)((long long)b->S * (g + 1) / G);
-    if (hipStreamWaitEvent(b->gs[g], b->fork, 0) != hipSuccess) return LEGO_EDEVICE;
-    int rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, b->gs[g], s0, s1 - s0);
+  int rc = ensure_streams(b, G);
+  if (rc) return rc;
+  if (b->pending && (b->pend_groups != G || b->pend_stream != st)) {
+    rc = flush_pending(b);
     if (rc) return rc;
-    rc = run_association(b, b->gs[g], s0, s1 - s0);
-    if (rc) return rc;
-    if (hipEventRecord(b->join[g], b->gs[g]) != hipSuccess) return LEGO_EDEVICE;
-    if (hipStreamWaitEvent(st, b->join[g], 0) != hipSuccess) return LEGO_EDEVICE;
   }
+  b->last_stream = st;
+  if (G <= 1) {
+    rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+    if (!rc) rc = run_association(b, st, 0, b->S, false, true, 0);
+  } else {
+    if (hipEventRecord(b->fork, st) != hipSuccess) return LEGO_EDEVICE;
+    for (int g = 0; g < G && !rc; ++g) {
+      const int s0 = (int)((long long)b->S * g / G), s1 = (int)((long long)b->S * (g + 1) / G);
+      if (hipStreamWaitEvent(b->gs[g], b->fork, 0) != hipSuccess) return LEGO_EDEVICE;
+      rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, b->gs[g], s0, s1 - s0);
+      if (!rc) rc = run_association(b, b->gs[g], s0, s1 - s0, false, true, g);
+      if (rc) break;
+      if (hipEventRecord(b->join[g], b->gs[g]) != hipSuccess) return LEGO_EDEVICE;
+      if (hipStreamWaitEvent(st, b->join[g], 0) != hipSuccess) return LEGO_EDEVICE;
+    }
+  }
+  if (rc) return rc;
+  b->pending = true;
+  b->pend_groups = G;
+  b->pend_stream = st;
+  b->par ^= 1;
   return LEGO_OK;
+}
+
+int lego_batch_flush(lego_batch* b) {
+  if (!b) return LEGO_EINVAL;
+  if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
+  return flush_pending(b);
 }
 
 int lego_batch_sync(lego_batch* b) {
   if (!b) return LEGO_EINVAL;
   hipSetDevice(b->device);
+  int rc = flush_pending(b);
+  if (rc) return rc;
   return hipDeviceSynchronize() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }
 
@@ -469,6 +568,7 @@ static int read_assoc(lego_batch* b, int s, lego_association_out* o) {
 int lego_batch_read(lego_batch* b, int32_t s, lego_projection_out* proj, lego_association_out* assoc) {
   if (!b || s < 0 || s >= b->S) return LEGO_EINVAL;
   hipSetDevice(b->device);
+  if (flush_pending(b) != LEGO_OK) return LEGO_EDEVICE;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
   if (proj) {
     int rc = read_proj(b, s, proj);
@@ -484,6 +584,7 @@ int lego_batch_read(lego_batch* b, int32_t s, lego_projection_out* proj, lego_as
 int lego_batch_read_poses(lego_batch* b, float* out, int32_t* status) {
   if (!b) return LEGO_EINVAL;
   hipSetDevice(b->device);
+  if (flush_pending(b) != LEGO_OK) return LEGO_EDEVICE;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
   std::vector<LgState> S(b->S);
   if (hipMemcpy(S.data(), b->B.state, S.size() * sizeof(LgState), hipMemcpyDeviceToHost) != hipSuccess)
@@ -502,6 +603,7 @@ int lego_batch_read_poses(lego_batch* b, float* out, int32_t* status) {
 int lego_batch_read_counts(lego_batch* b, int32_t* out) {
   if (!b || !out) return LEGO_EINVAL;
   hipSetDevice(b->device);
+  if (flush_pending(b) != LEGO_OK) return LEGO_EDEVICE;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
   std::vector<int32_t> c((size_t)b->S * CNT_N);
   if (hipMemcpy(c.data(), b->B.counts, c.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
@@ -582,15 +684,20 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
   return LEGO_OK;
 }
 
-int lego_feature_association(lego_ctx* c, lego_association_out* out) {
-  if (!c) return LEGO_EINVAL;
+static int feature_association(lego_ctx* c, lego_association_out* out, bool distort) {
   lego_batch* b = c->b;
   hipSetDevice(b->device);
-  int rc = run_association(b, nullptr, 0, 1);
+  b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
+  int rc = run_association(b, nullptr, 0, 1, distort);
   if (rc) return rc;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
   if (out) return read_assoc(b, 0, out);
   return LEGO_OK;
+}
+
+int lego_feature_association(lego_ctx* c, lego_association_out* out) {
+  if (!c) return LEGO_EINVAL;
+  return feature_association(c, out, false);
 }
 
 int lego_feature_association_from(lego_ctx* c, const lego_projection_out* in, lego_association_out* out) {
@@ -618,7 +725,7 @@ int lego_feature_association_from(lego_ctx* c, const lego_projection_out* in, le
   int32_t cnt[CNT_N] = {M, in->n_outlier, 0, 0, 0, 0, 0, 0};
   up(B.counts, cnt, sizeof(cnt));
   if (!ok) return LEGO_EDEVICE;
-  return lego_feature_association(c, out);
+  return feature_association(c, out, true);
 }
 
 }  // extern "C"

@@ -59,6 +59,20 @@ LG_DEVICE int popc_below(unsigned long long m) {
   return __popcll(m & ((1ull << lane_id()) - 1ull));
 }
 
+// Raw buffer access: a load whose byte offset is >= num_records returns 0 and touches no memory,
+// which makes per-lane predicated loads branch-free (no wait inside a divergent branch).
+LG_DEVICE __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+LG_DEVICE float4 buffer_load_f4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
+}
+LG_DEVICE float buffer_load_f1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __int_as_float((int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+
 template <typename T>
 LG_DEVICE T wave_min(T v) {
   for (int o = 32; o > 0; o >>= 1) {
@@ -134,9 +148,7 @@ LG_DEVICE int block_max_int(int v, int* scratch) {
 // The reference's scatter "later input point overwrites earlier ones in the same cell"
 // (imageProjection.cpp:214-222) is an atomicMax of the input index per cell, followed by a
 // column-parallel gather that writes every cell (so resetParameters' fill is fused in).
-// kRows > 0: the column pass keeps its (at most kRows) cells in registers, so the 2-D scan does not
-// re-read the range/cloud images it has just written (PMC: that re-read was 40% of FETCH_SIZE).
-template <bool kLdsWinner, int kRows>
+template <bool kLdsWinner>
 __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                   const int64_t* __restrict__ offs,
                                                   const int32_t* __restrict__ cnts) {
@@ -153,32 +165,39 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   PROF_ADD(20, t_p0);
   PROF_T(t_p1);
   int fmin = 0x7fffffff, fmax = -1;
-  constexpr int kUnroll = 4;  // four independent point loads in flight per lane
-  for (int i0 = tid; i0 < n; i0 += nt * kUnroll) {
-    float4 pk[kUnroll];
+  // kU point loads per lane are issued before any of them is used: the loads are unconditional
+  // (index clamped to n - 1), so no per-load branch forces a wait between them.
+  constexpr int kU = 8;
+  for (int i0 = tid; i0 < n; i0 += nt * kU) {
+    float4 pk[kU];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const int i = i0 + u * nt;
-      pk[u] = (i < n) ? in[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int u = 0; u < kU; ++u) pk[u] = in[min(i0 + u * nt, n - 1)];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < kU; ++u) {
       const int i = i0 + u * nt;
       const float4 p = pk[u];
-      if (i >= n) break;
-      if (!isfinite_f(p.x) || !isfinite_f(p.y) || !isfinite_f(p.z)) continue;  // removeNaNFromPointCloud
-      fmin = min(fmin, i);
-      fmax = max(fmax, i);
-      float range = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-      float verticalAngle = asinf_g(p.z / range);
-      int rowIdn = (int)((verticalAngle + P.ang_bottom) / P.ang_res_y);
-      if (rowIdn < 0 || rowIdn >= V) continue;
-      float horizonAngle = atan2f_g(p.x, p.y);
-      int columnIdn = (int)(-round(((double)horizonAngle - M_PI_2) / (double)P.ang_res_x) + H * 0.5);
-      if (columnIdn >= H) columnIdn -= H;
-      if (columnIdn < 0 || columnIdn >= H) continue;
-      if ((double)range < 0.1) continue;
-      atomicMax(&winner[rowIdn * H + columnIdn], i);
+      if (i < n && isfinite_f(p.x) && isfinite_f(p.y) && isfinite_f(p.z)) {  // removeNaNFromPointCloud
+        fmin = min(fmin, i);
+        fmax = max(fmax, i);
+#ifdef LG_EXPERIMENT_FAST
+        const float range = __fsqrt_rn(p.x * p.x + p.y * p.y + p.z * p.z);
+        const float verticalAngle = __ocml_asin_f32(p.z * __frsqrt_rn(p.x * p.x + p.y * p.y + p.z * p.z));
+        const int rowIdn = (int)((verticalAngle + P.ang_bottom) * (1.0f / P.ang_res_y));
+        if (rowIdn >= 0 && rowIdn < V) {
+          const float horizonAngle = __ocml_atan2_f32(p.x, p.y);
+          int columnIdn = (int)(-rintf((horizonAngle - (float)M_PI_2) * (1.0f / P.ang_res_x)) + H * 0.5f);
+#else
+        const float range = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+        const float verticalAngle = asinf_g(p.z / range);
+        const int rowIdn = (int)((verticalAngle + P.ang_bottom) / P.ang_res_y);
+        if (rowIdn >= 0 && rowIdn < V) {
+          const float horizonAngle = atan2f_g(p.x, p.y);
+          int columnIdn = (int)(-round(((double)horizonAngle - M_PI_2) / (double)P.ang_res_x) + H * 0.5);
+#endif
+          if (columnIdn >= H) columnIdn -= H;
+          if (columnIdn >= 0 && columnIdn < H && (double)range >= 0.1) atomicMax(&winner[rowIdn * H + columnIdn], i);
+        }
+      }
     }
   }
   PROF_ADD(21, t_p1);
@@ -204,67 +223,66 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   __syncthreads();
   PROF_ADD(22, t_p2);
   PROF_T(t_p3);
+  // Column pass: one lane per column walks the rows bottom-up.  Each chunk of 16 rows first reads
+  // its 16 winners and gathers their 16 points (unconditional loads, all in flight together), then
+  // writes range / cloud cells, the ground pairs (i-1, i) of groundRemoval (:271-285), and row i-1's
+  // ground flag and 2-D scan candidate (:312-330) as soon as pair (i-1, i) has settled it.
   float* range = B.range + (size_t)s * VH;
   float4* cloud = B.cloud + (size_t)s * VH;
   int8_t* ground = B.ground + (size_t)s * VH;
   const float qnan = __int_as_float(0x7fc00000);
+  const float4* src0 = n > 0 ? in : cloud;  // any readable address for empty cells (value unused)
   for (int j = tid; j < H; j += nt) {
     unsigned long long gmask = 0ull;
     float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
-    float rr[kRows > 0 ? kRows : 1], zz[kRows > 0 ? kRows : 1];
-    auto cell = [&](int i) {
-      const int c = i * H + j;
-      const int w = winner[c];
-      float4 q;
-      float r;
-      if (w >= 0) {
-        const float4 p = in[w];
-        r = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-        q = make_float4(p.x, p.y, p.z, (float)((double)(float)i + (double)(float)j / 10000.0));
-      } else {
-        r = FLT_MAX;
-        q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
-      }
-      range[c] = r;
-      cloud[c] = q;
-      if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
-        float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
-        float va = atan2f_g(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ));
-        if ((double)(va - P.mount) <= 10 * DEG_TO_RAD_D) gmask |= (3ull << (i - 1));
-      }
-      prev = q;
-      if constexpr (kRows > 0) {
-        rr[i] = r;
-        zz[i] = q.z;
-      }
-    };
-    if constexpr (kRows > 0) {
-#pragma unroll
-      for (int i = 0; i < kRows; ++i)
-        if (i < V) cell(i);
-    } else {
-      for (int i = 0; i < V; ++i) cell(i);
-    }
+    float prev_r = 0.f;
     float min_range = 1000.f;
     int id_min = -1;
-    auto scan = [&](int i, float r, float Z) {  // 2-D scan (:312-330)
+    const double jfrac = (double)(float)j / 10000.0;
+    auto scan = [&](int i, float r, float Z) {  // 2-D scan (:312-330), row i final
       const int c = i * H + j;
       const int g = (int)((gmask >> i) & 1ull);
       ground[c] = (int8_t)g;
-      if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f) {
-        if (r < min_range) {
-          min_range = r;
-          id_min = c;
-        }
+      if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f && r < min_range) {
+        min_range = r;
+        id_min = c;
       }
     };
-    if constexpr (kRows > 0) {
+    for (int i0 = 0; i0 < V; i0 += 16) {
+      int w[16];
+      float4 pk[16];
 #pragma unroll
-      for (int i = 0; i < kRows; ++i)
-        if (i < V) scan(i, rr[i], zz[i]);
-    } else {
-      for (int i = 0; i < V; ++i) scan(i, range[i * H + j], cloud[i * H + j].z);
+      for (int u = 0; u < 16; ++u) w[u] = (i0 + u < V) ? winner[(i0 + u) * H + j] : -1;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) pk[u] = src0[w[u] >= 0 ? w[u] : 0];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = i0 + u;
+        if (i >= V) continue;  // (not `break`: the loop must stay unrollable, pk[] in registers)
+        const int c = i * H + j;
+        float4 q;
+        float r;
+        if (w[u] >= 0) {
+          const float4 p = pk[u];
+          r = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+          q = make_float4(p.x, p.y, p.z, (float)((double)(float)i + jfrac));
+        } else {
+          r = FLT_MAX;
+          q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
+        }
+        range[c] = r;
+        cloud[c] = q;
+        if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
+          const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
+          const float va = atan2f_g(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ));
+          if ((double)(va - P.mount) <= 10 * DEG_TO_RAD_D) gmask |= (3ull << (i - 1));
+        }
+        if (i >= 1) scan(i - 1, prev_r, prev.z);
+        prev = q;
+        prev_r = r;
+      }
     }
+    scan(V - 1, prev_r, prev.z);
     B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
   }
   PROF_ADD(23, t_p3);
@@ -318,6 +336,34 @@ LG_DEVICE void uf_unite(PT parent, int a, int b) {
   } while (!done);
 }
 
+// ECL-CC style (Jaiganesh & Burtscher): parent[v] <= v always; the find halves the path it walks
+// (each store replaces a parent by one of its ancestors, so concurrent finds and hooks stay valid)
+// and a root is hooked under the smaller root with a CAS, retried from the value found.
+template <typename PT>
+LG_DEVICE int uf_rep(PT parent, int x) {
+  int curr = parent[x];
+  if (curr != x) {
+    int prev = x, next;
+    while (curr > (next = parent[curr])) {
+      parent[prev] = next;
+      prev = curr;
+      curr = next;
+    }
+  }
+  return curr;
+}
+
+template <typename PT>
+LG_DEVICE void uf_unite_rep(PT parent, int a, int b) {
+  int ra = uf_rep(parent, a), rb = uf_rep(parent, b);
+  while (ra != rb) {
+    if (ra > rb) { const int t = ra; ra = rb; rb = t; }
+    const int old = atomicCAS(&parent[rb], rb, ra);  // hook root rb under ra
+    if (old == rb) break;
+    rb = uf_rep(parent, old);
+  }
+}
+
 // Raster-order compaction without block-wide scans: wave w owns the contiguous cells
 // [w*L, w*L + L) (L a multiple of 64; one ring per wave for VLP-16), counts its two predicates with
 // ballots, publishes the totals in wt[] (2 * waves ints of LDS), and after one barrier knows its
@@ -358,13 +404,313 @@ LG_DEVICE int2 wave_raster_compact(int n, int* wt, Pred pred, Emit emit) {
   return make_int2(t1, t2);
 }
 
-template <bool kLds>
-__global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
+LG_DEVICE float ori_branch1(float ori, float so) {
+  if ((double)ori < (double)so - M_PI / 2) ori = (float)((double)ori + 2 * M_PI);
+  else if ((double)ori > (double)so + M_PI * 3 / 2) ori = (float)((double)ori - 2 * M_PI);
+  return ori;
+}
+LG_DEVICE float ori_branch2(float ori, float eo) {
+  ori = (float)((double)ori + 2 * M_PI);
+  if ((double)ori < (double)eo - M_PI * 3 / 2) ori = (float)((double)ori + 2 * M_PI);
+  else if ((double)ori > (double)eo + M_PI / 2) ori = (float)((double)ori - 2 * M_PI);
+  return ori;
+}
+
+// adjustDistortion (featureAssociation.cpp:161-197) over the segmented cloud seg_pts[0, M) ->
+// seg_fa.  halfPassed switches after the first point whose branch-1 orientation passes start + pi
+// (index h).  Tiles of nt * FP_U points run in point order: while h is not yet known, a tile's raw
+// orientations also give its first switching point (one block min); point i uses branch 1 iff
+// i <= h, so a tile before h's tile is all branch 1 and one after it all branch 2.  Loads are
+// unconditional (index clamped) and issued together.  Block-uniform; scratch >= 16 ints.
+#define FP_U 8
+LG_DEVICE void distort_segmented(const LgParams& P, const LgBufs& B, int s, int M, int* scratch) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const float so = B.orient[s * 4 + 0], eo = B.orient[s * 4 + 1], od = B.orient[s * 4 + 2];
+  const float4* __restrict__ seg = B.seg_pts + (size_t)s * P.VH;
+  float4* __restrict__ fa = B.seg_fa + (size_t)s * P.VH;
+  int h = 0x7fffffff;
+  for (int t0 = 0; t0 < M; t0 += nt * FP_U) {
+    float4 pk[FP_U];
+    float ori[FP_U];
+#pragma unroll
+    for (int u = 0; u < FP_U; ++u) pk[u] = seg[min(t0 + u * nt + tid, M - 1)];
+#pragma unroll
+    for (int u = 0; u < FP_U; ++u) ori[u] = -atan2f_g(pk[u].y, pk[u].x);  // point.x = y, point.z = x
+    if (h == 0x7fffffff) {
+      int hc = 0x7fffffff;
+#pragma unroll
+      for (int u = 0; u < FP_U; ++u) {
+        const int i = t0 + u * nt + tid;
+        if (i < M && (double)(ori_branch1(ori[u], so) - so) > M_PI) hc = min(hc, i);
+      }
+      h = block_min_int(hc, scratch);
+    }
+#pragma unroll
+    for (int u = 0; u < FP_U; ++u) {
+      const int i = t0 + u * nt + tid;
+      const float4 p = pk[u];
+      const float o = (i <= h) ? ori_branch1(ori[u], so) : ori_branch2(ori[u], eo);
+      const float relTime = (o - so) / od;
+      const float inten = (float)(int)p.w + P.scan_period * relTime;
+      if (i < M) fa[i] = make_float4(p.y, p.z, p.x, inten);
+    }
+  }
+}
+
+// ---- k_segment (LDS path: V <= 16, V*H < 32768) ---------------------------------------------
+// One LDS word per cell carries the whole labelling state:
+//   cell index (>= 0)        eligible cell: union-find parent, after path compression its root
+//   SEG_GND / SEG_EMPTY      ground cell / no return (label -1, :293-300)
+//   SEG_FLAG | payload       a root: first {count:15 << 16 | row mask of non-seed members:16},
+//                            then its label (k + 1 in seed raster order, or 999999)
+// so no per-cell state leaves LDS before the final label / compaction pass.  Global reads are
+// batched (kSegU cells per lane per round, all loads issued before use).
+#define SEG_GND 0x7ffffffe
+#define SEG_EMPTY 0x7fffffff
+#define SEG_FLAG 0x80000000u
+#define SEG_U 8
+#define SEG_ROUNDS 4  // 4 * 1024 * SEG_U = 32768 >= V*H on this path
+
+LG_DEVICE bool seg_eligible(int8_t g, float r) { return g != 1 && r != FLT_MAX; }  // _label_mat == 0
+
+__global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, H = P.H, VH = P.VH, G = P.G;
   int* scratch = smem;  // 64 ints
-  int* parent = kLds ? (smem + 64) : (B.cc_parent + (size_t)s * VH);
+  int* parent = smem + 64;
+  const float* __restrict__ range = B.range + (size_t)s * VH;
+  const int8_t* __restrict__ ground = B.ground + (size_t)s * VH;
+  const float4* __restrict__ cloud = B.cloud + (size_t)s * VH;
+  int32_t* __restrict__ label = B.label + (size_t)s * VH;
+
+  // ---- pass 1: the edges of every cell to its smaller-index neighbours: up (c - H), the horizontal
+  // wrap ((i, 0) for j = H - 1) and left (c - 1).  parent starts at the smallest connected one
+  // (ECL-CC's initialisation: short trees from the start); the other edges are united in pass 2.
+  PROF_T(t_s0);
+  unsigned ebits[SEG_ROUNDS];
+#pragma unroll
+  for (int rd = 0; rd < SEG_ROUNDS; ++rd) {
+    ebits[rd] = 0u;
+    const int cb = rd * nt * SEG_U;
+    if (cb >= VH) continue;
+    float r0[SEG_U], ru[SEG_U], rw[SEG_U], rl[SEG_U];
+    int8_t g0[SEG_U], gu[SEG_U], gw[SEG_U], gl[SEG_U];
+#pragma unroll
+    for (int u = 0; u < SEG_U; ++u) {
+      const int c = min(cb + u * nt + tid, VH - 1);
+      const int i = c / H, j = c - i * H;
+      const int cu = i > 0 ? c - H : c, cw = j == H - 1 ? i * H : c, cl = j > 0 ? c - 1 : c;
+      r0[u] = range[c]; ru[u] = range[cu]; rw[u] = range[cw]; rl[u] = range[cl];
+      g0[u] = ground[c]; gu[u] = ground[cu]; gw[u] = ground[cw]; gl[u] = ground[cl];
+    }
+#pragma unroll
+    for (int u = 0; u < SEG_U; ++u) {
+      const int c = cb + u * nt + tid;
+      if (c >= VH) continue;
+      const int i = c / H, j = c - i * H;
+      const bool e0 = seg_eligible(g0[u], r0[u]);
+      // the predicate is symmetric in its two ranges (d1 = max, d2 = min), as the BFS's is
+      const bool eu = e0 && i > 0 && seg_eligible(gu[u], ru[u]) && seg_edge(r0[u], ru[u], P.sinY, P.cosY, P.theta_thr);
+      const bool ew = e0 && j == H - 1 && H > 1 && seg_eligible(gw[u], rw[u]) &&
+                      seg_edge(r0[u], rw[u], P.sinX, P.cosX, P.theta_thr);
+      const bool el = e0 && j > 0 && seg_eligible(gl[u], rl[u]) && seg_edge(r0[u], rl[u], P.sinX, P.cosX, P.theta_thr);
+      int p0 = c;
+      unsigned rest = 0u;  // bit0 up, bit1 wrap, bit2 left: edges left for pass 2
+      if (eu) p0 = c - H;
+      if (ew) { if (p0 == c) p0 = i * H; else rest |= 2u; }
+      if (el) { if (p0 == c) p0 = c - 1; else rest |= 4u; }
+      parent[c] = e0 ? p0 : (g0[u] == 1 ? SEG_GND : SEG_EMPTY);
+      ebits[rd] |= rest << (3 * u);
+    }
+  }
+  __syncthreads();
+  PROF_ADD(25, t_s0);
+  // ---- pass 2: union the remaining edges (hook the larger root under the smaller: the root of a
+  // component is its minimum cell, the BFS seed) --------------------------------------------------
+  PROF_T(t_s1);
+#pragma unroll
+  for (int rd = 0; rd < SEG_ROUNDS; ++rd) {
+    unsigned m = ebits[rd];
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1u;
+      const int c = rd * nt * SEG_U + (b / 3) * nt + tid;
+      const int i = c / H;
+      const int k = b % 3;
+      const int o = k == 0 ? c - H : (k == 1 ? i * H : c - 1);
+      uf_unite_rep(parent, c, o);
+    }
+  }
+  __syncthreads();
+  PROF_ADD(26, t_s1);
+  // ---- pass 3: every eligible cell points at its root.  Only a cell's own word is written (a find
+  // that halved other cells' paths here could overwrite a root already stored by their owner).
+  PROF_T(t_s2);
+  for (int c = tid; c < VH; c += nt) {
+    const int p = parent[c];
+    if (p < SEG_GND && p != c) parent[c] = uf_find(parent, p);
+  }
+  __syncthreads();
+  PROF_ADD(27, t_s2);
+  // ---- pass 4: per-root size (seed included) and rows of the non-seed members (:466-470) ---------
+  PROF_T(t_s3);
+  for (int c = tid; c < VH; c += nt)
+    if (parent[c] == c) parent[c] = (int)(SEG_FLAG | (1u << 16));
+  __syncthreads();
+  for (int c = tid; c < VH; c += nt) {
+    const int r = parent[c];
+    if (r >= 0 && r < SEG_GND) {
+      atomicAdd((unsigned*)&parent[r], 1u << 16);
+      atomicOr((unsigned*)&parent[r], 1u << (c / H));
+    }
+  }
+  __syncthreads();
+  // feasible roots numbered in raster order of their seed (the BFS's _label_count++)
+  wave_raster_compact(
+      VH, scratch,
+      [&](int c, bool& feas, bool& isroot) {
+        const unsigned a = (unsigned)parent[c];
+        isroot = (a & SEG_FLAG) != 0u;
+        if (isroot) {
+          const int cnt = (int)((a >> 16) & 0x7fffu);
+          const int lines = __popc(a & 0xffffu);
+          feas = cnt >= 30 || (cnt >= P.seg_valid_pt && lines >= P.seg_valid_line);
+        }
+      },
+      [&](int c, bool feas, bool isroot, int k, int) {
+        if (isroot) parent[c] = (int)(SEG_FLAG | (feas ? (unsigned)(k + 1) : 999999u));
+      });
+  PROF_ADD(28, t_s3);
+  // ---- pass 5: label image + cloudSegmentation's raster-order compaction (:358-396) -------------
+  PROF_T(t_s4);
+  float4* __restrict__ seg_pts = B.seg_pts + (size_t)s * VH;
+  float* __restrict__ seg_range = B.seg_range + (size_t)s * VH;
+  uint32_t* __restrict__ seg_col = B.seg_col + (size_t)s * VH;
+  uint8_t* __restrict__ seg_ground = B.seg_ground + (size_t)s * VH;
+  float4* __restrict__ outlier = B.outlier + (size_t)s * VH;
+  float4* __restrict__ outlier_fa = B.outlier_fa + (size_t)s * VH;
+  int32_t* __restrict__ ring_start = B.ring_start + (size_t)s * V;
+  int32_t* __restrict__ ring_end = B.ring_end + (size_t)s * V;
+  // adjustOutlierCloud (fa.cpp:1273-1283) runs in publishCloudsLast, i.e. not on the
+  // initialisation scan (:1414-1416): the state read here is the one FeatureAssociation will see
+  const bool swap_axes = B.state[s].initialized != 0;
+  auto cell_label = [&](int c, int& lab, bool& gnd) {
+    const int v = parent[c];
+    gnd = v == SEG_GND;
+    if (v == SEG_GND || v == SEG_EMPTY) lab = -1;
+    else if (v < 0) lab = v & 0x7fffffff;
+    else lab = parent[v] & 0x7fffffff;
+  };
+  auto classify = [&](int c, int lab, bool gnd, bool& pseg, bool& pout) {
+    const int i = c / H, j = c - i * H;
+    pseg = pout = false;
+    if (lab > 0 || gnd) {
+      if (lab == 999999) pout = (i > G && j % 5 == 0);
+      else if (!(gnd && (j % 5 != 0 && j > 5 && j < H - 5))) pseg = true;
+    }
+  };
+  const int lane = lane_id(), w = wave_id(), nw = (int)(nt >> 6);
+  const int L = ((VH + nw - 1) / nw + 63) & ~63;
+  const int lo = min(w * L, VH), hi = min(lo + L, VH);
+  int c1 = 0, c2 = 0;
+  for (int base = lo; base < hi; base += 64) {  // count pass (LDS only) + label image
+    const int c = base + lane;
+    bool p1 = false, p2 = false;
+    if (c < hi) {
+      int lab;
+      bool gnd;
+      cell_label(c, lab, gnd);
+      label[c] = lab;
+      classify(c, lab, gnd, p1, p2);
+    }
+    c1 += __popcll(__ballot(p1));
+    c2 += __popcll(__ballot(p2));
+  }
+  if (lane == 0) { scratch[w] = c1; scratch[nw + w] = c2; }
+  __syncthreads();
+  int o1 = 0, o2 = 0, nseg = 0, nout = 0;
+  for (int k = 0; k < nw; ++k) {
+    const int a = scratch[k], b = scratch[nw + k];
+    if (k < w) { o1 += a; o2 += b; }
+    nseg += a;
+    nout += b;
+  }
+  // emit pass: kCU chunks of 64 cells per batch; the cloud / range loads are buffer loads whose
+  // offset is out of range for cells that are not emitted (they return 0 without a memory access)
+  constexpr int kCU = 8;
+  const __amdgpu_buffer_rsrc_t rs_cloud = buffer_rsrc(cloud, (uint32_t)VH * 16u);
+  const __amdgpu_buffer_rsrc_t rs_range = buffer_rsrc(range, (uint32_t)VH * 4u);
+  for (int base = lo; base < hi; base += 64 * kCU) {
+    float4 pc[kCU];
+    float rc[kCU];
+    bool ps[kCU], po[kCU], pg[kCU];
+#pragma unroll
+    for (int u = 0; u < kCU; ++u) {
+      const int c = base + 64 * u + lane;
+      ps[u] = po[u] = pg[u] = false;
+      if (c < hi) {
+        int lab;
+        cell_label(c, lab, pg[u]);
+        classify(c, lab, pg[u], ps[u], po[u]);
+      }
+      pc[u] = buffer_load_f4(rs_cloud, (ps[u] || po[u]) ? (uint32_t)c * 16u : 0xffffffffu);
+      rc[u] = buffer_load_f1(rs_range, ps[u] ? (uint32_t)c * 4u : 0xffffffffu);
+    }
+#pragma unroll
+    for (int u = 0; u < kCU; ++u) {
+      const int c = base + 64 * u + lane;
+      const bool p1 = ps[u], p2 = po[u], gnd = pg[u];
+      const unsigned long long m1 = __ballot(p1), m2 = __ballot(p2);
+      if (c < hi) {
+        const int i = c / H, j = c - i * H;
+        const int k1 = o1 + popc_below(m1), k2 = o2 + popc_below(m2);
+        if (j == 0) {  // k1 = segmented points before this ring
+          ring_start[i] = k1 - 1 + 5;
+          if (i > 0) ring_end[i - 1] = k1 - 1 - 5;
+        }
+        if (p1) {
+          seg_pts[k1] = pc[u];
+          seg_range[k1] = rc[u];
+          seg_col[k1] = (uint32_t)j;
+          seg_ground[k1] = (uint8_t)gnd;
+        }
+        if (p2) {
+          const float4 p = pc[u];
+          outlier[k2] = p;
+          outlier_fa[k2] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;
+        }
+      }
+      o1 += __popcll(m1);
+      o2 += __popcll(m2);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) ring_end[V - 1] = nseg - 1 - 5;
+  // 2-D scan compaction (column order)
+  const int32_t* cand = B.scan_cand + (size_t)s * H;
+  float4* scan = B.scan_msg + (size_t)s * H;
+  const int nscan = wave_raster_compact(H, scratch, [&](int j, bool& p, bool&) { p = cand[j] >= 0; },
+                                        [&](int j, bool p, bool, int k, int) { if (p) scan[k] = cloud[cand[j]]; }).x;
+  PROF_ADD(29, t_s4);
+  PROF_T(t_s5);
+  distort_segmented(P, B, s, nseg, scratch);
+  PROF_ADD(31, t_s5);
+  if (tid == 0) {
+    int32_t* cnt = B.counts + (size_t)s * CNT_N;
+    cnt[CNT_M] = nseg;
+    cnt[CNT_OUTLIER] = nout;
+    cnt[CNT_SCAN] = nscan;
+  }
+}
+
+// ---- k_segment (global path: V > 16 or V*H >= 32768) ----------------------------------------
+__global__ __launch_bounds__(1024) void k_segment_global(LgParams P, LgBufs B) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int V = P.V, H = P.H, VH = P.VH, G = P.G;
+  int* scratch = smem;  // 64 ints
+  int* parent = B.cc_parent + (size_t)s * VH;
   const float* range = B.range + (size_t)s * VH;
   const int8_t* ground = B.ground + (size_t)s * VH;
   const float4* cloud = B.cloud + (size_t)s * VH;
@@ -397,69 +743,35 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
   PROF_T(t_s3);
 
   // ---- per-root size and row mask (rows of non-seed members) ----
-  if constexpr (kLds) {
-    // park roots in the label image, reuse LDS as packed {count:16 | rowmask:16} (V <= 16)
-    for (int c = tid; c < VH; c += nt) label[c] = parent[c];
-    __syncthreads();
-    unsigned* agg = (unsigned*)parent;
-    for (int c = tid; c < VH; c += nt) agg[c] = 0u;
-    __syncthreads();
-    for (int c = tid; c < VH; c += nt) {
-      const int r = label[c];
-      if (r < 0) continue;
-      atomicAdd(&agg[r], 1u);
-      if (r != c) atomicOr(&agg[r], 1u << (16 + c / H));
-    }
-    __syncthreads();
-    // feasible roots numbered in raster order of their seed (= the BFS's _label_count++)
-    wave_raster_compact(
-        VH, scratch,
-        [&](int c, bool& feas, bool& isroot) {
-          isroot = label[c] == c;
-          if (isroot) {
-            const unsigned a = agg[c];
-            const int cnt = (int)(a & 0xffffu);
-            const int lines = __popc(a >> 16);
-            feas = cnt >= 30 || (cnt >= P.seg_valid_pt && lines >= P.seg_valid_line);
-          }
-        },
-        [&](int c, bool feas, bool isroot, int k, int) {
-          if (isroot) agg[c] = feas ? (unsigned)(k + 1) : 999999u;
-        });
-    for (int c = tid; c < VH; c += nt) {
-      const int r = label[c];
-      label[c] = (r < 0) ? -1 : (int)agg[r];
-    }
-  } else {
-    int32_t* cnt = B.cc_cnt + (size_t)s * VH;
-    unsigned long long* msk = B.cc_mask + (size_t)s * VH;
-    for (int c = tid; c < VH; c += nt) { cnt[c] = 0; msk[c] = 0ull; }
-    __syncthreads();
-    for (int c = tid; c < VH; c += nt) {
-      const int r = parent[c];
-      if (r < 0) continue;
-      atomicAdd(&cnt[r], 1);
-      if (r != c) atomicOr(&msk[r], 1ull << (c / H));
-    }
-    __syncthreads();
-    wave_raster_compact(
-        VH, scratch,
-        [&](int c, bool& feas, bool& isroot) {
-          isroot = parent[c] == c;
-          if (isroot) {
-            const int n = cnt[c];
-            const int lines = __popcll(msk[c]);
-            feas = n >= 30 || (n >= P.seg_valid_pt && lines >= P.seg_valid_line);
-          }
-        },
-        [&](int c, bool feas, bool isroot, int k, int) {
-          if (isroot) cnt[c] = feas ? k + 1 : 999999;
-        });
-    for (int c = tid; c < VH; c += nt) {
-      const int r = parent[c];
-      label[c] = (r < 0) ? -1 : cnt[r];
-    }
+  int32_t* cnt = B.cc_cnt + (size_t)s * VH;
+  unsigned long long* msk = B.cc_mask + (size_t)s * VH;
+  for (int c = tid; c < VH; c += nt) { cnt[c] = 0; msk[c] = 0ull; }
+  __syncthreads();
+  for (int c = tid; c < VH; c += nt) {
+    const int r = parent[c];
+    if (r < 0) continue;
+    atomicAdd(&cnt[r], 1);
+    if (r != c) atomicOr(&msk[r], 1ull << (c / H));
   }
+  __syncthreads();
+  wave_raster_compact(
+      VH, scratch,
+      [&](int c, bool& feas, bool& isroot) {
+        isroot = parent[c] == c;
+        if (isroot) {
+          const int n = cnt[c];
+          const int lines = __popcll(msk[c]);
+          feas = n >= 30 || (n >= P.seg_valid_pt && lines >= P.seg_valid_line);
+        }
+      },
+      [&](int c, bool feas, bool isroot, int k, int) {
+        if (isroot) cnt[c] = feas ? k + 1 : 999999;
+      });
+  for (int c = tid; c < VH; c += nt) {
+    const int r = parent[c];
+    label[c] = (r < 0) ? -1 : cnt[r];
+  }
+
   __syncthreads();
   PROF_ADD(28, t_s3);
   PROF_T(t_s4);
@@ -472,6 +784,8 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
   float4* outlier = B.outlier + (size_t)s * VH;
   int32_t* ring_start = B.ring_start + (size_t)s * V;
   int32_t* ring_end = B.ring_end + (size_t)s * V;
+  float4* outlier_fa = B.outlier_fa + (size_t)s * VH;
+  const bool swap_axes = B.state[s].initialized != 0;
   auto cls = [&](int c, bool& pseg, bool& pout) {
     const int i = c / H, j = c - i * H;
     const int lab = label[c], g = ground[c];
@@ -492,7 +806,11 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
       seg_col[k1] = (uint32_t)j;
       seg_ground[k1] = (uint8_t)(ground[c] == 1);
     }
-    if (pout) outlier[k2] = cloud[c];
+    if (pout) {
+      const float4 p = cloud[c];
+      outlier[k2] = p;
+      outlier_fa[k2] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;  // adjustOutlierCloud (fa.cpp:1273-1283)
+    }
   });
   const int nseg = tot.x, nout = tot.y;
   if (tid == 0) ring_end[V - 1] = nseg - 1 - 5;
@@ -502,6 +820,7 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
   const int nscan = wave_raster_compact(H, scratch, [&](int j, bool& p, bool&) { p = cand[j] >= 0; },
                                         [&](int j, bool p, bool, int k, int) { if (p) scan[k] = cloud[cand[j]]; }).x;
   PROF_ADD(29, t_s4);
+  distort_segmented(P, B, s, nseg, scratch);
   if (tid == 0) {
     int32_t* cnt = B.counts + (size_t)s * CNT_N;
     cnt[CNT_M] = nseg;
@@ -513,83 +832,117 @@ __global__ __launch_bounds__(1024) void k_segment(LgParams P, LgBufs B) {
 // ============================================================================================
 // k_fa_prep: adjustDistortion + calculateSmoothness + markOccludedPoints + adjustOutlierCloud
 // ============================================================================================
-LG_DEVICE float ori_branch1(float ori, float so) {
-  if ((double)ori < (double)so - M_PI / 2) ori = (float)((double)ori + 2 * M_PI);
-  else if ((double)ori > (double)so + M_PI * 3 / 2) ori = (float)((double)ori - 2 * M_PI);
-  return ori;
-}
-LG_DEVICE float ori_branch2(float ori, float eo) {
-  ori = (float)((double)ori + 2 * M_PI);
-  if ((double)ori < (double)eo - M_PI * 3 / 2) ori = (float)((double)ori + 2 * M_PI);
-  else if ((double)ori > (double)eo + M_PI / 2) ori = (float)((double)ori - 2 * M_PI);
-  return ori;
-}
-
+// calculateSmoothness + markOccludedPoints, one 1024-lane workgroup per scan, on LDS tiles of
+// FP_TILE positions whose range / column loads are issued together.  markOccludedPoints'
+// scattered OR-writes (:237-259) are evaluated in gather form, picked[k] = OR of the marks that land
+// on k, which equals the reference's "zero [5, M-5) then OR the marks" for every k (positions
+// outside [5, M-5) keep their stale value OR the marks, as there).  adjustDistortion and
+// adjustOutlierCloud run in k_segment's epilogue, on the cloud it has just compacted; kDistort
+// runs them here instead, for a ProjectionOut uploaded from the host (lego_feature_association_from).
+#define FP_TILE (1024 * FP_U)
+#define FP_HALO 8
+template <bool kDistort>
 __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
   __shared__ int scratch[64];
+  __shared__ float sr[FP_TILE + 2 * FP_HALO];     // segmentedCloudRange[t0 - FP_HALO + x]
+  __shared__ uint32_t sc[FP_TILE + 2 * FP_HALO];  // segmentedCloudColInd
+  __shared__ uint8_t sf[FP_TILE + 2 * FP_HALO];   // marks of i: bit0 A (i-5..i), bit1 B (i+1..i+6), bit2 C (i)
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int VH = P.VH;
   const int32_t* cnt = B.counts + (size_t)s * CNT_N;
   const int M = cnt[CNT_M];
-  const float so = B.orient[s * 4 + 0], eo = B.orient[s * 4 + 1], od = B.orient[s * 4 + 2];
-  const float4* seg = B.seg_pts + (size_t)s * VH;
-  float4* fa = B.seg_fa + (size_t)s * VH;
-  const float* r = B.seg_range + (size_t)s * VH;
-  const uint32_t* col = B.seg_col + (size_t)s * VH;
-  float* curv = B.curv + (size_t)s * VH;
-  uint8_t* picked = B.picked + (size_t)s * VH;
-  int8_t* flabel = B.flabel + (size_t)s * VH;
-  int2* smooth = B.smooth + (size_t)s * VH;
-
-  // halfPassed switches after the first point whose branch-1 orientation passes start + pi
-  int h = 0x7fffffff;
-  for (int i = tid; i < M; i += nt) {
-    const float4 p = seg[i];
-    float ori = ori_branch1(-atan2f_g(p.y, p.x), so);
-    if ((double)(ori - so) > M_PI) h = min(h, i);
-  }
-  h = block_min_int(h, scratch);
-  for (int i = tid; i < M; i += nt) {
-    const float4 p = seg[i];
-    float ori = -atan2f_g(p.y, p.x);  // point.x = y, point.z = x
-    ori = (i <= h) ? ori_branch1(ori, so) : ori_branch2(ori, eo);
-    float relTime = (ori - so) / od;
-    float inten = (float)(int)p.w + P.scan_period * relTime;
-    fa[i] = make_float4(p.y, p.z, p.x, inten);
-  }
+  const float* __restrict__ r = B.seg_range + (size_t)s * VH;
+  const uint32_t* __restrict__ col = B.seg_col + (size_t)s * VH;
+  float* __restrict__ curv = B.curv + (size_t)s * VH;
+  uint8_t* __restrict__ picked = B.picked + (size_t)s * VH;
+  int8_t* __restrict__ flabel = B.flabel + (size_t)s * VH;
+  int2* __restrict__ smooth = B.smooth + (size_t)s * VH;
   // k_extract's first pass may move the stale slot 4 while other rings check where it points
   if (tid == 0) B.fp_sync[2 * s] = smooth[4].y;
-  for (int i = 5 + tid; i < M - 5; i += nt) {
-    float d = r[i - 5] + r[i - 4] + r[i - 3] + r[i - 2] + r[i - 1] - r[i] * 10 + r[i + 1] + r[i + 2] +
-              r[i + 3] + r[i + 4] + r[i + 5];
-    const float cv = d * d;
-    curv[i] = cv;
-    picked[i] = 0;
-    flabel[i] = 0;
-    smooth[i] = make_int2(__float_as_int(cv), i);
+  if constexpr (kDistort) {
+    distort_segmented(P, B, s, M, scratch);
+    const int nout = cnt[CNT_OUTLIER];
+    const float4* __restrict__ outl = B.outlier + (size_t)s * VH;
+    float4* __restrict__ outa = B.outlier_fa + (size_t)s * VH;
+    const bool swap_axes = B.state[s].initialized != 0;  // not on the initialisation scan (:1414-1416)
+    for (int k = tid; k < nout; k += nt) {
+      const float4 p = outl[k];
+      outa[k] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;
+    }
   }
-  __syncthreads();
-  for (int i = 5 + tid; i < M - 6; i += nt) {
-    const float depth1 = r[i], depth2 = r[i + 1];
-    const int columnDiff = abs((int)(col[i + 1] - col[i]));
-    if (columnDiff < 10) {
-      if ((double)(depth1 - depth2) > 0.3) {
-        for (int k = 0; k <= 5; ++k) picked[i - k] = 1;
-      } else if ((double)(depth2 - depth1) > 0.3) {
-        for (int k = 1; k <= 6; ++k) picked[i + k] = 1;
+  const int nTiles = (M + FP_TILE - 1) / FP_TILE;
+  for (int tile = 0; tile < nTiles; ++tile) {
+    const int t0 = tile * FP_TILE;
+    PROF_T(t_f1);
+    {  // range / column of positions [t0 - FP_HALO, t0 + FP_TILE + FP_HALO) into LDS, one batch
+      float rv[FP_U];
+      uint32_t cv[FP_U];
+#pragma unroll
+      for (int u = 0; u < FP_U; ++u) {
+        const int q = min(t0 + u * nt + tid, M - 1);
+        rv[u] = r[q];
+        cv[u] = col[q];
+      }
+      float rh = 0.f;
+      uint32_t ch = 0u;
+      const int xh = tid < FP_HALO ? tid : FP_TILE + tid;  // halo slot of this lane (tid < 2 * FP_HALO)
+      if (tid < 2 * FP_HALO) {
+        const int q = min(max(t0 - FP_HALO + xh, 0), M - 1);
+        rh = r[q];
+        ch = col[q];
+      }
+#pragma unroll
+      for (int u = 0; u < FP_U; ++u) {
+        sr[FP_HALO + u * nt + tid] = rv[u];
+        sc[FP_HALO + u * nt + tid] = cv[u];
+      }
+      if (tid < 2 * FP_HALO) { sr[xh] = rh; sc[xh] = ch; }
+    }
+    __syncthreads();
+    PROF_ADD(33, t_f1);
+    PROF_T(t_f2);
+    // markOccludedPoints' per-i conditions for i in [t0 - 6, t0 + FP_TILE + 6), i in [5, M - 6)
+    for (int x = 2 + tid; x < FP_TILE + 2 * FP_HALO - 2; x += nt) {
+      const int i = t0 - FP_HALO + x;
+      uint8_t f = 0;
+      if (i >= 5 && i < M - 6) {
+        const float depth1 = sr[x], depth2 = sr[x + 1];
+        const int columnDiff = abs((int)(sc[x + 1] - sc[x]));
+        if (columnDiff < 10) {
+          if ((double)(depth1 - depth2) > 0.3) f |= 1;
+          else if ((double)(depth2 - depth1) > 0.3) f |= 2;
+        }
+        const float diff1 = fabsf(sr[x - 1] - depth1), diff2 = fabsf(sr[x + 1] - depth1);
+        if ((double)diff1 > 0.02 * (double)depth1 && (double)diff2 > 0.02 * (double)depth1) f |= 4;
+      }
+      sf[x] = f;
+    }
+    __syncthreads();
+    PROF_ADD(34, t_f2);
+    PROF_T(t_f3);
+    // calculateSmoothness (:200-223) + the marks landing on each k
+    for (int x = FP_HALO + tid; x < FP_HALO + FP_TILE; x += nt) {
+      const int k = t0 - FP_HALO + x;
+      if (k > M) break;
+      bool mk = (sf[x] & 4) != 0;
+#pragma unroll
+      for (int d = 0; d <= 5; ++d) mk |= (sf[x + d] & 1) != 0;   // A(k + d) marks k
+#pragma unroll
+      for (int d = 1; d <= 6; ++d) mk |= (sf[x - d] & 2) != 0;   // B(k - d) marks k
+      if (k >= 5 && k < M - 5) {
+        const float d = sr[x - 5] + sr[x - 4] + sr[x - 3] + sr[x - 2] + sr[x - 1] - sr[x] * 10 + sr[x + 1] + sr[x + 2] +
+                        sr[x + 3] + sr[x + 4] + sr[x + 5];
+        const float cv = d * d;
+        curv[k] = cv;
+        picked[k] = mk ? 1 : 0;
+        flabel[k] = 0;
+        smooth[k] = make_int2(__float_as_int(cv), k);
+      } else if (mk) {
+        picked[k] = 1;
       }
     }
-    const float diff1 = fabsf(r[i - 1] - r[i]), diff2 = fabsf(r[i + 1] - r[i]);
-    if ((double)diff1 > 0.02 * (double)r[i] && (double)diff2 > 0.02 * (double)r[i]) picked[i] = 1;
-  }
-  const int nout = cnt[CNT_OUTLIER];
-  const float4* outl = B.outlier + (size_t)s * VH;
-  float4* outa = B.outlier_fa + (size_t)s * VH;
-  // adjustOutlierCloud runs in publishCloudsLast, i.e. not on the initialisation scan (:1414-1416)
-  const bool swap_axes = B.state[s].initialized != 0;
-  for (int k = tid; k < nout; k += nt) {
-    const float4 p = outl[k];
-    outa[k] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;
+    __syncthreads();
+    PROF_ADD(35, t_f3);
   }
 }
 
@@ -664,6 +1017,79 @@ LG_DEVICE void adjust_heap_pf(const SortView<K, V>& a, int first, int hole, int 
   val[hole] = vv;
 }
 
+template <typename K>
+LG_DEVICE K rdlane(K v, int l) {
+  return __builtin_bit_cast(K, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+// __sort_heap (= repeated __pop_heap + __adjust_heap from the root) with the whole wave.
+// Each pop's hole descent depends on keys only.  A window is the 5-level subtree below a window
+// root x: lane l holds the key and value of one of its 62 nodes (level L = 1..5 at lanes
+// [2^L - 2, 2^(L+1) - 2), siblings in lanes l, l ^ 1), read with one LDS round trip.  A node is on
+// the descent path iff it and all its in-window ancestors win their sibling pair (right unless
+// right < left, as __adjust_heap) and its parent has two children (parent < (len - 1) / 2), or it
+// is the only (left) child of parent (len - 2) / 2 of an even-length heap whose in-window
+// ancestors win -- a few VALU operations per lane against a precomputed ancestor mask.
+// __push_heap then stops at the deepest path node p_u with !(k_u < value) (keys do not increase
+// along a heap path), so the pop is a[parent(p_d)] = old a[p_d] for d = 1..u, a[p_u] = value: each
+// path lane decides its own move (!(k_d < value)); the walk ends at the first path node that stays.
+template <typename K, typename V>
+LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
+  first = __builtin_amdgcn_readfirstlane(first);  // wave-uniform: keeps the pop loop scalar
+  last = __builtin_amdgcn_readfirstlane(last);
+  K* key = a.key + first;
+  V* val = a.val + first;
+  const int lane = lane_id();
+  const int lev = lane < 2 ? 1 : lane < 6 ? 2 : lane < 14 ? 3 : lane < 30 ? 4 : 5;
+  const int off = lane - ((1 << lev) - 2);
+  const int cst = (1 << lev) - 1 + off;  // node = (x << lev) + cst
+  const bool right = (off & 1) != 0;
+  unsigned long long anc = 0ull;  // lanes of the node's in-window ancestors (excluding itself)
+  for (int j = 1; j < lev; ++j) anc |= 1ull << ((1 << j) - 2 + (off >> (lev - j)));
+  const unsigned long long bottom = ((1ull << 32) - 1ull) << 30;  // level-5 lanes
+  for (int len = last - first - 1; len >= 1; --len) {
+    // __pop_heap(first, first + len, first + len): value = a[len]; a[len] = a[0]; adjust from 0.
+    // The first window's read also brings the root (lane 62) and a[len] (lane 63).
+    const int lim = (len - 1) / 2;
+    const int only = (len & 1) == 0 ? len - 1 : -1;  // the only (left) child of node lim
+    int x = 0;     // window root (the hole when the window is entered)
+    int hole = 0;  // deepest node that took its child's element so far
+    K vk = K(0);
+    V vv = V(0);
+    while (true) {
+      const int node = (x << lev) + cst;
+      const int par = (node - 1) >> 1;
+      const int nc = lane < 62 ? min(node, len - 1) : (lane == 62 ? x : len);
+      const K kk = key[nc];
+      const V vl = val[nc];
+      if (x == 0) {
+        vk = rdlane(kk, 63);
+        vv = (V)__builtin_amdgcn_readlane((int)vl, 63);
+        if (lane == 62) { key[len] = kk; val[len] = vl; }
+      }
+      const K ks = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, kk), 0xb1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]: the sibling
+      const bool wr = !(kk < ks), wl = ks < kk;
+      const bool win = lane < 62 && ((right && wr) || (!right && wl));
+      const unsigned long long W = __ballot(win);
+      const bool chain = (W & anc) == anc;
+      const bool onp = lane < 62 && chain && ((win && par < lim) || node == only);
+      const unsigned long long path = __ballot(onp);
+      const bool mv = onp && !(kk < vk);
+      const unsigned long long M = __ballot(mv);
+      if (mv) {
+        key[par] = kk;
+        val[par] = vl;
+      }
+      if (M) hole = __builtin_amdgcn_readlane(node, 63 - __clzll((long long)M));
+      if (M != path || !(M & bottom)) break;
+      x = hole;  // the path left the window through its bottom with every node moved
+      if (x > lim) break;
+    }
+    if (lane == 0) { key[hole] = vk; val[hole] = vv; }
+  }
+  __syncthreads();
+}
+
 // __partial_sort(first, last, last) = __make_heap + __sort_heap.  __make_heap sifts the parents
 // from (len-2)/2 down to 0; parents on one heap level have disjoint subtrees (and __push_heap stops
 // at `top`), so each level runs in parallel, deepest level first.  __sort_heap's pops are a chain
@@ -680,17 +1106,13 @@ LG_DEVICE void heap_sort_wave(const SortView<K, V>& a, int first, int last) {
       __syncthreads();
     }
   }
-  if (lane == 0) {  // __sort_heap
-    int l = last;
-    while (l - first > 1) {
-      --l;
-      const K vk = a.key[l];
-      const V vv = a.val[l];
-      a.move(l, first);
-      adjust_heap_pf(a, first, 0, l - first, vk, vv);
-    }
-  }
-  __syncthreads();
+  PROF_T(t_pop0);
+  // The pops are one dependent chain, usually the longest of the launch: let this wave win
+  // instruction arbitration against the other waves of its SIMD while it runs them.
+  __builtin_amdgcn_s_setprio(3);
+  sort_heap_wave(a, first, last);
+  __builtin_amdgcn_s_setprio(0);
+  PROF_ADD(36, t_pop0);
 }
 
 // __unguarded_partition_pivot on a range of 17..64 elements held one per lane; returns the cut.
@@ -1358,29 +1780,26 @@ LG_DEVICE int lessflat_list(const ScanView& v, int st, int en, uint16_t* list) {
 // ============================================================================================
 __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
   __shared__ ExtractLds L;
-  const int V = P.V, VH = P.VH;
+  const int V = P.V;
   const int b = blockIdx.x, sl = b / V, s = P.s0 + sl;
   const int ring = (b % V + sl / max(P.ncu / V, 1)) % V;  // ring rotation as in k_extract
-  const int st = B.ring_start[(size_t)s * V + ring], en = B.ring_end[(size_t)s * V + ring];
-  ScanView v;
-  v.M = B.counts[(size_t)s * CNT_N + CNT_M];
-  v.VH = VH;
-  v.flabel = B.flabel + (size_t)s * VH;
-  v.fa = B.seg_fa + (size_t)s * VH;
-  PROF_T(t_lf0);
-  const int nlist = lessflat_list(v, st, en, L.vval);
-  PROF_ADD(3, t_lf0);
-  RingOut o;
   const size_t rb = (size_t)s * V + ring;
+  const size_t sb = (size_t)P.par * P.S * V + rb;  // staging half P.par
+  ScanView v;
+  v.fa = B.lf_stage + sb * P.H;  // the ring's lessFlat points, in surfPointsLessFlatScan order
+  const int n = B.lf_count[sb];
+  for (int t = lane_id(); t < n; t += 64) L.vval[t] = (uint16_t)t;
+  __syncthreads();
+  RingOut o;
   o.lflat = B.r_lflat + rb * P.H;
   o.nLF = 0;
   o.status = 0;
   PROF_T(t_vox0);
-  voxel_ring(P, v, L, nlist, st, o);
+  voxel_ring(P, v, L, n, 0, o);
   PROF_ADD(4, t_vox0);
   if (lane_id() == 0) {
     B.r_counts[rb * 4 + 3] = o.nLF;
-    if (o.status) B.r_status[rb] |= o.status;
+    B.r_vstatus[rb] = o.status;
   }
 }
 
@@ -1467,20 +1886,17 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
 __global__ __launch_bounds__(256) void k_concat(LgParams P, LgBufs B) {
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V;
-  __shared__ int off[4][65];
-  __shared__ int st;
+  __shared__ int off[3][65];
   if (tid == 0) {
-    int a[4] = {0, 0, 0, 0};
+    int a[3] = {0, 0, 0};
     int status = 0;
     for (int r = 0; r < V; ++r) {
       const int32_t* rc = B.r_counts + ((size_t)s * V + r) * 4;
-      for (int k = 0; k < 4; ++k) { off[k][r] = a[k]; a[k] += rc[k]; }
+      for (int k = 0; k < 3; ++k) { off[k][r] = a[k]; a[k] += rc[k]; }
       status |= B.r_status[(size_t)s * V + r];
     }
-    for (int k = 0; k < 4; ++k) off[k][V] = a[k];
-    st = status;
     int32_t* cnt = B.counts + (size_t)s * CNT_N;
-    cnt[CNT_SHARP] = a[0]; cnt[CNT_LSHARP] = a[1]; cnt[CNT_FLAT] = a[2]; cnt[CNT_LFLAT] = a[3];
+    cnt[CNT_SHARP] = a[0]; cnt[CNT_LSHARP] = a[1]; cnt[CNT_FLAT] = a[2];
     cnt[CNT_STATUS] = status;
   }
   __syncthreads();
@@ -1499,8 +1915,84 @@ __global__ __launch_bounds__(256) void k_concat(LgParams P, LgBufs B) {
       B.f_flat[(size_t)s * V * P.cap_flat + off[2][r] + t] = B.r_flat[rb * P.cap_flat + t];
       B.f_flat_ind[(size_t)s * V * P.cap_flat + off[2][r] + t] = B.r_flat_ind[rb * P.cap_flat + t];
     }
-    for (int t = tid; t < rc[3]; t += nt)
-      B.f_lflat[(size_t)s * P.VH + off[3][r] + t] = B.r_lflat[rb * P.H + t];
+  }
+  // surfPointsLessFlatScan of every ring (:370-374) into staging half P.par, one wave per ring: the
+  // VoxelGrid (k_voxel) reads only this copy, so it may overlap the next scan's front end
+  ScanView v;
+  v.M = B.counts[(size_t)s * CNT_N + CNT_M];
+  v.VH = P.VH;
+  v.flabel = B.flabel + (size_t)s * P.VH;
+  const float4* fa = B.seg_fa + (size_t)s * P.VH;
+  const int lane = lane_id();
+  for (int r = wave_id(); r < V; r += nt >> 6) {
+    const size_t rb = (size_t)s * V + r;
+    const size_t sb = (size_t)P.par * P.S * V + rb;
+    float4* dst = B.lf_stage + sb * P.H;
+    const int st = B.ring_start[rb], en = B.ring_end[rb];
+    int nlist = 0;
+    for (int j = 0; j < 6; j++) {
+      const int sp = (st * (6 - j) + en * j) / 6;
+      const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
+      if (sp >= ep) continue;
+      for (int k0 = sp; k0 <= ep; k0 += 64) {
+        const int k = k0 + lane;
+        const bool pr = k <= ep && v.flabel[k] <= 0;
+        const unsigned long long m = __ballot(pr);
+        if (pr) dst[nlist + popc_below(m)] = fa[k];
+        nlist += __popcll(m);
+      }
+    }
+    if (lane == 0) B.lf_count[sb] = nlist;
+  }
+}
+
+// ============================================================================================
+// k_publish: the lessFlat half of publishCloudsLast (:1329-1383): concatenate the rings' VoxelGrid
+// outputs (surfPointsLessFlat) and TransformToEnd them into laserCloudSurfLast with the transform
+// k_lm has just produced (untransformed on the initialisation scan, :1181-1209).  Runs after both
+// k_lm and k_voxel of its scan, before the next scan's k_lm.
+// ============================================================================================
+LG_DEVICE float4 transform_to_end(const float4 pi, const float* cur);
+
+__global__ __launch_bounds__(256) void k_publish(LgParams P, LgBufs B) {
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int V = P.V, VH = P.VH;
+  __shared__ int off[65];
+  __shared__ float cur[6];
+  __shared__ int copy, nb, vst;
+  if (tid == 0) {
+    int a = 0, st = 0;
+    for (int r = 0; r < V; ++r) {
+      off[r] = a;
+      a += B.r_counts[((size_t)s * V + r) * 4 + 3];
+      st |= B.r_vstatus[(size_t)s * V + r];
+    }
+    off[V] = a;
+    vst = st;
+    const LgState& S = B.state[s];
+    for (int k = 0; k < 6; ++k) cur[k] = S.cur[k];
+    copy = S.pub_copy;
+    nb = S.last_buf;
+  }
+  __syncthreads();
+  float4* sl = B.surf_last + (size_t)s * 2 * VH + (size_t)nb * VH;
+  float4* fl = B.f_lflat + (size_t)s * VH;
+  for (int r = 0; r < V; ++r) {
+    const float4* src = B.r_lflat + ((size_t)s * V + r) * P.H;
+    const int n = off[r + 1] - off[r];
+    for (int t = tid; t < n; t += nt) {
+      const float4 p = src[t];
+      fl[off[r] + t] = p;
+      sl[off[r] + t] = copy ? p : transform_to_end(p, cur);
+    }
+  }
+  if (tid == 0) {
+    const int n_lflat = off[V];
+    LgState& S = B.state[s];
+    S.n_surf_last = n_lflat;
+    S.tree_stale = copy ? 0 : !(S.n_corner_last > 10 && n_lflat > 100);
+    S.status |= vst;
+    B.counts[(size_t)s * CNT_N + CNT_LFLAT] = n_lflat;
   }
 }
 
@@ -1716,7 +2208,9 @@ LG_DEVICE double eig_max_sym3(const float* Af) {
   return fmax(a[0][0], fmax(a[1][1], a[2][2]));
 }
 
+#define LM_LAST_LDS 2048  // Last clouds up to this size (the corner cloud) are searched in LDS
 struct LmLds {
+  float4 lastc[LM_LAST_LDS];
   float4 sel[LM_MAXQ];
   int ind1[LM_MAXQ], ind2[LM_MAXQ], ind3[LM_MAXQ];
   double red[LM_THREADS / 64][10];
@@ -1727,6 +2221,7 @@ struct LmLds {
   int iscan[LM_THREADS / 64];
   float cur[6];
   int flag;      // 1 = keep iterating
+  int iters;     // iterations run by the loop so far
   int status;
   int skip;
 };
@@ -1986,6 +2481,47 @@ LG_DEVICE void block_reduce10(LmLds& L, double* v) {
   }
 }
 
+// AtA/AtB -> solve -> degeneracy -> update of cur (registers; every lane of the wave computes the
+// same); returns keep-iterating
+LG_DEVICE bool lm_solve_reg(float* cur, int& is_degenerate, int& status, const double* red, int iter, bool surf) {
+  float AtA[9], AtB[3], x[3];
+  AtA[0] = (float)red[0]; AtA[1] = (float)red[1]; AtA[2] = (float)red[2];
+  AtA[3] = AtA[1]; AtA[4] = (float)red[3]; AtA[5] = (float)red[4];
+  AtA[6] = AtA[2]; AtA[7] = AtA[5]; AtA[8] = (float)red[5];
+  AtB[0] = (float)red[6]; AtB[1] = (float)red[7]; AtB[2] = (float)red[8];
+  qr_solve3(AtA, AtB, x);
+  if (iter == 0) {
+    is_degenerate = eig_max_sym3(AtA) < 10.0;
+  } else if (is_degenerate) {
+    status |= LEGO_ST_DEGEN_UB;
+  }
+  if (is_degenerate) {
+    status |= LEGO_ST_DEGENERATE;
+    x[0] = x[1] = x[2] = 0.f;
+  }
+  const float RAD2DEG = (float)(180.0 / M_PI);
+  float deltaR, deltaT;
+  if (surf) {
+    cur[0] += x[0]; cur[2] += x[1]; cur[4] += x[2];
+  } else {
+    cur[1] += x[0]; cur[3] += x[1]; cur[5] += x[2];
+  }
+  for (int i = 0; i < 6; i++)
+    if (isnan(cur[i])) cur[i] = 0;
+  if (surf) {
+    double a = (double)(RAD2DEG * x[0]), b = (double)(RAD2DEG * x[1]);
+    deltaR = (float)sqrt(a * a + b * b);
+    double c = (double)(x[2] * 100);
+    deltaT = (float)sqrt(c * c);
+  } else {
+    double a = (double)(RAD2DEG * x[0]);
+    deltaR = (float)sqrt(a * a);
+    double b = (double)(x[1] * 100), c = (double)(x[2] * 100);
+    deltaT = (float)sqrt(b * b + c * c);
+  }
+  return !((double)deltaR < 0.1 && (double)deltaT < 0.1);
+}
+
 // thread 0: AtA/AtB -> solve -> degeneracy -> update; returns keep-iterating
 LG_DEVICE bool lm_solve(LmLds& L, LgState& S, const double* red, int iter, bool surf) {
   float AtA[9], AtB[3], x[3];
@@ -2026,11 +2562,23 @@ LG_DEVICE bool lm_solve(LmLds& L, LgState& S, const double* red, int iter, bool 
   return !((double)deltaR < 0.1 && (double)deltaT < 0.1);
 }
 
-LG_DEVICE void accumulate_surf_row(const float* cur, const float4 po, const float4 cf, double* acc) {
+// sin / cos of transformCur's rotation, computed once per iteration (the reference computes them
+// once per calculateTransformation* call, outside its row loop)
+struct LmTrig {
+  float srx, crx, sry, cry, srz, crz, tx, ty, tz;
+};
+LG_DEVICE LmTrig lm_trig(const float* cur) {
+  LmTrig t;
+  t.srx = sinf_g(cur[0]); t.crx = cosf_g(cur[0]); t.sry = sinf_g(cur[1]); t.cry = cosf_g(cur[1]);
+  t.srz = sinf_g(cur[2]); t.crz = cosf_g(cur[2]);
+  t.tx = cur[3]; t.ty = cur[4]; t.tz = cur[5];
+  return t;
+}
+
+LG_DEVICE void accumulate_surf_row(const LmTrig& T, const float4 po, const float4 cf, double* acc) {
   // calculateTransformationSurf :797-857 (per-row Jacobian)
-  float srx = sinf_g(cur[0]), crx = cosf_g(cur[0]), sry = sinf_g(cur[1]), cry = cosf_g(cur[1]);
-  float srz = sinf_g(cur[2]), crz = cosf_g(cur[2]);
-  float tx = cur[3], ty = cur[4], tz = cur[5];
+  const float srx = T.srx, crx = T.crx, sry = T.sry, cry = T.cry, srz = T.srz, crz = T.crz;
+  const float tx = T.tx, ty = T.ty, tz = T.tz;
   float a1 = crx * sry * srz;
   float a2 = crx * crz * sry;
   float a3 = srx * sry;
@@ -2067,11 +2615,10 @@ LG_DEVICE void accumulate_surf_row(const float* cur, const float4 po, const floa
   acc[9] += 1.0;
 }
 
-LG_DEVICE void accumulate_corner_row(const float* cur, const float4 po, const float4 cf, double* acc) {
+LG_DEVICE void accumulate_corner_row(const LmTrig& T, const float4 po, const float4 cf, double* acc) {
   // calculateTransformationCorner :939-977
-  float srx = sinf_g(cur[0]), crx = cosf_g(cur[0]), sry = sinf_g(cur[1]), cry = cosf_g(cur[1]);
-  float srz = sinf_g(cur[2]), crz = cosf_g(cur[2]);
-  float tx = cur[3], ty = cur[4], tz = cur[5];
+  const float srx = T.srx, crx = T.crx, sry = T.sry, cry = T.cry, srz = T.srz, crz = T.crz;
+  const float tx = T.tx, ty = T.ty, tz = T.tz;
   float b1 = -crz * sry - cry * srx * srz;
   float b2 = cry * crz * srx - sry * srz;
   float b3 = crx * cry;
@@ -2137,23 +2684,61 @@ LG_DEVICE bool corner_coeff(const float4* last, int i1, int i2, float4 sel, int 
   return false;
 }
 
-// one LM loop (surf or corner), <= 25 iterations
+// Brute-force exact 1-NN over a Last cloud staged in LDS (small clouds: the corner cloud): the
+// (d, lowest index) minimum and the tie count over all points equal the grid search's (and so
+// nanoflann's) whenever the neighbour is accepted (d < r2).  tpq lanes per query, merged by xor
+// shuffles as in grid_nn.
+LG_DEVICE int lds_nn(const float4* last, int nl, float4 q, float r2, bool& tie, int sub, int tpq, bool act) {
+  float bd = FLT_MAX;
+  int bi = 0x7fffffff, bc = 0;
+  if (act)
+    for (int j = sub; j < nl; j += tpq) {
+      const float4 p = last[j];
+      const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+      const float d = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
+      if (d < bd) { bd = d; bi = j; bc = 1; }
+      else if (d == bd) { bc++; bi = min(bi, j); }
+    }
+  for (int o = tpq >> 1; o > 0; o >>= 1) {
+    const float d2 = __shfl_xor(bd, o);
+    const int i2 = __shfl_xor(bi, o), c2 = __shfl_xor(bc, o);
+    if (d2 < bd) { bd = d2; bi = i2; bc = c2; }
+    else if (d2 == bd) { bi = min(bi, i2); bc += c2; }
+  }
+  tie = (bd < r2) && bc > 1;
+  return (bd < r2) ? bi : -1;
+}
+
+// one LM loop (surf or corner), <= 25 iterations.  The correspondence search (iterations 0, 5, 10,
+// 15, 20) uses the whole workgroup; the other iterations only re-weight the same correspondences
+// with the updated transform, so wave 0 runs each block of up to 5 iterations on its own
+// (coefficients, a butterfly reduction that leaves the normal equations in every lane, the 3x3 solve
+// in registers) and the workgroup meets once per block instead of three times per iteration.
 LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __restrict__ feat, int nq,
-                       const float4* __restrict__ last, int nl, bool surf, float4* gp, int& iters) {
+                       const float4* __restrict__ last_g, int nl, bool surf, float4* gp, int& iters) {
   const int tid = threadIdx.x;
   const int nw = LM_THREADS / 64;
+  const bool small = nl <= LM_LAST_LDS;
   PROF_T(t_bg0);
-  build_grid(L, last, nl, gp, 1.1f * sqrtf(P.nn_dist_sqr) + 0.05f);
-  PROF_ADD(16, t_bg0);
-  for (int iter = 0; iter < 25; iter++) {
-    float cur[6];
-    for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
-    PROF_T(t_sel0);
-    for (int q = tid; q < nq; q += LM_THREADS) L.sel[q] = transform_to_start(feat[q], cur);
+  if (small) {
+    for (int j = tid; j < nl; j += LM_THREADS) L.lastc[j] = last_g[j];
     __syncthreads();
-    PROF_ADD(8, t_sel0);
-    PROF_T(t_srch0);
-    if (iter % 5 == 0) {
+  } else {
+    build_grid(L, last_g, nl, gp, 1.1f * sqrtf(P.nn_dist_sqr) + 0.05f);
+  }
+  const float4* last = small ? (const float4*)L.lastc : last_g;
+  PROF_ADD(16, t_bg0);
+  if (tid == 0) L.iters = 0;
+  for (int iter = 0; iter < 25; iter += 5) {
+    {  // search (all waves)
+      float cur[6];
+      for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
+      PROF_T(t_sel0);
+      for (int q = tid; q < nq; q += LM_THREADS) L.sel[q] = transform_to_start(feat[q], cur);
+      __syncthreads();
+      PROF_ADD(8, t_sel0);
+      PROF_T(t_srch0);
+      PROF_T(t_nn0);
       int st = 0;
       // as many lanes per query as the block allows (surf ~170 queries: 2; corner ~115: 4)
       const int tpq = nq * 8 <= LM_THREADS ? 8 : nq * 4 <= LM_THREADS ? 4 : nq * 2 <= LM_THREADS ? 2 : 1;
@@ -2161,14 +2746,17 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
         const int t = base + tid, q = t / tpq;
         const bool act = q < nq;
         bool tie = false;
-        const int c = grid_nn(L, gp, act ? L.sel[q] : make_float4(0.f, 0.f, 0.f, 0.f), P.nn_dist_sqr, tie, t % tpq,
-                              tpq, act);
+        const float4 qs = act ? L.sel[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int c = small ? lds_nn(last, nl, qs, P.nn_dist_sqr, tie, t % tpq, tpq, act)
+                            : grid_nn(L, gp, qs, P.nn_dist_sqr, tie, t % tpq, tpq, act);
         if (act && t % tpq == 0) {
           L.ind1[q] = c;
           if (tie) st |= LEGO_ST_NN_TIE;
         }
       }
       __syncthreads();
+      PROF_ADD(37, t_nn0);
+      PROF_T(t_rs0);
       for (int q = wave_id(); q < nq; q += nw) {
         const int c = L.ind1[q];
         int o2 = -1, o3 = -1;
@@ -2178,31 +2766,50 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
       st = wave_or(st);
       if (lane_id() == 0 && st) atomicOr(&L.status, st);
       __syncthreads();
+      PROF_ADD(38, t_rs0);
+      PROF_ADD(9, t_srch0);
     }
-    PROF_ADD(9, t_srch0);
     PROF_T(t_acc0);
-    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int q = tid; q < nq; q += LM_THREADS) {
-      float4 cf;
-      const bool ok = surf ? surf_coeff(last, L.ind1[q], L.ind2[q], L.ind3[q], L.sel[q], iter, cf)
-                           : corner_coeff(last, L.ind1[q], L.ind2[q], L.sel[q], iter, cf);
-      if (ok) {
-        if (surf) accumulate_surf_row(cur, feat[q], cf, acc);
-        else accumulate_corner_row(cur, feat[q], cf, acc);
+    if (wave_id() == 0) {  // iterations iter .. iter + 4 on wave 0
+      const int lane = lane_id();
+      float cur[6];
+      for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
+      int deg = S.is_degenerate, status = 0, it = iter, run = L.iters;
+      bool keep = true;
+      for (; it < iter + 5 && it < 25; ++it) {
+        const LmTrig T = lm_trig(cur);
+        double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int q = lane; q < nq; q += 64) {
+          const float4 sel = it == iter ? L.sel[q] : transform_to_start(feat[q], cur);
+          float4 cf;
+          const bool ok = surf ? surf_coeff(last, L.ind1[q], L.ind2[q], L.ind3[q], sel, it, cf)
+                               : corner_coeff(last, L.ind1[q], L.ind2[q], sel, it, cf);
+          if (ok) {
+            if (surf) accumulate_surf_row(T, feat[q], cf, acc);
+            else accumulate_corner_row(T, feat[q], cf, acc);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 10; ++k)
+          for (int o = 32; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o);
+        run = it + 1;
+        if (acc[9] < 10.0) continue;  // too few correspondences: `continue`
+        if (!lm_solve_reg(cur, deg, status, acc, it, surf)) { keep = false; break; }
+      }
+      if (lane == 0) {
+        for (int k = 0; k < 6; ++k) L.cur[k] = cur[k];
+        S.is_degenerate = deg;
+        if (status) L.status |= status;
+        L.iters = run;
+        L.flag = keep ? 1 : 0;
       }
     }
-    block_reduce10(L, acc);
-    PROF_ADD(10, t_acc0);
-    PROF_T(t_sol0);
-    if (tid == 0) {
-      iters = iter + 1;
-      if (acc[9] < 10.0) L.flag = 1;  // too few correspondences: `continue`
-      else L.flag = lm_solve(L, S, acc, iter, surf) ? 1 : 0;
-    }
     __syncthreads();
-    PROF_ADD(15, t_sol0);
+    PROF_ADD(10, t_acc0);
     if (!L.flag) break;
   }
+  iters = L.iters;
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
@@ -2211,11 +2818,10 @@ __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x;
   const int V = P.V, VH = P.VH;
   const int32_t* cnt = B.counts + (size_t)s * CNT_N;
-  const int n_sharp = cnt[CNT_SHARP], n_lsharp = cnt[CNT_LSHARP], n_flat = cnt[CNT_FLAT], n_lflat = cnt[CNT_LFLAT];
+  const int n_sharp = cnt[CNT_SHARP], n_lsharp = cnt[CNT_LSHARP], n_flat = cnt[CNT_FLAT];
   const float4* f_sharp = B.f_sharp + (size_t)s * V * P.cap_sharp;
   const float4* f_lsharp = B.f_lsharp + (size_t)s * V * P.cap_lsharp;
   const float4* f_flat = B.f_flat + (size_t)s * V * P.cap_flat;
-  const float4* f_lflat = B.f_lflat + (size_t)s * VH;
   if (tid == 0) {
     S = B.state[s];
     L.status = cnt[CNT_STATUS];
@@ -2227,13 +2833,11 @@ __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
   float4* surf_base = B.surf_last + (size_t)s * 2 * sl_stride;
   if (!S.initialized) {  // checkSystemInitialization (:1181-1209): Last = current, untransformed
     float4* cl = corner_base + (size_t)S.last_buf * cl_stride;
-    float4* sl = surf_base + (size_t)S.last_buf * sl_stride;
     for (int k = tid; k < n_lsharp; k += LM_THREADS) cl[k] = f_lsharp[k];
-    for (int k = tid; k < n_lflat; k += LM_THREADS) sl[k] = f_lflat[k];
-    if (tid == 0) {
+    if (tid == 0) {  // the lessFlat cloud follows in k_publish (untransformed)
       S.initialized = 1;
+      S.pub_copy = 1;
       S.n_corner_last = n_lsharp;
-      S.n_surf_last = n_lflat;
       S.tree_stale = 0;
       S.status = L.status | LEGO_ST_INIT;
       S.iters_surf = S.iters_corner = 0;
@@ -2301,21 +2905,19 @@ __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
   }
   __syncthreads();
   // publishCloudsLast (:1329-1383): TransformToEnd into the other half of the Last double buffer
+  // (the lessSharp half here; the lessFlat half is k_publish's, after the VoxelGrid)
   {
     float cur[6];
     for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
     const int nb = S.last_buf ^ 1;
     float4* cl = corner_base + (size_t)nb * cl_stride;
-    float4* sl = surf_base + (size_t)nb * sl_stride;
     for (int k = tid; k < n_lsharp; k += LM_THREADS) cl[k] = transform_to_end(f_lsharp[k], cur);
-    for (int k = tid; k < n_lflat; k += LM_THREADS) sl[k] = transform_to_end(f_lflat[k], cur);
   }
   __syncthreads();
   if (tid == 0) {
     S.last_buf ^= 1;
+    S.pub_copy = 0;
     S.n_corner_last = n_lsharp;
-    S.n_surf_last = n_lflat;
-    S.tree_stale = !(n_lsharp > 10 && n_lflat > 100);
     S.cycle++;
     if (S.cycle == P.map_div) {
       S.cycle = 0;
@@ -2336,18 +2938,15 @@ __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
   } while (0)
 
 bool lg_lds_projection(const LgParams& P) { return (size_t)(P.VH + 64) * 4 <= 160 * 1024; }
-bool lg_lds_segment(const LgParams& P) { return P.V <= 16 && (size_t)(P.VH + 64) * 4 <= 160 * 1024; }
+bool lg_lds_segment(const LgParams& P) { return P.V <= 16 && P.VH < 32768; }  // k_segment_lds packing
 
 int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
                       const int32_t* cnts, hipStream_t st) {
   if (lg_lds_projection(P)) {
     size_t sm = (size_t)(P.VH + 64) * 4;
-    if (P.V <= 16)
-      hipLaunchKernelGGL((k_project<true, 16>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
-    else
-      hipLaunchKernelGGL((k_project<true, 0>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
+    hipLaunchKernelGGL((k_project<true>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
   } else {
-    hipLaunchKernelGGL((k_project<false, 0>), dim3(S), dim3(1024), 64 * 4, st, P, B, pts, offs, cnts);
+    hipLaunchKernelGGL((k_project<false>), dim3(S), dim3(1024), 64 * 4, st, P, B, pts, offs, cnts);
   }
   LG_CHECK_LAUNCH();
   return LEGO_OK;
@@ -2356,16 +2955,17 @@ int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* p
 int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   if (lg_lds_segment(P)) {
     size_t sm = (size_t)(P.VH + 64) * 4;
-    hipLaunchKernelGGL((k_segment<true>), dim3(S), dim3(1024), sm, st, P, B);
+    hipLaunchKernelGGL(k_segment_lds, dim3(S), dim3(1024), sm, st, P, B);
   } else {
-    hipLaunchKernelGGL((k_segment<false>), dim3(S), dim3(1024), 64 * 4, st, P, B);
+    hipLaunchKernelGGL(k_segment_global, dim3(S), dim3(1024), 64 * 4, st, P, B);
   }
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
 
-int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  hipLaunchKernelGGL(k_fa_prep, dim3(S), dim3(1024), 0, st, P, B);
+int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st, bool distort) {
+  if (distort) hipLaunchKernelGGL(k_fa_prep<true>, dim3(S), dim3(1024), 0, st, P, B);
+  else hipLaunchKernelGGL(k_fa_prep<false>, dim3(S), dim3(1024), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
@@ -2373,7 +2973,17 @@ int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
 int lg_launch_extract(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   hipLaunchKernelGGL(k_extract, dim3(S * (P.V + 1)), dim3(64), 0, st, P, B);
   LG_CHECK_LAUNCH();
+  return LEGO_OK;
+}
+
+int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   hipLaunchKernelGGL(k_voxel, dim3(S * P.V), dim3(64), 0, st, P, B);
+  LG_CHECK_LAUNCH();
+  return LEGO_OK;
+}
+
+int lg_launch_publish(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
+  hipLaunchKernelGGL(k_publish, dim3(S), dim3(256), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }

@@ -47,6 +47,7 @@ def lib():
         L.lego_batch_destroy.argtypes = [C.c_void_p]
         L.lego_batch_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.lego_batch_sync.argtypes = [C.c_void_p]
+        L.lego_batch_flush.argtypes = [C.c_void_p]
         L.lego_batch_read.argtypes = [C.c_void_p, C.c_int32, P(LegoProjectionOut), P(LegoAssociationOut)]
         L.lego_batch_read_poses.argtypes = [C.c_void_p, P(C.c_float), P(C.c_int32)]
         L.lego_batch_reset.argtypes = [C.c_void_p]
@@ -154,6 +155,10 @@ class Batch:
 
     def sync(self):
         _check(lib().lego_batch_sync(self.h), "lego_batch_sync")
+
+    def flush(self):
+        """Enqueue the last step's pending lessFlat publish (asynchronous)."""
+        _check(lib().lego_batch_flush(self.h), "lego_batch_flush")
 
     def reset(self):
         _check(lib().lego_batch_reset(self.h), "lego_batch_reset")

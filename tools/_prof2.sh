@@ -1,0 +1,2 @@
+mkdir -p gpurun_out/p2
+LEGO_FRONTEND_LIB=lego-loam-bor_amd/lego_amd/liblego_frontend_prof.so timeout -k 10 200 python3 tools/phase_profile.py 256 1 > gpurun_out/p2/phase1.log 2>&1 && bash tools/_gpu_check.sh

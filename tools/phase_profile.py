@@ -22,7 +22,9 @@ NAMES = {0: "x:load+sort seg", 1: "x:sharp greedy", 2: "x:flat greedy", 3: "x:le
          12: "  seg: global load", 13: "  seg: sort", 8: "lm:transform sel", 9: "lm:search", 10: "lm:coeff+reduce",
          15: "lm:solve (thread 0)", 16: "lm:build grid", 17: "lm:surf loop", 18: "lm:corner loop",
          20: "p:init winner", 21: "p:scatter", 22: "p:reduce+orient", 23: "p:columns",
-         25: "s:init parents", 26: "s:edges+unite", 27: "s:find roots", 28: "s:sizes+rank+label", 29: "s:compaction"}
+         36: "  sort:heap pops", 37: "lm:  grid nn", 38: "lm:  ring scans",
+         32: "f:tile distort", 33: "f:tile LDS load", 34: "f:occl flags", 35: "f:smooth+picked",
+         25: "s:init parents", 26: "s:edges+unite", 27: "s:find roots", 28: "s:sizes+rank+label", 29: "s:compaction", 31: "s:distortion"}
 
 
 def main():
