@@ -2209,14 +2209,21 @@ LG_DEVICE double eig_max_sym3(const float* Af) {
 }
 
 #define LM_LAST_LDS 2048  // Last clouds up to this size (the corner cloud) are searched in LDS
+#define LM_RMAX 72        // ring values -1 .. 70 (V <= 64)
 struct LmLds {
-  float4 lastc[LM_LAST_LDS];
+  union {
+    float4 lastc[LM_LAST_LDS];  // small Last cloud, staged
+    int gcell[GRID_MAX + 1];    // larger cloud: uniform grid, end offset of every cell in grid_pts
+  } u;
+  float gmin[3], gcs;
+  int gdim[3];
   float4 sel[LM_MAXQ];
   int ind1[LM_MAXQ], ind2[LM_MAXQ], ind3[LM_MAXQ];
   double red[LM_THREADS / 64][10];
-  int gcell[GRID_MAX + 1];  // uniform grid over the Last cloud: end offset of every cell
-  float gmin[3], gcs;
-  int gdim[3];
+  int first_ge[LM_RMAX + 4];  // first index with ring >= r (index r + 1), nl if none
+  int last_le[LM_RMAX + 4];   // last index with ring <= r (index r + 1), -1 if none
+  int nfall;                  // queries whose ring breaks need the sequential scan
+  int fall[LM_MAXQ];
   float fred[6][LM_THREADS / 64];
   int iscan[LM_THREADS / 64];
   float cur[6];
@@ -2261,6 +2268,56 @@ LG_DEVICE int block_excl_scan_int(LmLds& L, int v, int& total) {
   return off + x - v;
 }
 
+// ---- correspondence search over the Last cloud ------------------------------------------------
+// The reference's searches only use points closer than nearest_feature_search_distance (5 m):
+// the 1-NN is used only when d^2 < 25 (fa.cpp:516,654) and the 2nd / 3rd points of the ring-limited
+// scans (:514-564, 652-713) start from the bound 25 with strict <.  So both searches are exact over
+// the points inside a 5 m ball around the query, in the reference's own order keys:
+//   1-NN: (d, lowest index) -- the brute-force answer, pinned against nanoflann (see grid_nn note);
+//   scans: the forward scan visits j = closest+1 .. up to the first ring break (or the bound), the
+//          backward scan closest-1 .. down to its break; (d, visit rank) lexicographic = the
+//          sequential strict-< scans.  The break positions come from per-ring first / last indices.
+// Small Last clouds (the corner cloud) are staged in LDS and scanned whole; larger ones (the surf
+// cloud) are bucketed into an (x, y) column grid with cells of c = 5.01/3 m, so the 5 m ball is a
+// handful of contiguous runs of columns.
+
+// first_ge / last_le from the Last cloud's rings (block-wide); ring(j) = (int)last[j].w
+LG_DEVICE void ring_index(LmLds& L, const float4* last, int nl) {
+  const int tid = threadIdx.x;
+  for (int r = tid; r < LM_RMAX + 4; r += LM_THREADS) { L.first_ge[r] = nl; L.last_le[r] = -1; }
+  __syncthreads();
+  for (int j = tid; j < nl; j += LM_THREADS) {
+    const int r = min(max((int)last[j].w + 1, 0), LM_RMAX - 1);
+    atomicMin(&L.first_ge[r], j);
+    atomicMax(&L.last_le[r], j);
+  }
+  __syncthreads();
+  if (tid == 0) {  // suffix min / prefix max
+    for (int r = LM_RMAX - 2; r >= 0; --r) L.first_ge[r] = min(L.first_ge[r], L.first_ge[r + 1]);
+    for (int r = 1; r < LM_RMAX; ++r) L.last_le[r] = max(L.last_le[r], L.last_le[r - 1]);
+  }
+  __syncthreads();
+}
+
+struct NnBest {  // (d, lowest index) and the number of points at d
+  float d;
+  int i, c;
+  LG_DEVICE void visit(float4 q, float4 p, int idx) {
+    const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+    const float dd = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
+    if (dd < d) { d = dd; i = idx; c = 1; }
+    else if (dd == d) { c++; i = min(i, idx); }
+  }
+  LG_DEVICE void merge(int tpq) {  // across the tpq lanes of a query
+    for (int o = tpq >> 1; o > 0; o >>= 1) {
+      const float d2 = __shfl_xor(d, o);
+      const int i2 = __shfl_xor(i, o), c2 = __shfl_xor(c, o);
+      if (d2 < d) { d = d2; i = i2; c = c2; }
+      else if (d2 == d) { i = min(i, i2); c += c2; }
+    }
+  }
+};
+
 LG_DEVICE int grid_coord(float v, float mn, float cs, int dim) {
   float f = floorf((v - mn) / cs);
   f = fminf(fmaxf(f, -2.f), (float)dim + 1.f);
@@ -2300,26 +2357,26 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
   }
   __syncthreads();
   const int ncell = L.gdim[0] * L.gdim[1] * L.gdim[2];
-  for (int c = tid; c <= ncell; c += LM_THREADS) L.gcell[c] = 0;
+  for (int c = tid; c <= ncell; c += LM_THREADS) L.u.gcell[c] = 0;
   __syncthreads();
   for (int j = tid; j < nl; j += LM_THREADS) {
     const float4 p = last[j];
     const int cx = min(max(grid_coord(p.x, L.gmin[0], L.gcs, L.gdim[0]), 0), L.gdim[0] - 1);
     const int cy = min(max(grid_coord(p.y, L.gmin[1], L.gcs, L.gdim[1]), 0), L.gdim[1] - 1);
     const int cz = min(max(grid_coord(p.z, L.gmin[2], L.gcs, L.gdim[2]), 0), L.gdim[2] - 1);
-    atomicAdd(&L.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
+    atomicAdd(&L.u.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
   }
   __syncthreads();
   // exclusive scan of the counts -> cell start offsets (each thread a contiguous chunk)
   const int per = (ncell + LM_THREADS - 1) / LM_THREADS;
   const int c0 = min(tid * per, ncell), c1 = min(c0 + per, ncell);
   int local = 0;
-  for (int c = c0; c < c1; ++c) local += L.gcell[c];
+  for (int c = c0; c < c1; ++c) local += L.u.gcell[c];
   int tot;
   int run = block_excl_scan_int(L, local, tot);
   for (int c = c0; c < c1; ++c) {
-    const int n = L.gcell[c];
-    L.gcell[c] = run;
+    const int n = L.u.gcell[c];
+    L.u.gcell[c] = run;
     run += n;
   }
   __syncthreads();
@@ -2329,7 +2386,7 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
     const int cx = min(max(grid_coord(p.x, L.gmin[0], L.gcs, L.gdim[0]), 0), L.gdim[0] - 1);
     const int cy = min(max(grid_coord(p.y, L.gmin[1], L.gcs, L.gdim[1]), 0), L.gdim[1] - 1);
     const int cz = min(max(grid_coord(p.z, L.gmin[2], L.gcs, L.gdim[2]), 0), L.gdim[2] - 1);
-    const int slot = atomicAdd(&L.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
+    const int slot = atomicAdd(&L.u.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
     gp[slot] = make_float4(p.x, p.y, p.z, __int_as_float(j));
   }
   __syncthreads();
@@ -2353,8 +2410,8 @@ LG_DEVICE int grid_nn(const LmLds& L, const float4* __restrict__ gp, float4 q, f
         const int row = (cz * L.gdim[1] + cy) * L.gdim[0];
         const int x0 = max(qx - 1, 0), x1 = min(qx + 1, L.gdim[0] - 1);
         if (x0 > x1) continue;
-        const int b = (row + x0 == 0) ? 0 : L.gcell[row + x0 - 1];
-        const int e = L.gcell[row + x1];  // cells x0..x1 of a row are contiguous
+        const int b = (row + x0 == 0) ? 0 : L.u.gcell[row + x0 - 1];
+        const int e = L.u.gcell[row + x1];  // cells x0..x1 of a row are contiguous
         // the (d, idx) minimum and tie count do not depend on the visiting order: 8 loads in flight
         auto visit = [&](const float4 p) {
           const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
@@ -2392,8 +2449,9 @@ LG_DEVICE void ring_scans(const LgParams& P, const float4* __restrict__ last, in
   const int lane = lane_id();
   o2 = -1; o3 = -1;
   const int ring0 = (int)last[closest].w;
+  // rank -1: a candidate at exactly the initial bound is not taken (the reference's strict <)
   float b2d = P.nn_dist_sqr, b3d = P.nn_dist_sqr;
-  int b2r = 0x7fffffff, b3r = 0x7fffffff, b2i = -1, b3i = -1;
+  int b2r = -1, b3r = -1, b2i = -1, b3i = -1;
   int bound = fwd_bound;  // reference bug: bounded by the current feature count (:522, :661)
   if (bound > nl) {
     if (closest + 1 < bound) status |= LEGO_ST_FWD_OOB;
@@ -2684,6 +2742,65 @@ LG_DEVICE bool corner_coeff(const float4* last, int i1, int i2, float4 sel, int 
   return false;
 }
 
+// The 2nd / 3rd correspondence of one query from candidate points, in the sequential scans' order
+// keys (ring_scans): forward candidates closest < j < fe, backward be < j < closest.
+struct ScanBest {
+  float d2, d3;
+  int r2, r3, i2, i3;
+  LG_DEVICE void init(float bound) { d2 = d3 = bound; r2 = r3 = -1; i2 = i3 = -1; }
+  LG_DEVICE void visit(float4 sel, float4 p, int j, int rj, int closest, int ring0, int fe, int be, bool surf) {
+    bool fwd;
+    if (j > closest && j < fe) fwd = true;
+    else if (j < closest && j > be) fwd = false;
+    else return;
+    const int rank = fwd ? j - closest : (1 << 24) + (closest - j);
+    const float d = (p.x - sel.x) * (p.x - sel.x) + (p.y - sel.y) * (p.y - sel.y) + (p.z - sel.z) * (p.z - sel.z);
+    if (surf) {
+      if (fwd ? rj <= ring0 : rj >= ring0) { if (key_lt(d, rank, d2, r2)) { d2 = d; r2 = rank; i2 = j; } }
+      else { if (key_lt(d, rank, d3, r3)) { d3 = d; r3 = rank; i3 = j; } }
+    } else if (fwd ? rj > ring0 : rj < ring0) {
+      if (key_lt(d, rank, d2, r2)) { d2 = d; r2 = rank; i2 = j; }
+    }
+  }
+  LG_DEVICE void merge(int tpq) {
+    for (int o = tpq >> 1; o > 0; o >>= 1) {
+      float d = __shfl_xor(d2, o);
+      int r = __shfl_xor(r2, o), i = __shfl_xor(i2, o);
+      if (key_lt(d, r, d2, r2)) { d2 = d; r2 = r; i2 = i; }
+      d = __shfl_xor(d3, o); r = __shfl_xor(r3, o); i = __shfl_xor(i3, o);
+      if (key_lt(d, r, d3, r3)) { d3 = d; r3 = r; i3 = i; }
+    }
+  }
+  LG_DEVICE void take(const ScanBest& o) {
+    if (key_lt(o.d2, o.r2, d2, r2)) { d2 = o.d2; r2 = o.r2; i2 = o.i2; }
+    if (key_lt(o.d3, o.r3, d3, r3)) { d3 = o.d3; r3 = o.r3; i3 = o.i3; }
+  }
+};
+
+// Scan ends around `closest`: fe = first j > closest with ring >= ring0 + 3 (the break, :522-524 /
+// :661-663) or the bound; be = last j < closest with ring <= ring0 - 3, or -1.  False when the
+// per-ring first / last indices cannot decide (a ring value out of order by 3 or more: never for
+// the intensity-derived rings, kept exact by the sequential fallback).
+LG_DEVICE bool scan_ends(const LmLds& L, int closest, int ring0, int bound, int& fe, int& be) {
+  const int tf = ring0 + 3 + 1, tb = ring0 - 3 + 1;
+  bool ok = true;
+  fe = bound;
+  if (closest + 1 < bound && tf >= 0 && tf < LM_RMAX) {
+    const int f = L.first_ge[tf];
+    if (f > closest) fe = min(f, bound);
+    else ok = false;
+  } else if (closest + 1 < bound && tf < 0) {
+    ok = false;
+  }
+  be = -1;
+  if (closest > 0 && tb >= 0) {
+    const int g = tb < LM_RMAX ? L.last_le[tb] : closest;
+    if (g < closest) be = g;
+    else ok = false;
+  }
+  return ok;
+}
+
 // Brute-force exact 1-NN over a Last cloud staged in LDS (small clouds: the corner cloud): the
 // (d, lowest index) minimum and the tie count over all points equal the grid search's (and so
 // nanoflann's) whenever the neighbour is accepted (d < r2).  tpq lanes per query, merged by xor
@@ -2721,12 +2838,12 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
   const bool small = nl <= LM_LAST_LDS;
   PROF_T(t_bg0);
   if (small) {
-    for (int j = tid; j < nl; j += LM_THREADS) L.lastc[j] = last_g[j];
+    for (int j = tid; j < nl; j += LM_THREADS) L.u.lastc[j] = last_g[j];
     __syncthreads();
-  } else {
-    build_grid(L, last_g, nl, gp, 1.1f * sqrtf(P.nn_dist_sqr) + 0.05f);
   }
-  const float4* last = small ? (const float4*)L.lastc : last_g;
+  if (!small) build_grid(L, last_g, nl, gp, 1.1f * sqrtf(P.nn_dist_sqr) + 0.05f);
+  const float4* last = small ? (const float4*)L.u.lastc : last_g;
+  ring_index(L, last, nl);
   PROF_ADD(16, t_bg0);
   if (tid == 0) L.iters = 0;
   for (int iter = 0; iter < 25; iter += 5) {
@@ -2742,14 +2859,24 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
       int st = 0;
       // as many lanes per query as the block allows (surf ~170 queries: 2; corner ~115: 4)
       const int tpq = nq * 8 <= LM_THREADS ? 8 : nq * 4 <= LM_THREADS ? 4 : nq * 2 <= LM_THREADS ? 2 : 1;
+      if (tid == 0) L.nfall = 0;
       for (int base = 0; base < nq * tpq; base += LM_THREADS) {
-        const int t = base + tid, q = t / tpq;
+        const int t = base + tid, q = t / tpq, sub = t % tpq;
         const bool act = q < nq;
         bool tie = false;
         const float4 qs = act ? L.sel[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const int c = small ? lds_nn(last, nl, qs, P.nn_dist_sqr, tie, t % tpq, tpq, act)
-                            : grid_nn(L, gp, qs, P.nn_dist_sqr, tie, t % tpq, tpq, act);
-        if (act && t % tpq == 0) {
+        int c;
+        if (small) {
+          NnBest b{FLT_MAX, 0x7fffffff, 0};
+          if (act)
+            for (int j = sub; j < nl; j += tpq) b.visit(qs, last[j], j);
+          b.merge(tpq);
+          tie = (b.d < P.nn_dist_sqr) && b.c > 1;
+          c = (b.d < P.nn_dist_sqr) ? b.i : -1;
+        } else {
+          c = grid_nn(L, gp, qs, P.nn_dist_sqr, tie, sub, tpq, act);
+        }
+        if (act && sub == 0) {
           L.ind1[q] = c;
           if (tie) st |= LEGO_ST_NN_TIE;
         }
@@ -2757,10 +2884,79 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
       __syncthreads();
       PROF_ADD(37, t_nn0);
       PROF_T(t_rs0);
-      for (int q = wave_id(); q < nq; q += nw) {
+      // ring-limited 2nd / 3rd points (fa.cpp:514-564, 652-713).  Larger clouds: one wave per query
+      // over the index ranges the per-ring first / last indices give, 8 loads in flight per lane.
+      if (!small) for (int q = wave_id(); q < nq; q += nw) {
         const int c = L.ind1[q];
         int o2 = -1, o3 = -1;
-        if (c >= 0) ring_scans(P, last, nl, L.sel[q], nq, surf, c, o2, o3, st);
+        if (c >= 0) {
+          const float4 qs = L.sel[q];
+          const int ring0 = (int)last[c].w;
+          int bound = nq;  // reference bug: bounded by the current feature count (:522, :661)
+          if (bound > nl) {
+            if (c + 1 < bound) st |= LEGO_ST_FWD_OOB;
+            bound = nl;
+          }
+          int fe, be;
+          if (scan_ends(L, c, ring0, bound, fe, be)) {
+            ScanBest sb;
+            sb.init(P.nn_dist_sqr);
+            const int je = max(fe, c);
+            int j = be + 1 + lane_id();
+            for (; j + 7 * 64 < je; j += 8 * 64) {
+              float4 p8[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) p8[u] = last[j + 64 * u];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) sb.visit(qs, p8[u], j + 64 * u, (int)p8[u].w, c, ring0, fe, be, surf);
+            }
+            for (; j < je; j += 64) {
+              const float4 p = last[j];
+              sb.visit(qs, p, j, (int)p.w, c, ring0, fe, be, surf);
+            }
+            sb.merge(64);
+            o2 = sb.i2;
+            o3 = surf ? sb.i3 : -1;
+          } else {
+            ring_scans(P, last, nl, qs, nq, surf, c, o2, o3, st);
+          }
+        }
+        if (lane_id() == 0) { L.ind2[q] = o2; L.ind3[q] = o3; }
+      }
+      // smaller clouds: tpq lanes a query
+      if (small) for (int base = 0; base < nq * tpq; base += LM_THREADS) {
+        const int t = base + tid, q = t / tpq, sub = t % tpq;
+        const bool act = q < nq;
+        const float4 qs = act ? L.sel[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int closest = act ? L.ind1[q] : -1;
+        ScanBest sb;
+        sb.init(P.nn_dist_sqr);
+        bool run = closest >= 0;
+        int fe = 0, be = 0, ring0 = 0;
+        if (run) {
+          ring0 = (int)last[closest].w;
+          int bound = nq;  // reference bug: bounded by the current feature count (:522, :661)
+          if (bound > nl) {
+            if (closest + 1 < bound) st |= LEGO_ST_FWD_OOB;
+            bound = nl;
+          }
+          if (!scan_ends(L, closest, ring0, bound, fe, be)) {
+            run = false;
+            if (sub == 0) L.fall[atomicAdd(&L.nfall, 1)] = q;
+          }
+        }
+        if (run)
+          for (int j = be + 1 + sub, je = max(fe, closest); j < je; j += tpq)
+            sb.visit(qs, last[j], j, (int)last[j].w, closest, ring0, fe, be, surf);
+        sb.merge(tpq);
+        if (act && sub == 0 && (closest < 0 || run)) { L.ind2[q] = sb.i2; L.ind3[q] = surf ? sb.i3 : -1; }
+      }
+      __syncthreads();
+      // sequential scans for the queries the per-ring indices could not decide (one wave each)
+      for (int k = wave_id(); k < L.nfall; k += nw) {
+        const int q = L.fall[k];
+        int o2 = -1, o3 = -1;
+        ring_scans(P, last, nl, L.sel[q], nq, surf, L.ind1[q], o2, o3, st);
         if (lane_id() == 0) { L.ind2[q] = o2; L.ind3[q] = o3; }
       }
       st = wave_or(st);

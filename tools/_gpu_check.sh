@@ -4,5 +4,5 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
 timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
 rc=$?
 tail -3 gpurun_out/gpu_tests.log
-cat gpurun_out/bench.log | grep metric | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["stages_ms"], d['roofline']['achieved'], d['roofline']['frac'], d.get('other_voxel_tie_order'))"
+grep metric gpurun_out/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['stages_ms'], d['roofline']['achieved'], d['roofline']['frac'], d.get('other_voxel_tie_order'))"
 exit $rc
