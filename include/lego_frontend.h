@@ -196,6 +196,10 @@ int  lego_test_libm(const float* a, const float* b, float* out, int32_t n, int32
  * keys are uint32 (is_float 0) or float bit patterns (1); is_float 2 runs k_extract's segment
  * sort (float keys, n <= 512: register sort when keys are distinct, else the emulation). */
 int  lego_test_sort(uint32_t* keys, int32_t* vals, int32_t n, int32_t is_float);
+/* Projection cell (row * H + col, or -1 = rejected) of n points (x, y, z, w float32) by the fast path
+ * of k_project (-2 = too close to a decision boundary, decided by the exact path) and by the exact
+ * glibc-faithful path (imageProjection.cpp:186-207). */
+int  lego_test_project_cells(const lego_params* p, const float* xyzw, int32_t n, int32_t* fast, int32_t* exact);
 /* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
  * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */
 int  lego_debug_prof(uint64_t* out256, int32_t reset);

@@ -33,6 +33,8 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int ncu;                              // compute units of the device (k_extract's ring rotation)
   int voxel_stable;                     // lego_params.voxel_tie_order == 1
   int epoch;                            // per-launch token for k_extract's first-pass flags
+  float inv_res_x, inv_res_y;           // (float)(1 / ang_res_*) for the fast projection path
+  int fast_proj;                        // the fast path's margins hold for these resolutions
   int par;                              // lessFlat staging half of this step (k_concat -> k_voxel)
   int S;                                // streams of the batch (staging stride)
 };

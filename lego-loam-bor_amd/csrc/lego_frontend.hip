@@ -66,6 +66,10 @@ LgParams derive(const lego_params& p) {
   P.cap_sharp = 12;   // 2 per segment x 6 (fa.cpp:295)
   P.cap_lsharp = 120; // 20 per segment x 6 (fa.cpp:299)
   P.cap_flat = 24;    // 4 per segment x 6 (fa.cpp:340)
+  // fast projection path (lego_kernels.hip proj_cell_fast): margins hold for resolutions >= 0.1 deg
+  P.inv_res_x = (float)(1.0 / (double)P.ang_res_x);
+  P.inv_res_y = (float)(1.0 / (double)P.ang_res_y);
+  P.fast_proj = (double)P.ang_res_x >= 0.1 * DEG_TO_RAD && (double)P.ang_res_y >= 0.1 * DEG_TO_RAD;
   return P;
 }
 
@@ -85,6 +89,13 @@ int d2h(std::vector<T>& h, const T* d, size_t n) {
 }
 
 }  // namespace
+
+int lg_derive_params(const lego_params& p, LgParams* out) {  // test hooks (lego_kernels.hip)
+  const int rc = lego_params_validate(&p);
+  if (rc != LEGO_OK) return rc;
+  *out = derive(p);
+  return LEGO_OK;
+}
 
 struct lego_batch {
   lego_params params;

@@ -142,12 +142,83 @@ LG_DEVICE int block_max_int(int v, int* scratch) {
   return r;
 }
 
+// ---- projection cell of a point: exact (glibc-faithful) and fast-with-margin ------------------
+// projectPointCloud (imageProjection.cpp:186-207): row = int((asin(z / range) + ang_bottom) /
+// ang_res_y), col = int(-round((atan2(x, y) - pi/2) / ang_res_x) + H/2) (wrapped), range >= 0.1.
+// Returns the cell (row * H + col) or -1 (rejected).
+LG_DEVICE int proj_cell_exact(const LgParams& P, float4 p) {
+  const float range = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+  const float verticalAngle = asinf_g(p.z / range);
+  const int rowIdn = (int)((verticalAngle + P.ang_bottom) / P.ang_res_y);
+  if (rowIdn < 0 || rowIdn >= P.V) return -1;
+  const float horizonAngle = atan2f_g(p.x, p.y);
+  int columnIdn = (int)(-round(((double)horizonAngle - M_PI_2) / (double)P.ang_res_x) + P.H * 0.5);
+  if (columnIdn >= P.H) columnIdn -= P.H;
+  if (columnIdn < 0 || columnIdn >= P.H) return -1;
+  if ((double)range < 0.1) return -1;
+  return rowIdn * P.H + columnIdn;
+}
+
+// atan(a) on [0, 1]: a * P(a^2), P a degree-8 least-squares fit; |error| < 1e-7 evaluated in float
+LG_DEVICE float atan01_poly(float a) {
+  const float s = a * a;
+  float p = 0.0024571234825998545f;
+  p = p * s + -0.014402952045202255f;
+  p = p * s + 0.03978383168578148f;
+  p = p * s + -0.07235082238912582f;
+  p = p * s + 0.10499055683612823f;
+  p = p * s + -0.14161258935928345f;
+  p = p * s + 0.1998591125011444f;
+  p = p * s + -0.33332598209381104f;
+  p = p * s + 0.9999998807907104f;
+  return a * p;
+}
+
+// The same decisions without the libm restatements, from approximations whose errors are bounded
+// far below the margins: the row from a reciprocal-sqrt and fdlibm's small-argument asin polynomial
+// (|v - v_exact| < 1e-4 row units; margin 2e-3), the column from a polynomial atan2 (< 2e-6 rad,
+// i.e. < 1e-3 column units with the rounding of the scaled angle; margin 4e-3 from the .5 rounding
+// boundary), the range test from |p|^2 against [0.0099, 0.0101].  Returns the cell, -1 (rejected) or
+// -2: too close to a decision boundary to tell, the exact path decides.  The margins hold for
+// ang_res_y >= 0.1 deg and ang_res_x >= 0.1 deg (lg_fast_projection checks them).
+LG_DEVICE int proj_cell_fast(const LgParams& P, float4 p) {
+  const float d2 = p.x * p.x + p.y * p.y + p.z * p.z;
+  if (!(d2 > 0.0101f)) return d2 < 0.0099f ? -1 : -2;
+  const float t = p.z * __builtin_amdgcn_rsqf(d2);
+  if (!(fabsf(t) < 0.49f)) return -2;
+  const float tt = t * t;
+  const float w = tt * (1.666675248e-1f + tt * (7.495297643e-2f + tt * (4.547037598e-2f + tt * (2.417951451e-2f + tt * 4.216630880e-2f))));
+  const float va = t + t * w;
+  const float v = (va + P.ang_bottom) * P.inv_res_y;
+  const float mr = 2e-3f;
+  const int r0 = (int)(v - mr), r1 = (int)(v + mr);
+  if (r0 != r1) return -2;
+  if (r0 < 0 || r0 >= P.V) return -1;
+  // horizonAngle = atan2(x, y)
+  const float ax = fabsf(p.y), ay = fabsf(p.x);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  if (!(mx > 0.f)) return -2;
+  float h = atan01_poly(mn * __builtin_amdgcn_rcpf(mx));
+  if (ay > ax) h = 1.57079637f - h;
+  if (p.y < 0.f) h = 3.14159274f - h;
+  if (p.x < 0.f) h = -h;
+  const float q = (h - 1.57079637f) * P.inv_res_x;
+  const float fq = floorf(q), fr = q - fq;
+  if (fabsf(fr - 0.5f) < 4e-3f) return -2;
+  const double k = (double)fq + (fr > 0.5f ? 1.0 : 0.0);  // round(q), q not near a half
+  int columnIdn = (int)(-k + P.H * 0.5);
+  if (columnIdn >= P.H) columnIdn -= P.H;
+  if (columnIdn < 0 || columnIdn >= P.H) return -1;
+  return r0 * P.H + columnIdn;
+}
+
 // ============================================================================================
 // k_project: reset + findStartEndAngle + projectPointCloud + groundRemoval + 2-D scan candidates
 // ============================================================================================
 // The reference's scatter "later input point overwrites earlier ones in the same cell"
 // (imageProjection.cpp:214-222) is an atomicMax of the input index per cell, followed by a
 // column-parallel gather that writes every cell (so resetParameters' fill is fused in).
+#define PQ_CAP (64 * 9)  // per-wave queue of undecided points (64 + 64 * kU)
 template <bool kLdsWinner>
 __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                   const int64_t* __restrict__ offs,
@@ -166,7 +237,19 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   PROF_T(t_p1);
   int fmin = 0x7fffffff, fmax = -1;
   // kU point loads per lane are issued before any of them is used: the loads are unconditional
-  // (index clamped to n - 1), so no per-load branch forces a wait between them.
+  // (index clamped to n - 1), so no per-load branch forces a wait between them.  Cells come from the
+  // fast path; the few points it cannot decide queue per wave and take the exact path 64 at a time.
+  int* queue = smem + 64 + (kLdsWinner ? VH : 0) + wave_id() * PQ_CAP;  // PQ_CAP ints per wave
+  int qn = 0;
+  auto drain = [&](int upto) {  // exact path for queue[qn - upto, qn)
+    const int l = lane_id();
+    if (l < upto) {
+      const int i = queue[qn - upto + l];
+      const int c = proj_cell_exact(P, in[i]);
+      if (c >= 0) atomicMax(&winner[c], i);
+    }
+    qn -= upto;
+  };
   constexpr int kU = 8;
   for (int i0 = tid; i0 < n; i0 += nt * kU) {
     float4 pk[kU];
@@ -176,30 +259,20 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
     for (int u = 0; u < kU; ++u) {
       const int i = i0 + u * nt;
       const float4 p = pk[u];
+      int c = -1;
       if (i < n && isfinite_f(p.x) && isfinite_f(p.y) && isfinite_f(p.z)) {  // removeNaNFromPointCloud
         fmin = min(fmin, i);
         fmax = max(fmax, i);
-#ifdef LG_EXPERIMENT_FAST
-        const float range = __fsqrt_rn(p.x * p.x + p.y * p.y + p.z * p.z);
-        const float verticalAngle = __ocml_asin_f32(p.z * __frsqrt_rn(p.x * p.x + p.y * p.y + p.z * p.z));
-        const int rowIdn = (int)((verticalAngle + P.ang_bottom) * (1.0f / P.ang_res_y));
-        if (rowIdn >= 0 && rowIdn < V) {
-          const float horizonAngle = __ocml_atan2_f32(p.x, p.y);
-          int columnIdn = (int)(-rintf((horizonAngle - (float)M_PI_2) * (1.0f / P.ang_res_x)) + H * 0.5f);
-#else
-        const float range = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-        const float verticalAngle = asinf_g(p.z / range);
-        const int rowIdn = (int)((verticalAngle + P.ang_bottom) / P.ang_res_y);
-        if (rowIdn >= 0 && rowIdn < V) {
-          const float horizonAngle = atan2f_g(p.x, p.y);
-          int columnIdn = (int)(-round(((double)horizonAngle - M_PI_2) / (double)P.ang_res_x) + H * 0.5);
-#endif
-          if (columnIdn >= H) columnIdn -= H;
-          if (columnIdn >= 0 && columnIdn < H && (double)range >= 0.1) atomicMax(&winner[rowIdn * H + columnIdn], i);
-        }
+        c = P.fast_proj ? proj_cell_fast(P, p) : proj_cell_exact(P, p);
+        if (c >= 0) atomicMax(&winner[c], i);
       }
+      const unsigned long long amb = __ballot(c == -2);
+      if (c == -2) queue[qn + popc_below(amb)] = i;
+      qn += __popcll(amb);
     }
+    while (qn >= 64) drain(64);  // qn < 64 + 64 * kU = PQ_CAP before each batch's appends
   }
+  while (qn > 0) drain(min(qn, 64));
   PROF_ADD(21, t_p1);
   PROF_T(t_p2);
   fmin = block_min_int(fmin, scratch);
@@ -3133,16 +3206,16 @@ __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
     if (e_ != hipSuccess) return LEGO_EDEVICE;             \
   } while (0)
 
-bool lg_lds_projection(const LgParams& P) { return (size_t)(P.VH + 64) * 4 <= 160 * 1024; }
+bool lg_lds_projection(const LgParams& P) { return (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4 <= 160 * 1024; }
 bool lg_lds_segment(const LgParams& P) { return P.V <= 16 && P.VH < 32768; }  // k_segment_lds packing
 
 int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
                       const int32_t* cnts, hipStream_t st) {
   if (lg_lds_projection(P)) {
-    size_t sm = (size_t)(P.VH + 64) * 4;
+    size_t sm = (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4;
     hipLaunchKernelGGL((k_project<true>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
   } else {
-    hipLaunchKernelGGL((k_project<false>), dim3(S), dim3(1024), 64 * 4, st, P, B, pts, offs, cnts);
+    hipLaunchKernelGGL((k_project<false>), dim3(S), dim3(1024), (64 + 16 * PQ_CAP) * 4, st, P, B, pts, offs, cnts);
   }
   LG_CHECK_LAUNCH();
   return LEGO_OK;
@@ -3209,6 +3282,40 @@ __global__ void k_libm_test(const float* a, const float* b, float* out, int n, i
   else if (which == 3) r = sqrtf(a[i]);
   else r = a[i] / b[i];
   out[i] = r;
+}
+
+int lg_derive_params(const lego_params& p, LgParams* out);  // lego_frontend.hip
+
+__global__ void k_proj_test(LgParams P, const float4* pts, int n, int* fast, int* exact) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fast[i] = proj_cell_fast(P, pts[i]);
+  exact[i] = proj_cell_exact(P, pts[i]);
+}
+
+
+// Projection cell of n points (x, y, z, w) by the fast path (-2 = undecided) and the exact path.
+extern "C" int lego_test_project_cells(const lego_params* p, const float* h_xyzw, int32_t n, int32_t* h_fast,
+                                       int32_t* h_exact) {
+  if (!p || n <= 0 || !h_xyzw || !h_fast || !h_exact) return LEGO_EINVAL;
+  LgParams P;
+  int rc = lg_derive_params(*p, &P);
+  if (rc) return rc;
+  float4* d = nullptr;
+  int *f = nullptr, *e = nullptr;
+  if (hipMalloc((void**)&d, (size_t)n * 16) != hipSuccess) return LEGO_ENOMEM;
+  if (hipMalloc((void**)&f, (size_t)n * 4) != hipSuccess) { hipFree(d); return LEGO_ENOMEM; }
+  if (hipMalloc((void**)&e, (size_t)n * 4) != hipSuccess) { hipFree(d); hipFree(f); return LEGO_ENOMEM; }
+  rc = LEGO_OK;
+  if (hipMemcpy(d, h_xyzw, (size_t)n * 16, hipMemcpyHostToDevice) != hipSuccess) rc = LEGO_EDEVICE;
+  if (rc == LEGO_OK) {
+    hipLaunchKernelGGL(k_proj_test, dim3((n + 255) / 256), dim3(256), 0, 0, P, d, n, f, e);
+    if (hipGetLastError() != hipSuccess || hipMemcpy(h_fast, f, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(h_exact, e, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = LEGO_EDEVICE;
+  }
+  hipFree(d); hipFree(f); hipFree(e);
+  return rc;
 }
 
 extern "C" int lego_test_libm(const float* h_a, const float* h_b, float* h_out, int32_t n, int32_t which) {

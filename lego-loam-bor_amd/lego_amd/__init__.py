@@ -57,6 +57,7 @@ def lib():
         L.lego_batch_read_counts.argtypes = [C.c_void_p, P(C.c_int32)]
         L.lego_test_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int32, C.c_int32]
         L.lego_test_libm.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_int32, C.c_int32]
+        L.lego_test_project_cells.argtypes = [P(LegoParams), P(C.c_float), C.c_int32, P(C.c_int32), P(C.c_int32)]
         _lib = L
     return _lib
 

@@ -89,6 +89,44 @@ def test_device_libm_matches_glibc(gpu):
     assert Hs.bits_equal(q, xy[0] / xy[1])  # numpy float32 division is IEEE
 
 
+@pytest.mark.parametrize("kind", ["vlp16", "hdl64"])
+def test_fast_projection_decides_like_the_exact_path(gpu, kind):
+    """k_project's fast path (rsqrt/polynomial asin and atan2 with decision margins) never disagrees
+    with the glibc-faithful path: on random directions, and on points placed within 1e-6 rad of
+    every row and column boundary, each cell is either identical or handed to the exact path (-2)."""
+    params = L.params_vlp16() if kind == "vlp16" else L.params_hdl64()
+    V, H = params.num_vertical_scans, params.num_horizontal_scans
+    rng = np.random.default_rng(11)
+    n = 1 << 20
+    az = rng.uniform(-np.pi, np.pi, n)
+    el = np.radians(rng.uniform(params.vertical_angle_bottom - 3, params.vertical_angle_top + 3, n))
+    # boundary points: column edges at pi/2 + (k + 0.5 - H/2) * res_x, row edges at
+    # (r * res_y - ang_bottom), each nudged by up to 1e-6 rad
+    res_x, res_y = 2 * np.pi / H, np.radians(params.vertical_angle_top - params.vertical_angle_bottom) / (V - 1)
+    ang_b = -np.radians(params.vertical_angle_bottom - 0.1)
+    m = n // 4
+    k = rng.integers(0, H, m)
+    az[:m] = np.pi / 2 - (k + 0.5 - H / 2) * res_x + rng.uniform(-1e-6, 1e-6, m)
+    r = rng.integers(0, V + 1, m)
+    el[m:2 * m] = r * res_y - ang_b + rng.uniform(-1e-6, 1e-6, m)
+    rr = rng.uniform(0.05, 120.0, n)
+    x = rr * np.cos(el) * np.sin(az)  # atan2(x, y) = az
+    y = rr * np.cos(el) * np.cos(az)
+    z = rr * np.sin(el)
+    pts = np.ascontiguousarray(np.stack([x, y, z, np.zeros(n)], 1).astype(np.float32))
+    fast = np.zeros(n, np.int32)
+    exact = np.zeros(n, np.int32)
+    ip = C.POINTER(C.c_int32)
+    rc = L.lib().lego_test_project_cells(C.byref(params), pts.ctypes.data_as(C.POINTER(C.c_float)), n,
+                                         fast.ctypes.data_as(ip), exact.ctypes.data_as(ip))
+    assert rc == 0
+    decided = fast != -2
+    assert np.array_equal(fast[decided], exact[decided])
+    assert (exact >= 0).sum() > n // 2
+    # undecided: the boundary-hugging quarter plus a small fraction of the random rest
+    assert (~decided[2 * m:]).mean() < 0.02
+
+
 def test_device_sort_matches_libstdcxx(gpu):
     """The wave-parallel introsort (segment + voxel sorts) gives libstdc++ std::sort's permutation."""
     import oracle as O
