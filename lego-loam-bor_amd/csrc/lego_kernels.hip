@@ -1956,35 +1956,40 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
 // ============================================================================================
 // k_concat: ring-ordered concatenation (cornerPointsSharp etc. are appended ring by ring)
 // ============================================================================================
-__global__ __launch_bounds__(256) void k_concat(LgParams P, LgBufs B) {
+__global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V;
-  __shared__ int off[3][65];
+  __shared__ int cnt3[3][65], off[3][65], stat[65];
+  if (tid < V) {  // per-ring counts and status, one thread a ring
+    const int32_t* rc = B.r_counts + ((size_t)s * V + tid) * 4;
+    cnt3[0][tid] = rc[0]; cnt3[1][tid] = rc[1]; cnt3[2][tid] = rc[2];
+    stat[tid] = B.r_status[(size_t)s * V + tid];
+  }
+  __syncthreads();
   if (tid == 0) {
     int a[3] = {0, 0, 0};
     int status = 0;
     for (int r = 0; r < V; ++r) {
-      const int32_t* rc = B.r_counts + ((size_t)s * V + r) * 4;
-      for (int k = 0; k < 3; ++k) { off[k][r] = a[k]; a[k] += rc[k]; }
-      status |= B.r_status[(size_t)s * V + r];
+      for (int k = 0; k < 3; ++k) { off[k][r] = a[k]; a[k] += cnt3[k][r]; }
+      status |= stat[r];
     }
     int32_t* cnt = B.counts + (size_t)s * CNT_N;
     cnt[CNT_SHARP] = a[0]; cnt[CNT_LSHARP] = a[1]; cnt[CNT_FLAT] = a[2];
     cnt[CNT_STATUS] = status;
   }
   __syncthreads();
-  for (int r = 0; r < V; ++r) {
+  for (int r = wave_id(); r < V; r += nt >> 6) {  // one wave a ring: ring-ordered concatenation
     const size_t rb = (size_t)s * V + r;
-    const int32_t* rc = B.r_counts + rb * 4;
-    for (int t = tid; t < rc[0]; t += nt) {
+    const int l = lane_id();
+    for (int t = l; t < cnt3[0][r]; t += 64) {
       B.f_sharp[(size_t)s * V * P.cap_sharp + off[0][r] + t] = B.r_sharp[rb * P.cap_sharp + t];
       B.f_sharp_ind[(size_t)s * V * P.cap_sharp + off[0][r] + t] = B.r_sharp_ind[rb * P.cap_sharp + t];
     }
-    for (int t = tid; t < rc[1]; t += nt) {
+    for (int t = l; t < cnt3[1][r]; t += 64) {
       B.f_lsharp[(size_t)s * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp[rb * P.cap_lsharp + t];
       B.f_lsharp_ind[(size_t)s * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp_ind[rb * P.cap_lsharp + t];
     }
-    for (int t = tid; t < rc[2]; t += nt) {
+    for (int t = l; t < cnt3[2][r]; t += 64) {
       B.f_flat[(size_t)s * V * P.cap_flat + off[2][r] + t] = B.r_flat[rb * P.cap_flat + t];
       B.f_flat_ind[(size_t)s * V * P.cap_flat + off[2][r] + t] = B.r_flat_ind[rb * P.cap_flat + t];
     }
@@ -1997,6 +2002,10 @@ __global__ __launch_bounds__(256) void k_concat(LgParams P, LgBufs B) {
   v.flabel = B.flabel + (size_t)s * P.VH;
   const float4* fa = B.seg_fa + (size_t)s * P.VH;
   const int lane = lane_id();
+  // The six segments [sp, ep] of a ring tile [st, en'] without gaps (ep_j + 1 = sp_{j+1}); segments
+  // with sp >= ep are skipped (their positions are not lessFlat candidates).  Eight chunks of 64
+  // positions per batch: label loads issued together, point loads buffer-masked.
+  const __amdgpu_buffer_rsrc_t rs_fa = buffer_rsrc(fa, (uint32_t)P.VH * 16u);
   for (int r = wave_id(); r < V; r += nt >> 6) {
     const size_t rb = (size_t)s * V + r;
     const size_t sb = (size_t)P.par * P.S * V + rb;
@@ -2007,67 +2016,30 @@ __global__ __launch_bounds__(256) void k_concat(LgParams P, LgBufs B) {
       const int sp = (st * (6 - j) + en * j) / 6;
       const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
       if (sp >= ep) continue;
-      for (int k0 = sp; k0 <= ep; k0 += 64) {
-        const int k = k0 + lane;
-        const bool pr = k <= ep && v.flabel[k] <= 0;
-        const unsigned long long m = __ballot(pr);
-        if (pr) dst[nlist + popc_below(m)] = fa[k];
-        nlist += __popcll(m);
+      for (int k0 = sp; k0 <= ep; k0 += 64 * 8) {
+        int8_t lab[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) lab[u] = v.flabel[min(k0 + 64 * u + lane, ep)];
+        float4 pt[8];
+        bool pr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + 64 * u + lane;
+          pr[u] = k <= ep && lab[u] <= 0;
+          pt[u] = buffer_load_f4(rs_fa, pr[u] ? (uint32_t)k * 16u : 0xffffffffu);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const unsigned long long m = __ballot(pr[u]);
+          if (pr[u]) dst[nlist + popc_below(m)] = pt[u];
+          nlist += __popcll(m);
+        }
       }
     }
     if (lane == 0) B.lf_count[sb] = nlist;
   }
 }
 
-// ============================================================================================
-// k_publish: the lessFlat half of publishCloudsLast (:1329-1383): concatenate the rings' VoxelGrid
-// outputs (surfPointsLessFlat) and TransformToEnd them into laserCloudSurfLast with the transform
-// k_lm has just produced (untransformed on the initialisation scan, :1181-1209).  Runs after both
-// k_lm and k_voxel of its scan, before the next scan's k_lm.
-// ============================================================================================
-LG_DEVICE float4 transform_to_end(const float4 pi, const float* cur);
-
-__global__ __launch_bounds__(256) void k_publish(LgParams P, LgBufs B) {
-  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  const int V = P.V, VH = P.VH;
-  __shared__ int off[65];
-  __shared__ float cur[6];
-  __shared__ int copy, nb, vst;
-  if (tid == 0) {
-    int a = 0, st = 0;
-    for (int r = 0; r < V; ++r) {
-      off[r] = a;
-      a += B.r_counts[((size_t)s * V + r) * 4 + 3];
-      st |= B.r_vstatus[(size_t)s * V + r];
-    }
-    off[V] = a;
-    vst = st;
-    const LgState& S = B.state[s];
-    for (int k = 0; k < 6; ++k) cur[k] = S.cur[k];
-    copy = S.pub_copy;
-    nb = S.last_buf;
-  }
-  __syncthreads();
-  float4* sl = B.surf_last + (size_t)s * 2 * VH + (size_t)nb * VH;
-  float4* fl = B.f_lflat + (size_t)s * VH;
-  for (int r = 0; r < V; ++r) {
-    const float4* src = B.r_lflat + ((size_t)s * V + r) * P.H;
-    const int n = off[r + 1] - off[r];
-    for (int t = tid; t < n; t += nt) {
-      const float4 p = src[t];
-      fl[off[r] + t] = p;
-      sl[off[r] + t] = copy ? p : transform_to_end(p, cur);
-    }
-  }
-  if (tid == 0) {
-    const int n_lflat = off[V];
-    LgState& S = B.state[s];
-    S.n_surf_last = n_lflat;
-    S.tree_stale = copy ? 0 : !(S.n_corner_last > 10 && n_lflat > 100);
-    S.status |= vst;
-    B.counts[(size_t)s * CNT_N + CNT_LFLAT] = n_lflat;
-  }
-}
 
 // ============================================================================================
 // k_lm: updateTransformation + integrateTransformation + publishOdometry + publishCloudsLast
@@ -2093,6 +2065,47 @@ LG_DEVICE float4 transform_to_start(const float4 pi, const float* cur) {  // :38
   float y2 = crx * y1 + srx * z1;
   float z2 = -srx * y1 + crx * z1;
   return make_float4(cry * x2 - sry * z2, y2, sry * x2 + cry * z2, pi.w);
+}
+
+// cos / sin of transformCur's rotation for TransformToEnd's second half (constant per scan)
+struct EndTrig {
+  float cx, sx, cy, sy, cz, sz;
+};
+LG_DEVICE EndTrig end_trig(const float* cur) {
+  return EndTrig{cosf_g(cur[0]), sinf_g(cur[0]), cosf_g(cur[1]), sinf_g(cur[1]), cosf_g(cur[2]), sinf_g(cur[2])};
+}
+LG_DEVICE float4 transform_to_end_t(const float4 pi, const float* cur, const EndTrig& E) {  // :422-471
+  float s = 10 * (pi.w - (float)(int)pi.w);
+  float rx = s * cur[0];
+  float ry = s * cur[1];
+  float rz = s * cur[2];
+  float tx = s * cur[3];
+  float ty = s * cur[4];
+  float tz = s * cur[5];
+  float c, sn;
+  c = cosf_g(rz); sn = sinf_g(rz);
+  float x1 = c * (pi.x - tx) + sn * (pi.y - ty);
+  float y1 = -sn * (pi.x - tx) + c * (pi.y - ty);
+  float z1 = (pi.z - tz);
+  c = cosf_g(rx); sn = sinf_g(rx);
+  float x2 = x1;
+  float y2 = c * y1 + sn * z1;
+  float z2 = -sn * y1 + c * z1;
+  c = cosf_g(ry); sn = sinf_g(ry);
+  float x3 = c * x2 - sn * z2;
+  float y3 = y2;
+  float z3 = sn * x2 + c * z2;
+  tx = cur[3]; ty = cur[4]; tz = cur[5];
+  float x4 = E.cy * x3 + E.sy * z3;
+  float y4 = y3;
+  float z4 = -E.sy * x3 + E.cy * z3;
+  float x5 = x4;
+  float y5 = E.cx * y4 - E.sx * z4;
+  float z5 = E.sx * y4 + E.cx * z4;
+  float x6 = E.cz * x5 - E.sz * y5 + tx;
+  float y6 = E.sz * x5 + E.cz * y5 + ty;
+  float z6 = z5 + tz;
+  return make_float4(x6, y6, z6, (float)(int)pi.w);
 }
 
 LG_DEVICE float4 transform_to_end(const float4 pi, const float* cur) {  // :422-471
@@ -3081,6 +3094,69 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
   __syncthreads();
 }
 
+// ============================================================================================
+// k_publish: the lessFlat half of publishCloudsLast (:1329-1383): concatenate the rings' VoxelGrid
+// outputs (surfPointsLessFlat) and TransformToEnd them into laserCloudSurfLast with the transform
+// k_lm has just produced (untransformed on the initialisation scan, :1181-1209).  Runs after both
+// k_lm and k_voxel of its scan, before the next scan's k_lm.
+// ============================================================================================
+__global__ __launch_bounds__(1024) void k_publish(LgParams P, LgBufs B) {
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int V = P.V, VH = P.VH;
+  __shared__ int off[65], cnt[65], vst[65];
+  __shared__ float cur[6];
+  __shared__ int copy, nb;
+  if (tid < V) {
+    cnt[tid] = B.r_counts[((size_t)s * V + tid) * 4 + 3];
+    vst[tid] = B.r_vstatus[(size_t)s * V + tid];
+  }
+  if (tid == 64) {
+    const LgState& S = B.state[s];
+    for (int k = 0; k < 6; ++k) cur[k] = S.cur[k];
+    copy = S.pub_copy;
+    nb = S.last_buf;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int a = 0;
+    for (int r = 0; r < V; ++r) { off[r] = a; a += cnt[r]; }
+    off[V] = a;
+  }
+  __syncthreads();
+  float c6[6];
+  for (int k = 0; k < 6; ++k) c6[k] = cur[k];
+  const EndTrig E = end_trig(c6);
+  float4* sl = B.surf_last + (size_t)s * 2 * VH + (size_t)nb * VH;
+  float4* fl = B.f_lflat + (size_t)s * VH;
+  for (int r = wave_id(); r < V; r += nt >> 6) {  // one wave a ring
+    const float4* src = B.r_lflat + ((size_t)s * V + r) * P.H;
+    const int n = cnt[r], o = off[r];
+    for (int t0 = lane_id(); t0 < n; t0 += 64 * 4) {
+      float4 p4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p4[u] = src[min(t0 + 64 * u, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + 64 * u;
+        if (t < n) {
+          fl[o + t] = p4[u];
+          sl[o + t] = copy ? p4[u] : transform_to_end_t(p4[u], c6, E);
+        }
+      }
+    }
+  }
+  if (tid == 0) {
+    int st = 0;
+    for (int r = 0; r < V; ++r) st |= vst[r];
+    const int n_lflat = off[V];
+    LgState& S = B.state[s];
+    S.n_surf_last = n_lflat;
+    S.tree_stale = copy ? 0 : !(S.n_corner_last > 10 && n_lflat > 100);
+    S.status |= st;
+    B.counts[(size_t)s * CNT_N + CNT_LFLAT] = n_lflat;
+  }
+}
+
 __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
   __shared__ LmLds L;
   __shared__ LgState S;
@@ -3180,7 +3256,8 @@ __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
     for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
     const int nb = S.last_buf ^ 1;
     float4* cl = corner_base + (size_t)nb * cl_stride;
-    for (int k = tid; k < n_lsharp; k += LM_THREADS) cl[k] = transform_to_end(f_lsharp[k], cur);
+    const EndTrig E = end_trig(cur);
+    for (int k = tid; k < n_lsharp; k += LM_THREADS) cl[k] = transform_to_end_t(f_lsharp[k], cur, E);
   }
   __syncthreads();
   if (tid == 0) {
@@ -3252,13 +3329,13 @@ int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
 }
 
 int lg_launch_publish(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  hipLaunchKernelGGL(k_publish, dim3(S), dim3(256), 0, st, P, B);
+  hipLaunchKernelGGL(k_publish, dim3(S), dim3(1024), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
 
 int lg_launch_concat(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  hipLaunchKernelGGL(k_concat, dim3(S), dim3(256), 0, st, P, B);
+  hipLaunchKernelGGL(k_concat, dim3(S), dim3(1024), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
