@@ -177,10 +177,12 @@ int  lego_batch_read_poses(lego_batch* b, float* out, int32_t* status);
 int  lego_batch_read_counts(lego_batch* b, int32_t* out);
 /* Reset every stream to the freshly constructed state (systemInitedLM = false, transforms 0). */
 int  lego_batch_reset(lego_batch* b);
-/* Kernel timing of the last step (ms, measured with hipEvents on the step's stream):
- * [0] project, [1] segment, [2] distortion+smoothness+occlusion, [3] features, [4] concat, [5] LM. */
+/* Kernel timing of the last step (ms, hipEvents on the step's stream, the pipelined path itself):
+ * [0] project, [1] segment + distortion, [2] smoothness + occlusion, [3] feature extraction,
+ * [4] concat + the previous step's lessFlat publish, [5] LM (the VoxelGrid overlaps it on an
+ * internal stream). */
 int  lego_batch_stage_times(lego_batch* b, float* ms6);
-/* While timing is enabled, steps run as one slice on the caller's stream. */
+/* While timing is enabled, steps run as one slice on the caller's stream (plus the VoxelGrid stream). */
 int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
 /* Split the streams into `groups` (1..LEGO_MAX_GROUPS) slices, each launched on its own internal HIP
  * stream (forked from and joined back into the step's stream), so one slice's long-tail kernels

@@ -353,6 +353,7 @@ static int run_association(lego_batch* b, hipStream_t st, int s0, int n, bool di
     if (b->timing) hipEventRecord(b->ev[6], st);
     return LEGO_OK;
   }
+  if (b->timing) hipEventRecord(b->ev[4], st);
   rc = lg_launch_concat(P, b->B, n, st);
   if (rc) return rc;
   if (b->pending) {  // scan k-1's lessFlat publish: after its k_voxel, before this scan's k_lm
@@ -365,7 +366,10 @@ static int run_association(lego_batch* b, hipStream_t st, int s0, int n, bool di
   rc = lg_launch_voxel(P, b->B, n, b->vs[g]);
   if (rc) return rc;
   if (hipEventRecord(b->ev_vox[g], b->vs[g]) != hipSuccess) return LEGO_EDEVICE;
-  return lg_launch_lm(P, b->B, n, st);
+  if (b->timing) hipEventRecord(b->ev[5], st);
+  rc = lg_launch_lm(P, b->B, n, st);
+  if (b->timing) hipEventRecord(b->ev[6], st);
+  return rc;
 }
 
 static int ensure_streams(lego_batch* b, int groups) {
@@ -417,15 +421,23 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   hipStream_t st = (hipStream_t)hip_stream;
   b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
-  if (b->timing) {  // per-stage timing: one stream, stages in order, nothing left pending
-    int rc = flush_pending(b);
+  if (b->timing) {  // per-stage events on the caller's stream (one slice): the pipelined path itself
+    int rc = ensure_streams(b, 1);
     if (rc) return rc;
+    if (b->pending && (b->pend_groups != 1 || b->pend_stream != st)) {
+      rc = flush_pending(b);
+      if (rc) return rc;
+    }
     b->last_stream = st;
     hipEventRecord(b->ev[0], st);
     rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
-    if (!rc) rc = run_association(b, st, 0, b->S);
+    if (!rc) rc = run_association(b, st, 0, b->S, false, true, 0);
+    if (rc) return rc;
+    b->pending = true;
+    b->pend_groups = 1;
+    b->pend_stream = st;
     b->par ^= 1;
-    return rc;
+    return LEGO_OK;
   }
   const int G = b->groups;
   int rc = ensure_streams(b, G);
