@@ -2367,15 +2367,43 @@ LG_DEVICE int block_excl_scan_int(LmLds& L, int v, int& total) {
 // cloud) are bucketed into an (x, y) column grid with cells of c = 5.01/3 m, so the 5 m ball is a
 // handful of contiguous runs of columns.
 
-// first_ge / last_le from the Last cloud's rings (block-wide); ring(j) = (int)last[j].w
+// f(j, last[j]) over the whole Last cloud, block-wide, 8 loads in flight per lane; lanes of a wave
+// hold consecutive j.
+template <typename F>
+LG_DEVICE void for_last_batched(const float4* __restrict__ last, int nl, F f) {
+  for (int j0 = threadIdx.x; j0 < nl; j0 += LM_THREADS * 8) {
+    float4 p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] = last[min(j0 + u * LM_THREADS, nl - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) f(j0 + u * LM_THREADS, p[u]);  // j may be >= nl: f checks
+  }
+}
+
+LG_DEVICE int ring_of(float w) { return min(max((int)w + 1, 0), LM_RMAX - 1); }  // index of ring (int)w
+
+// first_ge / last_le from the Last cloud's rings (block-wide); ring(j) = (int)last[j].w.  Only the
+// positions where the ring value changes can be a ring's first / last index.
 LG_DEVICE void ring_index(LmLds& L, const float4* last, int nl) {
   const int tid = threadIdx.x;
   for (int r = tid; r < LM_RMAX + 4; r += LM_THREADS) { L.first_ge[r] = nl; L.last_le[r] = -1; }
   __syncthreads();
-  for (int j = tid; j < nl; j += LM_THREADS) {
-    const int r = min(max((int)last[j].w + 1, 0), LM_RMAX - 1);
-    atomicMin(&L.first_ge[r], j);
-    atomicMax(&L.last_le[r], j);
+  for (int j0 = tid; j0 < nl; j0 += LM_THREADS * 4) {
+    float w[4], wp[4], wn[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * LM_THREADS;
+      w[u] = last[min(j, nl - 1)].w;
+      wp[u] = last[min(max(j - 1, 0), nl - 1)].w;
+      wn[u] = last[min(j + 1, nl - 1)].w;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * LM_THREADS;
+      const int r = ring_of(w[u]);
+      if (j < nl && (j == 0 || ring_of(wp[u]) != r)) atomicMin(&L.first_ge[r], j);
+      if (j < nl && (j == nl - 1 || ring_of(wn[u]) != r)) atomicMax(&L.last_le[r], j);
+    }
   }
   __syncthreads();
   if (tid == 0) {  // suffix min / prefix max
@@ -2413,11 +2441,11 @@ LG_DEVICE int grid_coord(float v, float mn, float cs, int dim) {
 LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, float4* gp, float cs0) {
   const int tid = threadIdx.x;
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  for (int j = tid; j < nl; j += LM_THREADS) {
-    const float4 p = last[j];
+  for_last_batched(last, nl, [&](int j, const float4 p) {
+    if (j >= nl) return;
     mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
     mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-  }
+  });
   for (int d = 0; d < 3; ++d) {
     const float a = wave_min(mn[d]), b = wave_max(mx[d]);
     if (lane_id() == 0) { L.fred[d][wave_id()] = a; L.fred[3 + d][wave_id()] = b; }
@@ -2445,13 +2473,13 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
   const int ncell = L.gdim[0] * L.gdim[1] * L.gdim[2];
   for (int c = tid; c <= ncell; c += LM_THREADS) L.u.gcell[c] = 0;
   __syncthreads();
-  for (int j = tid; j < nl; j += LM_THREADS) {
-    const float4 p = last[j];
+  for_last_batched(last, nl, [&](int j, const float4 p) {
+    if (j >= nl) return;
     const int cx = min(max(grid_coord(p.x, L.gmin[0], L.gcs, L.gdim[0]), 0), L.gdim[0] - 1);
     const int cy = min(max(grid_coord(p.y, L.gmin[1], L.gcs, L.gdim[1]), 0), L.gdim[1] - 1);
     const int cz = min(max(grid_coord(p.z, L.gmin[2], L.gcs, L.gdim[2]), 0), L.gdim[2] - 1);
     atomicAdd(&L.u.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
-  }
+  });
   __syncthreads();
   // exclusive scan of the counts -> cell start offsets (each thread a contiguous chunk)
   const int per = (ncell + LM_THREADS - 1) / LM_THREADS;
@@ -2467,14 +2495,14 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
   }
   __syncthreads();
   // scatter; afterwards gcell[c] = end of cell c = start of cell c+1
-  for (int j = tid; j < nl; j += LM_THREADS) {
-    const float4 p = last[j];
+  for_last_batched(last, nl, [&](int j, const float4 p) {
+    if (j >= nl) return;
     const int cx = min(max(grid_coord(p.x, L.gmin[0], L.gcs, L.gdim[0]), 0), L.gdim[0] - 1);
     const int cy = min(max(grid_coord(p.y, L.gmin[1], L.gcs, L.gdim[1]), 0), L.gdim[1] - 1);
     const int cz = min(max(grid_coord(p.z, L.gmin[2], L.gcs, L.gdim[2]), 0), L.gdim[2] - 1);
     const int slot = atomicAdd(&L.u.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
     gp[slot] = make_float4(p.x, p.y, p.z, __int_as_float(j));
-  }
+  });
   __syncthreads();
 }
 
