@@ -2294,6 +2294,30 @@ LG_DEVICE double eig_max_sym3(const float* Af) {
   return fmax(a[0][0], fmax(a[1][1], a[2][2]));
 }
 
+// eig_max_sym3(A) < thr, decided without the Jacobi sweeps when the bounds settle it: for a
+// symmetric A, max_i a_ii <= lambda_max <= max_i sum_j |a_ij| (Rayleigh quotient / Gershgorin).  The
+// margin (1e-12 of the Frobenius norm) is far above the sweeps' rounding error, so the decision is
+// the sweeps' decision; anything closer (or non-finite) runs them.
+LG_DEVICE bool lambda_max_below(const float* Af, double thr) {
+  double maxd = -1e300, gers = 0.0, fro = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    double row = 0.0;
+    for (int j = 0; j < 3; ++j) {
+      const double v = Af[i * 3 + j];
+      row += fabs(v);
+      fro += v * v;
+    }
+    maxd = fmax(maxd, (double)Af[i * 4]);
+    gers = fmax(gers, row);
+  }
+  const double tol = 1e-12 * sqrt(fro);
+  if (isfinite(fro)) {
+    if (maxd - tol > thr) return false;
+    if (gers + tol < thr) return true;
+  }
+  return eig_max_sym3(Af) < thr;
+}
+
 #define LM_LAST_LDS 2048  // Last clouds up to this size (the corner cloud) are searched in LDS
 #define LM_RMAX 72        // ring values -1 .. 70 (V <= 64)
 struct LmLds {
@@ -2304,6 +2328,8 @@ struct LmLds {
   float gmin[3], gcs;
   int gdim[3];
   float4 sel[LM_MAXQ];
+  float4 featl[LM_MAXQ];  // the loop's feature points (pointOri), staged once
+  float4 plane[LM_MAXQ];  // surf: each correspondence's plane, once per search
   int ind1[LM_MAXQ], ind2[LM_MAXQ], ind3[LM_MAXQ];
   double red[LM_THREADS / 64][10];
   int first_ge[LM_RMAX + 4];  // first index with ring >= r (index r + 1), nl if none
@@ -2663,7 +2689,7 @@ LG_DEVICE bool lm_solve_reg(float* cur, int& is_degenerate, int& status, const d
   AtB[0] = (float)red[6]; AtB[1] = (float)red[7]; AtB[2] = (float)red[8];
   qr_solve3(AtA, AtB, x);
   if (iter == 0) {
-    is_degenerate = eig_max_sym3(AtA) < 10.0;
+    is_degenerate = lambda_max_below(AtA, 10.0);
   } else if (is_degenerate) {
     status |= LEGO_ST_DEGEN_UB;
   }
@@ -2811,9 +2837,10 @@ LG_DEVICE void accumulate_corner_row(const LmTrig& T, const float4 po, const flo
   acc[9] += 1.0;
 }
 
-// coefficient of one correspondence (surf: plane :721-776, corner: line :571-635); returns accepted
-LG_DEVICE bool surf_coeff(const float4* last, int i1, int i2, int i3, float4 sel, int iter, float4& cf) {
-  if (!(i2 >= 0 && i3 >= 0)) return false;
+// coefficient of one correspondence (surf: plane :721-776, corner: line :571-635); returns accepted.
+// The plane through the three Last points (:721-731) depends only on the correspondence, so it is
+// computed once per search (surf_plane) and re-used by the iterations until the next search.
+LG_DEVICE float4 surf_plane(const float4* last, int i1, int i2, int i3) {
   const float4 t1 = last[i1], t2 = last[i2], t3 = last[i3];
   float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
   float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
@@ -2821,6 +2848,10 @@ LG_DEVICE bool surf_coeff(const float4* last, int i1, int i2, int i3, float4 sel
   float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
   float ps = sqrtf(pa * pa + pb * pb + pc * pc);
   pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+  return make_float4(pa, pb, pc, pd);
+}
+LG_DEVICE bool surf_coeff_pl(const float4 pl, float4 sel, int iter, float4& cf) {
+  const float pa = pl.x, pb = pl.y, pc = pl.z, pd = pl.w;
   float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
   float s = 1;
   if (iter >= 5)
@@ -2951,6 +2982,7 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
   const int nw = LM_THREADS / 64;
   const bool small = nl <= LM_LAST_LDS;
   PROF_T(t_bg0);
+  for (int q = tid; q < nq; q += LM_THREADS) L.featl[q] = feat[q];  // read back by the same thread first
   if (small) {
     for (int j = tid; j < nl; j += LM_THREADS) L.u.lastc[j] = last_g[j];
     __syncthreads();
@@ -2958,14 +2990,14 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
   if (!small) build_grid(L, last_g, nl, gp, 1.1f * sqrtf(P.nn_dist_sqr) + 0.05f);
   const float4* last = small ? (const float4*)L.u.lastc : last_g;
   ring_index(L, last, nl);
-  PROF_ADD(16, t_bg0);
+  PROF_ADD(surf ? 16 : 48, t_bg0);
   if (tid == 0) L.iters = 0;
   for (int iter = 0; iter < 25; iter += 5) {
     {  // search (all waves)
       float cur[6];
       for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
       PROF_T(t_sel0);
-      for (int q = tid; q < nq; q += LM_THREADS) L.sel[q] = transform_to_start(feat[q], cur);
+      for (int q = tid; q < nq; q += LM_THREADS) L.sel[q] = transform_to_start(L.featl[q], cur);
       __syncthreads();
       PROF_ADD(8, t_sel0);
       PROF_T(t_srch0);
@@ -2996,7 +3028,7 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
         }
       }
       __syncthreads();
-      PROF_ADD(37, t_nn0);
+      PROF_ADD(surf ? 37 : 46, t_nn0);
       PROF_T(t_rs0);
       // ring-limited 2nd / 3rd points (fa.cpp:514-564, 652-713).  Larger clouds: one wave per query
       // over the index ranges the per-ring first / last indices give, 8 loads in flight per lane.
@@ -3076,7 +3108,12 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
       st = wave_or(st);
       if (lane_id() == 0 && st) atomicOr(&L.status, st);
       __syncthreads();
-      PROF_ADD(38, t_rs0);
+      if (surf) {
+        for (int q = tid; q < nq; q += LM_THREADS)
+          if (L.ind2[q] >= 0 && L.ind3[q] >= 0) L.plane[q] = surf_plane(last, L.ind1[q], L.ind2[q], L.ind3[q]);
+        __syncthreads();
+      }
+      PROF_ADD(surf ? 38 : 47, t_rs0);
       PROF_ADD(9, t_srch0);
     }
     PROF_T(t_acc0);
@@ -3087,24 +3124,35 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
       int deg = S.is_degenerate, status = 0, it = iter, run = L.iters;
       bool keep = true;
       for (; it < iter + 5 && it < 25; ++it) {
+        PROF_T(t_i0);
         const LmTrig T = lm_trig(cur);
         double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (int q = lane; q < nq; q += 64) {
-          const float4 sel = it == iter ? L.sel[q] : transform_to_start(feat[q], cur);
+          const float4 po = L.featl[q];
+          const float4 sel = it == iter ? L.sel[q] : transform_to_start(po, cur);
           float4 cf;
-          const bool ok = surf ? surf_coeff(last, L.ind1[q], L.ind2[q], L.ind3[q], sel, it, cf)
+          const bool ok = surf ? (L.ind2[q] >= 0 && L.ind3[q] >= 0 && surf_coeff_pl(L.plane[q], sel, it, cf))
                                : corner_coeff(last, L.ind1[q], L.ind2[q], sel, it, cf);
           if (ok) {
-            if (surf) accumulate_surf_row(T, feat[q], cf, acc);
-            else accumulate_corner_row(T, feat[q], cf, acc);
+            if (surf) accumulate_surf_row(T, po, cf, acc);
+            else accumulate_corner_row(T, po, cf, acc);
           }
         }
+        PROF_ADD(surf ? 40 : 41, t_i0);
+        PROF_T(t_i1);
 #pragma unroll
         for (int k = 0; k < 10; ++k)
           for (int o = 32; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o);
+        PROF_ADD(42, t_i1);
+        PROF_T(t_i2);
         run = it + 1;
         if (acc[9] < 10.0) continue;  // too few correspondences: `continue`
-        if (!lm_solve_reg(cur, deg, status, acc, it, surf)) { keep = false; break; }
+        const bool go = lm_solve_reg(cur, deg, status, acc, it, surf);
+        PROF_ADD(43, t_i2);
+#ifdef LG_PROFILE
+        if (lane_id() == 0) atomicAdd(&PROF_SLOT(surf ? 44 : 45), 1ull);
+#endif
+        if (!go) { keep = false; break; }
       }
       if (lane == 0) {
         for (int k = 0; k < 6; ++k) L.cur[k] = cur[k];
