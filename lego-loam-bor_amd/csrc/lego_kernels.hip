@@ -1733,20 +1733,11 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
     const int sp = (st * (6 - j) + en * j) / 6;
     const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
     if (sp >= ep) continue;
-    const int n = ep - sp;  // sorted range [sp, ep); ep itself is visited unsorted
+    const int n = ep - sp;  // sorted range [sp, ep) (k_sortseg); ep itself is visited unsorted
     PROF_T(t_seg0);
-    for (int t = lane; t <= n; t += 64) {
-      const int2 e = smooth[sp + t];
-      L.u.seg.skey[t] = __int_as_float(e.x);
-      L.u.seg.sval[t] = e.y;
-    }
+    for (int t = lane; t <= n; t += 64) L.u.seg.sval[t] = smooth[sp + t].y;
     __syncthreads();
     PROF_ADD(12, t_seg0);
-    PROF_T(t_rs0);
-    sort_segment(L, n);
-    PROF_ADD(13, t_rs0);
-    for (int t = lane; t < n; t += 64) smooth[sp + t] = make_int2(__float_as_int(L.u.seg.skey[t]), L.u.seg.sval[t]);
-
     PROF_ADD(0, t_seg0);
     PROF_T(t_sharp0);
     // sharp: k = ep .. sp (descending curvature), first 2 eligible -> sharp, up to 20 -> less sharp.
@@ -1874,6 +1865,35 @@ __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
     B.r_counts[rb * 4 + 3] = o.nLF;
     B.r_vstatus[rb] = o.status;
   }
+}
+
+// ============================================================================================
+// k_sortseg: extractFeatures' std::sort of every segment (:285-286), one wave per (ring, segment).
+// The six sorted ranges [sp, ep) of a ring are disjoint and the greedy passes only read them, so
+// all segments of a scan sort up front (the stale slot 4 is sorted with ring 0's first segment, as
+// there) and k_extract's ring-waves keep only the sequential greedy passes.
+// ============================================================================================
+__global__ __launch_bounds__(64) void k_sortseg(LgParams P, LgBufs B) {
+  __shared__ SegLds L;
+  const int V = P.V;
+  const int b = blockIdx.x, sl = b / (V * 6), r = (b / 6) % V, j = b % 6;
+  const int s = P.s0 + sl;
+  const int st = B.ring_start[(size_t)s * V + r], en = B.ring_end[(size_t)s * V + r];
+  const int sp = (st * (6 - j) + en * j) / 6;
+  const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
+  if (sp >= ep) return;
+  const int n = ep - sp;
+  int2* smooth = B.smooth + (size_t)s * P.VH + sp;
+  for (int t = lane_id(); t < n; t += 64) {
+    const int2 e = smooth[t];
+    L.u.seg.skey[t] = __int_as_float(e.x);
+    L.u.seg.sval[t] = e.y;
+  }
+  __syncthreads();
+  PROF_T(t_rs0);
+  sort_segment(L, n);
+  PROF_ADD(13, t_rs0);
+  for (int t = lane_id(); t < n; t += 64) smooth[t] = make_int2(__float_as_int(L.u.seg.skey[t]), L.u.seg.sval[t]);
 }
 
 __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
@@ -3393,6 +3413,8 @@ int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st,
 }
 
 int lg_launch_extract(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
+  hipLaunchKernelGGL(k_sortseg, dim3(S * P.V * 6), dim3(64), 0, st, P, B);
+  LG_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_extract, dim3(S * (P.V + 1)), dim3(64), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
