@@ -730,6 +730,15 @@ int lego_feature_association_from(lego_ctx* c, const lego_projection_out* in, le
   const LgBufs& B = b->B;
   const int M = in->n_segmented;
   if (M < 0 || M > P.VH || in->n_outlier < 0 || in->n_outlier > P.VH) return LEGO_EINVAL;
+  // cloud_info as imageProjection builds it (:358-396): column indices < H, and each ring's
+  // [start, end] inside the cloud and at most one point per column wide (k_extract stages a ring's
+  // window of H + 11 positions)
+  for (int i = 0; i < M; ++i)
+    if (in->segmented_cloud_col_ind[i] >= (uint32_t)P.H) return LEGO_EINVAL;
+  for (int r = 0; r < P.V; ++r) {
+    const int st = in->start_ring_index[r], en = in->end_ring_index[r];
+    if (st < 0 || st > M + 4 || en < -6 || en >= M || en - st > P.H - 10) return LEGO_EINVAL;
+  }
   hipSetDevice(b->device);
   // the reference's Channel<ProjectionOut>::receive (fa.cpp:1389-1397): upload the message
   bool ok = true;

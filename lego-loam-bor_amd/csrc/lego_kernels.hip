@@ -1726,33 +1726,141 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
   o.nLF = running;
 }
 
-LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, int st, int en,
-                            SegLds& L, RingOut& o) {
+// Per-position greedy state of one ring's window [st - 5, en + 6), staged in LDS by its ring-wave:
+// the static eligibility of each pass, the suppression extent (supp_extent: depends only on colInd)
+// and picked[], kept in step with the global writes.  Rings never reach into each other's windows
+// (a pick's +-5 stays inside [st - 5, en + 5], which lies strictly between the neighbouring rings'
+// windows); the one exception, the stale slot 4's index, is read from global memory (info_global)
+// and rings whose window it meets stage only after the first pass has run (k_extract).
+#define EXT_STAGE 2064  // window <= H + 1 positions (H <= 2048)
+#define IF_PK 0x100     // picked
+#define IF_SH 0x40      // sharp-eligible: curvature > edge threshold, not ground
+#define IF_FL 0x80      // flat-eligible: curvature < surf threshold, ground
+struct ExtLds {  // k_extract: 9.3 KB per wave
+  union {
+    int sval[SEG_MAX];             // the segment's sorted positions (k_sortseg)
+    uint16_t col[EXT_STAGE + 16];  // colInd of the window +-5 while the info words are built
+  } u;
+  uint16_t info[EXT_STAGE];  // ff | fb << 3 | IF_SH | IF_FL | IF_PK
+  int pk_s[16], pk_ls[128], pk_f[32];  // this ring's picks, in pick order
+};
+
+LG_DEVICE int info_global(const LgParams& P, const ScanView& v, int ind) {
+  int ff, fb;
+  supp_extent(v, ind, ff, fb);
+  const float c = v.curv[ind];
+  const bool g = v.ground_at(ind);
+  return ff | (fb << 3) | (c > P.edge_thr && !g ? IF_SH : 0) | (c < P.surf_thr && g ? IF_FL : 0) |
+         (v.picked[ind] != 0 ? IF_PK : 0);
+}
+
+LG_DEVICE void stage_ring(const LgParams& P, const ScanView& v, int lo, int nwin, ExtLds& L) {
   const int lane = lane_id();
+  const int c0 = lo - 5;
+  for (int t0 = lane; t0 < nwin + 10; t0 += 64 * 8) {  // col_at with the supp_extent bounds, 8 loads in flight
+    uint32_t cv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) cv[u] = v.col[min(max(c0 + t0 + 64 * u, 0), max(v.M - 1, 0))];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + 64 * u, k = c0 + t;
+      if (t < nwin + 10) L.u.col[t] = (uint16_t)((k >= 0 && k < v.M) ? cv[u] : 0u);
+    }
+  }
+  __syncthreads();
+  for (int t0 = lane; t0 < nwin; t0 += 64 * 8) {
+    float cv[8];
+    uint8_t pk[8], gf[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = min(lo + t0 + 64 * u, lo + nwin - 1);
+      cv[u] = v.curv[k];
+      pk[u] = v.picked[k];
+      gf[u] = k < v.M ? v.gflag[k] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + 64 * u;
+      if (t >= nwin) break;
+      const int ind = lo + t;
+      const int x = t + 5;  // ind's slot in u.col
+      int ff = 0;
+#pragma unroll
+      for (int l = 1; l <= 5; ++l) {
+        if (ff != l - 1) break;
+        if ((unsigned)(ind + l) >= (unsigned)v.VH) break;
+        if (abs((int)L.u.col[x + l] - (int)L.u.col[x + l - 1]) > 10) break;
+        ff = l;
+      }
+      int fb = 0;
+#pragma unroll
+      for (int l = 1; l <= 5; ++l) {
+        if (fb != l - 1) break;
+        if (ind - l < 0) break;
+        if (abs((int)L.u.col[x - l] - (int)L.u.col[x - l + 1]) > 10) break;
+        fb = l;
+      }
+      const bool g = gf[u] != 0;
+      L.info[t] = (uint16_t)(ff | (fb << 3) | (cv[u] > P.edge_thr && !g ? IF_SH : 0) |
+                             (cv[u] < P.surf_thr && g ? IF_FL : 0) | (pk[u] != 0 ? IF_PK : 0));
+    }
+  }
+  __syncthreads();
+}
+
+LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, int st, int en,
+                            ExtLds& L, RingOut& o) {
+  const int lane = lane_id();
+  if (en <= st) return;  // no segment with sp < ep
+  const int lo = max(st - 5, 0), nwin = min(en + 6, v.VH) - lo;
+  PROF_T(t_st0);
+  stage_ring(P, v, lo, nwin, L);
+  PROF_ADD(12, t_st0);
+  // info word of a candidate position (global for the stale index outside the window)
+  auto info_of = [&](int ind) -> int {
+    const int rel = ind - lo;
+    return (unsigned)rel < (unsigned)nwin ? (int)L.info[rel] : info_global(P, v, ind);
+  };
+  // a pick's suppression: picked[] in global memory (persistent state) and in the window
+  auto suppress = [&](int aind, int aff, int afb) {
+    if (lane <= aff + afb) {
+      const int k = aind - afb + lane;
+      v.picked[k] = 1;
+      if ((unsigned)(k - lo) < (unsigned)nwin) L.info[k - lo] |= IF_PK;
+    }
+  };
+  int nS = 0, nLS = 0, nF = 0;
   for (int j = 0; j < 6; j++) {
     const int sp = (st * (6 - j) + en * j) / 6;
     const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
     if (sp >= ep) continue;
     const int n = ep - sp;  // sorted range [sp, ep) (k_sortseg); ep itself is visited unsorted
     PROF_T(t_seg0);
-    for (int t = lane; t <= n; t += 64) L.u.seg.sval[t] = smooth[sp + t].y;
+    __syncthreads();  // the previous segment's reads of u.sval are done
+    for (int t0 = lane; t0 <= n; t0 += 64 * 8) {
+      int sv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sv[u] = smooth[sp + min(t0 + 64 * u, n)].y;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (t0 + 64 * u <= n) L.u.sval[t0 + 64 * u] = sv[u];
+    }
     __syncthreads();
-    PROF_ADD(12, t_seg0);
     PROF_ADD(0, t_seg0);
     PROF_T(t_sharp0);
     // sharp: k = ep .. sp (descending curvature), first 2 eligible -> sharp, up to 20 -> less sharp.
-    // picked[] is read once per chunk; a pick then kills the chunk's lanes inside its suppression
-    // extent in registers (the same writes still go to picked[] for later chunks and passes).
+    // A chunk of 64 candidates reads its info words once; a pick then kills the chunk's lanes inside
+    // its suppression extent in registers (the same writes go to the window for later chunks).
     int largest = 0;
     bool stop = false;
     for (int base = n; base >= 0 && !stop; base -= 64) {
       const int t = base - lane;
       const bool valid = t >= 0;
-      const int ind = valid ? L.u.seg.sval[t] : 0;
-      bool cand = valid && v.picked[ind] == 0 && v.curv[ind] > P.edge_thr && !v.ground_at(ind);
+      const int ind = valid ? L.u.sval[t] : 0;
+      const int w = valid ? info_of(ind) : 0;
+      bool cand = valid && !(w & IF_PK) && (w & IF_SH);
       if (__ballot(cand) == 0ull) continue;
-      int ff = 0, fb = 0;
-      if (cand) supp_extent(v, ind, ff, fb);
+      const int ff = w & 7, fb = (w >> 3) & 7;
       while (true) {
         const unsigned long long m = __ballot(cand);
         if (m == 0ull) break;
@@ -1761,20 +1869,17 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
         largest++;
         if (largest > 20) { stop = true; break; }
         if (lane == 0) {
-          const float4 pt = seg_point(v, aind, o.status);
           if (largest <= 2) {
             v.flabel[aind] = 2;
-            o.sharp[o.nS] = pt;
-            o.sharp_ind[o.nS] = aind;
+            L.pk_s[nS] = aind;
           } else {
             v.flabel[aind] = 1;
           }
-          o.lsharp[o.nLS] = pt;
-          o.lsharp_ind[o.nLS] = aind;
+          L.pk_ls[nLS] = aind;
         }
-        if (lane <= aff + afb) v.picked[aind - afb + lane] = 1;
-        if (largest <= 2) o.nS++;
-        o.nLS++;
+        suppress(aind, aff, afb);
+        if (largest <= 2) nS++;
+        nLS++;
         cand = cand && lane > f && !(ind >= aind - afb && ind <= aind + aff);
       }
       __syncthreads();  // picked[] writes land before the next chunk reads them
@@ -1787,11 +1892,11 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
     for (int base = 0; base <= n && !stop; base += 64) {
       const int t = base + lane;
       const bool valid = t <= n;
-      const int ind = valid ? L.u.seg.sval[t] : 0;
-      bool cand = valid && v.picked[ind] == 0 && v.curv[ind] < P.surf_thr && v.ground_at(ind);
+      const int ind = valid ? L.u.sval[t] : 0;
+      const int w = valid ? info_of(ind) : 0;
+      bool cand = valid && !(w & IF_PK) && (w & IF_FL);
       if (__ballot(cand) == 0ull) continue;
-      int ff = 0, fb = 0;
-      if (cand) supp_extent(v, ind, ff, fb);
+      const int ff = w & 7, fb = (w >> 3) & 7;
       while (true) {
         const unsigned long long m = __ballot(cand);
         if (m == 0ull) break;
@@ -1800,12 +1905,11 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
         smallest++;
         if (lane == 0) {
           v.flabel[aind] = -1;
-          o.flat[o.nF] = seg_point(v, aind, o.status);
-          o.flat_ind[o.nF] = aind;
+          L.pk_f[nF] = aind;
         }
-        o.nF++;
+        nF++;
         if (smallest >= 4) { stop = true; break; }  // the 4th breaks before its suppression
-        if (lane <= aff + afb) v.picked[aind - afb + lane] = 1;
+        suppress(aind, aff, afb);
         cand = cand && lane > f && !(ind >= aind - afb && ind <= aind + aff);
       }
       __syncthreads();
@@ -1813,6 +1917,26 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
     __syncthreads();
     PROF_ADD(2, t_flat0);
   }
+  // the picked points, all loads in flight together
+  int st_bits = 0;
+  for (int t = lane; t < nLS; t += 64) {
+    const int ind = L.pk_ls[t];
+    o.lsharp[t] = seg_point(v, ind, st_bits);
+    o.lsharp_ind[t] = ind;
+  }
+  for (int t = lane; t < nS; t += 64) {
+    const int ind = L.pk_s[t];
+    o.sharp[t] = seg_point(v, ind, st_bits);
+    o.sharp_ind[t] = ind;
+  }
+  for (int t = lane; t < nF; t += 64) {
+    const int ind = L.pk_f[t];
+    o.flat[t] = seg_point(v, ind, st_bits);
+    o.flat_ind[t] = ind;
+  }
+  o.status |= wave_or(st_bits);
+  o.nS = nS; o.nLS = nLS; o.nF = nF;
+  __syncthreads();
 }
 
 // lessFlat list of one ring: positions k in [sp, ep] of each segment whose label <= 0 (position
@@ -1897,7 +2021,7 @@ __global__ __launch_bounds__(64) void k_sortseg(LgParams P, LgBufs B) {
 }
 
 __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
-  __shared__ SegLds L;
+  __shared__ ExtLds L;
   const int V = P.V, VH = P.VH;
   // Blocks [0, n): the first pass of scan s0 + b.  Rings whose range starts at position 4 (the
   // leading rings) read the stale slot 4 of the persistent smoothness array, whose index may point
