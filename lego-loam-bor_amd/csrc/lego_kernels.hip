@@ -2471,6 +2471,7 @@ struct LmLds {
   } u;
   float gmin[3], gcs;
   int gdim[3];
+  int grid_ring_ok;  // every grid record carries its ring ((int)w in [-1, 70])
   float4 sel[LM_MAXQ];
   float4 featl[LM_MAXQ];  // the loop's feature points (pointOri), staged once
   float4 plane[LM_MAXQ];  // surf: each correspondence's plane, once per search
@@ -2638,6 +2639,7 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
     }
     for (int d = 0; d < 3; ++d) { L.gmin[d] = lo[d]; L.gdim[d] = dim[d]; }
     L.gcs = cs;
+    L.grid_ring_ok = 1;
   }
   __syncthreads();
   const int ncell = L.gdim[0] * L.gdim[1] * L.gdim[2];
@@ -2671,50 +2673,80 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
     const int cy = min(max(grid_coord(p.y, L.gmin[1], L.gcs, L.gdim[1]), 0), L.gdim[1] - 1);
     const int cz = min(max(grid_coord(p.z, L.gmin[2], L.gcs, L.gdim[2]), 0), L.gdim[2] - 1);
     const int slot = atomicAdd(&L.u.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
-    gp[slot] = make_float4(p.x, p.y, p.z, __int_as_float(j));
+    const int rp = (p.w > -2.f && p.w < (float)(LM_RMAX - 1)) ? (int)p.w + 1 : 0;  // (int)w in [-1, 70]
+    if (!(p.w > -2.f && p.w < (float)(LM_RMAX - 1))) L.grid_ring_ok = 0;
+    gp[slot] = make_float4(p.x, p.y, p.z, __int_as_float(j | (rp << 24)));
   });
   __syncthreads();
 }
 
-// one thread: nearest neighbour of q; returns index (or -1 if none closer than the radius) and ties
-// tpq adjacent lanes (1, 2, 4 or 8; a power of two, so a group never straddles a wave) share one
-// query: lane `sub` of the group visits every tpq-th candidate of each run, and the group merges
-// (d, lowest idx among equal d, points at that d) with xor shuffles.  Inactive lanes (act = false)
-// only join the shuffles.
-LG_DEVICE int grid_nn(const LmLds& L, const float4* __restrict__ gp, float4 q, float r2, bool& tie, int sub,
-                      int tpq, bool act) {
+// Squared distance from q to grid cell (cx, cy, cz), the box shrunk by 1 mm against the rounding of
+// the points' cell coordinates: no point of the cell is closer.
+LG_DEVICE float cell_boxd2(const LmLds& L, float4 q, int cx, int cy, int cz) {
+  const float cs = L.gcs;
+  const float qv[3] = {q.x, q.y, q.z};
+  const int cv[3] = {cx, cy, cz};
+  float d2 = 0.f;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float lo = L.gmin[a] + (float)cv[a] * cs, hi = lo + cs;
+    float e = fmaxf(fmaxf(lo - qv[a], qv[a] - hi), 0.f);
+    e = fmaxf(e - 1e-3f, 0.f);
+    d2 += e * e;
+  }
+  return d2;
+}
+
+// Visit the grid cells of q's 3x3x3 neighbourhood, q's own cell first; a cell whose box lies
+// farther than `bound()` (the group's current bound) is skipped, since none of its points can
+// improve or tie the best.  tpq adjacent lanes share a query: lane `sub` takes every tpq-th point of
+// a cell.  f(point) per candidate.
+template <typename B, typename F>
+LG_DEVICE void grid_visit_pruned(const LmLds& L, const float4* __restrict__ gp, float4 q, int sub, int tpq, bool act,
+                                 B bound, F f) {
   const int qx = grid_coord(q.x, L.gmin[0], L.gcs, L.gdim[0]);
   const int qy = grid_coord(q.y, L.gmin[1], L.gcs, L.gdim[1]);
   const int qz = grid_coord(q.z, L.gmin[2], L.gcs, L.gdim[2]);
+  for (int t = 0; t < 27; ++t) {
+    const int o = t == 0 ? 13 : (t <= 13 ? t - 1 : t);  // 13 = (0, 0, 0) first
+    const int cx = qx + o % 3 - 1, cy = qy + (o / 3) % 3 - 1, cz = qz + o / 9 - 1;
+    const bool in = act && cx >= 0 && cx < L.gdim[0] && cy >= 0 && cy < L.gdim[1] && cz >= 0 && cz < L.gdim[2];
+    const float bd = bound();  // group-uniform (every lane of the group joins the shuffles)
+    if (!in || (t > 0 && cell_boxd2(L, q, cx, cy, cz) > bd)) continue;
+    const int c = (cz * L.gdim[1] + cy) * L.gdim[0] + cx;
+    const int b = c == 0 ? 0 : L.u.gcell[c - 1], e = L.u.gcell[c];
+    int k = b + sub;
+    for (; k + 3 * tpq < e; k += 4 * tpq) {
+      float4 p4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p4[u] = gp[k + u * tpq];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) f(p4[u]);
+    }
+    for (; k < e; k += tpq) f(gp[k]);
+  }
+}
+
+LG_DEVICE float group_min(float v, int tpq) {
+  for (int o = tpq >> 1; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// 1-NN of q (index or -1 when none is closer than the radius) with the tie flag, tpq lanes a query.
+// Inactive lanes (act = false) only join the shuffles.
+LG_DEVICE int grid_nn(const LmLds& L, const float4* __restrict__ gp, float4 q, float r2, bool& tie, int sub,
+                      int tpq, bool act) {
   float bd = FLT_MAX;
   int bi = 0x7fffffff, bc = 0;
-  if (act) {
-    for (int cz = max(qz - 1, 0); cz <= min(qz + 1, L.gdim[2] - 1); ++cz)
-      for (int cy = max(qy - 1, 0); cy <= min(qy + 1, L.gdim[1] - 1); ++cy) {
-        const int row = (cz * L.gdim[1] + cy) * L.gdim[0];
-        const int x0 = max(qx - 1, 0), x1 = min(qx + 1, L.gdim[0] - 1);
-        if (x0 > x1) continue;
-        const int b = (row + x0 == 0) ? 0 : L.u.gcell[row + x0 - 1];
-        const int e = L.u.gcell[row + x1];  // cells x0..x1 of a row are contiguous
-        // the (d, idx) minimum and tie count do not depend on the visiting order: 8 loads in flight
-        auto visit = [&](const float4 p) {
-          const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
-          const float d = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
-          const int idx = __float_as_int(p.w);
-          if (d < bd) { bd = d; bi = idx; bc = 1; }
-          else if (d == bd) { bc++; bi = min(bi, idx); }
-        };
-        int k = b + sub;
-        for (; k + 7 * tpq < e; k += 8 * tpq) {
-          float4 p8[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) p8[u] = gp[k + u * tpq];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) visit(p8[u]);
-        }
-        for (; k < e; k += tpq) visit(gp[k]);
-      }
-  }
+  grid_visit_pruned(L, gp, q, sub, tpq, act,
+                    [&]() { return fminf(group_min(bd, tpq), r2); },
+                    [&](const float4 p) {
+                      const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+                      const float d = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
+                      const int idx = __float_as_int(p.w) & 0xffffff;
+                      if (d < bd) { bd = d; bi = idx; bc = 1; }
+                      else if (d == bd) { bc++; bi = min(bi, idx); }
+                    });
   for (int o = tpq >> 1; o > 0; o >>= 1) {
     const float d2 = __shfl_xor(bd, o);
     const int i2 = __shfl_xor(bi, o), c2 = __shfl_xor(bc, o);
