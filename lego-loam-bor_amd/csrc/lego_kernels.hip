@@ -2189,7 +2189,7 @@ __global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
 // k_lm: updateTransformation + integrateTransformation + publishOdometry + publishCloudsLast
 // ============================================================================================
 #define LM_THREADS 512
-#define GRID_MAX 4096
+#define GRID_MAX 8191  // grid cells (end offsets share LDS with the staged small cloud)
 #define LM_MAXQ 1536  // 24 * 64 rings
 
 LG_DEVICE float4 transform_to_start(const float4 pi, const float* cur) {  // :388-418
@@ -2472,6 +2472,7 @@ struct LmLds {
   float gmin[3], gcs;
   int gdim[3];
   int grid_ring_ok;  // every grid record carries its ring ((int)w in [-1, 70])
+  int grid_r;        // search radius in cells
   float4 sel[LM_MAXQ];
   float4 featl[LM_MAXQ];  // the loop's feature points (pointOri), staged once
   float4 plane[LM_MAXQ];  // surf: each correspondence's plane, once per search
@@ -2639,6 +2640,7 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
     }
     for (int d = 0; d < 3; ++d) { L.gmin[d] = lo[d]; L.gdim[d] = dim[d]; }
     L.gcs = cs;
+    L.grid_r = cs >= 3.f * cs0 ? 1 : cs >= 1.5f * cs0 ? 2 : 3;  // grid_r * cs >= 3 * cs0 = 5.01 m
     L.grid_ring_ok = 1;
   }
   __syncthreads();
@@ -2697,33 +2699,49 @@ LG_DEVICE float cell_boxd2(const LmLds& L, float4 q, int cx, int cy, int cz) {
   return d2;
 }
 
-// Visit the grid cells of q's 3x3x3 neighbourhood, q's own cell first; a cell whose box lies
-// farther than `bound()` (the group's current bound) is skipped, since none of its points can
-// improve or tie the best.  tpq adjacent lanes share a query: lane `sub` takes every tpq-th point of
-// a cell.  f(point) per candidate.
+// Visit the grid cells around q in shells of Chebyshev radius k = 0 .. L.grid_r (cells of size cs
+// with grid_r * cs >= 5.01 m, so every point closer than the 5 m search radius is inside): a cell
+// whose box lies farther than the lane's bound() is skipped, and shell k ends the search once
+// (k - 1) * cs exceeds it, since none of those points can improve or tie the lane's best.  Bounds
+// are per lane: a lane skips only its own share of a cell's points, each of which is farther than
+// that lane's best and so farther than the group's final best.  tpq adjacent lanes share a query:
+// lane `sub` takes every tpq-th point of a cell.  f(point) per candidate.
 template <typename B, typename F>
 LG_DEVICE void grid_visit_pruned(const LmLds& L, const float4* __restrict__ gp, float4 q, int sub, int tpq, bool act,
                                  B bound, F f) {
-  const int qx = grid_coord(q.x, L.gmin[0], L.gcs, L.gdim[0]);
-  const int qy = grid_coord(q.y, L.gmin[1], L.gcs, L.gdim[1]);
-  const int qz = grid_coord(q.z, L.gmin[2], L.gcs, L.gdim[2]);
-  for (int t = 0; t < 27; ++t) {
-    const int o = t == 0 ? 13 : (t <= 13 ? t - 1 : t);  // 13 = (0, 0, 0) first
-    const int cx = qx + o % 3 - 1, cy = qy + (o / 3) % 3 - 1, cz = qz + o / 9 - 1;
-    const bool in = act && cx >= 0 && cx < L.gdim[0] && cy >= 0 && cy < L.gdim[1] && cz >= 0 && cz < L.gdim[2];
-    const float bd = bound();  // group-uniform (every lane of the group joins the shuffles)
-    if (!in || (t > 0 && cell_boxd2(L, q, cx, cy, cz) > bd)) continue;
-    const int c = (cz * L.gdim[1] + cy) * L.gdim[0] + cx;
-    const int b = c == 0 ? 0 : L.u.gcell[c - 1], e = L.u.gcell[c];
-    int k = b + sub;
-    for (; k + 3 * tpq < e; k += 4 * tpq) {
-      float4 p4[4];
+  if (!act) return;
+  const int R = L.grid_r;
+  int qc[3];
+  const float qv[3] = {q.x, q.y, q.z};
 #pragma unroll
-      for (int u = 0; u < 4; ++u) p4[u] = gp[k + u * tpq];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) f(p4[u]);
+  for (int a = 0; a < 3; ++a) {
+    const float t = floorf((qv[a] - L.gmin[a]) / L.gcs);
+    qc[a] = (int)fminf(fmaxf(t, (float)(-R - 1)), (float)(L.gdim[a] + R));
+  }
+  for (int k = 0; k <= R; ++k) {
+    if (k >= 2) {
+      const float e = (float)(k - 1) * L.gcs - 1e-3f;
+      if (e * e > bound()) break;
     }
-    for (; k < e; k += tpq) f(gp[k]);
+    for (int dz = -k; dz <= k; ++dz)
+      for (int dy = -k; dy <= k; ++dy)
+        for (int dx = -k; dx <= k; ++dx) {
+          if (max(abs(dx), max(abs(dy), abs(dz))) != k) continue;
+          const int cx = qc[0] + dx, cy = qc[1] + dy, cz = qc[2] + dz;
+          if (cx < 0 || cx >= L.gdim[0] || cy < 0 || cy >= L.gdim[1] || cz < 0 || cz >= L.gdim[2]) continue;
+          if (k > 0 && cell_boxd2(L, q, cx, cy, cz) > bound()) continue;
+          const int c = (cz * L.gdim[1] + cy) * L.gdim[0] + cx;
+          const int b = c == 0 ? 0 : L.u.gcell[c - 1], e = L.u.gcell[c];
+          int j = b + sub;
+          for (; j + 3 * tpq < e; j += 4 * tpq) {
+            float4 p4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) p4[u] = gp[j + u * tpq];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) f(p4[u]);
+          }
+          for (; j < e; j += tpq) f(gp[j]);
+        }
   }
 }
 
@@ -2739,7 +2757,7 @@ LG_DEVICE int grid_nn(const LmLds& L, const float4* __restrict__ gp, float4 q, f
   float bd = FLT_MAX;
   int bi = 0x7fffffff, bc = 0;
   grid_visit_pruned(L, gp, q, sub, tpq, act,
-                    [&]() { return fminf(group_min(bd, tpq), r2); },
+                    [&]() { return fminf(bd, r2); },
                     [&](const float4 p) {
                       const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
                       const float d = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
@@ -3163,7 +3181,7 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
     for (int j = tid; j < nl; j += LM_THREADS) L.u.lastc[j] = last_g[j];
     __syncthreads();
   }
-  if (!small) build_grid(L, last_g, nl, gp, 1.1f * sqrtf(P.nn_dist_sqr) + 0.05f);
+  if (!small) build_grid(L, last_g, nl, gp, (sqrtf(P.nn_dist_sqr) + 0.01f) / 3.f);
   const float4* last = small ? (const float4*)L.u.lastc : last_g;
   ring_index(L, last, nl);
   PROF_ADD(surf ? 16 : 48, t_bg0);
