@@ -2190,6 +2190,7 @@ __global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
 // ============================================================================================
 #define LM_THREADS 512
 #define GRID_MAX 8191  // grid cells (end offsets share LDS with the staged small cloud)
+#define CGRID_MAX 2047  // grid cells over a staged small cloud
 #define LM_MAXQ 1536  // 24 * 64 rings
 
 LG_DEVICE float4 transform_to_start(const float4 pi, const float* cur) {  // :388-418
@@ -2471,6 +2472,7 @@ struct LmLds {
   } u;
   float gmin[3], gcs;
   int gdim[3];
+  int cgcell[CGRID_MAX + 1];  // grid cell table of a staged small cloud
   int grid_ring_ok;  // every grid record carries its ring ((int)w in [-1, 70])
   int grid_r;        // search radius in cells
   float4 sel[LM_MAXQ];
@@ -2585,32 +2587,14 @@ LG_DEVICE void ring_index(LmLds& L, const float4* last, int nl) {
   __syncthreads();
 }
 
-struct NnBest {  // (d, lowest index) and the number of points at d
-  float d;
-  int i, c;
-  LG_DEVICE void visit(float4 q, float4 p, int idx) {
-    const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
-    const float dd = dx * dx + dy * dy + dz * dz;  // nanoflann L2_Simple_Adaptor order
-    if (dd < d) { d = dd; i = idx; c = 1; }
-    else if (dd == d) { c++; i = min(i, idx); }
-  }
-  LG_DEVICE void merge(int tpq) {  // across the tpq lanes of a query
-    for (int o = tpq >> 1; o > 0; o >>= 1) {
-      const float d2 = __shfl_xor(d, o);
-      const int i2 = __shfl_xor(i, o), c2 = __shfl_xor(c, o);
-      if (d2 < d) { d = d2; i = i2; c = c2; }
-      else if (d2 == d) { i = min(i, i2); c += c2; }
-    }
-  }
-};
-
 LG_DEVICE int grid_coord(float v, float mn, float cs, int dim) {
   float f = floorf((v - mn) / cs);
   f = fminf(fmaxf(f, -2.f), (float)dim + 1.f);
   return (int)f;
 }
 
-LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, float4* gp, float cs0) {
+LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, float4* gp, float cs0, int* gcell,
+                           int maxcells) {
   const int tid = threadIdx.x;
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
   for_last_batched(last, nl, [&](int j, const float4 p) {
@@ -2635,7 +2619,7 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
     while (true) {
       long long tot = 1;
       for (int d = 0; d < 3; ++d) { dim[d] = (int)((hi[d] - lo[d]) / cs) + 1; tot *= dim[d]; }
-      if (tot <= GRID_MAX) break;
+      if (tot <= maxcells) break;
       cs *= 2.f;
     }
     for (int d = 0; d < 3; ++d) { L.gmin[d] = lo[d]; L.gdim[d] = dim[d]; }
@@ -2645,26 +2629,26 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
   }
   __syncthreads();
   const int ncell = L.gdim[0] * L.gdim[1] * L.gdim[2];
-  for (int c = tid; c <= ncell; c += LM_THREADS) L.u.gcell[c] = 0;
+  for (int c = tid; c <= ncell; c += LM_THREADS) gcell[c] = 0;
   __syncthreads();
   for_last_batched(last, nl, [&](int j, const float4 p) {
     if (j >= nl) return;
     const int cx = min(max(grid_coord(p.x, L.gmin[0], L.gcs, L.gdim[0]), 0), L.gdim[0] - 1);
     const int cy = min(max(grid_coord(p.y, L.gmin[1], L.gcs, L.gdim[1]), 0), L.gdim[1] - 1);
     const int cz = min(max(grid_coord(p.z, L.gmin[2], L.gcs, L.gdim[2]), 0), L.gdim[2] - 1);
-    atomicAdd(&L.u.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
+    atomicAdd(&gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
   });
   __syncthreads();
   // exclusive scan of the counts -> cell start offsets (each thread a contiguous chunk)
   const int per = (ncell + LM_THREADS - 1) / LM_THREADS;
   const int c0 = min(tid * per, ncell), c1 = min(c0 + per, ncell);
   int local = 0;
-  for (int c = c0; c < c1; ++c) local += L.u.gcell[c];
+  for (int c = c0; c < c1; ++c) local += gcell[c];
   int tot;
   int run = block_excl_scan_int(L, local, tot);
   for (int c = c0; c < c1; ++c) {
-    const int n = L.u.gcell[c];
-    L.u.gcell[c] = run;
+    const int n = gcell[c];
+    gcell[c] = run;
     run += n;
   }
   __syncthreads();
@@ -2674,7 +2658,7 @@ LG_DEVICE void build_grid(LmLds& L, const float4* __restrict__ last, int nl, flo
     const int cx = min(max(grid_coord(p.x, L.gmin[0], L.gcs, L.gdim[0]), 0), L.gdim[0] - 1);
     const int cy = min(max(grid_coord(p.y, L.gmin[1], L.gcs, L.gdim[1]), 0), L.gdim[1] - 1);
     const int cz = min(max(grid_coord(p.z, L.gmin[2], L.gcs, L.gdim[2]), 0), L.gdim[2] - 1);
-    const int slot = atomicAdd(&L.u.gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
+    const int slot = atomicAdd(&gcell[(cz * L.gdim[1] + cy) * L.gdim[0] + cx], 1);
     const int rp = (p.w > -2.f && p.w < (float)(LM_RMAX - 1)) ? (int)p.w + 1 : 0;  // (int)w in [-1, 70]
     if (!(p.w > -2.f && p.w < (float)(LM_RMAX - 1))) L.grid_ring_ok = 0;
     gp[slot] = make_float4(p.x, p.y, p.z, __int_as_float(j | (rp << 24)));
@@ -2707,7 +2691,8 @@ LG_DEVICE float cell_boxd2(const LmLds& L, float4 q, int cx, int cy, int cz) {
 // that lane's best and so farther than the group's final best.  tpq adjacent lanes share a query:
 // lane `sub` takes every tpq-th point of a cell.  f(point) per candidate.
 template <typename B, typename F>
-LG_DEVICE void grid_visit_pruned(const LmLds& L, const float4* __restrict__ gp, float4 q, int sub, int tpq, bool act,
+LG_DEVICE void grid_visit_pruned(const LmLds& L, const int* gcell, const float4* __restrict__ gp, float4 q, int sub,
+                                 int tpq, bool act,
                                  B bound, F f) {
   if (!act) return;
   const int R = L.grid_r;
@@ -2731,7 +2716,7 @@ LG_DEVICE void grid_visit_pruned(const LmLds& L, const float4* __restrict__ gp, 
           if (cx < 0 || cx >= L.gdim[0] || cy < 0 || cy >= L.gdim[1] || cz < 0 || cz >= L.gdim[2]) continue;
           if (k > 0 && cell_boxd2(L, q, cx, cy, cz) > bound()) continue;
           const int c = (cz * L.gdim[1] + cy) * L.gdim[0] + cx;
-          const int b = c == 0 ? 0 : L.u.gcell[c - 1], e = L.u.gcell[c];
+          const int b = c == 0 ? 0 : gcell[c - 1], e = gcell[c];
           int j = b + sub;
           for (; j + 3 * tpq < e; j += 4 * tpq) {
             float4 p4[4];
@@ -2752,11 +2737,12 @@ LG_DEVICE float group_min(float v, int tpq) {
 
 // 1-NN of q (index or -1 when none is closer than the radius) with the tie flag, tpq lanes a query.
 // Inactive lanes (act = false) only join the shuffles.
-LG_DEVICE int grid_nn(const LmLds& L, const float4* __restrict__ gp, float4 q, float r2, bool& tie, int sub,
+LG_DEVICE int grid_nn(const LmLds& L, const int* gcell, const float4* __restrict__ gp, float4 q, float r2, bool& tie,
+                      int sub,
                       int tpq, bool act) {
   float bd = FLT_MAX;
   int bi = 0x7fffffff, bc = 0;
-  grid_visit_pruned(L, gp, q, sub, tpq, act,
+  grid_visit_pruned(L, gcell, gp, q, sub, tpq, act,
                     [&]() { return fminf(bd, r2); },
                     [&](const float4 p) {
                       const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
@@ -3181,7 +3167,11 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
     for (int j = tid; j < nl; j += LM_THREADS) L.u.lastc[j] = last_g[j];
     __syncthreads();
   }
-  if (!small) build_grid(L, last_g, nl, gp, (sqrtf(P.nn_dist_sqr) + 0.01f) / 3.f);
+  // uniform grid for the 1-NN: the surf cloud's cell table takes the LDS of the staged small cloud;
+  // a small (staged) cloud gets a coarser table of its own
+  int* gcell = small ? L.cgcell : L.u.gcell;
+  build_grid(L, small ? (const float4*)L.u.lastc : last_g, nl, gp, (sqrtf(P.nn_dist_sqr) + 0.01f) / 3.f, gcell,
+             small ? CGRID_MAX : GRID_MAX);
   const float4* last = small ? (const float4*)L.u.lastc : last_g;
   ring_index(L, last, nl);
   PROF_ADD(surf ? 16 : 48, t_bg0);
@@ -3206,16 +3196,7 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
         bool tie = false;
         const float4 qs = act ? L.sel[q] : make_float4(0.f, 0.f, 0.f, 0.f);
         int c;
-        if (small) {
-          NnBest b{FLT_MAX, 0x7fffffff, 0};
-          if (act)
-            for (int j = sub; j < nl; j += tpq) b.visit(qs, last[j], j);
-          b.merge(tpq);
-          tie = (b.d < P.nn_dist_sqr) && b.c > 1;
-          c = (b.d < P.nn_dist_sqr) ? b.i : -1;
-        } else {
-          c = grid_nn(L, gp, qs, P.nn_dist_sqr, tie, sub, tpq, act);
-        }
+        c = grid_nn(L, gcell, gp, qs, P.nn_dist_sqr, tie, sub, tpq, act);
         if (act && sub == 0) {
           L.ind1[q] = c;
           if (tie) st |= LEGO_ST_NN_TIE;
