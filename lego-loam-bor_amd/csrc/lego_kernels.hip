@@ -1656,15 +1656,23 @@ LG_DEVICE void voxel_sort_reg(unsigned* key, uint16_t* val, int n) {
   __syncthreads();
 }
 
+// kMode 2: rings of more than 1024 points (R = 32, 64 VGPRs of keys) only; mode 1 keeps R <= 16.
+template <int kMode>
 LG_DEVICE void voxel_sort_stable(unsigned* key, uint16_t* val, int n) {
-  if (n <= 64) voxel_sort_reg<1>(key, val, n);
-  else if (n <= 128) voxel_sort_reg<2>(key, val, n);
-  else if (n <= 256) voxel_sort_reg<4>(key, val, n);
-  else if (n <= 512) voxel_sort_reg<8>(key, val, n);
-  else if (n <= 1024) voxel_sort_reg<16>(key, val, n);
-  else voxel_sort_reg<32>(key, val, n);
+  if constexpr (kMode == 2) {
+    voxel_sort_reg<32>(key, val, n);
+  } else {
+    if (n <= 64) voxel_sort_reg<1>(key, val, n);
+    else if (n <= 128) voxel_sort_reg<2>(key, val, n);
+    else if (n <= 256) voxel_sort_reg<4>(key, val, n);
+    else if (n <= 512) voxel_sort_reg<8>(key, val, n);
+    else voxel_sort_reg<16>(key, val, n);
+  }
 }
 
+// kMode 0: voxel_tie_order 0 (libstdc++ introsort permutation); 1 / 2: stable order, rings of at most /
+// more than 1024 points.  One kernel per mode, so each carries only its own sort's registers.
+template <int kMode>
 LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, int n, int base_pos, RingOut& o) {
   const float4* fa = v.fa + base_pos;  // L.vval holds positions relative to the ring start
   const int lane = lane_id();
@@ -1702,8 +1710,8 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
   }
   __syncthreads();
   PROF_T(t_vs0);
-  if (P.voxel_stable) voxel_sort_stable(L.u.vkey, L.vval, n);
-  else wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
+  if constexpr (kMode == 0) wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
+  else voxel_sort_stable<kMode>(L.u.vkey, L.vval, n);
   PROF_ADD(5, t_vs0);
   int running = 0;
   for (int base = 0; base < n; base += 64) {
@@ -1966,6 +1974,8 @@ LG_DEVICE int lessflat_list(const ScanView& v, int st, int en, uint16_t* list) {
 // k_voxel: surfPointsLessFlatScan -> VoxelGrid (leaf 0.2) per ring, one wave per ring.  A kernel
 // of its own so the register-resident voxel sort's VGPRs do not cut k_extract's occupancy.
 // ============================================================================================
+// kMode as voxel_ring: 0 for voxel_tie_order 0; 1 and 2 split the stable order's rings by size.
+template <int kMode>
 __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
   __shared__ ExtractLds L;
   const int V = P.V;
@@ -1976,6 +1986,7 @@ __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
   ScanView v;
   v.fa = B.lf_stage + sb * P.H;  // the ring's lessFlat points, in surfPointsLessFlatScan order
   const int n = B.lf_count[sb];
+  if ((P.voxel_stable ? (n > 1024 ? 2 : 1) : 0) != kMode) return;
   for (int t = lane_id(); t < n; t += 64) L.vval[t] = (uint16_t)t;
   __syncthreads();
   RingOut o;
@@ -1983,7 +1994,7 @@ __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
   o.nLF = 0;
   o.status = 0;
   PROF_T(t_vox0);
-  voxel_ring(P, v, L, n, 0, o);
+  voxel_ring<kMode>(P, v, L, n, 0, o);
   PROF_ADD(4, t_vox0);
   if (lane_id() == 0) {
     B.r_counts[rb * 4 + 3] = o.nLF;
@@ -3576,7 +3587,13 @@ int lg_launch_extract(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
 }
 
 int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  hipLaunchKernelGGL(k_voxel, dim3(S * P.V), dim3(64), 0, st, P, B);
+  if (P.voxel_stable) {
+    hipLaunchKernelGGL(k_voxel<1>, dim3(S * P.V), dim3(64), 0, st, P, B);
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_voxel<2>, dim3(S * P.V), dim3(64), 0, st, P, B);
+  } else {
+    hipLaunchKernelGGL(k_voxel<0>, dim3(S * P.V), dim3(64), 0, st, P, B);
+  }
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
