@@ -149,7 +149,9 @@ int  lego_cloud_handler(lego_ctx* ctx, const void* points, int32_t n_points, int
 /* One runFeatureAssociation iteration (featureAssociation.cpp:1389-1448) on the projection the last
  * lego_cloud_handler call produced (device-resident; the reference's Channel<ProjectionOut> hop). */
 int  lego_feature_association(lego_ctx* ctx, lego_association_out* out);
-/* Same, on a ProjectionOut supplied by the caller (host arrays), e.g. from another producer. */
+/* Same, on a ProjectionOut supplied by the caller (host arrays), e.g. from another producer.
+ * LEGO_EINVAL for a cloud_info imageProjection cannot produce (:358-396): a column index >= H, or a
+ * ring whose [start, end] leaves [0, n_segmented) or spans more than H - 10 positions. */
 int  lego_feature_association_from(lego_ctx* ctx, const lego_projection_out* in, lego_association_out* out);
 
 /* ---- batched multi-sequence engine (throughput path) ------------------------------ */

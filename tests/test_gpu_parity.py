@@ -289,6 +289,32 @@ def test_injected_projection_lm_parity(gpu):
         np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
 
 
+def test_injected_projection_rejects_malformed_cloud_info(gpu):
+    """A ProjectionOut that imageProjection cannot produce (column index >= H, a ring wider than H
+    columns) is refused with LEGO_EINVAL before anything reaches the device, and the context stays
+    usable."""
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    fe = L.Frontend(params)
+    orc = oracle_for(params)
+    pr = orc.cloud_handler(A.synth_scan(cfg, 3, 0))
+    bad_col = dict(pr)
+    bad_col["segmented_cloud_col_ind"] = np.array(pr["segmented_cloud_col_ind"], copy=True)
+    bad_col["segmented_cloud_col_ind"][len(bad_col["segmented_cloud_col_ind"]) // 2] = params.num_horizontal_scans
+    with pytest.raises(L.LegoError, match="rc=-1"):
+        fe.feature_association(bad_col)
+    bad_ring = dict(pr)
+    bad_ring["start_ring_index"] = np.array(pr["start_ring_index"], copy=True)
+    bad_ring["end_ring_index"] = np.array(pr["end_ring_index"], copy=True)
+    bad_ring["start_ring_index"][1] = 4
+    bad_ring["end_ring_index"][1] = 4 + params.num_horizontal_scans
+    with pytest.raises(L.LegoError, match="rc=-1"):
+        fe.feature_association(bad_ring)
+    fr = orc.feature_association()
+    fg = fe.feature_association(pr)
+    assert not Hs.diff_report(Hs.FEAT_KEYS, fg, fr)
+
+
 @pytest.mark.parametrize("groups", [1, 3])
 def test_batch_streams_match_oracle(gpu, groups):
     """The batched engine (S sequences, one launch per stage, optionally as `groups` slices on their
