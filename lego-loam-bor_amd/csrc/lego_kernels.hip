@@ -1656,10 +1656,14 @@ LG_DEVICE void voxel_sort_reg(unsigned* key, uint16_t* val, int n) {
   __syncthreads();
 }
 
-// kMode 2: rings of more than 1024 points (R = 32, 64 VGPRs of keys) only; mode 1 keeps R <= 16.
+// kMode 2: rings of more than 1024 points (R = 32, 64 VGPRs of keys) only; mode 1 keeps R <= 16;
+// mode 3 takes any ring.
 template <int kMode>
 LG_DEVICE void voxel_sort_stable(unsigned* key, uint16_t* val, int n) {
-  if constexpr (kMode == 2) {
+  if constexpr (kMode == 3) {
+    if (n > 1024) voxel_sort_reg<32>(key, val, n);
+    else voxel_sort_stable<1>(key, val, n);
+  } else if constexpr (kMode == 2) {
     voxel_sort_reg<32>(key, val, n);
   } else {
     if (n <= 64) voxel_sort_reg<1>(key, val, n);
@@ -1671,7 +1675,7 @@ LG_DEVICE void voxel_sort_stable(unsigned* key, uint16_t* val, int n) {
 }
 
 // kMode 0: voxel_tie_order 0 (libstdc++ introsort permutation); 1 / 2: stable order, rings of at most /
-// more than 1024 points.  One kernel per mode, so each carries only its own sort's registers.
+// more than 1024 points; 3: either order, any ring (one kernel for the whole step).
 template <int kMode>
 LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, int n, int base_pos, RingOut& o) {
   const float4* fa = v.fa + base_pos;  // L.vval holds positions relative to the ring start
@@ -1710,8 +1714,14 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
   }
   __syncthreads();
   PROF_T(t_vs0);
-  if constexpr (kMode == 0) wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
-  else voxel_sort_stable<kMode>(L.u.vkey, L.vval, n);
+  if constexpr (kMode == 0) {
+    wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
+  } else if constexpr (kMode == 3) {
+    if (P.voxel_stable) voxel_sort_stable<3>(L.u.vkey, L.vval, n);
+    else wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
+  } else {
+    voxel_sort_stable<kMode>(L.u.vkey, L.vval, n);
+  }
   PROF_ADD(5, t_vs0);
   int running = 0;
   for (int base = 0; base < n; base += 64) {
@@ -1986,7 +1996,7 @@ __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
   ScanView v;
   v.fa = B.lf_stage + sb * P.H;  // the ring's lessFlat points, in surfPointsLessFlatScan order
   const int n = B.lf_count[sb];
-  if ((P.voxel_stable ? (n > 1024 ? 2 : 1) : 0) != kMode) return;
+  if (kMode != 3 && (P.voxel_stable ? (n > 1024 ? 2 : 1) : 0) != kMode) return;
   for (int t = lane_id(); t < n; t += 64) L.vval[t] = (uint16_t)t;
   __syncthreads();
   RingOut o;
@@ -3587,7 +3597,13 @@ int lg_launch_extract(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
 }
 
 int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  if (P.voxel_stable) {
+  // At most one scan per CU (S <= ncu), one kernel for all rings: its register budget keeps its waves
+  // off the SIMDs k_lm holds, which measured faster there.  With more scans than CUs the split
+  // kernels (the common one at 83 VGPRs shares SIMDs with k_lm) measured faster: 245k vs 226k
+  // scans/s at S = 512.
+  if (S <= P.ncu) {
+    hipLaunchKernelGGL(k_voxel<3>, dim3(S * P.V), dim3(64), 0, st, P, B);
+  } else if (P.voxel_stable) {
     hipLaunchKernelGGL(k_voxel<1>, dim3(S * P.V), dim3(64), 0, st, P, B);
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_voxel<2>, dim3(S * P.V), dim3(64), 0, st, P, B);

@@ -429,13 +429,15 @@ def test_stale_slot_points_into_later_ring(gpu):
     assert foreign >= 2, foreign  # the case under test actually happened
 
 
-def test_full_size_batch_properties(gpu):
-    """Bench-size batch (256 sequences): size-independent properties on every stream and exact
-    parity on a sample of streams."""
+@pytest.mark.parametrize("S,order", [(256, 0), (320, 1)])
+def test_full_size_batch_properties(gpu, S, order):
+    """Bench-size batch (256 sequences; 320 takes the per-mode VoxelGrid kernels that run when there
+    are more scans than CUs): size-independent properties on every stream and exact parity on a
+    sample of streams."""
     import torch
-    params = L.params_vlp16()
+    params = L.params_vlp16(voxel_tie_order=order)
     cfg = A.synth_cfg("vlp16")
-    S, steps = 256, 3
+    steps = 3
     cap = params.num_vertical_scans * params.num_horizontal_scans
     seqs = np.repeat(np.arange(S)[None, :] + 1000, steps, 0).reshape(-1)
     scans = np.repeat(np.arange(steps)[:, None], S, 1).reshape(-1)
@@ -459,7 +461,7 @@ def test_full_size_batch_properties(gpu):
         M = len(pg["segmented_cloud"])
         assert pg["start_ring_index"][0] == 4 and pg["end_ring_index"][-1] == M - 6
         assert np.all(fg["sharp_ind"] < M) and np.all(fg["flat_ind"] < M)
-    for s in (0, 77, 255):  # exact parity on a sample
+    for s in (0, 77, S - 1):  # exact parity on a sample
         orc = oracle_for(params)
         for k in range(steps):
             pr = orc.cloud_handler(pts[k * S + s, :cnt[k * S + s]])
