@@ -222,8 +222,9 @@ def main():
                                "k_fa_prep": {"bytes": int(b_smooth), "ms": round(stage[2], 4),
                                              "GBps": round(b_smooth / (stage[2] * 1e-3) / 1e9, 1)}},
                 "traffic_source": traffic_src,
-                "note": "%d scans per launch: working set below the 256 MiB Infinity Cache (cache-assisted)" % S
-                        if S < 2048 else "working set above the Infinity Cache"}
+                "note": ("%d scans per launch: working set below the 256 MiB Infinity Cache (cache-assisted)" % S
+                         if b_proj + b_smooth < 256 * 2**20 else
+                         "%d scans per launch: working set above the 256 MiB Infinity Cache" % S)}
 
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K, "warmup": W,

@@ -2500,7 +2500,6 @@ struct LmLds {
   float4 featl[LM_MAXQ];  // the loop's feature points (pointOri), staged once
   float4 plane[LM_MAXQ];  // surf: each correspondence's plane, once per search
   int ind1[LM_MAXQ], ind2[LM_MAXQ], ind3[LM_MAXQ];
-  double red[LM_THREADS / 64][10];
   int first_ge[LM_RMAX + 4];  // first index with ring >= r (index r + 1), nl if none
   int last_le[LM_RMAX + 4];   // last index with ring <= r (index r + 1), -1 if none
   int nfall;                  // queries whose ring breaks need the sequential scan
@@ -2861,25 +2860,6 @@ LG_DEVICE void ring_scans(const LgParams& P, const float4* __restrict__ last, in
   }
 }
 
-// block reduce of 9 doubles + count; result valid on thread 0
-LG_DEVICE void block_reduce10(LmLds& L, double* v) {
-  for (int k = 0; k < 10; ++k) {
-    double x = v[k];
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o);
-    v[k] = x;
-  }
-  if (lane_id() == 0)
-    for (int k = 0; k < 10; ++k) L.red[wave_id()][k] = v[k];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < 10; ++k) {
-      double t = 0.0;
-      for (int w = 0; w < LM_THREADS / 64; ++w) t += L.red[w][k];
-      v[k] = t;
-    }
-  }
-}
-
 // AtA/AtB -> solve -> degeneracy -> update of cur (registers; every lane of the wave computes the
 // same); returns keep-iterating
 LG_DEVICE bool lm_solve_reg(float* cur, int& is_degenerate, int& status, const double* red, int iter, bool surf) {
@@ -2907,46 +2887,6 @@ LG_DEVICE bool lm_solve_reg(float* cur, int& is_degenerate, int& status, const d
   }
   for (int i = 0; i < 6; i++)
     if (isnan(cur[i])) cur[i] = 0;
-  if (surf) {
-    double a = (double)(RAD2DEG * x[0]), b = (double)(RAD2DEG * x[1]);
-    deltaR = (float)sqrt(a * a + b * b);
-    double c = (double)(x[2] * 100);
-    deltaT = (float)sqrt(c * c);
-  } else {
-    double a = (double)(RAD2DEG * x[0]);
-    deltaR = (float)sqrt(a * a);
-    double b = (double)(x[1] * 100), c = (double)(x[2] * 100);
-    deltaT = (float)sqrt(b * b + c * c);
-  }
-  return !((double)deltaR < 0.1 && (double)deltaT < 0.1);
-}
-
-// thread 0: AtA/AtB -> solve -> degeneracy -> update; returns keep-iterating
-LG_DEVICE bool lm_solve(LmLds& L, LgState& S, const double* red, int iter, bool surf) {
-  float AtA[9], AtB[3], x[3];
-  AtA[0] = (float)red[0]; AtA[1] = (float)red[1]; AtA[2] = (float)red[2];
-  AtA[3] = AtA[1]; AtA[4] = (float)red[3]; AtA[5] = (float)red[4];
-  AtA[6] = AtA[2]; AtA[7] = AtA[5]; AtA[8] = (float)red[5];
-  AtB[0] = (float)red[6]; AtB[1] = (float)red[7]; AtB[2] = (float)red[8];
-  qr_solve3(AtA, AtB, x);
-  if (iter == 0) {
-    S.is_degenerate = eig_max_sym3(AtA) < 10.0;
-  } else if (S.is_degenerate) {
-    L.status |= LEGO_ST_DEGEN_UB;
-  }
-  if (S.is_degenerate) {
-    L.status |= LEGO_ST_DEGENERATE;
-    x[0] = x[1] = x[2] = 0.f;
-  }
-  const float RAD2DEG = (float)(180.0 / M_PI);
-  float deltaR, deltaT;
-  if (surf) {
-    L.cur[0] += x[0]; L.cur[2] += x[1]; L.cur[4] += x[2];
-  } else {
-    L.cur[1] += x[0]; L.cur[3] += x[1]; L.cur[5] += x[2];
-  }
-  for (int i = 0; i < 6; i++)
-    if (isnan(L.cur[i])) L.cur[i] = 0;
   if (surf) {
     double a = (double)(RAD2DEG * x[0]), b = (double)(RAD2DEG * x[1]);
     deltaR = (float)sqrt(a * a + b * b);
