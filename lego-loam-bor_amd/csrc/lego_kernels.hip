@@ -760,11 +760,44 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   }
   __syncthreads();
   if (tid == 0) ring_end[V - 1] = nseg - 1 - 5;
-  // 2-D scan compaction (column order)
+  // 2-D scan compaction (column order): each wave's columns read their candidate once and gather the
+  // scan points with all loads in flight, then one barrier gives the waves' offsets
   const int32_t* cand = B.scan_cand + (size_t)s * H;
   float4* scan = B.scan_msg + (size_t)s * H;
-  const int nscan = wave_raster_compact(H, scratch, [&](int j, bool& p, bool&) { p = cand[j] >= 0; },
-                                        [&](int j, bool p, bool, int k, int) { if (p) scan[k] = cloud[cand[j]]; }).x;
+  int nscan = 0;
+  {
+    constexpr int kJ = 4;  // 64 * kJ * 16 waves >= H
+    const int Lc = ((H + nw - 1) / nw + 63) & ~63;
+    const int jlo = min(w * Lc, H), jhi = min(jlo + Lc, H);
+    int cj[kJ];
+#pragma unroll
+    for (int u = 0; u < kJ; ++u) {
+      const int j = jlo + 64 * u + lane;
+      cj[u] = (j < jhi) ? cand[j] : -1;
+    }
+    float4 pc[kJ];
+    int cnt_w = 0;
+#pragma unroll
+    for (int u = 0; u < kJ; ++u) {
+      pc[u] = buffer_load_f4(rs_cloud, cj[u] >= 0 ? (uint32_t)cj[u] * 16u : 0xffffffffu);
+      cnt_w += __popcll(__ballot(cj[u] >= 0));
+    }
+    if (lane == 0) scratch[w] = cnt_w;
+    __syncthreads();
+    int off = 0;
+    for (int k = 0; k < nw; ++k) {
+      const int a = scratch[k];
+      if (k < w) off += a;
+      nscan += a;
+    }
+#pragma unroll
+    for (int u = 0; u < kJ; ++u) {
+      const unsigned long long m = __ballot(cj[u] >= 0);
+      if (cj[u] >= 0) scan[off + popc_below(m)] = pc[u];
+      off += __popcll(m);
+    }
+    __syncthreads();  // scratch reusable
+  }
   PROF_ADD(29, t_s4);
   PROF_T(t_s5);
   distort_segmented(P, B, s, nseg, scratch);
