@@ -88,6 +88,7 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   uint8_t* picked;       // [S][VH]
   int8_t* flabel;        // [S][VH]
   int2* smooth;          // [S][VH]  {float bits of value, ind}
+  uint16_t* xinfo;       // [S][VH]  k_extract's per-position greedy state, built by k_sortseg
   int32_t* fp_sync;      // [S][2]   stale ind of smoothness slot 4, first-pass done epoch
   float4* seg_fa;        // [S][VH]  segmentedCloud after adjustDistortion
   float4* outlier_fa;    // [S][VH]  adjustOutlierCloud

@@ -251,7 +251,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   A(scan_cand, S * H); A(orient, S * 4);
   A(seg_pts, S * VH); A(seg_range, S * VH); A(seg_col, S * VH); A(seg_ground, S * VH);
   A(ring_start, S * V); A(ring_end, S * V); A(outlier, S * VH); A(scan_msg, S * H); A(counts, S * CNT_N);
-  A(curv, S * VH); A(picked, S * VH); A(flabel, S * VH); A(smooth, S * VH); A(fp_sync, S * 2); A(seg_fa, S * VH); A(outlier_fa, S * VH);
+  A(curv, S * VH); A(picked, S * VH); A(flabel, S * VH); A(smooth, S * VH); A(xinfo, S * VH); A(fp_sync, S * 2); A(seg_fa, S * VH); A(outlier_fa, S * VH);
   A(r_sharp, S * V * P.cap_sharp); A(r_sharp_ind, S * V * P.cap_sharp);
   A(r_lsharp, S * V * P.cap_lsharp); A(r_lsharp_ind, S * V * P.cap_lsharp);
   A(r_flat, S * V * P.cap_flat); A(r_flat_ind, S * V * P.cap_flat);

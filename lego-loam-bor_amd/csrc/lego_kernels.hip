@@ -1069,9 +1069,10 @@ struct ExtractLds {  // k_voxel (and the sort test hooks): 13.5 KB per wave
   int tab[128];                 // lane-pairing / stop-queue scratch of the partitions
 };
 
-struct SegLds {  // k_extract: 5.6 KB per wave
+struct SegLds {  // k_sortseg: 5.6 KB per wave
   union {
     struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;  // segment sort
+    uint16_t col[SEG_MAX + 16];                             // colInd around the segment (info words)
   } u;
   unsigned blk[RING_MAX / 32];
   int stk[3 * 64];
@@ -1787,10 +1788,9 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
 #define IF_PK 0x100     // picked
 #define IF_SH 0x40      // sharp-eligible: curvature > edge threshold, not ground
 #define IF_FL 0x80      // flat-eligible: curvature < surf threshold, ground
-struct ExtLds {  // k_extract: 9.3 KB per wave
+struct ExtLds {  // k_extract: 6.9 KB per wave
   union {
-    int sval[SEG_MAX];             // the segment's sorted positions (k_sortseg)
-    uint16_t col[EXT_STAGE + 16];  // colInd of the window +-5 while the info words are built
+    int sval[SEG_MAX];  // the segment's sorted positions (k_sortseg)
   } u;
   uint16_t info[EXT_STAGE];  // ff | fb << 3 | IF_SH | IF_FL | IF_PK
   int pk_s[16], pk_ls[128], pk_f[32];  // this ring's picks, in pick order
@@ -1805,42 +1805,44 @@ LG_DEVICE int info_global(const LgParams& P, const ScanView& v, int ind) {
          (v.picked[ind] != 0 ? IF_PK : 0);
 }
 
-LG_DEVICE void stage_ring(const LgParams& P, const ScanView& v, int lo, int nwin, ExtLds& L) {
+// Info words of positions [k0, k0 + cnt) (one segment [sp, ep]) into xinfo; colbuf: LDS of at least
+// cnt + 10 entries for the colInd window (col_at with supp_extent's bounds).
+LG_DEVICE void build_info(const LgParams& P, const ScanView& v, int k0, int cnt, uint16_t* xinfo, uint16_t* colbuf) {
   const int lane = lane_id();
-  const int c0 = lo - 5;
-  for (int t0 = lane; t0 < nwin + 10; t0 += 64 * 8) {  // col_at with the supp_extent bounds, 8 loads in flight
-    uint32_t cv[8];
+  const int c0 = k0 - 5;
+  for (int t0 = lane; t0 < cnt + 10; t0 += 64 * 4) {
+    uint32_t cv[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) cv[u] = v.col[min(max(c0 + t0 + 64 * u, 0), max(v.M - 1, 0))];
+    for (int u = 0; u < 4; ++u) cv[u] = v.col[min(max(c0 + t0 + 64 * u, 0), max(v.M - 1, 0))];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int t = t0 + 64 * u, k = c0 + t;
-      if (t < nwin + 10) L.u.col[t] = (uint16_t)((k >= 0 && k < v.M) ? cv[u] : 0u);
+      if (t < cnt + 10) colbuf[t] = (uint16_t)((k >= 0 && k < v.M) ? cv[u] : 0u);
     }
   }
   __syncthreads();
-  for (int t0 = lane; t0 < nwin; t0 += 64 * 8) {
-    float cv[8];
-    uint8_t pk[8], gf[8];
+  for (int t0 = lane; t0 < cnt; t0 += 64 * 4) {
+    float cv[4];
+    uint8_t pk[4], gf[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int k = min(lo + t0 + 64 * u, lo + nwin - 1);
+    for (int u = 0; u < 4; ++u) {
+      const int k = min(k0 + t0 + 64 * u, k0 + cnt - 1);
       cv[u] = v.curv[k];
       pk[u] = v.picked[k];
       gf[u] = k < v.M ? v.gflag[k] : 0;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int t = t0 + 64 * u;
-      if (t >= nwin) break;
-      const int ind = lo + t;
-      const int x = t + 5;  // ind's slot in u.col
+      if (t >= cnt) break;
+      const int ind = k0 + t;
+      const int x = t + 5;  // ind's slot in colbuf
       int ff = 0;
 #pragma unroll
       for (int l = 1; l <= 5; ++l) {
         if (ff != l - 1) break;
         if ((unsigned)(ind + l) >= (unsigned)v.VH) break;
-        if (abs((int)L.u.col[x + l] - (int)L.u.col[x + l - 1]) > 10) break;
+        if (abs((int)colbuf[x + l] - (int)colbuf[x + l - 1]) > 10) break;
         ff = l;
       }
       int fb = 0;
@@ -1848,24 +1850,38 @@ LG_DEVICE void stage_ring(const LgParams& P, const ScanView& v, int lo, int nwin
       for (int l = 1; l <= 5; ++l) {
         if (fb != l - 1) break;
         if (ind - l < 0) break;
-        if (abs((int)L.u.col[x - l] - (int)L.u.col[x - l + 1]) > 10) break;
+        if (abs((int)colbuf[x - l] - (int)colbuf[x - l + 1]) > 10) break;
         fb = l;
       }
       const bool g = gf[u] != 0;
-      L.info[t] = (uint16_t)(ff | (fb << 3) | (cv[u] > P.edge_thr && !g ? IF_SH : 0) |
-                             (cv[u] < P.surf_thr && g ? IF_FL : 0) | (pk[u] != 0 ? IF_PK : 0));
+      xinfo[ind] = (uint16_t)(ff | (fb << 3) | (cv[u] > P.edge_thr && !g ? IF_SH : 0) |
+                              (cv[u] < P.surf_thr && g ? IF_FL : 0) | (pk[u] != 0 ? IF_PK : 0));
     }
   }
-  __syncthreads();
 }
 
-LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, int st, int en,
-                            ExtLds& L, RingOut& o) {
+LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, int st, int en, const uint16_t* xinfo,
+                            int stale, ExtLds& L, RingOut& o) {
   const int lane = lane_id();
   if (en <= st) return;  // no segment with sp < ep
-  const int lo = max(st - 5, 0), nwin = min(en + 6, v.VH) - lo;
+  // the window is the ring's candidate range [st, en]: its info words (k_sortseg) into LDS
+  const int lo = st, nwin = en - st + 1;
   PROF_T(t_st0);
-  stage_ring(P, v, lo, nwin, L);
+  for (int t0 = lane; t0 < nwin; t0 += 64 * 8) {
+    uint16_t w8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) w8[u] = xinfo[lo + min(t0 + 64 * u, nwin - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (t0 + 64 * u < nwin) L.info[t0 + 64 * u] = w8[u];
+  }
+  // the first pass's stale-slot pick may have marked picked[] around its index after k_sortseg built
+  // the words (a ring whose window meets that zone waited for it): refresh those bits
+  if (stale >= 0 && lane < 11) {
+    const int k = stale - 5 + lane;
+    if (k >= lo && k < lo + nwin && k < v.VH && v.picked[k]) L.info[k - lo] |= IF_PK;
+  }
+  __syncthreads();
   PROF_ADD(12, t_st0);
   // info word of a candidate position (global for the stale index outside the window)
   auto info_of = [&](int ind) -> int {
@@ -2059,19 +2075,31 @@ __global__ __launch_bounds__(64) void k_sortseg(LgParams P, LgBufs B) {
   const int st = B.ring_start[(size_t)s * V + r], en = B.ring_end[(size_t)s * V + r];
   const int sp = (st * (6 - j) + en * j) / 6;
   const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
-  if (sp >= ep) return;
+  if (sp > ep) return;
   const int n = ep - sp;
   int2* smooth = B.smooth + (size_t)s * P.VH + sp;
-  for (int t = lane_id(); t < n; t += 64) {
-    const int2 e = smooth[t];
-    L.u.seg.skey[t] = __int_as_float(e.x);
-    L.u.seg.sval[t] = e.y;
+  if (n > 0) {  // sorted range [sp, ep) (a one-position segment is never sorted, only visited)
+    for (int t = lane_id(); t < n; t += 64) {
+      const int2 e = smooth[t];
+      L.u.seg.skey[t] = __int_as_float(e.x);
+      L.u.seg.sval[t] = e.y;
+    }
+    __syncthreads();
+    PROF_T(t_rs0);
+    sort_segment(L, n);
+    PROF_ADD(13, t_rs0);
+    for (int t = lane_id(); t < n; t += 64) smooth[t] = make_int2(__float_as_int(L.u.seg.skey[t]), L.u.seg.sval[t]);
   }
-  __syncthreads();
-  PROF_T(t_rs0);
-  sort_segment(L, n);
-  PROF_ADD(13, t_rs0);
-  for (int t = lane_id(); t < n; t += 64) smooth[t] = make_int2(__float_as_int(L.u.seg.skey[t]), L.u.seg.sval[t]);
+  __syncthreads();  // u.seg is free for the colInd window
+  // k_extract's info words for the segment's positions [sp, ep] (candidates are only ever there)
+  ScanView v;
+  v.M = B.counts[(size_t)s * CNT_N + CNT_M];
+  v.VH = P.VH;
+  v.curv = B.curv + (size_t)s * P.VH;
+  v.picked = B.picked + (size_t)s * P.VH;
+  v.col = B.seg_col + (size_t)s * P.VH;
+  v.gflag = B.seg_ground + (size_t)s * P.VH;
+  build_info(P, v, sp, n + 1, B.xinfo + (size_t)s * P.VH, L.u.col);
 }
 
 __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
@@ -2107,9 +2135,10 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
   v.gflag = B.seg_ground + (size_t)s * VH;
   v.fa = B.seg_fa + (size_t)s * VH;
   int2* smooth = B.smooth + (size_t)s * VH;
+  int stale = -1;  // index the stale slot 4 holds (rings after the first pass only)
   if (!first_pass) {
     if (rs[ring] == 4) return;  // a leading ring: done by the first pass
-    const int stale = sync[0];
+    stale = sync[0];
     if (stale + 5 >= rs[ring] - 5 && stale - 5 <= re[ring] + 5) {
       while (__hip_atomic_load(sync + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != P.epoch)
         __builtin_amdgcn_s_sleep(4);
@@ -2130,7 +2159,7 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
     o.nS = o.nLS = o.nF = o.nLF = 0;
     o.status = 0;
     PROF_T(t_ring0);
-    extract_ring(P, v, smooth, rs[r], re[r], L, o);
+    extract_ring(P, v, smooth, rs[r], re[r], B.xinfo + (size_t)s * VH, stale, L, o);
 #ifdef LG_PROFILE
     if (lane_id() == 0) {
       const unsigned long long dt = __builtin_amdgcn_s_memtime() - t_ring0;
