@@ -1788,10 +1788,8 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
 #define IF_PK 0x100     // picked
 #define IF_SH 0x40      // sharp-eligible: curvature > edge threshold, not ground
 #define IF_FL 0x80      // flat-eligible: curvature < surf threshold, ground
-struct ExtLds {  // k_extract: 6.9 KB per wave
-  union {
-    int sval[SEG_MAX];  // the segment's sorted positions (k_sortseg)
-  } u;
+struct ExtLds {  // k_extract: 8.9 KB per wave
+  uint16_t sv[EXT_STAGE];    // the ring's sorted entries (k_sortseg), as indices relative to st
   uint16_t info[EXT_STAGE];  // ff | fb << 3 | IF_SH | IF_FL | IF_PK
   int pk_s[16], pk_ls[128], pk_f[32];  // this ring's picks, in pick order
 };
@@ -1867,13 +1865,21 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
   // the window is the ring's candidate range [st, en]: its info words (k_sortseg) into LDS
   const int lo = st, nwin = en - st + 1;
   PROF_T(t_st0);
-  for (int t0 = lane; t0 < nwin; t0 += 64 * 8) {
+  for (int t0 = lane; t0 < nwin; t0 += 64 * 8) {  // with the sorted entries of every segment (k_sortseg)
     uint16_t w8[8];
+    int e8[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) w8[u] = xinfo[lo + min(t0 + 64 * u, nwin - 1)];
+    for (int u = 0; u < 8; ++u) {
+      const int k = lo + min(t0 + 64 * u, nwin - 1);
+      w8[u] = xinfo[k];
+      e8[u] = smooth[k].y;
+    }
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (t0 + 64 * u < nwin) L.info[t0 + 64 * u] = w8[u];
+      if (t0 + 64 * u < nwin) {
+        L.info[t0 + 64 * u] = w8[u];
+        L.sv[t0 + 64 * u] = (uint16_t)((unsigned)(e8[u] - lo) < (unsigned)nwin ? e8[u] - lo : 0xffff);
+      }
   }
   // the first pass's stale-slot pick may have marked picked[] around its index after k_sortseg built
   // the words (a ring whose window meets that zone waited for it): refresh those bits
@@ -1902,18 +1908,12 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
     const int ep = (st * (5 - j) + en * (j + 1)) / 6 - 1;
     if (sp >= ep) continue;
     const int n = ep - sp;  // sorted range [sp, ep) (k_sortseg); ep itself is visited unsorted
-    PROF_T(t_seg0);
-    __syncthreads();  // the previous segment's reads of u.sval are done
-    for (int t0 = lane; t0 <= n; t0 += 64 * 8) {
-      int sv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sv[u] = smooth[sp + min(t0 + 64 * u, n)].y;
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (t0 + 64 * u <= n) L.u.sval[t0 + 64 * u] = sv[u];
-    }
-    __syncthreads();
-    PROF_ADD(0, t_seg0);
+    // the entry at position sp + t: its index relative to st from LDS, or (0xffff: the stale slot's
+    // index outside the window) from the smoothness array itself
+    auto entry = [&](int t) -> int {
+      const int r = L.sv[sp - lo + t];
+      return r != 0xffff ? lo + r : smooth[sp + t].y;
+    };
     PROF_T(t_sharp0);
     // sharp: k = ep .. sp (descending curvature), first 2 eligible -> sharp, up to 20 -> less sharp.
     // A chunk of 64 candidates reads its info words once; a pick then kills the chunk's lanes inside
@@ -1923,7 +1923,7 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
     for (int base = n; base >= 0 && !stop; base -= 64) {
       const int t = base - lane;
       const bool valid = t >= 0;
-      const int ind = valid ? L.u.sval[t] : 0;
+      const int ind = valid ? entry(t) : 0;
       const int w = valid ? info_of(ind) : 0;
       bool cand = valid && !(w & IF_PK) && (w & IF_SH);
       if (__ballot(cand) == 0ull) continue;
@@ -1959,7 +1959,7 @@ LG_DEVICE void extract_ring(const LgParams& P, const ScanView& v, int2* smooth, 
     for (int base = 0; base <= n && !stop; base += 64) {
       const int t = base + lane;
       const bool valid = t <= n;
-      const int ind = valid ? L.u.sval[t] : 0;
+      const int ind = valid ? entry(t) : 0;
       const int w = valid ? info_of(ind) : 0;
       bool cand = valid && !(w & IF_PK) && (w & IF_FL);
       if (__ballot(cand) == 0ull) continue;
