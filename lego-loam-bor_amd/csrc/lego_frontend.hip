@@ -81,11 +81,36 @@ int dalloc(T** p, size_t n, std::vector<void*>& owned) {
   return LEGO_OK;
 }
 
+// Pinned (page-locked) host buffer, grown on demand: device-to-host copies into it are truly
+// asynchronous, so a read issues all its copies on one stream and waits once.
+struct Pinned {
+  void* p = nullptr;
+  size_t cap = 0;
+  template <typename T>
+  T* get(size_t n) {
+    const size_t bytes = (n > 0 ? n : 1) * sizeof(T);
+    if (bytes > cap) {
+      if (p) hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+      if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+      cap = bytes;
+    }
+    return (T*)p;
+  }
+  ~Pinned() {
+    if (p) hipHostFree(p);
+  }
+};
+
+// async copy of n elements into pinned h; *out = host pointer (valid until the next read)
 template <typename T>
-int d2h(std::vector<T>& h, const T* d, size_t n) {
-  h.resize(n > 0 ? n : 1);
+int d2h(Pinned& h, const T* d, size_t n, hipStream_t st, T** out) {
+  T* hp = h.get<T>(n);
+  if (!hp) return LEGO_ENOMEM;
+  *out = hp;
   if (n == 0) return LEGO_OK;
-  return hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost) == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+  return hipMemcpyAsync(hp, d, n * sizeof(T), hipMemcpyDeviceToHost, st) == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }
 
 }  // namespace
@@ -124,13 +149,10 @@ struct lego_batch {
   int pend_groups = 1;       // slices of that step
   hipStream_t pend_stream = nullptr;
   int par = 0;               // lessFlat staging half of the next step
-  // host mirrors for lego_batch_read
-  std::vector<lego_point> h_seg, h_out, h_scan, h_sharp, h_lsharp, h_flat, h_lflat, h_clast, h_slast, h_olast;
-  std::vector<int32_t> h_rs, h_re, h_label, h_sharp_ind, h_lsharp_ind, h_flat_ind;
-  std::vector<uint8_t> h_gflag;
-  std::vector<uint32_t> h_col;
-  std::vector<float> h_range_seg, h_range;
-  std::vector<int8_t> h_ground;
+  // pinned host mirrors for lego_batch_read / the single-context outputs
+  Pinned h_seg, h_out, h_scan, h_sharp, h_lsharp, h_flat, h_lflat, h_clast, h_slast, h_olast;
+  Pinned h_rs, h_re, h_label, h_sharp_ind, h_lsharp_ind, h_flat_ind, h_gflag, h_col, h_range_seg, h_range, h_ground;
+  Pinned h_hdr;  // counts, orientation and state of the stream being read
   ~lego_batch() {
     hipSetDevice(device);
     for (void* p : owned) hipFree(p);
@@ -153,7 +175,8 @@ struct lego_ctx {
   int64_t* d_off = nullptr;
   int32_t* d_cnt = nullptr;
   int cap = 0;
-  std::vector<float4> h_pts;
+  Pinned h_pts;  // fromROSMsg gather target (pinned: the upload is asynchronous)
+  Pinned h_n;    // the point count, uploaded with the points
   ~lego_ctx() {
     if (b) {
       hipSetDevice(b->device);
@@ -496,81 +519,108 @@ int lego_batch_stage_times(lego_batch* b, float* ms6) {
   return LEGO_OK;
 }
 
-static int read_proj(lego_batch* b, int s, lego_projection_out* o) {
-  const LgParams& P = b->P;
-  const LgBufs& B = b->B;
-  const size_t VH = P.VH;
+// Header of stream s (counts, orientation, state) into pinned memory, on st, then wait for it.
+struct ReadHdr {
   int32_t cnt[CNT_N];
-  if (hipMemcpy(cnt, B.counts + (size_t)s * CNT_N, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
   float ori[4];
-  if (hipMemcpy(ori, B.orient + (size_t)s * 4, sizeof(ori), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
-  const int M = cnt[CNT_M];
-  int rc = LEGO_OK;
-  rc |= d2h(b->h_seg, (const lego_point*)(B.seg_pts + s * VH), M);
-  rc |= d2h(b->h_out, (const lego_point*)(B.outlier + s * VH), cnt[CNT_OUTLIER]);
-  rc |= d2h(b->h_scan, (const lego_point*)(B.scan_msg + (size_t)s * P.H), cnt[CNT_SCAN]);
-  rc |= d2h(b->h_rs, B.ring_start + (size_t)s * P.V, P.V);
-  rc |= d2h(b->h_re, B.ring_end + (size_t)s * P.V, P.V);
-  rc |= d2h(b->h_gflag, B.seg_ground + s * VH, M);
-  rc |= d2h(b->h_col, B.seg_col + s * VH, M);
-  rc |= d2h(b->h_range_seg, B.seg_range + s * VH, M);
-  rc |= d2h(b->h_label, B.label + s * VH, VH);
-  rc |= d2h(b->h_ground, B.ground + s * VH, VH);
-  rc |= d2h(b->h_range, B.range + s * VH, VH);
-  if (rc) return LEGO_EDEVICE;
-  o->n_segmented = M;
-  o->n_outlier = cnt[CNT_OUTLIER];
-  o->n_scan = cnt[CNT_SCAN];
-  o->segmented_cloud = b->h_seg.data();
-  o->outlier_cloud = b->h_out.data();
-  o->scan_msg = b->h_scan.data();
-  o->start_ring_index = b->h_rs.data();
-  o->end_ring_index = b->h_re.data();
-  o->start_orientation = ori[0];
-  o->end_orientation = ori[1];
-  o->orientation_diff = ori[2];
-  o->segmented_cloud_ground_flag = b->h_gflag.data();
-  o->segmented_cloud_col_ind = b->h_col.data();
-  o->segmented_cloud_range = b->h_range_seg.data();
-  o->label_mat = b->h_label.data();
-  o->ground_mat = b->h_ground.data();
-  o->range_mat = b->h_range.data();
+  LgState S;
+};
+static int read_hdr(lego_batch* b, int s, hipStream_t st, ReadHdr** out) {
+  const LgBufs& B = b->B;
+  ReadHdr* h = b->h_hdr.get<ReadHdr>(1);
+  if (!h) return LEGO_ENOMEM;
+  if (hipMemcpyAsync(h->cnt, B.counts + (size_t)s * CNT_N, sizeof(h->cnt), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(h->ori, B.orient + (size_t)s * 4, sizeof(h->ori), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(&h->S, B.state + s, sizeof(h->S), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return LEGO_EDEVICE;
+  *out = h;
   return LEGO_OK;
 }
 
-static int read_assoc(lego_batch* b, int s, lego_association_out* o) {
+// ProjectionOut of stream s: every array copy issued on st, one wait (h = read_hdr's header)
+static int read_proj(lego_batch* b, int s, const ReadHdr* h, hipStream_t st, lego_projection_out* o) {
+  const LgParams& P = b->P;
+  const LgBufs& B = b->B;
+  const size_t VH = P.VH;
+  const int M = h->cnt[CNT_M];
+  int rc = LEGO_OK;
+  lego_point *seg, *outl, *scan;
+  int32_t *rs, *re, *label;
+  uint8_t* gflag;
+  uint32_t* col;
+  float *range_seg, *range;
+  int8_t* ground;
+  rc |= d2h(b->h_seg, (const lego_point*)(B.seg_pts + s * VH), M, st, &seg);
+  rc |= d2h(b->h_out, (const lego_point*)(B.outlier + s * VH), h->cnt[CNT_OUTLIER], st, &outl);
+  rc |= d2h(b->h_scan, (const lego_point*)(B.scan_msg + (size_t)s * P.H), h->cnt[CNT_SCAN], st, &scan);
+  rc |= d2h(b->h_rs, B.ring_start + (size_t)s * P.V, P.V, st, &rs);
+  rc |= d2h(b->h_re, B.ring_end + (size_t)s * P.V, P.V, st, &re);
+  rc |= d2h(b->h_gflag, B.seg_ground + s * VH, M, st, &gflag);
+  rc |= d2h(b->h_col, B.seg_col + s * VH, M, st, &col);
+  rc |= d2h(b->h_range_seg, B.seg_range + s * VH, M, st, &range_seg);
+  rc |= d2h(b->h_label, B.label + s * VH, VH, st, &label);
+  rc |= d2h(b->h_ground, B.ground + s * VH, VH, st, &ground);
+  rc |= d2h(b->h_range, B.range + s * VH, VH, st, &range);
+  if (rc) return LEGO_EDEVICE;
+  if (hipStreamSynchronize(st) != hipSuccess) return LEGO_EDEVICE;
+  o->n_segmented = M;
+  o->n_outlier = h->cnt[CNT_OUTLIER];
+  o->n_scan = h->cnt[CNT_SCAN];
+  o->segmented_cloud = seg;
+  o->outlier_cloud = outl;
+  o->scan_msg = scan;
+  o->start_ring_index = rs;
+  o->end_ring_index = re;
+  o->start_orientation = h->ori[0];
+  o->end_orientation = h->ori[1];
+  o->orientation_diff = h->ori[2];
+  o->segmented_cloud_ground_flag = gflag;
+  o->segmented_cloud_col_ind = col;
+  o->segmented_cloud_range = range_seg;
+  o->label_mat = label;
+  o->ground_mat = ground;
+  o->range_mat = range;
+  return LEGO_OK;
+}
+
+// AssociationOut of stream s (as read_proj)
+static int read_assoc(lego_batch* b, int s, const ReadHdr* h, hipStream_t st, lego_association_out* o) {
   const LgParams& P = b->P;
   const LgBufs& B = b->B;
   const size_t VH = P.VH, V = P.V;
-  int32_t cnt[CNT_N];
-  LgState S;
-  if (hipMemcpy(cnt, B.counts + (size_t)s * CNT_N, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
-  if (hipMemcpy(&S, B.state + s, sizeof(S), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
+  const int32_t* cnt = h->cnt;
+  const LgState& S = h->S;
   int rc = LEGO_OK;
-  rc |= d2h(b->h_sharp, (const lego_point*)(B.f_sharp + (size_t)s * V * P.cap_sharp), cnt[CNT_SHARP]);
-  rc |= d2h(b->h_sharp_ind, B.f_sharp_ind + (size_t)s * V * P.cap_sharp, cnt[CNT_SHARP]);
-  rc |= d2h(b->h_lsharp, (const lego_point*)(B.f_lsharp + (size_t)s * V * P.cap_lsharp), cnt[CNT_LSHARP]);
-  rc |= d2h(b->h_lsharp_ind, B.f_lsharp_ind + (size_t)s * V * P.cap_lsharp, cnt[CNT_LSHARP]);
-  rc |= d2h(b->h_flat, (const lego_point*)(B.f_flat + (size_t)s * V * P.cap_flat), cnt[CNT_FLAT]);
-  rc |= d2h(b->h_flat_ind, B.f_flat_ind + (size_t)s * V * P.cap_flat, cnt[CNT_FLAT]);
-  rc |= d2h(b->h_lflat, (const lego_point*)(B.f_lflat + s * VH), cnt[CNT_LFLAT]);
+  lego_point *sharp, *lsharp, *flat, *lflat, *clast, *slast, *olast;
+  int32_t *sharp_ind, *lsharp_ind, *flat_ind;
+  rc |= d2h(b->h_sharp, (const lego_point*)(B.f_sharp + (size_t)s * V * P.cap_sharp), cnt[CNT_SHARP], st, &sharp);
+  rc |= d2h(b->h_sharp_ind, B.f_sharp_ind + (size_t)s * V * P.cap_sharp, cnt[CNT_SHARP], st, &sharp_ind);
+  rc |= d2h(b->h_lsharp, (const lego_point*)(B.f_lsharp + (size_t)s * V * P.cap_lsharp), cnt[CNT_LSHARP], st, &lsharp);
+  rc |= d2h(b->h_lsharp_ind, B.f_lsharp_ind + (size_t)s * V * P.cap_lsharp, cnt[CNT_LSHARP], st, &lsharp_ind);
+  rc |= d2h(b->h_flat, (const lego_point*)(B.f_flat + (size_t)s * V * P.cap_flat), cnt[CNT_FLAT], st, &flat);
+  rc |= d2h(b->h_flat_ind, B.f_flat_ind + (size_t)s * V * P.cap_flat, cnt[CNT_FLAT], st, &flat_ind);
+  rc |= d2h(b->h_lflat, (const lego_point*)(B.f_lflat + s * VH), cnt[CNT_LFLAT], st, &lflat);
   const size_t cls = V * P.cap_lsharp;
-  rc |= d2h(b->h_clast, (const lego_point*)(B.corner_last + (size_t)s * 2 * cls + (size_t)S.last_buf * cls), S.n_corner_last);
-  rc |= d2h(b->h_slast, (const lego_point*)(B.surf_last + (size_t)s * 2 * VH + (size_t)S.last_buf * VH), S.n_surf_last);
-  rc |= d2h(b->h_olast, (const lego_point*)(B.outlier_fa + s * VH), cnt[CNT_OUTLIER]);
+  rc |= d2h(b->h_clast, (const lego_point*)(B.corner_last + (size_t)s * 2 * cls + (size_t)S.last_buf * cls),
+            S.n_corner_last, st, &clast);
+  rc |= d2h(b->h_slast, (const lego_point*)(B.surf_last + (size_t)s * 2 * VH + (size_t)S.last_buf * VH),
+            S.n_surf_last, st, &slast);
+  rc |= d2h(b->h_olast, (const lego_point*)(B.outlier_fa + s * VH), cnt[CNT_OUTLIER], st, &olast);
   if (rc) return LEGO_EDEVICE;
+  if (hipStreamSynchronize(st) != hipSuccess) return LEGO_EDEVICE;
   o->status = S.status;
   o->n_sharp = cnt[CNT_SHARP];
   o->n_less_sharp = cnt[CNT_LSHARP];
   o->n_flat = cnt[CNT_FLAT];
   o->n_less_flat = cnt[CNT_LFLAT];
-  o->corner_points_sharp = b->h_sharp.data();
-  o->corner_points_less_sharp = b->h_lsharp.data();
-  o->surf_points_flat = b->h_flat.data();
-  o->surf_points_less_flat = b->h_lflat.data();
-  o->sharp_ind = b->h_sharp_ind.data();
-  o->less_sharp_ind = b->h_lsharp_ind.data();
-  o->flat_ind = b->h_flat_ind.data();
+  o->corner_points_sharp = sharp;
+  o->corner_points_less_sharp = lsharp;
+  o->surf_points_flat = flat;
+  o->surf_points_less_flat = lflat;
+  o->sharp_ind = sharp_ind;
+  o->less_sharp_ind = lsharp_ind;
+  o->flat_ind = flat_ind;
   for (int i = 0; i < 6; ++i) {
     o->transform_cur[i] = S.cur[i];
     o->transform_sum[i] = S.sum[i];
@@ -582,9 +632,9 @@ static int read_assoc(lego_batch* b, int s, lego_association_out* o) {
   o->n_corner_last = S.n_corner_last;
   o->n_surf_last = S.n_surf_last;
   o->n_outlier_last = cnt[CNT_OUTLIER];
-  o->cloud_corner_last = b->h_clast.data();
-  o->cloud_surf_last = b->h_slast.data();
-  o->cloud_outlier_last = b->h_olast.data();
+  o->cloud_corner_last = clast;
+  o->cloud_surf_last = slast;
+  o->cloud_outlier_last = olast;
   return LEGO_OK;
 }
 
@@ -593,15 +643,11 @@ int lego_batch_read(lego_batch* b, int32_t s, lego_projection_out* proj, lego_as
   hipSetDevice(b->device);
   if (flush_pending(b) != LEGO_OK) return LEGO_EDEVICE;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
-  if (proj) {
-    int rc = read_proj(b, s, proj);
-    if (rc) return rc;
-  }
-  if (assoc) {
-    int rc = read_assoc(b, s, assoc);
-    if (rc) return rc;
-  }
-  return LEGO_OK;
+  ReadHdr* h = nullptr;
+  int rc = read_hdr(b, s, nullptr, &h);
+  if (!rc && proj) rc = read_proj(b, s, h, nullptr, proj);
+  if (!rc && assoc) rc = read_assoc(b, s, h, nullptr, assoc);
+  return rc;
 }
 
 int lego_batch_read_poses(lego_batch* b, float* out, int32_t* status) {
@@ -678,7 +724,9 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
   lego_batch* b = c->b;
   hipSetDevice(b->device);
   // fromROSMsg: gather x,y,z from the strided PointCloud2 payload (intensity is not used by the path)
-  c->h_pts.resize(n > 0 ? n : 1);
+  float4* hp = c->h_pts.get<float4>(n);
+  int32_t* hn = c->h_n.get<int32_t>(1);
+  if (!hp || !hn) return LEGO_ENOMEM;
   const char* base = (const char*)points;
   for (int i = 0; i < n; ++i) {
     float4 q;
@@ -686,24 +734,27 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
     memcpy(&q.y, base + (size_t)i * step + oy, 4);
     memcpy(&q.z, base + (size_t)i * step + oz, 4);
     q.w = 0.f;
-    c->h_pts[i] = q;
+    hp[i] = q;
   }
+  *hn = n;
   if (n > c->cap) {
     if (c->d_pts) hipFree(c->d_pts);
     c->d_pts = nullptr;
     if (hipMalloc((void**)&c->d_pts, (size_t)n * sizeof(float4)) != hipSuccess) return LEGO_ENOMEM;
     c->cap = n;
   }
-  if (n > 0 && hipMemcpy(c->d_pts, c->h_pts.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess)
+  // everything in order on the null stream: upload, kernels, then one wait for the header and one
+  // for the output arrays (pinned host buffers throughout)
+  if (n > 0 && hipMemcpyAsync(c->d_pts, hp, (size_t)n * sizeof(float4), hipMemcpyHostToDevice, nullptr) != hipSuccess)
     return LEGO_EDEVICE;
-  if (hipMemcpy(c->d_cnt, &n, sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemcpyAsync(c->d_cnt, hn, sizeof(int32_t), hipMemcpyHostToDevice, nullptr) != hipSuccess) return LEGO_EDEVICE;
   int rc = run_projection(b, c->d_pts ? c->d_pts : (const float4*)c->d_off, c->d_off, c->d_cnt, nullptr, 0, 1);
   if (rc) return rc;
-  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
-  LgState S;
-  if (hipMemcpy(&S, b->B.state, sizeof(S), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
-  if (S.proj_status != LEGO_OK) return S.proj_status;
-  if (out) return read_proj(b, 0, out);
+  ReadHdr* h = nullptr;
+  rc = read_hdr(b, 0, nullptr, &h);
+  if (rc) return rc;
+  if (h->S.proj_status != LEGO_OK) return h->S.proj_status;
+  if (out) return read_proj(b, 0, h, nullptr, out);
   return LEGO_OK;
 }
 
@@ -713,8 +764,10 @@ static int feature_association(lego_ctx* c, lego_association_out* out, bool dist
   b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
   int rc = run_association(b, nullptr, 0, 1, distort);
   if (rc) return rc;
-  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
-  if (out) return read_assoc(b, 0, out);
+  ReadHdr* h = nullptr;
+  rc = read_hdr(b, 0, nullptr, &h);  // also the wait for the kernels
+  if (rc) return rc;
+  if (out) return read_assoc(b, 0, h, nullptr, out);
   return LEGO_OK;
 }
 
