@@ -762,7 +762,14 @@ static int feature_association(lego_ctx* c, lego_association_out* out, bool dist
   lego_batch* b = c->b;
   hipSetDevice(b->device);
   b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
-  int rc = run_association(b, nullptr, 0, 1, distort);
+  // VoxelGrid on the side stream while k_lm runs, then k_publish (joined with it) before the reads
+  int rc = ensure_streams(b, 1);
+  if (!rc) rc = run_association(b, nullptr, 0, 1, distort, true, 0);
+  if (rc) return rc;
+  b->pending = true;
+  b->pend_groups = 1;
+  b->pend_stream = nullptr;
+  rc = flush_pending(b);
   if (rc) return rc;
   ReadHdr* h = nullptr;
   rc = read_hdr(b, 0, nullptr, &h);  // also the wait for the kernels
