@@ -2271,7 +2271,7 @@ __global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
 // ============================================================================================
 // k_lm: updateTransformation + integrateTransformation + publishOdometry + publishCloudsLast
 // ============================================================================================
-#define LM_THREADS 512
+#define LM_THREADS 768
 #define GRID_MAX 8191  // grid cells (end offsets share LDS with the staged small cloud)
 #define CGRID_MAX 2047  // grid cells over a staged small cloud
 #define LM_MAXQ 1536  // 24 * 64 rings
