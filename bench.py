@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (test rehearsal)")
     ap.add_argument("--groups", type=int, default=1, help="stream slices launched on separate HIP streams")
+    ap.add_argument("--lag", type=int, default=1, choices=[0, 1],
+                    help="pipeline depth (lego_batch_set_lag): 1 = a step runs the previous scan's LM")
     ap.add_argument("--voxel-tie-order", type=int, default=1, choices=[0, 1],
                     help="lego_params.voxel_tie_order of the measured path: 1 = VoxelGrid sums each voxel in "
                          "point order (stable); 0 = libstdc++ std::sort order, bit-identical to the GCC-built "
@@ -142,15 +144,19 @@ def main():
     d_cnt = torch.from_numpy(host_cnt.astype(np.int32)).to(dev)
     batch = L.Batch(params, S, cap, device=local_dev)
     batch.set_groups(args.groups)
+    batch.set_lag(args.lag)
     stream = torch.cuda.current_stream(dev)
 
     def step(k, b=None):
         (b or batch).step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
 
     def timed(b):
-        """W untimed warm-up steps, then exactly K timed steps between barrier + sync; max over ranks."""
+        """W untimed warm-up steps, then exactly K timed steps between barrier + sync; max over ranks.
+        The pipeline is drained (flush) at the end of the warm-up and inside the timed region, so the
+        timed region runs exactly K scans' work per stream, the last scan's LM and publish included."""
         for k in range(W):
             step(k, b)
+        b.flush()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -158,6 +164,7 @@ def main():
         t0 = time.perf_counter()
         for k in range(W, W + K):
             step(k, b)
+        b.flush()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -187,6 +194,7 @@ def main():
         params_alt = (L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64)(voxel_tie_order=alt_order)
         batch_alt = L.Batch(params_alt, S, cap, device=local_dev)
         batch_alt.set_groups(args.groups)
+        batch_alt.set_lag(args.lag)
         el_alt = timed(batch_alt)
         batch_alt.close()
         alt = {"voxel_tie_order": alt_order, "value": round(total_scans / el_alt, 1),
@@ -233,7 +241,7 @@ def main():
         "config": {"workload": "C3: batched synthetic %s sweeps, %d independent sequences per GPU x 1 scan per step"
                                % (args.kind.upper(), S),
                    "V": V, "H": H, "points_per_scan": round(n_mean, 1), "streams_per_gpu": S,
-                   "parallelism": "sequence-sharded x%d" % world, "stream_groups": args.groups,
+                   "parallelism": "sequence-sharded x%d" % world, "stream_groups": args.groups, "lag": args.lag,
                    "voxel_tie_order": args.voxel_tie_order},
         "roofline": roofline,
         "stages_ms": {"project": round(stage[0], 4), "segment": round(stage[1], 4), "fa_prep": round(stage[2], 4),

@@ -161,13 +161,17 @@ void lego_batch_destroy(lego_batch* b);
 /* Advance every stream by one scan.  d_points: DEVICE array of lego_point (x,y,z,intensity);
  * stream s's scan is d_points[d_offsets[s] .. d_offsets[s] + d_counts[s]).  d_offsets / d_counts are
  * DEVICE arrays (int64 / int32) of length n_streams.  Asynchronous on hip_stream (NULL = default).
- * The step's VoxelGrid runs on an internal stream, overlapping its LM and the next step's front end;
- * the lessFlat half of publishCloudsLast is issued by the next step (before its LM) or by
- * lego_batch_flush / lego_batch_sync / lego_batch_read*, which all see completed scans. */
+ * The step's VoxelGrid runs on an internal stream, overlapping other work.  With lag 1 (the default,
+ * lego_batch_set_lag) the step runs its scan's front end and the PREVIOUS scan's LM, so the VoxelGrid
+ * has two steps to finish; with lag 0 it runs its own scan's LM.  Whatever is left (the last scan's
+ * LM and the lessFlat half of publishCloudsLast) is issued by the next step or by lego_batch_flush /
+ * lego_batch_sync / lego_batch_read*, which all see completed scans.  Consecutive calls may use
+ * different hip_streams: a call on a new stream first waits for all work enqueued on the previous
+ * one. */
 int  lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_offsets,
                      const int32_t* d_counts, void* hip_stream);
-/* Enqueue the last step's pending work on its stream (asynchronous); then a device synchronize sees
- * every output of that step. */
+/* Enqueue the pending work (the last scan's LM / publish) on the last step's stream (asynchronous);
+ * then a synchronize of that stream sees every output of the last step. */
 int  lego_batch_flush(lego_batch* b);
 int  lego_batch_sync(lego_batch* b);
 /* Copy one stream's last projection / association outputs to host (blocking). */
@@ -181,8 +185,8 @@ int  lego_batch_read_counts(lego_batch* b, int32_t* out);
 int  lego_batch_reset(lego_batch* b);
 /* Kernel timing of the last step (ms, hipEvents on the step's stream, the pipelined path itself):
  * [0] project, [1] segment + distortion, [2] smoothness + occlusion, [3] feature extraction,
- * [4] concat + the previous step's lessFlat publish, [5] LM (the VoxelGrid overlaps it on an
- * internal stream). */
+ * [4] concat + the pending lessFlat publish, [5] LM (of the previous scan with lag 1; the VoxelGrid
+ * overlaps it on an internal stream). */
 int  lego_batch_stage_times(lego_batch* b, float* ms6);
 /* While timing is enabled, steps run as one slice on the caller's stream (plus the VoxelGrid stream). */
 int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
@@ -191,6 +195,9 @@ int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
  * overlap the others'.  Results do not depend on the grouping. */
 #define LEGO_MAX_GROUPS 4
 int  lego_batch_set_groups(lego_batch* b, int32_t groups);
+/* Pipeline depth of lego_batch_step: 0 = a step runs its own scan's LM, 1 (default) = the previous
+ * scan's (see lego_batch_step).  Results do not depend on it. */
+int  lego_batch_set_lag(lego_batch* b, int32_t lag);
 
 /* ---- test hooks ------------------------------------------------------------------ */
 /* Evaluate the device libm restatement on host arrays: which = 0 asinf(a), 1 atan2f(a, b),

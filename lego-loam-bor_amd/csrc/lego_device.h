@@ -35,7 +35,8 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int epoch;                            // per-launch token for k_extract's first-pass flags
   float inv_res_x, inv_res_y;           // (float)(1 / ang_res_*) for the fast projection path
   int fast_proj;                        // the fast path's margins hold for these resolutions
-  int par;                              // lessFlat staging half of this step (k_concat -> k_voxel)
+  int par;                              // parity of the launch's scan: the half of the double-buffered
+                                        // staging (features, lessFlat, VoxelGrid output) it uses
   int S;                                // streams of the batch (staging stride)
 };
 
@@ -96,16 +97,20 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   float4* r_sharp; int32_t* r_sharp_ind;    // [S][V][cap_sharp]
   float4* r_lsharp; int32_t* r_lsharp_ind;  // [S][V][cap_lsharp]
   float4* r_flat; int32_t* r_flat_ind;      // [S][V][cap_flat]
-  float4* r_lflat;                          // [S][V][H]   VoxelGrid output per ring
-  int32_t* r_counts;                        // [S][V][4]   sharp, lessSharp, flat, lessFlat (k_voxel)
+  int32_t* r_counts;                        // [S][V][4]   sharp, lessSharp, flat (k_extract), unused
   int32_t* r_status;                        // [S][V]      k_extract status bits
-  int32_t* r_vstatus;                       // [S][V]      k_voxel status bits
+  // [2][...]: halves by scan parity (LgParams.par), so scan k's VoxelGrid / publish / LM may run
+  // while scan k+1's front end fills the other half
   float4* lf_stage;                         // [2][S][V][H] surfPointsLessFlatScan per ring (k_concat)
   int32_t* lf_count;                        // [2][S][V]
+  float4* r_lflat;                          // [2][S][V][H] VoxelGrid output per ring (k_voxel)
+  int32_t* r_vcount;                        // [2][S][V]    its point count
+  int32_t* r_vstatus;                       // [2][S][V]    k_voxel status bits
   // concatenated features
-  float4* f_sharp; int32_t* f_sharp_ind;    // [S][V*cap_sharp]
-  float4* f_lsharp; int32_t* f_lsharp_ind;  // [S][V*cap_lsharp]
-  float4* f_flat; int32_t* f_flat_ind;      // [S][V*cap_flat]
+  float4* f_sharp; int32_t* f_sharp_ind;    // [2][S][V*cap_sharp]
+  float4* f_lsharp; int32_t* f_lsharp_ind;  // [2][S][V*cap_lsharp]
+  float4* f_flat; int32_t* f_flat_ind;      // [2][S][V*cap_flat]
+  int32_t* fcnt;                            // [2][S][4]  sharp, lessSharp, flat counts, status (k_lm)
   float4* f_lflat;                          // [S][VH]
   // Last clouds, double-buffered
   float4* corner_last;   // [S][2][V*cap_lsharp]

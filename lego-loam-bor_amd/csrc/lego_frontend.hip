@@ -139,22 +139,35 @@ struct lego_batch {
   int groups = 1;
   hipStream_t gs[LEGO_MAX_GROUPS] = {};
   hipEvent_t fork = nullptr, join[LEGO_MAX_GROUPS] = {};
+  // The stream of the last call that enqueued work; a step on another stream first waits for
+  // everything enqueued there (ev_chain), so the pending kernels it issues are ordered after it.
   hipStream_t last_stream = nullptr;
-  // VoxelGrid overlap: each slice's k_voxel runs on a side stream (vs) while the slice goes on with
-  // k_lm and the next scan's front end; the lessFlat half of publishCloudsLast (k_publish) of scan k
-  // is issued just before scan k+1's k_lm, or by lego_batch_flush.
+  bool has_last = false;
+  hipEvent_t ev_chain = nullptr;
+  // Pipeline (per scan k of every stream): front end(k) -> k_concat(k) -> k_voxel(k) on the side
+  // stream vs -> k_publish(k) after k_lm(k) and k_voxel(k), before k_lm(k+1).  Each scan uses the
+  // staging half of its parity, so the next scan's front end never waits for it.
+  //   lag 0: step k runs k_publish(k-1), then k_lm(k);  k_publish(k) stays pending.
+  //   lag 1: step k runs k_publish(k-2), then k_lm(k-1); k_publish(k-1) and k_lm(k) stay pending,
+  //          so k_voxel(k) has two steps of other work to hide behind.
+  // lego_batch_flush (and every read) issues what is pending.
+  int lag = 1;
   hipStream_t vs[LEGO_MAX_GROUPS] = {};
-  hipEvent_t ev_cat[LEGO_MAX_GROUPS] = {}, ev_vox[LEGO_MAX_GROUPS] = {};
-  bool pending = false;      // k_publish of the last step not issued yet
-  int pend_groups = 1;       // slices of that step
-  hipStream_t pend_stream = nullptr;
-  int par = 0;               // lessFlat staging half of the next step
+  hipEvent_t ev_cat[LEGO_MAX_GROUPS] = {}, ev_vox[LEGO_MAX_GROUPS][2] = {};
+  int par = 0;               // parity of the next front-end scan
+  int last_par = 0;          // parity of the last front-end scan (reads)
+  bool pend_pub = false;     // k_publish of a scan whose k_lm has run (parity pub_par)
+  int pub_par = 0;
+  bool pend_lm = false;      // k_lm of the last front-end scan (lag 1; parity lm_par)
+  int lm_par = 0;
+  int pend_groups = 1;       // slicing of the pending work
   // pinned host mirrors for lego_batch_read / the single-context outputs
   Pinned h_seg, h_out, h_scan, h_sharp, h_lsharp, h_flat, h_lflat, h_clast, h_slast, h_olast;
   Pinned h_rs, h_re, h_label, h_sharp_ind, h_lsharp_ind, h_flat_ind, h_gflag, h_col, h_range_seg, h_range, h_ground;
   Pinned h_hdr;  // counts, orientation and state of the stream being read
   ~lego_batch() {
     hipSetDevice(device);
+    hipDeviceSynchronize();  // nothing of this batch may still run on its buffers or streams
     for (void* p : owned) hipFree(p);
     if (events)
       for (int i = 0; i < 8; ++i) hipEventDestroy(ev[i]);
@@ -163,9 +176,11 @@ struct lego_batch {
       if (join[g]) hipEventDestroy(join[g]);
       if (vs[g]) hipStreamDestroy(vs[g]);
       if (ev_cat[g]) hipEventDestroy(ev_cat[g]);
-      if (ev_vox[g]) hipEventDestroy(ev_vox[g]);
+      for (int h = 0; h < 2; ++h)
+        if (ev_vox[g][h]) hipEventDestroy(ev_vox[g][h]);
     }
     if (fork) hipEventDestroy(fork);
+    if (ev_chain) hipEventDestroy(ev_chain);
   }
 };
 
@@ -278,11 +293,12 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   A(r_sharp, S * V * P.cap_sharp); A(r_sharp_ind, S * V * P.cap_sharp);
   A(r_lsharp, S * V * P.cap_lsharp); A(r_lsharp_ind, S * V * P.cap_lsharp);
   A(r_flat, S * V * P.cap_flat); A(r_flat_ind, S * V * P.cap_flat);
-  A(r_lflat, S * V * H); A(r_counts, S * V * 4); A(r_status, S * V); A(r_vstatus, S * V);
+  A(r_counts, S * V * 4); A(r_status, S * V);
   A(lf_stage, 2 * S * V * H); A(lf_count, 2 * S * V);
-  A(f_sharp, S * V * P.cap_sharp); A(f_sharp_ind, S * V * P.cap_sharp);
-  A(f_lsharp, S * V * P.cap_lsharp); A(f_lsharp_ind, S * V * P.cap_lsharp);
-  A(f_flat, S * V * P.cap_flat); A(f_flat_ind, S * V * P.cap_flat);
+  A(r_lflat, 2 * S * V * H); A(r_vcount, 2 * S * V); A(r_vstatus, 2 * S * V);
+  A(f_sharp, 2 * S * V * P.cap_sharp); A(f_sharp_ind, 2 * S * V * P.cap_sharp);
+  A(f_lsharp, 2 * S * V * P.cap_lsharp); A(f_lsharp_ind, 2 * S * V * P.cap_lsharp);
+  A(f_flat, 2 * S * V * P.cap_flat); A(f_flat_ind, 2 * S * V * P.cap_flat); A(fcnt, 2 * S * 4);
   A(f_lflat, S * VH);
   A(corner_last, S * 2 * V * P.cap_lsharp); A(surf_last, S * 2 * VH); A(grid_pts, S * VH);
   A(state, S);
@@ -305,6 +321,9 @@ void lego_batch_destroy(lego_batch* b) { delete b; }
 int lego_batch_reset(lego_batch* b) {
   if (!b) return LEGO_EINVAL;
   hipSetDevice(b->device);
+  // no kernel of an unsynchronised step may still write the state cleared below (the memsets go on
+  // the null stream, which is not ordered against non-blocking streams); pending work is dropped
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
   const size_t S = b->S, VH = b->P.VH;
   LgBufs& B = b->B;
   // FeatureAssociation's vectors are value-initialised (fa.cpp:96-128); transforms zero (:135-138)
@@ -314,8 +333,8 @@ int lego_batch_reset(lego_batch* b) {
   if (hipMemset(B.smooth, 0, S * VH * sizeof(int2)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fp_sync, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   b->epoch = 0;
-  b->pending = false;
-  b->par = 0;
+  b->pend_pub = b->pend_lm = false;
+  b->par = b->last_par = 0;
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.counts, 0, S * CNT_N * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
@@ -348,13 +367,27 @@ static int run_projection(lego_batch* b, const float4* pts, const int64_t* offs,
   return LEGO_OK;
 }
 
-// One slice [s0, s0 + n) of the streams through FeatureAssociation.  distort: the ProjectionOut came
-// from the host (adjustDistortion / adjustOutlierCloud run in k_fa_prep instead of k_segment).
-// overlap == false: everything in order on st, k_publish included (single context, stage timing).
-// overlap == true: k_voxel on the slice's side stream vs[g]; the previous step's k_publish (joined
-// with its k_voxel) goes in before this step's k_lm, this step's stays pending.
-static int run_association(lego_batch* b, hipStream_t st, int s0, int n, bool distort = false, bool overlap = false,
-                           int g = 0) {
+// k_publish of the slice [s0, s0 + n) for its scan of parity `par`, after that scan's k_voxel.
+static int issue_publish(lego_batch* b, hipStream_t st, int g, int s0, int n, int par) {
+  LgParams P = b->P;
+  P.s0 = s0;
+  P.par = par;
+  if (hipStreamWaitEvent(st, b->ev_vox[g][par], 0) != hipSuccess) return LEGO_EDEVICE;
+  return lg_launch_publish(P, b->B, n, st);
+}
+
+static int issue_lm(lego_batch* b, hipStream_t st, int s0, int n, int par) {
+  LgParams P = b->P;
+  P.s0 = s0;
+  P.par = par;
+  return lg_launch_lm(P, b->B, n, st);
+}
+
+// One slice [s0, s0 + n) of the streams through FeatureAssociation (slice g, on st), for the scan of
+// parity b->par whose projection has run.  distort: the ProjectionOut came from the host
+// (adjustDistortion / adjustOutlierCloud run in k_fa_prep instead of k_segment).  lag: as
+// lego_batch::lag; the pending flags are read here and advanced by the caller (advance_pipeline).
+static int run_association(lego_batch* b, hipStream_t st, int s0, int n, bool distort, int g, bool lag) {
   LgParams P = b->P;
   P.s0 = s0;
   P.epoch = b->epoch;
@@ -364,65 +397,85 @@ static int run_association(lego_batch* b, hipStream_t st, int s0, int n, bool di
   if (b->timing) hipEventRecord(b->ev[3], st);
   rc = lg_launch_extract(P, b->B, n, st);
   if (rc) return rc;
-  if (!overlap) {
-    if (b->timing) hipEventRecord(b->ev[4], st);
-    rc = lg_launch_concat(P, b->B, n, st);
-    if (!rc) rc = lg_launch_voxel(P, b->B, n, st);
-    if (rc) return rc;
-    if (b->timing) hipEventRecord(b->ev[5], st);
-    rc = lg_launch_lm(P, b->B, n, st);
-    if (!rc) rc = lg_launch_publish(P, b->B, n, st);
-    if (rc) return rc;
-    if (b->timing) hipEventRecord(b->ev[6], st);
-    return LEGO_OK;
-  }
   if (b->timing) hipEventRecord(b->ev[4], st);
+  // a pending publish frees the staging half this scan's k_concat / k_voxel are about to fill
+  if (b->pend_pub && (rc = issue_publish(b, st, g, s0, n, b->pub_par))) return rc;
   rc = lg_launch_concat(P, b->B, n, st);
   if (rc) return rc;
-  if (b->pending) {  // scan k-1's lessFlat publish: after its k_voxel, before this scan's k_lm
-    if (hipStreamWaitEvent(st, b->ev_vox[g], 0) != hipSuccess) return LEGO_EDEVICE;
-    rc = lg_launch_publish(P, b->B, n, st);
-    if (rc) return rc;
-  }
   if (hipEventRecord(b->ev_cat[g], st) != hipSuccess) return LEGO_EDEVICE;
   if (hipStreamWaitEvent(b->vs[g], b->ev_cat[g], 0) != hipSuccess) return LEGO_EDEVICE;
   rc = lg_launch_voxel(P, b->B, n, b->vs[g]);
   if (rc) return rc;
-  if (hipEventRecord(b->ev_vox[g], b->vs[g]) != hipSuccess) return LEGO_EDEVICE;
+  if (hipEventRecord(b->ev_vox[g][P.par], b->vs[g]) != hipSuccess) return LEGO_EDEVICE;
   if (b->timing) hipEventRecord(b->ev[5], st);
-  rc = lg_launch_lm(P, b->B, n, st);
+  if (!lag) rc = issue_lm(b, st, s0, n, P.par);
+  else if (b->pend_lm) rc = issue_lm(b, st, s0, n, b->lm_par);
   if (b->timing) hipEventRecord(b->ev[6], st);
   return rc;
 }
 
+// After every slice of a step ran run_association(lag): what is pending now.
+static void advance_pipeline(lego_batch* b, bool lag, int groups) {
+  if (lag) {
+    b->pend_pub = b->pend_lm;  // the LM that ran leaves its publish
+    b->pub_par = b->lm_par;
+    b->pend_lm = true;
+    b->lm_par = b->par;
+  } else {
+    b->pend_pub = true;
+    b->pub_par = b->par;
+    b->pend_lm = false;
+  }
+  b->pend_groups = groups;
+  b->last_par = b->par;
+  b->par ^= 1;
+}
+
 static int ensure_streams(lego_batch* b, int groups) {
   if (!b->fork && hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
+  if (!b->ev_chain && hipEventCreateWithFlags(&b->ev_chain, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   for (int g = 0; g < groups; ++g) {
     if (!b->gs[g] && hipStreamCreateWithFlags(&b->gs[g], hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
     if (!b->join[g] && hipEventCreateWithFlags(&b->join[g], hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
     if (!b->vs[g] && hipStreamCreateWithFlags(&b->vs[g], hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
     if (!b->ev_cat[g] && hipEventCreateWithFlags(&b->ev_cat[g], hipEventDisableTiming) != hipSuccess)
       return LEGO_EDEVICE;
-    if (!b->ev_vox[g] && hipEventCreateWithFlags(&b->ev_vox[g], hipEventDisableTiming) != hipSuccess)
-      return LEGO_EDEVICE;
+    for (int h = 0; h < 2; ++h)
+      if (!b->ev_vox[g][h] && hipEventCreateWithFlags(&b->ev_vox[g][h], hipEventDisableTiming) != hipSuccess)
+        return LEGO_EDEVICE;
   }
   return LEGO_OK;
 }
 
-// Issue the pending k_publish (joined with its k_voxel) on the stream of the step that left it.
+// Work is about to be enqueued on st: if the last call enqueued on another stream, st first waits
+// for all of it (the pending kernels issued on st read what those launches write).
+static int chain_stream(lego_batch* b, hipStream_t st) {
+  if (b->has_last && b->last_stream != st) {
+    if (!b->ev_chain && hipEventCreateWithFlags(&b->ev_chain, hipEventDisableTiming) != hipSuccess)
+      return LEGO_EDEVICE;
+    if (hipEventRecord(b->ev_chain, b->last_stream) != hipSuccess) return LEGO_EDEVICE;
+    if (hipStreamWaitEvent(st, b->ev_chain, 0) != hipSuccess) return LEGO_EDEVICE;
+  }
+  b->last_stream = st;
+  b->has_last = true;
+  return LEGO_OK;
+}
+
+// Issue the pending k_publish / k_lm (each publish joined with its k_voxel) on the stream of the
+// call that left them, in the pending work's slicing.
 static int flush_pending(lego_batch* b) {
-  if (!b->pending) return LEGO_OK;
+  if (!b->pend_pub && !b->pend_lm) return LEGO_OK;
   const int G = b->pend_groups;
+  hipStream_t st = b->last_stream;
   for (int g = 0; g < G; ++g) {
     const int s0 = (int)((long long)b->S * g / G), s1 = (int)((long long)b->S * (g + 1) / G);
-    LgParams P = b->P;
-    P.s0 = s0;
-    hipStream_t st = b->pend_stream;
-    if (hipStreamWaitEvent(st, b->ev_vox[g], 0) != hipSuccess) return LEGO_EDEVICE;
-    int rc = lg_launch_publish(P, b->B, s1 - s0, st);
+    int rc = LEGO_OK;
+    if (b->pend_pub) rc = issue_publish(b, st, g, s0, s1 - s0, b->pub_par);
+    if (!rc && b->pend_lm) rc = issue_lm(b, st, s0, s1 - s0, b->lm_par);
+    if (!rc && b->pend_lm) rc = issue_publish(b, st, g, s0, s1 - s0, b->lm_par);
     if (rc) return rc;
   }
-  b->pending = false;
+  b->pend_pub = b->pend_lm = false;
   return LEGO_OK;
 }
 
@@ -430,11 +483,20 @@ int lego_batch_set_groups(lego_batch* b, int32_t groups) {
   if (!b || groups < 1 || groups > LEGO_MAX_GROUPS) return LEGO_EINVAL;
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   groups = groups > b->S ? b->S : groups;
-  int rc = flush_pending(b);  // the pending publish belongs to the old slicing
+  int rc = flush_pending(b);  // the pending work belongs to the old slicing
   if (rc) return rc;
   rc = ensure_streams(b, groups);
   if (rc) return rc;
   b->groups = groups;
+  return LEGO_OK;
+}
+
+int lego_batch_set_lag(lego_batch* b, int32_t lag) {
+  if (!b || lag < 0 || lag > 1) return LEGO_EINVAL;
+  if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
+  int rc = flush_pending(b);  // the pending work belongs to the old schedule
+  if (rc) return rc;
+  b->lag = lag;
   return LEGO_OK;
 }
 
@@ -444,52 +506,35 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   hipStream_t st = (hipStream_t)hip_stream;
   b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
-  if (b->timing) {  // per-stage events on the caller's stream (one slice): the pipelined path itself
-    int rc = ensure_streams(b, 1);
-    if (rc) return rc;
-    if (b->pending && (b->pend_groups != 1 || b->pend_stream != st)) {
-      rc = flush_pending(b);
-      if (rc) return rc;
-    }
-    b->last_stream = st;
-    hipEventRecord(b->ev[0], st);
-    rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
-    if (!rc) rc = run_association(b, st, 0, b->S, false, true, 0);
-    if (rc) return rc;
-    b->pending = true;
-    b->pend_groups = 1;
-    b->pend_stream = st;
-    b->par ^= 1;
-    return LEGO_OK;
-  }
-  const int G = b->groups;
+  const bool lag = b->lag != 0;
+  // timing: per-stage events on the caller's stream, one slice (the pipelined path itself)
+  const int G = b->timing ? 1 : b->groups;
   int rc = ensure_streams(b, G);
   if (rc) return rc;
-  if (b->pending && (b->pend_groups != G || b->pend_stream != st)) {
+  if ((b->pend_pub || b->pend_lm) && b->pend_groups != G) {
     rc = flush_pending(b);
     if (rc) return rc;
   }
-  b->last_stream = st;
+  rc = chain_stream(b, st);
+  if (rc) return rc;
   if (G <= 1) {
+    if (b->timing) hipEventRecord(b->ev[0], st);
     rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
-    if (!rc) rc = run_association(b, st, 0, b->S, false, true, 0);
+    if (!rc) rc = run_association(b, st, 0, b->S, false, 0, lag);
   } else {
     if (hipEventRecord(b->fork, st) != hipSuccess) return LEGO_EDEVICE;
     for (int g = 0; g < G && !rc; ++g) {
       const int s0 = (int)((long long)b->S * g / G), s1 = (int)((long long)b->S * (g + 1) / G);
       if (hipStreamWaitEvent(b->gs[g], b->fork, 0) != hipSuccess) return LEGO_EDEVICE;
       rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, b->gs[g], s0, s1 - s0);
-      if (!rc) rc = run_association(b, b->gs[g], s0, s1 - s0, false, true, g);
+      if (!rc) rc = run_association(b, b->gs[g], s0, s1 - s0, false, g, lag);
       if (rc) break;
       if (hipEventRecord(b->join[g], b->gs[g]) != hipSuccess) return LEGO_EDEVICE;
       if (hipStreamWaitEvent(st, b->join[g], 0) != hipSuccess) return LEGO_EDEVICE;
     }
   }
   if (rc) return rc;
-  b->pending = true;
-  b->pend_groups = G;
-  b->pend_stream = st;
-  b->par ^= 1;
+  advance_pipeline(b, lag, G);
   return LEGO_OK;
 }
 
@@ -594,12 +639,13 @@ static int read_assoc(lego_batch* b, int s, const ReadHdr* h, hipStream_t st, le
   int rc = LEGO_OK;
   lego_point *sharp, *lsharp, *flat, *lflat, *clast, *slast, *olast;
   int32_t *sharp_ind, *lsharp_ind, *flat_ind;
-  rc |= d2h(b->h_sharp, (const lego_point*)(B.f_sharp + (size_t)s * V * P.cap_sharp), cnt[CNT_SHARP], st, &sharp);
-  rc |= d2h(b->h_sharp_ind, B.f_sharp_ind + (size_t)s * V * P.cap_sharp, cnt[CNT_SHARP], st, &sharp_ind);
-  rc |= d2h(b->h_lsharp, (const lego_point*)(B.f_lsharp + (size_t)s * V * P.cap_lsharp), cnt[CNT_LSHARP], st, &lsharp);
-  rc |= d2h(b->h_lsharp_ind, B.f_lsharp_ind + (size_t)s * V * P.cap_lsharp, cnt[CNT_LSHARP], st, &lsharp_ind);
-  rc |= d2h(b->h_flat, (const lego_point*)(B.f_flat + (size_t)s * V * P.cap_flat), cnt[CNT_FLAT], st, &flat);
-  rc |= d2h(b->h_flat_ind, B.f_flat_ind + (size_t)s * V * P.cap_flat, cnt[CNT_FLAT], st, &flat_ind);
+  const size_t hs = (size_t)b->last_par * b->S + s;  // the feature half of the last scan
+  rc |= d2h(b->h_sharp, (const lego_point*)(B.f_sharp + hs * V * P.cap_sharp), cnt[CNT_SHARP], st, &sharp);
+  rc |= d2h(b->h_sharp_ind, B.f_sharp_ind + hs * V * P.cap_sharp, cnt[CNT_SHARP], st, &sharp_ind);
+  rc |= d2h(b->h_lsharp, (const lego_point*)(B.f_lsharp + hs * V * P.cap_lsharp), cnt[CNT_LSHARP], st, &lsharp);
+  rc |= d2h(b->h_lsharp_ind, B.f_lsharp_ind + hs * V * P.cap_lsharp, cnt[CNT_LSHARP], st, &lsharp_ind);
+  rc |= d2h(b->h_flat, (const lego_point*)(B.f_flat + hs * V * P.cap_flat), cnt[CNT_FLAT], st, &flat);
+  rc |= d2h(b->h_flat_ind, B.f_flat_ind + hs * V * P.cap_flat, cnt[CNT_FLAT], st, &flat_ind);
   rc |= d2h(b->h_lflat, (const lego_point*)(B.f_lflat + s * VH), cnt[CNT_LFLAT], st, &lflat);
   const size_t cls = V * P.cap_lsharp;
   rc |= d2h(b->h_clast, (const lego_point*)(B.corner_last + (size_t)s * 2 * cls + (size_t)S.last_buf * cls),
@@ -748,7 +794,9 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
   if (n > 0 && hipMemcpyAsync(c->d_pts, hp, (size_t)n * sizeof(float4), hipMemcpyHostToDevice, nullptr) != hipSuccess)
     return LEGO_EDEVICE;
   if (hipMemcpyAsync(c->d_cnt, hn, sizeof(int32_t), hipMemcpyHostToDevice, nullptr) != hipSuccess) return LEGO_EDEVICE;
-  int rc = run_projection(b, c->d_pts ? c->d_pts : (const float4*)c->d_off, c->d_off, c->d_cnt, nullptr, 0, 1);
+  int rc = chain_stream(b, nullptr);
+  if (rc) return rc;
+  rc = run_projection(b, c->d_pts ? c->d_pts : (const float4*)c->d_off, c->d_off, c->d_cnt, nullptr, 0, 1);
   if (rc) return rc;
   ReadHdr* h = nullptr;
   rc = read_hdr(b, 0, nullptr, &h);
@@ -762,13 +810,13 @@ static int feature_association(lego_ctx* c, lego_association_out* out, bool dist
   lego_batch* b = c->b;
   hipSetDevice(b->device);
   b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
-  // VoxelGrid on the side stream while k_lm runs, then k_publish (joined with it) before the reads
+  // lag 0, then flushed: VoxelGrid on the side stream while k_lm runs, then k_publish (joined with
+  // it) before the reads
   int rc = ensure_streams(b, 1);
-  if (!rc) rc = run_association(b, nullptr, 0, 1, distort, true, 0);
+  if (!rc) rc = chain_stream(b, nullptr);
+  if (!rc) rc = run_association(b, nullptr, 0, 1, distort, 0, false);
   if (rc) return rc;
-  b->pending = true;
-  b->pend_groups = 1;
-  b->pend_stream = nullptr;
+  advance_pipeline(b, false, 1);
   rc = flush_pending(b);
   if (rc) return rc;
   ReadHdr* h = nullptr;

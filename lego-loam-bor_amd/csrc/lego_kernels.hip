@@ -218,7 +218,23 @@ LG_DEVICE int proj_cell_fast(const LgParams& P, float4 p) {
 // The reference's scatter "later input point overwrites earlier ones in the same cell"
 // (imageProjection.cpp:214-222) is an atomicMax of the input index per cell, followed by a
 // column-parallel gather that writes every cell (so resetParameters' fill is fused in).
-#define PQ_CAP (64 * 9)  // per-wave queue of undecided points (64 + 64 * kU)
+#define PQ_CAP 128  // per-wave queue of undecided points: < 64 before an append of <= 64
+// The exact path for the 64 queued points q[0, 64) (lane l takes q[l]).  Out of line: it runs for
+// ~0.3% of the points, and one copy of the libm restatements serves every call site.
+// (The projection constants go by value: a reference into the kernel arguments would be copied to
+// the stack for the call.)
+__attribute__((noinline)) __device__ void proj_drain(float ang_bottom, float res_x, float res_y, int V, int H,
+                                                     const float4* in, const int* q, int* winner) {
+  LgParams P;
+  P.ang_bottom = ang_bottom;
+  P.ang_res_x = res_x;
+  P.ang_res_y = res_y;
+  P.V = V;
+  P.H = H;
+  const int i = q[lane_id()];
+  const int c = proj_cell_exact(P, in[i]);
+  if (c >= 0) atomicMax(&winner[c], i);
+}
 template <bool kLdsWinner>
 __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                   const int64_t* __restrict__ offs,
@@ -241,15 +257,6 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   // fast path; the few points it cannot decide queue per wave and take the exact path 64 at a time.
   int* queue = smem + 64 + (kLdsWinner ? VH : 0) + wave_id() * PQ_CAP;  // PQ_CAP ints per wave
   int qn = 0;
-  auto drain = [&](int upto) {  // exact path for queue[qn - upto, qn)
-    const int l = lane_id();
-    if (l < upto) {
-      const int i = queue[qn - upto + l];
-      const int c = proj_cell_exact(P, in[i]);
-      if (c >= 0) atomicMax(&winner[c], i);
-    }
-    qn -= upto;
-  };
   constexpr int kU = 8;
   for (int i0 = tid; i0 < n; i0 += nt * kU) {
     float4 pk[kU];
@@ -269,10 +276,16 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
       const unsigned long long amb = __ballot(c == -2);
       if (c == -2) queue[qn + popc_below(amb)] = i;
       qn += __popcll(amb);
+      if (qn >= 64) {  // wave-uniform, rare: the oldest 64 take the exact path
+        proj_drain(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue + qn - 64, winner);
+        qn -= 64;
+      }
     }
-    while (qn >= 64) drain(64);  // qn < 64 + 64 * kU = PQ_CAP before each batch's appends
   }
-  while (qn > 0) drain(min(qn, 64));
+  if (qn > 0) {  // the rest (< 64): lanes past qn repeat entry 0 (the same max, harmless)
+    if (lane_id() >= qn) queue[lane_id()] = queue[0];
+    proj_drain(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue, winner);
+  }
   PROF_ADD(21, t_p1);
   PROF_T(t_p2);
   fmin = block_min_int(fmin, scratch);
@@ -2049,15 +2062,15 @@ __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
   for (int t = lane_id(); t < n; t += 64) L.vval[t] = (uint16_t)t;
   __syncthreads();
   RingOut o;
-  o.lflat = B.r_lflat + rb * P.H;
+  o.lflat = B.r_lflat + sb * P.H;  // output half P.par too (k_publish of this scan reads it)
   o.nLF = 0;
   o.status = 0;
   PROF_T(t_vox0);
   voxel_ring<kMode>(P, v, L, n, 0, o);
   PROF_ADD(4, t_vox0);
   if (lane_id() == 0) {
-    B.r_counts[rb * 4 + 3] = o.nLF;
-    B.r_vstatus[rb] = o.status;
+    B.r_vcount[sb] = o.nLF;
+    B.r_vstatus[sb] = o.status;
   }
 }
 
@@ -2155,7 +2168,7 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
     o.sharp = B.r_sharp + rb * P.cap_sharp; o.sharp_ind = B.r_sharp_ind + rb * P.cap_sharp;
     o.lsharp = B.r_lsharp + rb * P.cap_lsharp; o.lsharp_ind = B.r_lsharp_ind + rb * P.cap_lsharp;
     o.flat = B.r_flat + rb * P.cap_flat; o.flat_ind = B.r_flat_ind + rb * P.cap_flat;
-    o.lflat = B.r_lflat + rb * P.H;
+    o.lflat = nullptr;  // the VoxelGrid output is k_voxel's
     o.nS = o.nLS = o.nF = o.nLF = 0;
     o.status = 0;
     PROF_T(t_ring0);
@@ -2169,7 +2182,7 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
 #endif
     if (lane_id() == 0) {
       int32_t* rc = B.r_counts + rb * 4;
-      rc[0] = o.nS; rc[1] = o.nLS; rc[2] = o.nF;  // rc[3]: k_voxel
+      rc[0] = o.nS; rc[1] = o.nLS; rc[2] = o.nF;  // rc[3] unused
       B.r_status[rb] = o.status;
     }
     __syncthreads();
@@ -2203,22 +2216,26 @@ __global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
     int32_t* cnt = B.counts + (size_t)s * CNT_N;
     cnt[CNT_SHARP] = a[0]; cnt[CNT_LSHARP] = a[1]; cnt[CNT_FLAT] = a[2];
     cnt[CNT_STATUS] = status;
+    int32_t* fc = B.fcnt + ((size_t)P.par * P.S + s) * 4;  // k_lm's copy, half P.par
+    fc[0] = a[0]; fc[1] = a[1]; fc[2] = a[2]; fc[3] = status;
   }
   __syncthreads();
+  // feature clouds into half P.par: k_lm of this scan may run after the next scan's k_concat
+  const size_t hs = (size_t)P.par * P.S + s;
   for (int r = wave_id(); r < V; r += nt >> 6) {  // one wave a ring: ring-ordered concatenation
     const size_t rb = (size_t)s * V + r;
     const int l = lane_id();
     for (int t = l; t < cnt3[0][r]; t += 64) {
-      B.f_sharp[(size_t)s * V * P.cap_sharp + off[0][r] + t] = B.r_sharp[rb * P.cap_sharp + t];
-      B.f_sharp_ind[(size_t)s * V * P.cap_sharp + off[0][r] + t] = B.r_sharp_ind[rb * P.cap_sharp + t];
+      B.f_sharp[hs * V * P.cap_sharp + off[0][r] + t] = B.r_sharp[rb * P.cap_sharp + t];
+      B.f_sharp_ind[hs * V * P.cap_sharp + off[0][r] + t] = B.r_sharp_ind[rb * P.cap_sharp + t];
     }
     for (int t = l; t < cnt3[1][r]; t += 64) {
-      B.f_lsharp[(size_t)s * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp[rb * P.cap_lsharp + t];
-      B.f_lsharp_ind[(size_t)s * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp_ind[rb * P.cap_lsharp + t];
+      B.f_lsharp[hs * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp[rb * P.cap_lsharp + t];
+      B.f_lsharp_ind[hs * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp_ind[rb * P.cap_lsharp + t];
     }
     for (int t = l; t < cnt3[2][r]; t += 64) {
-      B.f_flat[(size_t)s * V * P.cap_flat + off[2][r] + t] = B.r_flat[rb * P.cap_flat + t];
-      B.f_flat_ind[(size_t)s * V * P.cap_flat + off[2][r] + t] = B.r_flat_ind[rb * P.cap_flat + t];
+      B.f_flat[hs * V * P.cap_flat + off[2][r] + t] = B.r_flat[rb * P.cap_flat + t];
+      B.f_flat_ind[hs * V * P.cap_flat + off[2][r] + t] = B.r_flat_ind[rb * P.cap_flat + t];
     }
   }
   // surfPointsLessFlatScan of every ring (:370-374) into staging half P.par, one wave per ring: the
@@ -3380,9 +3397,10 @@ __global__ __launch_bounds__(1024) void k_publish(LgParams P, LgBufs B) {
   __shared__ int off[65], cnt[65], vst[65];
   __shared__ float cur[6];
   __shared__ int copy, nb;
+  const size_t hb = ((size_t)P.par * P.S + s) * V;  // k_voxel's output half of this scan
   if (tid < V) {
-    cnt[tid] = B.r_counts[((size_t)s * V + tid) * 4 + 3];
-    vst[tid] = B.r_vstatus[(size_t)s * V + tid];
+    cnt[tid] = B.r_vcount[hb + tid];
+    vst[tid] = B.r_vstatus[hb + tid];
   }
   if (tid == 64) {
     const LgState& S = B.state[s];
@@ -3403,7 +3421,7 @@ __global__ __launch_bounds__(1024) void k_publish(LgParams P, LgBufs B) {
   float4* sl = B.surf_last + (size_t)s * 2 * VH + (size_t)nb * VH;
   float4* fl = B.f_lflat + (size_t)s * VH;
   for (int r = wave_id(); r < V; r += nt >> 6) {  // one wave a ring
-    const float4* src = B.r_lflat + ((size_t)s * V + r) * P.H;
+    const float4* src = B.r_lflat + (hb + r) * P.H;
     const int n = cnt[r], o = off[r];
     for (int t0 = lane_id(); t0 < n; t0 += 64 * 4) {
       float4 p4[4];
@@ -3436,14 +3454,16 @@ __global__ __launch_bounds__(LM_THREADS) void k_lm(LgParams P, LgBufs B) {
   __shared__ LgState S;
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x;
   const int V = P.V, VH = P.VH;
-  const int32_t* cnt = B.counts + (size_t)s * CNT_N;
-  const int n_sharp = cnt[CNT_SHARP], n_lsharp = cnt[CNT_LSHARP], n_flat = cnt[CNT_FLAT];
-  const float4* f_sharp = B.f_sharp + (size_t)s * V * P.cap_sharp;
-  const float4* f_lsharp = B.f_lsharp + (size_t)s * V * P.cap_lsharp;
-  const float4* f_flat = B.f_flat + (size_t)s * V * P.cap_flat;
+  // the scan's features: half P.par (k_concat), which the next scan's front end does not touch
+  const size_t hs = (size_t)P.par * P.S + s;
+  const int32_t* fc = B.fcnt + hs * 4;
+  const int n_sharp = fc[0], n_lsharp = fc[1], n_flat = fc[2];
+  const float4* f_sharp = B.f_sharp + hs * V * P.cap_sharp;
+  const float4* f_lsharp = B.f_lsharp + hs * V * P.cap_lsharp;
+  const float4* f_flat = B.f_flat + hs * V * P.cap_flat;
   if (tid == 0) {
     S = B.state[s];
-    L.status = cnt[CNT_STATUS];
+    L.status = fc[3];
     for (int k = 0; k < 6; ++k) L.cur[k] = S.cur[k];
   }
   __syncthreads();

@@ -54,6 +54,7 @@ def lib():
         L.lego_batch_stage_times.argtypes = [C.c_void_p, P(C.c_float)]
         L.lego_batch_set_timing.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_groups.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_batch_set_lag.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_read_counts.argtypes = [C.c_void_p, P(C.c_int32)]
         L.lego_test_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int32, C.c_int32]
         L.lego_test_libm.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_int32, C.c_int32]
@@ -158,7 +159,7 @@ class Batch:
         _check(lib().lego_batch_sync(self.h), "lego_batch_sync")
 
     def flush(self):
-        """Enqueue the last step's pending lessFlat publish (asynchronous)."""
+        """Enqueue the pending work of the last steps (LM / lessFlat publish; asynchronous)."""
         _check(lib().lego_batch_flush(self.h), "lego_batch_flush")
 
     def reset(self):
@@ -170,6 +171,10 @@ class Batch:
     def set_groups(self, groups):
         """Launch the streams as `groups` slices on separate HIP streams (overlapping kernel tails)."""
         _check(lib().lego_batch_set_groups(self.h, int(groups)), "lego_batch_set_groups")
+
+    def set_lag(self, lag):
+        """Pipeline depth: 0 = a step runs its own scan's LM, 1 (default) = the previous scan's."""
+        _check(lib().lego_batch_set_lag(self.h, int(lag)), "lego_batch_set_lag")
 
     def counts(self):
         """[S, 7] int32: segmented, outlier, scan_msg, sharp, less sharp, flat, less flat counts."""

@@ -348,6 +348,46 @@ def test_batch_streams_match_oracle(gpu, groups):
     b.close()
 
 
+@pytest.mark.parametrize("groups,lag,alternate", [(1, 1, False), (3, 1, False), (3, 0, False), (2, 1, True),
+                                                  (1, 0, True)])
+def test_batch_back_to_back_matches_oracle(gpu, groups, lag, alternate):
+    """Steps enqueued back to back with one sync at the end: the grouped slices then issue the
+    deferred k_publish / k_lm inside the next step (per group, on its own streams) rather than in a
+    flush.  alternate: consecutive steps go to two different non-blocking streams without any sync
+    in between (each step must order itself after the previous step's work).  The last scan and the
+    accumulated poses equal S independent oracle runs."""
+    import torch
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    S, steps = 6, 6
+    cap = params.num_vertical_scans * params.num_horizontal_scans
+    seqs = np.repeat(np.arange(S)[None, :] + 60, steps, 0).reshape(-1)
+    scans = np.repeat(np.arange(steps)[:, None], S, 1).reshape(-1)
+    pts, cnt = A.synth_batch(cfg, seqs, scans)
+    d_pts = torch.from_numpy(pts).cuda()
+    offs = torch.from_numpy((np.arange(S * steps, dtype=np.int64) * cap).reshape(steps, S)).cuda()
+    cnts = torch.from_numpy(cnt.reshape(steps, S).astype(np.int32)).cuda()
+    torch.cuda.synchronize()
+    b = L.Batch(params, S, cap)
+    b.set_groups(groups)
+    b.set_lag(lag)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()] if alternate else [torch.cuda.current_stream()]
+    for k in range(steps):
+        b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), streams[k % len(streams)].cuda_stream)
+    b.sync()
+    poses, st = b.poses()
+    for s in range(S):
+        orc = oracle_for(params)
+        for k in range(steps):
+            pr = orc.cloud_handler(pts[k * S + s, :cnt[k * S + s]])
+            fr = orc.feature_association()
+        pg, fg = b.read(s)
+        assert_scan_parity(steps - 1, pg, pr, fg, fr)
+        np.testing.assert_allclose(poses[s, 6:], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
+        np.testing.assert_allclose(poses[s, :6], fr["transform_cur"], atol=Hs.TF_TOL, rtol=0)
+    b.close()
+
+
 def test_edge_inputs(gpu):
     """Empty / all-NaN clouds fail like the oracle; sparse, tiny, colliding and out-of-FOV clouds match."""
     params = L.params_vlp16()
