@@ -3227,7 +3227,8 @@ LG_DEVICE void lm_loop(const LgParams& P, LmLds& L, LgState& S, const float4* __
       PROF_T(t_srch0);
       PROF_T(t_nn0);
       int st = 0;
-      // as many lanes per query as the block allows (surf ~170 queries: 2; corner ~115: 4)
+      // as many lanes per query as the 768-thread block allows: 8 up to 96 queries, 4 up to 192
+      // (surf ~170 and corner ~115 queries both get 4), 2 up to 384
       const int tpq = nq * 8 <= LM_THREADS ? 8 : nq * 4 <= LM_THREADS ? 4 : nq * 2 <= LM_THREADS ? 2 : 1;
       if (tid == 0) L.nfall = 0;
       for (int base = 0; base < nq * tpq; base += LM_THREADS) {

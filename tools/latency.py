@@ -2,7 +2,7 @@
 single-context drop-in, lego_cloud_handler + lego_feature_association with host buffers in and out,
 i.e. what a rosbag replay through the C-ABI sees.
 
-  python tools/latency.py [--scans 60] [--warmup 5]
+  python tools/latency.py [--scans 60] [--warmup 5] [--voxel-order 0|1]
 
 Prints one JSON line: mean / median / p99 per-scan latency (ms) and the resulting scans/s.
 """
@@ -26,8 +26,10 @@ def main():
     ap.add_argument("--scans", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seq", type=int, default=5)
+    ap.add_argument("--voxel-order", type=int, default=0, choices=(0, 1),
+                    help="0 = libstdc++ introsort tie order (reference-exact), 1 = stable order")
     args = ap.parse_args()
-    params = L.params_vlp16(voxel_tie_order=1)
+    params = L.params_vlp16(voxel_tie_order=args.voxel_order)
     cfg = A.synth_cfg("vlp16")
     n = args.warmup + args.scans
     scans = [np.ascontiguousarray(A.synth_scan(cfg, args.seq, k), dtype=np.float32) for k in range(n)]
@@ -49,7 +51,7 @@ def main():
     tot = np.array(t_ih) + np.array(t_fa)
     fe.close()
     print(json.dumps({"mode": "one scan in flight (single-context C-ABI, host buffers in/out)",
-                      "scans": args.scans, "cloud_handler_ms": round(1e3 * float(np.mean(t_ih)), 3),
+                      "scans": args.scans, "voxel_tie_order": args.voxel_order, "cloud_handler_ms": round(1e3 * float(np.mean(t_ih)), 3),
                       "feature_association_ms": round(1e3 * float(np.mean(t_fa)), 3),
                       "scan_ms_mean": round(1e3 * float(tot.mean()), 3),
                       "scan_ms_median": round(1e3 * float(np.median(tot)), 3),
