@@ -951,22 +951,26 @@ __global__ __launch_bounds__(1024) void k_segment_global(LgParams P, LgBufs B) {
 // ============================================================================================
 // k_fa_prep: adjustDistortion + calculateSmoothness + markOccludedPoints + adjustOutlierCloud
 // ============================================================================================
-// calculateSmoothness + markOccludedPoints, one 1024-lane workgroup per scan, on LDS tiles of
-// FP_TILE positions whose range / column loads are issued together.  markOccludedPoints'
+// calculateSmoothness + markOccludedPoints on LDS tiles of FP_TILE positions (+ halo) whose range /
+// column loads are issued together.  markOccludedPoints'
 // scattered OR-writes (:237-259) are evaluated in gather form, picked[k] = OR of the marks that land
 // on k, which equals the reference's "zero [5, M-5) then OR the marks" for every k (positions
 // outside [5, M-5) keep their stale value OR the marks, as there).  adjustDistortion and
 // adjustOutlierCloud run in k_segment's epilogue, on the cloud it has just compacted; kDistort
 // runs them here instead, for a ProjectionOut uploaded from the host (lego_feature_association_from).
-#define FP_TILE (1024 * FP_U)
+// kNT threads a workgroup, FP_TILE = kNT * FP_U positions a tile.  The device-resident path
+// (!kDistort) runs one tile per workgroup, grid (scans, tiles of V*H): ~8 workgroups a scan keep
+// enough loads in flight to stream at HBM rate; kDistort (whole-scan block minimum) loops over the
+// tiles of its scan in one workgroup.
 #define FP_HALO 8
-template <bool kDistort>
-__global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
+template <bool kDistort, int kNT>
+__global__ __launch_bounds__(kNT) void k_fa_prep(LgParams P, LgBufs B) {
+  constexpr int FP_TILE = kNT * FP_U;
   __shared__ int scratch[64];
   __shared__ float sr[FP_TILE + 2 * FP_HALO];     // segmentedCloudRange[t0 - FP_HALO + x]
   __shared__ uint32_t sc[FP_TILE + 2 * FP_HALO];  // segmentedCloudColInd
   __shared__ uint8_t sf[FP_TILE + 2 * FP_HALO];   // marks of i: bit0 A (i-5..i), bit1 B (i+1..i+6), bit2 C (i)
-  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = kNT;
   const int VH = P.VH;
   const int32_t* cnt = B.counts + (size_t)s * CNT_N;
   const int M = cnt[CNT_M];
@@ -977,7 +981,7 @@ __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
   int8_t* __restrict__ flabel = B.flabel + (size_t)s * VH;
   int2* __restrict__ smooth = B.smooth + (size_t)s * VH;
   // k_extract's first pass may move the stale slot 4 while other rings check where it points
-  if (tid == 0) B.fp_sync[2 * s] = smooth[4].y;
+  if (tid == 0 && blockIdx.y == 0) B.fp_sync[2 * s] = smooth[4].y;
   if constexpr (kDistort) {
     distort_segmented(P, B, s, M, scratch);
     const int nout = cnt[CNT_OUTLIER];
@@ -990,7 +994,8 @@ __global__ __launch_bounds__(1024) void k_fa_prep(LgParams P, LgBufs B) {
     }
   }
   const int nTiles = (M + FP_TILE - 1) / FP_TILE;
-  for (int tile = 0; tile < nTiles; ++tile) {
+  const int tile_lo = kDistort ? 0 : (int)blockIdx.y, tile_hi = kDistort ? nTiles : min((int)blockIdx.y + 1, nTiles);
+  for (int tile = tile_lo; tile < tile_hi; ++tile) {
     const int t0 = tile * FP_TILE;
     PROF_T(t_f1);
     {  // range / column of positions [t0 - FP_HALO, t0 + FP_TILE + FP_HALO) into LDS, one batch
@@ -3605,8 +3610,12 @@ int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
 }
 
 int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st, bool distort) {
-  if (distort) hipLaunchKernelGGL(k_fa_prep<true>, dim3(S), dim3(1024), 0, st, P, B);
-  else hipLaunchKernelGGL(k_fa_prep<false>, dim3(S), dim3(1024), 0, st, P, B);
+  if (distort) {
+    hipLaunchKernelGGL((k_fa_prep<true, 1024>), dim3(S), dim3(1024), 0, st, P, B);
+  } else {
+    const int tiles = (P.VH + 256 * FP_U - 1) / (256 * FP_U);
+    hipLaunchKernelGGL((k_fa_prep<false, 256>), dim3(S, tiles), dim3(256), 0, st, P, B);
+  }
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
