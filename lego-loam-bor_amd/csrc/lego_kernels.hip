@@ -69,6 +69,11 @@ LG_DEVICE float4 buffer_load_f4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
   return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
 }
+LG_DEVICE float3 buffer_load_f3(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  typedef int i32x3 __attribute__((ext_vector_type(3)));
+  const i32x3 v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)off, 0, 0);
+  return make_float3(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z));
+}
 LG_DEVICE float buffer_load_f1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __int_as_float((int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
@@ -205,11 +210,28 @@ LG_DEVICE int proj_cell_fast(const LgParams& P, float4 p) {
   const float q = (h - 1.57079637f) * P.inv_res_x;
   const float fq = floorf(q), fr = q - fq;
   if (fabsf(fr - 0.5f) < 4e-3f) return -2;
-  const double k = (double)fq + (fr > 0.5f ? 1.0 : 0.0);  // round(q), q not near a half
-  int columnIdn = (int)(-k + P.H * 0.5);
+  const int k = (int)fq + (fr > 0.5f ? 1 : 0);  // round(q), q not near a half
+  // (int)(-k + H * 0.5) in double: the real (H - 2k) / 2 truncated toward zero, as C++ int division
+  int columnIdn = (P.H - 2 * k) / 2;
   if (columnIdn >= P.H) columnIdn -= P.H;
   if (columnIdn < 0 || columnIdn >= P.H) return -1;
   return r0 * P.H + columnIdn;
+}
+
+// groundRemoval's test (imageProjection.cpp:276-285): (double)(atan2f(dZ, r) - mount) <= 10 deg, r =
+// |(dX, dY, dZ)| >= |dZ|, so the angle lies in [-pi/4, pi/4].  A polynomial atan (error < 1e-6 rad
+// with the reciprocal) decides every pair farther than 1e-5 rad from the threshold; the rest, and
+// r == 0 or NaN (empty cells), take the glibc-faithful atan2f.
+LG_DEVICE bool ground_pair(float dZ, float r, float mount) {
+  const double thr = 10 * DEG_TO_RAD_D;
+  if (r > 0.f && r < FLT_MAX) {
+    float h = atan01_poly(fminf(fabsf(dZ) * __builtin_amdgcn_rcpf(r), 1.f));
+    const float d = (dZ < 0.f ? -h : h) - mount;
+    if (d < (float)thr - 1e-5f) return true;
+    if (d > (float)thr + 1e-5f) return false;
+  }
+  const float va = atan2f_g(dZ, r);
+  return (double)(va - mount) <= thr;
 }
 
 // ============================================================================================
@@ -252,20 +274,25 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   PROF_ADD(20, t_p0);
   PROF_T(t_p1);
   int fmin = 0x7fffffff, fmax = -1;
-  // kU point loads per lane are issued before any of them is used: the loads are unconditional
-  // (index clamped to n - 1), so no per-load branch forces a wait between them.  Cells come from the
-  // fast path; the few points it cannot decide queue per wave and take the exact path 64 at a time.
+  // The points' x, y, z (12-byte buffer loads; the input intensity is not used) in batches of kU per
+  // lane, the next batch's loads issued before the current batch is processed.  Lanes past n load
+  // nothing (buffer range check).  Cells come from the fast path; the few points it cannot decide
+  // queue per wave and take the exact path 64 at a time.
   int* queue = smem + 64 + (kLdsWinner ? VH : 0) + wave_id() * PQ_CAP;  // PQ_CAP ints per wave
   int qn = 0;
   constexpr int kU = 8;
-  for (int i0 = tid; i0 < n; i0 += nt * kU) {
-    float4 pk[kU];
+  const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
+  float3 pk[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) pk[u] = in[min(i0 + u * nt, n - 1)];
+  for (int u = 0; u < kU; ++u) pk[u] = buffer_load_f3(rin, (uint32_t)(tid + u * nt) * 16u);
+  for (int i0 = tid; i0 < n; i0 += nt * kU) {
+    float3 nx[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) nx[u] = buffer_load_f3(rin, (uint32_t)(i0 + (kU + u) * nt) * 16u);
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int i = i0 + u * nt;
-      const float4 p = pk[u];
+      const float4 p = make_float4(pk[u].x, pk[u].y, pk[u].z, 0.f);
       int c = -1;
       if (i < n && isfinite_f(p.x) && isfinite_f(p.y) && isfinite_f(p.z)) {  // removeNaNFromPointCloud
         fmin = min(fmin, i);
@@ -281,6 +308,8 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
         qn -= 64;
       }
     }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) pk[u] = nx[u];
   }
   if (qn > 0) {  // the rest (< 64): lanes past qn repeat entry 0 (the same max, harmless)
     if (lane_id() >= qn) queue[lane_id()] = queue[0];
@@ -288,23 +317,13 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   }
   PROF_ADD(21, t_p1);
   PROF_T(t_p2);
-  fmin = block_min_int(fmin, scratch);
-  fmax = block_max_int(fmax, scratch);
-  if (tid == 0) {
-    float so = 0.f, eo = 0.f, od = 0.f;
-    if (fmax >= 0) {  // findStartEndAngle (:234-249)
-      float4 a = in[fmin], b = in[fmax];
-      so = -atan2f_g(a.y, a.x);
-      eo = (float)(-(double)atan2f_g(b.y, b.x) + 2 * M_PI);
-      if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
-      else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
-      od = eo - so;
-    }
-    B.orient[s * 4 + 0] = so;
-    B.orient[s * 4 + 1] = eo;
-    B.orient[s * 4 + 2] = od;
-    B.orient[s * 4 + 3] = (float)(fmax >= 0);
-    B.state[s].proj_status = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
+  // first / last finite point: per-wave results now, combined by thread 0 after the column pass
+  // (findStartEndAngle's result is not needed before then; no extra barrier)
+  fmin = wave_min(fmin);
+  fmax = wave_max(fmax);
+  if (lane_id() == 0) {
+    scratch[wave_id()] = fmin;
+    scratch[32 + wave_id()] = fmax;
   }
   __syncthreads();
   PROF_ADD(22, t_p2);
@@ -360,8 +379,7 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
         cloud[c] = q;
         if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
           const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
-          const float va = atan2f_g(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ));
-          if ((double)(va - P.mount) <= 10 * DEG_TO_RAD_D) gmask |= (3ull << (i - 1));
+          if (ground_pair(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ), P.mount)) gmask |= (3ull << (i - 1));
         }
         if (i >= 1) scan(i - 1, prev_r, prev.z);
         prev = q;
@@ -372,6 +390,26 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
     B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
   }
   PROF_ADD(23, t_p3);
+  if (tid == 0) {  // findStartEndAngle (:234-249)
+    for (int w = 1; w < (nt >> 6); ++w) {
+      fmin = min(fmin, scratch[w]);
+      fmax = max(fmax, scratch[32 + w]);
+    }
+    float so = 0.f, eo = 0.f, od = 0.f;
+    if (fmax >= 0) {
+      float4 a = in[fmin], b = in[fmax];
+      so = -atan2f_g(a.y, a.x);
+      eo = (float)(-(double)atan2f_g(b.y, b.x) + 2 * M_PI);
+      if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
+      else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
+      od = eo - so;
+    }
+    B.orient[s * 4 + 0] = so;
+    B.orient[s * 4 + 1] = eo;
+    B.orient[s * 4 + 2] = od;
+    B.orient[s * 4 + 3] = (float)(fmax >= 0);
+    B.state[s].proj_status = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
+  }
 }
 
 // ============================================================================================
@@ -3675,7 +3713,9 @@ __global__ void k_libm_test(const float* a, const float* b, float* out, int n, i
   else if (which == 1) r = atan2f_g(a[i], b[i]);
   else if (which == 2) r = atanf_g(a[i]);
   else if (which == 3) r = sqrtf(a[i]);
-  else r = a[i] / b[i];
+  else if (which == 4) r = a[i] / b[i];
+  else if (which == 5) r = ground_pair(a[i], b[i], 0.f) ? 1.f : 0.f;                       // fast + exact
+  else r = (double)atan2f_g(a[i], b[i]) <= 10 * DEG_TO_RAD_D ? 1.f : 0.f;                  // exact only
   out[i] = r;
 }
 

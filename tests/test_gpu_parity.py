@@ -89,6 +89,33 @@ def test_device_libm_matches_glibc(gpu):
     assert Hs.bits_equal(q, xy[0] / xy[1])  # numpy float32 division is IEEE
 
 
+def test_fast_ground_pair_decides_like_the_exact_path(gpu):
+    """groundRemoval's pair test (imageProjection.cpp:276-285) as k_project decides it (polynomial
+    atan with a margin) equals the glibc-faithful decision: random pairs, pairs within 1e-6 rad of the
+    10-degree threshold, identical points (r = 0) and empty cells (NaN)."""
+    rng = np.random.default_rng(5)
+    n = 1 << 20
+    thr = np.deg2rad(10.0)
+    ang = np.concatenate([rng.uniform(-np.pi / 4, np.pi / 4, n // 2),
+                          thr + rng.uniform(-1e-6, 1e-6, n // 2)])
+    r = rng.uniform(1e-3, 50.0, n)
+    dz = (r * np.sin(ang)).astype(np.float32)
+    rr = r.astype(np.float32)
+    dz[:64] = 0.0
+    rr[:64] = 0.0
+    dz[64:128] = np.nan
+    rr[64:128] = np.nan
+    fp = C.POINTER(C.c_float)
+    out = {}
+    for which in (5, 6):
+        o = np.zeros(n, dtype=np.float32)
+        assert L.lib().lego_test_libm(dz.ctypes.data_as(fp), rr.ctypes.data_as(fp), o.ctypes.data_as(fp), n,
+                                      which) == 0
+        out[which] = o
+    assert np.array_equal(out[5], out[6])
+    assert 0.2 < out[5].mean() < 0.9
+
+
 @pytest.mark.parametrize("kind", ["vlp16", "hdl64"])
 def test_fast_projection_decides_like_the_exact_path(gpu, kind):
     """k_project's fast path (rsqrt/polynomial asin and atan2 with decision margins) never disagrees
