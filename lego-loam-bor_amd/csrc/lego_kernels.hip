@@ -222,6 +222,10 @@ LG_DEVICE int proj_cell_fast(const LgParams& P, float4 p) {
 // |(dX, dY, dZ)| >= |dZ|, so the angle lies in [-pi/4, pi/4].  A polynomial atan (error < 1e-6 rad
 // with the reciprocal) decides every pair farther than 1e-5 rad from the threshold; the rest, and
 // r == 0 or NaN (empty cells), take the glibc-faithful atan2f.
+__attribute__((noinline)) __device__ bool ground_pair_exact(float dZ, float r, float mount) {  // one copy
+  const float va = atan2f_g(dZ, r);
+  return (double)(va - mount) <= 10 * DEG_TO_RAD_D;
+}
 LG_DEVICE bool ground_pair(float dZ, float r, float mount) {
   const double thr = 10 * DEG_TO_RAD_D;
   if (r > 0.f && r < FLT_MAX) {
@@ -230,8 +234,7 @@ LG_DEVICE bool ground_pair(float dZ, float r, float mount) {
     if (d < (float)thr - 1e-5f) return true;
     if (d > (float)thr + 1e-5f) return false;
   }
-  const float va = atan2f_g(dZ, r);
-  return (double)(va - mount) <= thr;
+  return ground_pair_exact(dZ, r, mount);
 }
 
 // ============================================================================================
@@ -245,6 +248,16 @@ LG_DEVICE bool ground_pair(float dZ, float r, float mount) {
 // ~0.3% of the points, and one copy of the libm restatements serves every call site.
 // (The projection constants go by value: a reference into the kernel arguments would be copied to
 // the stack for the call.)
+__attribute__((noinline)) __device__ int proj_cell_exact_ni(float ang_bottom, float res_x, float res_y, int V, int H,
+                                                          float4 p) {  // one out-of-line copy
+  LgParams P;
+  P.ang_bottom = ang_bottom;
+  P.ang_res_x = res_x;
+  P.ang_res_y = res_y;
+  P.V = V;
+  P.H = H;
+  return proj_cell_exact(P, p);
+}
 __attribute__((noinline)) __device__ void proj_drain(float ang_bottom, float res_x, float res_y, int V, int H,
                                                      const float4* in, const int* q, int* winner) {
   LgParams P;
@@ -297,7 +310,7 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
       if (i < n && isfinite_f(p.x) && isfinite_f(p.y) && isfinite_f(p.z)) {  // removeNaNFromPointCloud
         fmin = min(fmin, i);
         fmax = max(fmax, i);
-        c = P.fast_proj ? proj_cell_fast(P, p) : proj_cell_exact(P, p);
+        c = P.fast_proj ? proj_cell_fast(P, p) : proj_cell_exact_ni(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, p);
         if (c >= 0) atomicMax(&winner[c], i);
       }
       const unsigned long long amb = __ballot(c == -2);
