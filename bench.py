@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (test rehearsal)")
     ap.add_argument("--groups", type=int, default=1, help="stream slices launched on separate HIP streams")
+    ap.add_argument("--wide", type=int, default=-1, choices=[-1, 0, 1],
+                    help="projection / segmentation layout (lego_batch_set_wide): -1 automatic")
     ap.add_argument("--lag", type=int, default=1, choices=[0, 1],
                     help="pipeline depth (lego_batch_set_lag): 1 = a step runs the previous scan's LM")
     ap.add_argument("--voxel-tie-order", type=int, default=1, choices=[0, 1],
@@ -145,6 +147,7 @@ def main():
     batch = L.Batch(params, S, cap, device=local_dev)
     batch.set_groups(args.groups)
     batch.set_lag(args.lag)
+    batch.set_wide(args.wide)
     stream = torch.cuda.current_stream(dev)
 
     def step(k, b=None):
@@ -195,6 +198,7 @@ def main():
         batch_alt = L.Batch(params_alt, S, cap, device=local_dev)
         batch_alt.set_groups(args.groups)
         batch_alt.set_lag(args.lag)
+        batch_alt.set_wide(args.wide)
         el_alt = timed(batch_alt)
         batch_alt.close()
         alt = {"voxel_tie_order": alt_order, "value": round(total_scans / el_alt, 1),
@@ -238,11 +242,11 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K, "warmup": W,
         "ms_per_step": round(1e3 * elapsed / K, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "C3: batched synthetic %s sweeps, %d independent sequences per GPU x 1 scan per step"
-                               % (args.kind.upper(), S),
+        "config": {"workload": "%s: batched synthetic %s sweeps, %d independent sequences per GPU x 1 scan per step"
+                               % ("C3" if args.kind == "vlp16" else "C4", args.kind.upper(), S),
                    "V": V, "H": H, "points_per_scan": round(n_mean, 1), "streams_per_gpu": S,
                    "parallelism": "sequence-sharded x%d" % world, "stream_groups": args.groups, "lag": args.lag,
-                   "voxel_tie_order": args.voxel_tie_order},
+                   "voxel_tie_order": args.voxel_tie_order, "wide": int(batch.wide())},
         "roofline": roofline,
         "stages_ms": {"project": round(stage[0], 4), "segment": round(stage[1], 4), "fa_prep": round(stage[2], 4),
                       "extract": round(stage[3], 4), "concat_publish": round(stage[4], 4),

@@ -198,6 +198,14 @@ int  lego_batch_set_groups(lego_batch* b, int32_t groups);
 /* Pipeline depth of lego_batch_step: 0 = a step runs its own scan's LM, 1 (default) = the previous
  * scan's (see lego_batch_step).  Results do not depend on it. */
 int  lego_batch_set_lag(lego_batch* b, int32_t lag);
+/* Kernel layout of the projection and segmentation: 1 = wide (a scan's work over many workgroups,
+ * per-scan images in HBM), 0 = one workgroup a scan with its images in LDS (only where they fit:
+ * V <= 16, V*H < 32768; else LEGO_EINVAL), -1 (default) = automatic: wide where the images do not
+ * fit LDS or where fewer than (compute units / 8) streams are in flight.  Results do not depend on
+ * it. */
+int  lego_batch_set_wide(lego_batch* b, int32_t mode);
+/* The layout in effect (1 wide, 0 one workgroup a scan), or LEGO_EINVAL. */
+int  lego_batch_wide(const lego_batch* b);
 
 /* ---- test hooks ------------------------------------------------------------------ */
 /* Evaluate the device libm restatement on host arrays: which = 0 asinf(a), 1 atan2f(a, b),

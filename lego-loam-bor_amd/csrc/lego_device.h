@@ -38,6 +38,8 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int par;                              // parity of the launch's scan: the half of the double-buffered
                                         // staging (features, lessFlat, VoxelGrid output) it uses
   int S;                                // streams of the batch (staging stride)
+  int wide;                             // wide mode: k_pw_* / k_sw_* (many workgroups a scan)
+  int max_points;                       // input capacity per scan (wide scatter grid)
 };
 
 struct LgState {  // FeatureAssociation members that persist across scans (featureAssociation.h)
@@ -69,10 +71,12 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   float4* cloud;         // [S][VH]  _full_cloud
   int8_t* ground;        // [S][VH]
   int32_t* label;        // [S][VH]
-  int32_t* winner;       // [S][VH]  (global-winner path only)
-  int32_t* cc_parent;    // [S][VH]  (global union-find path only)
-  int32_t* cc_cnt;       // [S][VH]
-  unsigned long long* cc_mask;  // [S][VH]
+  int32_t* winner;       // [S][VH]  wide mode: "later point wins" image, -1 between launches
+  int32_t* proj_mm;      // [S][2]   wide mode: first / last finite input point
+  int32_t* cc_parent;    // [S][VH]  wide mode: union-find parent (or -1: not eligible)
+  int32_t* cc_cnt;       // [S][VH]  component size of a root, then its label
+  unsigned long long* cc_mask;  // [S][VH]  rows of a root's non-seed members
+  int4* seg_tiles;       // [S][tiles] wide mode: per tile feasible roots, segmented cells, outliers
   int32_t* scan_cand;    // [S][H]
   float* orient;         // [S][4]
   float4* seg_pts;       // [S][VH]

@@ -122,9 +122,20 @@ int lg_derive_params(const lego_params& p, LgParams* out) {  // test hooks (lego
   return LEGO_OK;
 }
 
+bool lg_lds_projection(const LgParams& P);  // lego_kernels.hip
+bool lg_lds_segment(const LgParams& P);
+
+// Wide mode (k_pw_* / k_sw_*: a scan's projection and segmentation over many workgroups) where one
+// workgroup a scan cannot hold the images in LDS, and where too few scans are in flight to fill
+// the device with one workgroup each.
+static int lg_wide_auto(const LgParams& P, int S) {
+  return (!lg_lds_projection(P) || !lg_lds_segment(P) || S * 8 <= P.ncu) ? 1 : 0;
+}
+
 struct lego_batch {
   lego_params params;
   LgParams P;
+  int wide_req = -1;  // lego_batch_set_wide: -1 auto, 0 / 1 forced
   LgBufs B;
   int S = 0;
   int max_points = 0;
@@ -279,13 +290,15 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   memset(&B, 0, sizeof(B));
   const size_t S = n_streams, VH = P.VH, V = P.V, H = P.H;
   std::vector<void*>& o = b->owned;
-  bool lds_proj = (size_t)(P.VH + 64) * 4 <= 160 * 1024;
-  bool lds_seg = P.V <= 16 && P.VH < 32768;  // lg_lds_segment
+  b->P.max_points = max_points;
+  b->wide_req = -1;
+  b->P.wide = lg_wide_auto(P, n_streams);
+  const size_t tiles = (VH + 1023) / 1024;  // SW_TILE
   rc = LEGO_OK;
 #define A(ptr, n) if (rc == LEGO_OK) rc = dalloc(&B.ptr, (n), o)
   A(range, S * VH); A(cloud, S * VH); A(ground, S * VH); A(label, S * VH);
-  A(winner, lds_proj ? 1 : S * VH);
-  A(cc_parent, lds_seg ? 1 : S * VH); A(cc_cnt, lds_seg ? 1 : S * VH); A(cc_mask, lds_seg ? 1 : S * VH);
+  A(winner, S * VH); A(proj_mm, S * 2); A(seg_tiles, S * tiles);
+  A(cc_parent, S * VH); A(cc_cnt, S * VH); A(cc_mask, S * VH);
   A(scan_cand, S * H); A(orient, S * 4);
   A(seg_pts, S * VH); A(seg_range, S * VH); A(seg_col, S * VH); A(seg_ground, S * VH);
   A(ring_start, S * V); A(ring_end, S * V); A(outlier, S * VH); A(scan_msg, S * H); A(counts, S * CNT_N);
@@ -337,6 +350,15 @@ int lego_batch_reset(lego_batch* b) {
   b->par = b->last_par = 0;
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.counts, 0, S * CNT_N * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
+  // wide mode's per-scan scratch starts (and is left by every launch) reset: winner -1, first point
+  // INT_MAX, last point -1
+  if (hipMemset(B.winner, 0xff, S * VH * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
+  {
+    std::vector<int32_t> mm(2 * S);
+    for (size_t s = 0; s < S; ++s) { mm[2 * s] = 0x7fffffff; mm[2 * s + 1] = -1; }
+    if (hipMemcpy(B.proj_mm, mm.data(), mm.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
+      return LEGO_EDEVICE;
+  }
   if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
   return LEGO_OK;
 }
@@ -499,6 +521,17 @@ int lego_batch_set_lag(lego_batch* b, int32_t lag) {
   b->lag = lag;
   return LEGO_OK;
 }
+
+int lego_batch_set_wide(lego_batch* b, int32_t mode) {
+  if (!b || mode < -1 || mode > 1) return LEGO_EINVAL;
+  if (mode == 0 && (!lg_lds_projection(b->P) || !lg_lds_segment(b->P))) return LEGO_EINVAL;
+  // both layouts keep the persistent state alike and leave their scratch reset: switchable at any step
+  b->wide_req = mode;
+  b->P.wide = mode < 0 ? lg_wide_auto(b->P, b->S) : mode;
+  return LEGO_OK;
+}
+
+int lego_batch_wide(const lego_batch* b) { return b ? b->P.wide : LEGO_EINVAL; }
 
 int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_offsets, const int32_t* d_counts,
                     void* hip_stream) {

@@ -78,6 +78,10 @@ LG_DEVICE float buffer_load_f1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __int_as_float((int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
 
+LG_DEVICE unsigned long long shfl64(unsigned long long v, int l) {
+  return ((unsigned long long)(unsigned)__shfl((int)(v >> 32), l) << 32) | (unsigned)__shfl((int)(unsigned)v, l);
+}
+
 template <typename T>
 LG_DEVICE T wave_min(T v) {
   for (int o = 32; o > 0; o >>= 1) {
@@ -186,6 +190,7 @@ LG_DEVICE float atan01_poly(float a) {
 // boundary), the range test from |p|^2 against [0.0099, 0.0101].  Returns the cell, -1 (rejected) or
 // -2: too close to a decision boundary to tell, the exact path decides.  The margins hold for
 // ang_res_y >= 0.1 deg and ang_res_x >= 0.1 deg (lg_fast_projection checks them).
+template <bool kColMajor = false>
 LG_DEVICE int proj_cell_fast(const LgParams& P, float4 p) {
   const float d2 = p.x * p.x + p.y * p.y + p.z * p.z;
   if (!(d2 > 0.0101f)) return d2 < 0.0099f ? -1 : -2;
@@ -215,7 +220,7 @@ LG_DEVICE int proj_cell_fast(const LgParams& P, float4 p) {
   int columnIdn = (P.H - 2 * k) / 2;
   if (columnIdn >= P.H) columnIdn -= P.H;
   if (columnIdn < 0 || columnIdn >= P.H) return -1;
-  return r0 * P.H + columnIdn;
+  return kColMajor ? columnIdn * P.V + r0 : r0 * P.H + columnIdn;
 }
 
 // groundRemoval's test (imageProjection.cpp:276-285): (double)(atan2f(dZ, r) - mount) <= 10 deg, r =
@@ -258,6 +263,24 @@ __attribute__((noinline)) __device__ int proj_cell_exact_ni(float ang_bottom, fl
   P.H = H;
   return proj_cell_exact(P, p);
 }
+// cell (row-major, or -1) -> column-major index j * V + i (wide mode's winner image)
+LG_DEVICE int cell_cm(int c, int V, int H) {
+  if (c < 0) return c;
+  const int i = c / H;
+  return (c - i * H) * V + i;
+}
+__attribute__((noinline)) __device__ void proj_drain_cm(float ang_bottom, float res_x, float res_y, int V, int H,
+                                                        const float4* in, const int* q, int* winner) {
+  LgParams P;
+  P.ang_bottom = ang_bottom;
+  P.ang_res_x = res_x;
+  P.ang_res_y = res_y;
+  P.V = V;
+  P.H = H;
+  const int i = q[lane_id()];
+  const int c = cell_cm(proj_cell_exact(P, in[i]), V, H);
+  if (c >= 0) atomicMax(&winner[c], i);
+}
 __attribute__((noinline)) __device__ void proj_drain(float ang_bottom, float res_x, float res_y, int V, int H,
                                                      const float4* in, const int* q, int* winner) {
   LgParams P;
@@ -270,7 +293,6 @@ __attribute__((noinline)) __device__ void proj_drain(float ang_bottom, float res
   const int c = proj_cell_exact(P, in[i]);
   if (c >= 0) atomicMax(&winner[c], i);
 }
-template <bool kLdsWinner>
 __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                   const int64_t* __restrict__ offs,
                                                   const int32_t* __restrict__ cnts) {
@@ -278,7 +300,7 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, H = P.H, VH = P.VH;
   int* scratch = smem;                 // 64 ints
-  int* winner = kLdsWinner ? (smem + 64) : (B.winner + (size_t)s * VH);
+  int* winner = smem + 64;  // LDS image: V*H ints
   const float4* in = pts + offs[s];
   const int n = cnts[s];
   PROF_T(t_p0);
@@ -291,7 +313,7 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   // lane, the next batch's loads issued before the current batch is processed.  Lanes past n load
   // nothing (buffer range check).  Cells come from the fast path; the few points it cannot decide
   // queue per wave and take the exact path 64 at a time.
-  int* queue = smem + 64 + (kLdsWinner ? VH : 0) + wave_id() * PQ_CAP;  // PQ_CAP ints per wave
+  int* queue = smem + 64 + VH + wave_id() * PQ_CAP;  // PQ_CAP ints per wave
   int qn = 0;
   constexpr int kU = 8;
   const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
@@ -408,6 +430,190 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
       fmin = min(fmin, scratch[w]);
       fmax = max(fmax, scratch[32 + w]);
     }
+    float so = 0.f, eo = 0.f, od = 0.f;
+    if (fmax >= 0) {
+      float4 a = in[fmin], b = in[fmax];
+      so = -atan2f_g(a.y, a.x);
+      eo = (float)(-(double)atan2f_g(b.y, b.x) + 2 * M_PI);
+      if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
+      else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
+      od = eo - so;
+    }
+    B.orient[s * 4 + 0] = so;
+    B.orient[s * 4 + 1] = eo;
+    B.orient[s * 4 + 2] = od;
+    B.orient[s * 4 + 3] = (float)(fmax >= 0);
+    B.state[s].proj_status = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
+  }
+}
+
+// ============================================================================================
+// Wide mode (large images: HDL-64E's 64 x 2048; few scans in flight): each scan's projection and
+// segmentation spread over many workgroups instead of one, with the per-scan state in HBM.
+// ============================================================================================
+// k_pw_scatter: grid (point chunks of PW_PTS, scans).  "Later point wins" is a device-scope
+// atomicMax of the input index into the scan's winner image (-1 between launches: k_pw_columns
+// resets every cell it reads); the first / last finite point go to proj_mm by atomicMin / Max.  The
+// image is column-major (cell (i, j) at j * V + i): one firing's lasers are consecutive points and
+// land in consecutive words, so a wave's atomics touch a few cache lines instead of one per lane.
+#define PW_NT 256
+#define PW_PTS (PW_NT * 8)
+__global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, const float4* __restrict__ pts,
+                                                      const int64_t* __restrict__ offs,
+                                                      const int32_t* __restrict__ cnts) {
+  __shared__ int queue_all[(PW_NT / 64) * PQ_CAP];
+  const int s = P.s0 + blockIdx.y, tid = threadIdx.x;
+  const int V = P.V, H = P.H;
+  const int n = cnts[s];
+  const int i0 = blockIdx.x * PW_PTS;
+  if (i0 >= n) return;
+  int* winner = B.winner + (size_t)s * P.VH;
+  const float4* in = pts + offs[s];
+  const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
+  int* queue = queue_all + wave_id() * PQ_CAP;
+  int qn = 0;
+  int fmin = 0x7fffffff, fmax = -1;
+  constexpr int kU = PW_PTS / PW_NT;
+  float3 pk[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) pk[u] = buffer_load_f3(rin, (uint32_t)(i0 + u * PW_NT + tid) * 16u);
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int i = i0 + u * PW_NT + tid;
+    const float4 p = make_float4(pk[u].x, pk[u].y, pk[u].z, 0.f);
+    int c = -1;
+    if (i < n && isfinite_f(p.x) && isfinite_f(p.y) && isfinite_f(p.z)) {  // removeNaNFromPointCloud
+      fmin = min(fmin, i);
+      fmax = max(fmax, i);
+      c = P.fast_proj ? proj_cell_fast<true>(P, p)
+                      : cell_cm(proj_cell_exact_ni(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, p), V, H);
+      if (c >= 0) atomicMax(&winner[c], i);
+    }
+    const unsigned long long amb = __ballot(c == -2);
+    if (c == -2) queue[qn + popc_below(amb)] = i;
+    qn += __popcll(amb);
+    if (qn >= 64) {
+      proj_drain_cm(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue + qn - 64, winner);
+      qn -= 64;
+    }
+  }
+  if (qn > 0) {
+    if (lane_id() >= qn) queue[lane_id()] = queue[0];
+    proj_drain_cm(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue, winner);
+  }
+  fmin = wave_min(fmin);
+  fmax = wave_max(fmax);
+  if (lane_id() == 0 && fmax >= 0) {
+    atomicMin(&B.proj_mm[2 * s], fmin);
+    atomicMax(&B.proj_mm[2 * s + 1], fmax);
+  }
+}
+
+// k_pw_columns: grid (column blocks of PW_NT, scans), one lane per column: the column pass of
+// k_project over the scan's winner image in HBM (each cell read once, then reset to -1), plus
+// labelComponents' initial state for k_sw_*: parent = cell (eligible: not ground, has a return) or
+// -1, component size / row mask 0.  Block (0, s) settles findStartEndAngle from proj_mm.
+#define PC_NT 128  // columns a workgroup
+__global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, const float4* __restrict__ pts,
+                                                      const int64_t* __restrict__ offs,
+                                                      const int32_t* __restrict__ cnts) {
+  // the workgroup's PC_NT columns of the column-major winner image, read and reset with coalesced
+  // 16-byte accesses, staged in LDS with a (V + 1)-word column stride (conflict-free column reads)
+  __shared__ int wl[PC_NT * 65];
+  const int s = P.s0 + blockIdx.y, tid = threadIdx.x;
+  const int V = P.V, H = P.H, VH = P.VH;
+  {
+    int* wsrc = B.winner + (size_t)s * VH + (size_t)blockIdx.x * PC_NT * V;
+    const int nw = min(PC_NT, H - (int)blockIdx.x * PC_NT) * V;
+    if ((V & 3) == 0) {  // 16-byte aligned, 4 words of one column at a time
+      int4* wg = (int4*)wsrc;
+      for (int q = tid; q < (nw >> 2); q += PC_NT) {
+        const int4 v = wg[q];
+        wg[q] = make_int4(-1, -1, -1, -1);
+        const int e = 4 * q, jj = e / V, i = e - jj * V;
+        int* d = wl + jj * (V + 1) + i;
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+      }
+    } else {
+      for (int e = tid; e < nw; e += PC_NT) {
+        const int v = wsrc[e];
+        wsrc[e] = -1;
+        const int jj = e / V;
+        wl[jj * (V + 1) + e - jj * V] = v;
+      }
+    }
+  }
+  __syncthreads();
+  const int n = cnts[s];
+  const float4* in = pts + offs[s];
+  float* range = B.range + (size_t)s * VH;
+  float4* cloud = B.cloud + (size_t)s * VH;
+  int8_t* ground = B.ground + (size_t)s * VH;
+  int* parent = B.cc_parent + (size_t)s * VH;
+  int* ccnt = B.cc_cnt + (size_t)s * VH;
+  unsigned long long* cmsk = B.cc_mask + (size_t)s * VH;
+  const float qnan = __int_as_float(0x7fc00000);
+  const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
+  const int j = blockIdx.x * PC_NT + tid;
+  if (j < H) {
+    unsigned long long gmask = 0ull;
+    float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
+    float prev_r = 0.f;
+    float min_range = 1000.f;
+    int id_min = -1;
+    const double jfrac = (double)(float)j / 10000.0;
+    auto settle = [&](int i, float r, float Z) {  // row i final: ground flag, 2-D scan (:312-330)
+      const int c = i * H + j;
+      const int g = (int)((gmask >> i) & 1ull);
+      ground[c] = (int8_t)g;
+      parent[c] = (g != 1 && r != FLT_MAX) ? c : -1;  // _label_mat == 0 (:293-300)
+      ccnt[c] = 0;
+      cmsk[c] = 0ull;
+      if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f && r < min_range) {
+        min_range = r;
+        id_min = c;
+      }
+    };
+    for (int i0 = 0; i0 < V; i0 += 16) {
+      int w[16];
+      float4 pk[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) w[u] = (i0 + u < V) ? wl[tid * (V + 1) + i0 + u] : -1;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) pk[u] = buffer_load_f4(rin, w[u] >= 0 ? (uint32_t)w[u] * 16u : 0xffffffffu);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = i0 + u;
+        if (i >= V) continue;
+        const int c = i * H + j;
+        float4 q;
+        float r;
+        if (w[u] >= 0) {
+          const float4 p = pk[u];
+          r = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+          q = make_float4(p.x, p.y, p.z, (float)((double)(float)i + jfrac));
+        } else {
+          r = FLT_MAX;
+          q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
+        }
+        range[c] = r;
+        cloud[c] = q;
+        if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
+          const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
+          if (ground_pair(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ), P.mount)) gmask |= (3ull << (i - 1));
+        }
+        if (i >= 1) settle(i - 1, prev_r, prev.z);
+        prev = q;
+        prev_r = r;
+      }
+    }
+    settle(V - 1, prev_r, prev.z);
+    B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
+  }
+  if (blockIdx.x == 0 && tid == 0) {  // findStartEndAngle (:234-249)
+    const int fmin = B.proj_mm[2 * s], fmax = B.proj_mm[2 * s + 1];
+    B.proj_mm[2 * s] = 0x7fffffff;
+    B.proj_mm[2 * s + 1] = -1;
     float so = 0.f, eo = 0.f, od = 0.f;
     if (fmax >= 0) {
       float4 a = in[fmin], b = in[fmax];
@@ -874,122 +1080,346 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   }
 }
 
-// ---- k_segment (global path: V > 16 or V*H >= 32768) ----------------------------------------
-__global__ __launch_bounds__(1024) void k_segment_global(LgParams P, LgBufs B) {
-  extern __shared__ __attribute__((aligned(16))) int smem[];
-  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  const int V = P.V, H = P.H, VH = P.VH, G = P.G;
-  int* scratch = smem;  // 64 ints
+// ---- wide-mode segmentation: k_sw_* over tiles of SW_TILE cells, grid (tiles, scans) ----------
+// labelComponents' result (imageProjection.cpp:412-496, :354-356) as in k_segment_lds: components
+// of the edge relation by union-find (root = smallest member = the BFS seed), then each feasible
+// root ranked in raster order.  k_pw_columns has set parent (cell or -1), size and row mask.
+//   k_sw_local   union of the edges inside 2-D tiles in LDS (parent := tile-local root)
+//   k_sw_bound   union of the edges crossing tile borders (and the wrap), on the global parent[]
+//   k_sw_roots   full path compression; size and non-seed row mask of every root
+//   k_sw_count   per tile: feasible roots, segmented cells, outliers
+//   k_sw_rank    label of every root: 1 + its raster rank among feasible roots, or 999999
+//   k_sw_emit    label image and the raster-order compaction (:358-396) at tile offsets
+//   k_sw_finish  one workgroup a scan: 2-D scan compaction, adjustDistortion, counts
+#define SW_NT 256
+#define SW_TILE (SW_NT * 4)
+
+LG_DEVICE int sw_load(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// uf_find / uf_unite on parent[] shared by the workgroups of a scan: reads through L2 (another
+// CU's hook may be newer than this CU's L1), hooks by device-scope atomicMin.
+LG_DEVICE int sw_find(int* parent, int x) {
+  int p = sw_load(parent + x);
+  while (p != x) {
+    x = p;
+    p = sw_load(parent + x);
+  }
+  return x;
+}
+LG_DEVICE void sw_unite(int* parent, int a, int b) {
+  bool done;
+  do {
+    a = sw_find(parent, a);
+    b = sw_find(parent, b);
+    if (a < b) {
+      const int old = atomicMin(&parent[b], a);
+      done = (old == b);
+      b = old;
+    } else if (b < a) {
+      const int old = atomicMin(&parent[a], b);
+      done = (old == a);
+      a = old;
+    } else {
+      done = true;
+    }
+  } while (!done);
+}
+
+// k_sw_local: 2-D tiles of SW_TR x SW_TC cells, grid (column tiles, row tiles, scans).  The edges
+// inside a tile are united in LDS (local indices; the smallest local index is the smallest global
+// one, rows dominating both orders) and every cell's parent becomes its tile-local root.
+#define SW_TR 8
+#define SW_TC 128
+__global__ __launch_bounds__(SW_NT) void k_sw_local(LgParams P, LgBufs B) {
+  __shared__ int lp[SW_TR * SW_TC];
+  __shared__ float lrg[SW_TR * SW_TC];
+  const int s = P.s0 + blockIdx.z, V = P.V, H = P.H, VH = P.VH;
+  const int i0 = blockIdx.y * SW_TR, j0 = blockIdx.x * SW_TC;
   int* parent = B.cc_parent + (size_t)s * VH;
   const float* range = B.range + (size_t)s * VH;
-  const int8_t* ground = B.ground + (size_t)s * VH;
-  const float4* cloud = B.cloud + (size_t)s * VH;
-  int32_t* label = B.label + (size_t)s * VH;
-  auto eligible = [&](int c) { return ground[c] != 1 && range[c] != FLT_MAX; };  // _label_mat == 0
-
-  PROF_T(t_s0);
-  for (int c = tid; c < VH; c += nt) parent[c] = eligible(c) ? c : -1;
+  int pv[4];
+  float rv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = u * SW_NT + threadIdx.x, i = i0 + t / SW_TC, j = j0 + t % SW_TC;
+    const int c = min(i, V - 1) * H + min(j, H - 1);
+    pv[u] = (i < V && j < H) ? parent[c] : -1;
+    rv[u] = range[c];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = u * SW_NT + threadIdx.x;
+    lp[t] = pv[u] >= 0 ? t : -1;
+    lrg[t] = rv[u];
+  }
   __syncthreads();
-  PROF_ADD(25, t_s0);
-  PROF_T(t_s1);
-  for (int c = tid; c < VH; c += nt) {
-    if (parent[c] < 0) continue;
-    const int i = c / H, j = c - i * H;
-    const float rc = range[c];
-    const int cr = (j + 1 < H) ? c + 1 : i * H;  // right neighbour, horizontal wrap
-    if (parent[cr] >= 0 && seg_edge(rc, range[cr], P.sinX, P.cosX, P.theta_thr)) uf_unite(parent, c, cr);
-    if (i + 1 < V) {
-      const int cd = c + H;
-      if (parent[cd] >= 0 && seg_edge(rc, range[cd], P.sinY, P.cosY, P.theta_thr)) uf_unite(parent, c, cd);
+  const bool wrap_local = H <= SW_TC;  // one column tile: the horizontal wrap edge is inside it
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = u * SW_NT + threadIdx.x, lr = t / SW_TC, lc = t % SW_TC;
+    const int i = i0 + lr, j = j0 + lc;
+    if (lp[t] < 0) continue;
+    const float r = lrg[t];
+    int tr = -1;
+    if (lc + 1 < SW_TC && j + 1 < H) tr = t + 1;
+    else if (wrap_local && j == H - 1) tr = lr * SW_TC;  // (i, H-1) -> (i, 0)
+    if (tr >= 0 && lp[tr] >= 0 && seg_edge(r, lrg[tr], P.sinX, P.cosX, P.theta_thr)) uf_unite(lp, t, tr);
+    const int td = t + SW_TC;
+    if (lr + 1 < SW_TR && i + 1 < V && lp[td] >= 0 && seg_edge(r, lrg[td], P.sinY, P.cosY, P.theta_thr))
+      uf_unite(lp, t, td);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = u * SW_NT + threadIdx.x, i = i0 + t / SW_TC, j = j0 + t % SW_TC;
+    if (i < V && j < H && pv[u] >= 0) {
+      const int rt = uf_find(lp, t);
+      parent[i * H + j] = (i0 + rt / SW_TC) * H + j0 + rt % SW_TC;
     }
   }
-  __syncthreads();
-  PROF_ADD(26, t_s1);
-  PROF_T(t_s2);
-  for (int c = tid; c < VH; c += nt)
-    if (parent[c] >= 0) parent[c] = uf_find(parent, c);
-  __syncthreads();
-  PROF_ADD(27, t_s2);
-  PROF_T(t_s3);
+}
 
-  // ---- per-root size and row mask (rows of non-seed members) ----
-  int32_t* cnt = B.cc_cnt + (size_t)s * VH;
-  unsigned long long* msk = B.cc_mask + (size_t)s * VH;
-  for (int c = tid; c < VH; c += nt) { cnt[c] = 0; msk[c] = 0ull; }
-  __syncthreads();
-  for (int c = tid; c < VH; c += nt) {
+// k_sw_bound: the edges that cross a tile's right edge (the horizontal wrap for the last column
+// tile) or bottom edge, united on the scan's global parent[] (one thread an edge).
+__global__ __launch_bounds__(SW_NT) void k_sw_bound(LgParams P, LgBufs B) {
+  const int s = P.s0 + blockIdx.z, V = P.V, H = P.H, VH = P.VH;
+  const int i0 = blockIdx.y * SW_TR, j0 = blockIdx.x * SW_TC;
+  int* parent = B.cc_parent + (size_t)s * VH;
+  const float* range = B.range + (size_t)s * VH;
+  const int t = threadIdx.x;
+  int c = -1, cn = -1;
+  bool horiz = false;
+  if (t < SW_TR) {  // right edge of row i0 + t
+    const int i = i0 + t, j = min(j0 + SW_TC, H) - 1;
+    if (i < V && !(H <= SW_TC)) {
+      c = i * H + j;
+      cn = (j + 1 < H) ? c + 1 : i * H;
+      horiz = true;
+    }
+  } else if (t < SW_TR + SW_TC) {  // bottom edge of column j0 + t - SW_TR
+    const int j = j0 + t - SW_TR, i = i0 + SW_TR - 1;
+    if (j < H && i + 1 < V) {
+      c = i * H + j;
+      cn = c + H;
+    }
+  }
+  if (c < 0) return;
+  if (parent[c] < 0 || parent[cn] < 0) return;
+  if (seg_edge(range[c], range[cn], horiz ? P.sinX : P.sinY, horiz ? P.cosX : P.cosY, P.theta_thr))
+    sw_unite(parent, c, cn);
+}
+
+__global__ __launch_bounds__(SW_NT) void k_sw_roots(LgParams P, LgBufs B) {
+  const int s = P.s0 + blockIdx.y, H = P.H, VH = P.VH;
+  int* parent = B.cc_parent + (size_t)s * VH;
+  int* ccnt = B.cc_cnt + (size_t)s * VH;
+  unsigned long long* cmsk = B.cc_mask + (size_t)s * VH;
+  const int lane = lane_id();
+#pragma unroll 1
+  for (int u = 0; u < 4; ++u) {
+    const int c = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
+    int r = -1;
+    if (c < VH && parent[c] >= 0) {
+      r = uf_find(parent, c);  // no hooks any more: plain (L1-cached) reads see valid ancestors
+      parent[c] = r;
+    }
+    // one atomic per distinct root of the wave (neighbouring cells mostly share a component)
+    unsigned long long todo = __ballot(r >= 0);
+    while (todo) {
+      const int r0 = __shfl(r, __ffsll((long long)todo) - 1);
+      const unsigned long long m = __ballot(r == r0);
+      unsigned long long rows = (r == r0 && c != r0) ? (1ull << (c / H)) : 0ull;
+      for (int o = 32; o > 0; o >>= 1) rows |= shfl64(rows, lane ^ o);
+      if (lane == __ffsll((long long)m) - 1) {
+        atomicAdd(&ccnt[r0], __popcll(m));
+        if (rows) atomicOr(&cmsk[r0], rows);
+      }
+      todo &= ~m;
+    }
+  }
+}
+
+LG_DEVICE bool sw_feasible(const LgParams& P, int n, unsigned long long rows) {  // :469-486
+  return n >= 30 || (n >= P.seg_valid_pt && __popcll(rows) >= P.seg_valid_line);
+}
+
+// cloudSegmentation's classification of cell c (:358-396) from its label kind.
+LG_DEVICE void sw_classify(const LgParams& P, int c, int lab, int g, bool& pseg, bool& pout) {
+  const int i = c / P.H, j = c - i * P.H;
+  pseg = pout = false;
+  if (lab > 0 || g == 1) {
+    if (lab == 999999) pout = (i > P.G && j % 5 == 0);
+    else if (!(g == 1 && (j % 5 != 0 && j > 5 && j < P.H - 5))) pseg = true;
+  }
+}
+
+__global__ __launch_bounds__(SW_NT) void k_sw_count(LgParams P, LgBufs B) {
+  __shared__ int red[3 * (SW_NT / 64)];
+  const int s = P.s0 + blockIdx.y, VH = P.VH;
+  const int* parent = B.cc_parent + (size_t)s * VH;
+  const int* ccnt = B.cc_cnt + (size_t)s * VH;
+  const unsigned long long* cmsk = B.cc_mask + (size_t)s * VH;
+  const int8_t* ground = B.ground + (size_t)s * VH;
+  int nroot = 0, nseg = 0, nout = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
+    if (c >= VH) continue;
     const int r = parent[c];
-    if (r < 0) continue;
-    atomicAdd(&cnt[r], 1);
-    if (r != c) atomicOr(&msk[r], 1ull << (c / H));
+    int lab = -1;
+    if (r >= 0) {
+      const bool feas = sw_feasible(P, ccnt[r], cmsk[r]);
+      lab = feas ? 1 : 999999;
+      nroot += (r == c && feas) ? 1 : 0;
+    }
+    bool pseg, pout;
+    sw_classify(P, c, lab, ground[c], pseg, pout);
+    nseg += pseg;
+    nout += pout;
+  }
+  nroot = wave_sum(nroot);
+  nseg = wave_sum(nseg);
+  nout = wave_sum(nout);
+  if (lane_id() == 0) { red[wave_id()] = nroot; red[4 + wave_id()] = nseg; red[8 + wave_id()] = nout; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int4 t = make_int4(0, 0, 0, 0);
+    for (int w = 0; w < SW_NT / 64; ++w) { t.x += red[w]; t.y += red[4 + w]; t.z += red[8 + w]; }
+    B.seg_tiles[(size_t)s * gridDim.x + blockIdx.x] = t;
+  }
+}
+
+// Exclusive prefix of the tile counts before this tile (wave 0), in shared memory.
+LG_DEVICE int4 sw_tile_base(const LgBufs& B, int s, int4* sh) {
+  if (wave_id() == 0) {
+    const int4* tc = B.seg_tiles + (size_t)s * gridDim.x;
+    int4 a = make_int4(0, 0, 0, 0);
+    for (int t = lane_id(); t < (int)blockIdx.x; t += 64) {
+      const int4 v = tc[t];
+      a.x += v.x; a.y += v.y; a.z += v.z;
+    }
+    a.x = wave_sum(a.x); a.y = wave_sum(a.y); a.z = wave_sum(a.z);
+    if (lane_id() == 0) *sh = a;
   }
   __syncthreads();
-  wave_raster_compact(
-      VH, scratch,
-      [&](int c, bool& feas, bool& isroot) {
-        isroot = parent[c] == c;
-        if (isroot) {
-          const int n = cnt[c];
-          const int lines = __popcll(msk[c]);
-          feas = n >= 30 || (n >= P.seg_valid_pt && lines >= P.seg_valid_line);
-        }
-      },
-      [&](int c, bool feas, bool isroot, int k, int) {
-        if (isroot) cnt[c] = feas ? k + 1 : 999999;
-      });
-  for (int c = tid; c < VH; c += nt) {
-    const int r = parent[c];
-    label[c] = (r < 0) ? -1 : cnt[r];
-  }
+  return *sh;
+}
 
+// Workgroup-wide exclusive scan of up to three predicates over the tile's cells in raster order
+// (cell cb + u * SW_NT + tid, u = 0..3: the waves own contiguous 64-cell chunks per u).
+LG_DEVICE int sw_tile_scan(bool p, int* wt, int& total) {
+  const unsigned long long m = __ballot(p);
+  if (lane_id() == 0) wt[wave_id()] = __popcll(m);
   __syncthreads();
-  PROF_ADD(28, t_s3);
-  PROF_T(t_s4);
+  int before = 0;
+  total = 0;
+  for (int w = 0; w < SW_NT / 64; ++w) {
+    const int v = wt[w];
+    if (w < wave_id()) before += v;
+    total += v;
+  }
+  __syncthreads();
+  return before + popc_below(m);
+}
 
-  // ---- cloudSegmentation extraction (:358-396): raster-order compaction ----
+__global__ __launch_bounds__(SW_NT) void k_sw_rank(LgParams P, LgBufs B) {
+  __shared__ int4 base;
+  __shared__ int wt[SW_NT / 64];
+  const int s = P.s0 + blockIdx.y, VH = P.VH;
+  const int* parent = B.cc_parent + (size_t)s * VH;
+  int* ccnt = B.cc_cnt + (size_t)s * VH;
+  const unsigned long long* cmsk = B.cc_mask + (size_t)s * VH;
+  int k = sw_tile_base(B, s, &base).x;
+  for (int u = 0; u < 4; ++u) {
+    const int c = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
+    const bool root = c < VH && parent[c] == c;
+    const bool feas = root && sw_feasible(P, ccnt[c], cmsk[c]);
+    int tot;
+    const int o = sw_tile_scan(feas, wt, tot);
+    if (root) ccnt[c] = feas ? k + o + 1 : 999999;  // the root's word now holds its label
+    k += tot;
+  }
+}
+
+__global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
+  __shared__ int4 base;
+  __shared__ int wt[SW_NT / 64];
+  const int s = P.s0 + blockIdx.y, V = P.V, H = P.H, VH = P.VH;
+  const int* parent = B.cc_parent + (size_t)s * VH;
+  const int* clab = B.cc_cnt + (size_t)s * VH;
+  const int8_t* ground = B.ground + (size_t)s * VH;
+  const float* range = B.range + (size_t)s * VH;
+  const float4* cloud = B.cloud + (size_t)s * VH;
+  int32_t* label = B.label + (size_t)s * VH;
   float4* seg_pts = B.seg_pts + (size_t)s * VH;
   float* seg_range = B.seg_range + (size_t)s * VH;
   uint32_t* seg_col = B.seg_col + (size_t)s * VH;
   uint8_t* seg_ground = B.seg_ground + (size_t)s * VH;
   float4* outlier = B.outlier + (size_t)s * VH;
+  float4* outlier_fa = B.outlier_fa + (size_t)s * VH;
   int32_t* ring_start = B.ring_start + (size_t)s * V;
   int32_t* ring_end = B.ring_end + (size_t)s * V;
-  float4* outlier_fa = B.outlier_fa + (size_t)s * VH;
   const bool swap_axes = B.state[s].initialized != 0;
-  auto cls = [&](int c, bool& pseg, bool& pout) {
-    const int i = c / H, j = c - i * H;
-    const int lab = label[c], g = ground[c];
-    if (lab > 0 || g == 1) {
-      if (lab == 999999) pout = (i > G && j % 5 == 0);
-      else if (!(g == 1 && (j % 5 != 0 && j > 5 && j < H - 5))) pseg = true;
+  const int4 b0 = sw_tile_base(B, s, &base);
+  int kseg = b0.y, kout = b0.z;
+  for (int u = 0; u < 4; ++u) {
+    const int c = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
+    const bool in = c < VH;
+    int lab = -1, g = 0;
+    if (in) {
+      const int r = parent[c];
+      lab = r < 0 ? -1 : clab[r];
+      g = ground[c];
+      label[c] = lab;
     }
-  };
-  const int2 tot = wave_raster_compact(VH, scratch, cls, [&](int c, bool pseg, bool pout, int k1, int k2) {
-    const int i = c / H, j = c - i * H;
-    if (j == 0) {  // k1 = segmented points before this ring
-      ring_start[i] = k1 - 1 + 5;
-      if (i > 0) ring_end[i - 1] = k1 - 1 - 5;
+    bool pseg = false, pout = false;
+    if (in) sw_classify(P, c, lab, g, pseg, pout);
+    int tseg, tout;
+    const int oseg = kseg + sw_tile_scan(pseg, wt, tseg);
+    const int oout = kout + sw_tile_scan(pout, wt, tout);
+    if (in) {
+      const int i = c / H, j = c - i * H;
+      if (j == 0) {  // oseg = segmented points before this ring
+        ring_start[i] = oseg - 1 + 5;
+        if (i > 0) ring_end[i - 1] = oseg - 1 - 5;
+      }
+      if (pseg) {
+        seg_pts[oseg] = cloud[c];
+        seg_range[oseg] = range[c];
+        seg_col[oseg] = (uint32_t)j;
+        seg_ground[oseg] = (uint8_t)(g == 1);
+      }
+      if (pout) {
+        const float4 p = cloud[c];
+        outlier[oout] = p;
+        outlier_fa[oout] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;  // adjustOutlierCloud (fa.cpp:1273-1283)
+      }
     }
-    if (pseg) {
-      seg_pts[k1] = cloud[c];
-      seg_range[k1] = range[c];
-      seg_col[k1] = (uint32_t)j;
-      seg_ground[k1] = (uint8_t)(ground[c] == 1);
-    }
-    if (pout) {
-      const float4 p = cloud[c];
-      outlier[k2] = p;
-      outlier_fa[k2] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;  // adjustOutlierCloud (fa.cpp:1273-1283)
-    }
-  });
-  const int nseg = tot.x, nout = tot.y;
-  if (tid == 0) ring_end[V - 1] = nseg - 1 - 5;
-  // 2-D scan compaction (column order)
+    kseg += tseg;
+    kout += tout;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_sw_finish(LgParams P, LgBufs B, int tiles) {
+  __shared__ int scratch[64];
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, V = P.V, H = P.H, VH = P.VH;
+  __shared__ int tot[2];
+  if (tid < 64) {
+    const int4* tc = B.seg_tiles + (size_t)s * tiles;
+    int a = 0, b = 0;
+    for (int t = tid; t < tiles; t += 64) { a += tc[t].y; b += tc[t].z; }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (tid == 0) { tot[0] = a; tot[1] = b; }
+  }
+  __syncthreads();
+  const int nseg = tot[0], nout = tot[1];
+  if (tid == 0) B.ring_end[(size_t)s * V + V - 1] = nseg - 1 - 5;
   const int32_t* cand = B.scan_cand + (size_t)s * H;
+  const float4* cloud = B.cloud + (size_t)s * VH;
   float4* scan = B.scan_msg + (size_t)s * H;
   const int nscan = wave_raster_compact(H, scratch, [&](int j, bool& p, bool&) { p = cand[j] >= 0; },
                                         [&](int j, bool p, bool, int k, int) { if (p) scan[k] = cloud[cand[j]]; }).x;
-  PROF_ADD(29, t_s4);
   distort_segmented(P, B, s, nseg, scratch);
   if (tid == 0) {
     int32_t* cnt = B.counts + (size_t)s * CNT_N;
@@ -3639,22 +4069,39 @@ bool lg_lds_segment(const LgParams& P) { return P.V <= 16 && P.VH < 32768; }  //
 
 int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
                       const int32_t* cnts, hipStream_t st) {
-  if (lg_lds_projection(P)) {
+  if (P.wide) {
+    hipLaunchKernelGGL(k_pw_scatter, dim3((P.max_points + PW_PTS - 1) / PW_PTS, S), dim3(PW_NT), 0, st, P, B, pts,
+                       offs, cnts);
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_pw_columns, dim3((P.H + PC_NT - 1) / PC_NT, S), dim3(PC_NT), 0, st, P, B, pts, offs, cnts);
+  } else {  // !wide implies the LDS images fit (lego_batch_set_wide)
     size_t sm = (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4;
-    hipLaunchKernelGGL((k_project<true>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
-  } else {
-    hipLaunchKernelGGL((k_project<false>), dim3(S), dim3(1024), (64 + 16 * PQ_CAP) * 4, st, P, B, pts, offs, cnts);
+    hipLaunchKernelGGL(k_project, dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
   }
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
 
 int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  if (lg_lds_segment(P)) {
+  if (P.wide) {
+    const dim3 g((P.VH + SW_TILE - 1) / SW_TILE, S);
+    const dim3 g2((P.H + SW_TC - 1) / SW_TC, (P.V + SW_TR - 1) / SW_TR, S);
+    hipLaunchKernelGGL(k_sw_local, g2, dim3(SW_NT), 0, st, P, B);
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_sw_bound, g2, dim3(SW_NT), 0, st, P, B);
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_sw_roots, g, dim3(SW_NT), 0, st, P, B);
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_sw_count, g, dim3(SW_NT), 0, st, P, B);
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_sw_rank, g, dim3(SW_NT), 0, st, P, B);
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_sw_emit, g, dim3(SW_NT), 0, st, P, B);
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_sw_finish, dim3(S), dim3(1024), 0, st, P, B, (int)g.x);
+  } else {
     size_t sm = (size_t)(P.VH + 64) * 4;
     hipLaunchKernelGGL(k_segment_lds, dim3(S), dim3(1024), sm, st, P, B);
-  } else {
-    hipLaunchKernelGGL(k_segment_global, dim3(S), dim3(1024), 64 * 4, st, P, B);
   }
   LG_CHECK_LAUNCH();
   return LEGO_OK;

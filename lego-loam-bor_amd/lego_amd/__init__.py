@@ -55,6 +55,8 @@ def lib():
         L.lego_batch_set_timing.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_groups.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_lag.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_batch_set_wide.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_batch_wide.argtypes = [C.c_void_p]
         L.lego_batch_read_counts.argtypes = [C.c_void_p, P(C.c_int32)]
         L.lego_test_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int32, C.c_int32]
         L.lego_test_libm.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_int32, C.c_int32]
@@ -175,6 +177,14 @@ class Batch:
     def set_lag(self, lag):
         """Pipeline depth: 0 = a step runs its own scan's LM, 1 (default) = the previous scan's."""
         _check(lib().lego_batch_set_lag(self.h, int(lag)), "lego_batch_set_lag")
+
+    def set_wide(self, mode):
+        """Projection / segmentation layout: 1 wide (many workgroups a scan), 0 one workgroup a scan
+        (LDS images), -1 automatic."""
+        _check(lib().lego_batch_set_wide(self.h, int(mode)), "lego_batch_set_wide")
+
+    def wide(self):
+        return bool(lib().lego_batch_wide(self.h))
 
     def counts(self):
         """[S, 7] int32: segmented, outlier, scan_msg, sharp, less sharp, flat, less flat counts."""

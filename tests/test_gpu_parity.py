@@ -273,7 +273,7 @@ def test_vlp16_noise_free_ties(gpu):
 
 
 def test_hdl64_parity(gpu):
-    """HDL-64E-like config: global-memory union-find / winner paths (V*H > LDS)."""
+    """HDL-64E-like config: the wide layout (k_pw_* / k_sw_*: the V*H images do not fit LDS)."""
     params = L.params_hdl64()
     cfg = A.synth_cfg("hdl64")
     for row in run_pair(params, cfg, 0, 3):
@@ -342,10 +342,12 @@ def test_injected_projection_rejects_malformed_cloud_info(gpu):
     assert not Hs.diff_report(Hs.FEAT_KEYS, fg, fr)
 
 
-@pytest.mark.parametrize("groups", [1, 3])
-def test_batch_streams_match_oracle(gpu, groups):
+@pytest.mark.parametrize("groups,wide", [(1, -1), (3, -1), (1, 0), (3, 0)])
+def test_batch_streams_match_oracle(gpu, groups, wide):
     """The batched engine (S sequences, one launch per stage, optionally as `groups` slices on their
-    own HIP streams) equals S independent oracle runs."""
+    own HIP streams) equals S independent oracle runs, in both kernel layouts of the projection and
+    segmentation (wide: many workgroups a scan, the default at this S; 0: one workgroup a scan with
+    the images in LDS, the default at bench scale)."""
     import torch
     params = L.params_vlp16()
     cfg = A.synth_cfg("vlp16")
@@ -360,6 +362,7 @@ def test_batch_streams_match_oracle(gpu, groups):
     b = L.Batch(params, S, cap)
     if groups > 1:
         b.set_groups(groups)
+    b.set_wide(wide)
     oracles = [oracle_for(params) for _ in range(S)]
     for k in range(steps):
         b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), torch.cuda.current_stream().cuda_stream)
