@@ -55,6 +55,9 @@ struct LgState {  // FeatureAssociation members that persist across scans (featu
   int iters_surf, iters_corner;
   int proj_status;       // 0 or LEGO_EEMPTY for the last projection
   int pub_copy;          // k_publish stores the lessFlat cloud untransformed (checkSystemInitialization)
+  int fe_scans;          // scans whose features k_concat has assembled: > 0 at a scan's front end iff that
+                         // scan's FeatureAssociation pass is not the initialising one (adjustOutlierCloud runs
+                         // in publishCloudsLast, :1273-1283, which the first pass skips), whatever the LM lag
   double quat[4];
   double pos[3];
 };
