@@ -53,11 +53,7 @@ struct LgState {  // FeatureAssociation members that persist across scans (featu
   int tree_stale;        // kd-trees were not rebuilt at the last publishCloudsLast
   int status;            // LEGO_ST_* of the last association
   int iters_surf, iters_corner;
-  int proj_status;       // 0 or LEGO_EEMPTY for the last projection
   int pub_copy;          // k_publish stores the lessFlat cloud untransformed (checkSystemInitialization)
-  int fe_scans;          // scans whose features k_concat has assembled: > 0 at a scan's front end iff that
-                         // scan's FeatureAssociation pass is not the initialising one (adjustOutlierCloud runs
-                         // in publishCloudsLast, :1273-1283, which the first pass skips), whatever the LM lag
   double quat[4];
   double pos[3];
 };
@@ -123,5 +119,10 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   float4* corner_last;   // [S][2][V*cap_lsharp]
   float4* surf_last;     // [S][2][VH]
   float4* grid_pts;      // [S][VH]  LM scratch: Last cloud bucketed by grid cell (xyz, index bits)
-  LgState* state;        // [S]
+  LgState* state;        // [S]      written by k_lm / k_publish only (k_lm stores it whole)
+  int32_t* fe_state;     // [S][2]   written by the front end only: [0] 0 or LEGO_EEMPTY for the last
+                         // projection; [1] scans whose features k_concat has assembled, > 0 at a scan's
+                         // front end iff its FeatureAssociation pass is not the initialising one
+                         // (adjustOutlierCloud runs in publishCloudsLast, :1273-1283, which the first
+                         // pass skips), however far the LM lags behind
 };

@@ -172,6 +172,14 @@ struct lego_batch {
   bool pend_lm = false;      // k_lm of the last front-end scan (lag 1; parity lm_par)
   int lm_par = 0;
   int pend_groups = 1;       // slicing of the pending work
+  // Overlap schedule (one slice, lag 1, timing off): k_publish(k-2) and k_lm(k-1) go to the internal
+  // LM stream ls at the start of step k, ordered after k_concat(k-1) (ev_cat) and k_voxel(k-2)
+  // (ev_vox), so a CU whose scan's LM has finished takes the next front end's workgroups instead of
+  // idling until the slowest LM of the launch ends.  k_concat(k) waits for k_publish(k-2) (ev_pub),
+  // which follows k_lm(k-2) on ls: the feature / staging halves of parity k are free then.
+  bool pend_ovl = false;     // the pending work belongs to the overlap schedule
+  hipStream_t ls = nullptr;
+  hipEvent_t ev_pub = nullptr, ev_ls = nullptr;
   // pinned host mirrors for lego_batch_read / the single-context outputs
   Pinned h_seg, h_out, h_scan, h_sharp, h_lsharp, h_flat, h_lflat, h_clast, h_slast, h_olast;
   Pinned h_rs, h_re, h_label, h_sharp_ind, h_lsharp_ind, h_flat_ind, h_gflag, h_col, h_range_seg, h_range, h_ground;
@@ -192,6 +200,9 @@ struct lego_batch {
     }
     if (fork) hipEventDestroy(fork);
     if (ev_chain) hipEventDestroy(ev_chain);
+    if (ls) hipStreamDestroy(ls);
+    if (ev_pub) hipEventDestroy(ev_pub);
+    if (ev_ls) hipEventDestroy(ev_ls);
   }
 };
 
@@ -314,7 +325,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   A(f_flat, 2 * S * V * P.cap_flat); A(f_flat_ind, 2 * S * V * P.cap_flat); A(fcnt, 2 * S * 4);
   A(f_lflat, S * VH);
   A(corner_last, S * 2 * V * P.cap_lsharp); A(surf_last, S * 2 * VH); A(grid_pts, S * VH);
-  A(state, S);
+  A(state, S); A(fe_state, S * 2);
 #undef A
   if (rc != LEGO_OK) {
     delete b;
@@ -346,9 +357,10 @@ int lego_batch_reset(lego_batch* b) {
   if (hipMemset(B.smooth, 0, S * VH * sizeof(int2)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fp_sync, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   b->epoch = 0;
-  b->pend_pub = b->pend_lm = false;
+  b->pend_pub = b->pend_lm = b->pend_ovl = false;
   b->par = b->last_par = 0;
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemset(B.fe_state, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.counts, 0, S * CNT_N * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   // wide mode's per-scan scratch starts (and is left by every launch) reset: winner -1, first point
   // INT_MAX, last point -1
@@ -483,10 +495,52 @@ static int chain_stream(lego_batch* b, hipStream_t st) {
   return LEGO_OK;
 }
 
+static int ensure_ls(lego_batch* b) {
+  if (!b->ls && hipStreamCreateWithFlags(&b->ls, hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
+  if (!b->ev_pub && hipEventCreateWithFlags(&b->ev_pub, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
+  if (!b->ev_ls && hipEventCreateWithFlags(&b->ev_ls, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
+  return ensure_streams(b, 1);
+}
+
+// The front end of the overlap schedule after the projection: smoothness, extraction, then (after
+// publish(k-2) on ls when one was issued) k_concat and the side stream's k_voxel.
+static int run_association_ovl(lego_batch* b, hipStream_t st, bool wait_pub) {
+  LgParams P = b->P;
+  P.s0 = 0;
+  P.epoch = b->epoch;
+  P.par = b->par;
+  int rc = lg_launch_fa_prep(P, b->B, b->S, st, false);
+  if (!rc) rc = lg_launch_extract(P, b->B, b->S, st);
+  if (rc) return rc;
+  if (wait_pub && hipStreamWaitEvent(st, b->ev_pub, 0) != hipSuccess) return LEGO_EDEVICE;
+  rc = lg_launch_concat(P, b->B, b->S, st);
+  if (rc) return rc;
+  if (hipEventRecord(b->ev_cat[0], st) != hipSuccess) return LEGO_EDEVICE;
+  if (hipStreamWaitEvent(b->vs[0], b->ev_cat[0], 0) != hipSuccess) return LEGO_EDEVICE;
+  rc = lg_launch_voxel(P, b->B, b->S, b->vs[0]);
+  if (rc) return rc;
+  if (hipEventRecord(b->ev_vox[0][P.par], b->vs[0]) != hipSuccess) return LEGO_EDEVICE;
+  return LEGO_OK;
+}
+
 // Issue the pending k_publish / k_lm (each publish joined with its k_voxel) on the stream of the
 // call that left them, in the pending work's slicing.
 static int flush_pending(lego_batch* b) {
   if (!b->pend_pub && !b->pend_lm) return LEGO_OK;
+  if (b->pend_ovl) {  // on ls: publish(k-1), k_lm(k), publish(k); then the last step's stream waits for ls
+    int rc = LEGO_OK;
+    if (b->pend_pub) rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
+    if (!rc && b->pend_lm) {
+      if (hipStreamWaitEvent(b->ls, b->ev_cat[0], 0) != hipSuccess) return LEGO_EDEVICE;
+      rc = issue_lm(b, b->ls, 0, b->S, b->lm_par);
+      if (!rc) rc = issue_publish(b, b->ls, 0, 0, b->S, b->lm_par);
+    }
+    if (rc) return rc;
+    if (hipEventRecord(b->ev_ls, b->ls) != hipSuccess) return LEGO_EDEVICE;
+    if (hipStreamWaitEvent(b->last_stream, b->ev_ls, 0) != hipSuccess) return LEGO_EDEVICE;
+    b->pend_pub = b->pend_lm = b->pend_ovl = false;
+    return LEGO_OK;
+  }
   const int G = b->pend_groups;
   hipStream_t st = b->last_stream;
   for (int g = 0; g < G; ++g) {
@@ -550,6 +604,37 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   }
   rc = chain_stream(b, st);
   if (rc) return rc;
+  const bool ovl = G <= 1 && lag && !b->timing;
+  if (ovl != b->pend_ovl && (b->pend_pub || b->pend_lm)) {  // the pending work belongs to the other schedule
+    rc = flush_pending(b);
+    if (rc) return rc;
+  }
+  if (ovl) {
+    rc = ensure_ls(b);
+    if (rc) return rc;
+    const bool pub_now = b->pend_pub;
+    if (b->pend_pub) {  // publish(k-2) on ls, after its k_voxel (issue_publish waits for ev_vox)
+      rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
+      if (!rc && hipEventRecord(b->ev_pub, b->ls) != hipSuccess) rc = LEGO_EDEVICE;
+    }
+    if (!rc && b->pend_lm) {  // k_lm(k-1) on ls, after k_concat(k-1)
+      if (hipStreamWaitEvent(b->ls, b->ev_cat[0], 0) != hipSuccess) return LEGO_EDEVICE;
+      rc = issue_lm(b, b->ls, 0, b->S, b->lm_par);
+    }
+    if (!rc) rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+    if (!rc) rc = run_association_ovl(b, st, pub_now);
+    if (rc) return rc;
+    // pending now: publish(k-1) (its k_lm was just issued), k_lm(k)
+    b->pend_pub = b->pend_lm;
+    b->pub_par = b->lm_par;
+    b->pend_lm = true;
+    b->lm_par = b->par;
+    b->pend_groups = 1;
+    b->pend_ovl = true;
+    b->last_par = b->par;
+    b->par ^= 1;
+    return LEGO_OK;
+  }
   if (G <= 1) {
     if (b->timing) hipEventRecord(b->ev[0], st);
     rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
@@ -601,6 +686,7 @@ int lego_batch_stage_times(lego_batch* b, float* ms6) {
 struct ReadHdr {
   int32_t cnt[CNT_N];
   float ori[4];
+  int32_t fe[2];  // proj_status, front-end scans
   LgState S;
 };
 static int read_hdr(lego_batch* b, int s, hipStream_t st, ReadHdr** out) {
@@ -610,6 +696,7 @@ static int read_hdr(lego_batch* b, int s, hipStream_t st, ReadHdr** out) {
   if (hipMemcpyAsync(h->cnt, B.counts + (size_t)s * CNT_N, sizeof(h->cnt), hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipMemcpyAsync(h->ori, B.orient + (size_t)s * 4, sizeof(h->ori), hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipMemcpyAsync(&h->S, B.state + s, sizeof(h->S), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(h->fe, B.fe_state + (size_t)s * 2, sizeof(h->fe), hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return LEGO_EDEVICE;
   *out = h;
@@ -834,7 +921,7 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
   ReadHdr* h = nullptr;
   rc = read_hdr(b, 0, nullptr, &h);
   if (rc) return rc;
-  if (h->S.proj_status != LEGO_OK) return h->S.proj_status;
+  if (h->fe[0] != LEGO_OK) return h->fe[0];
   if (out) return read_proj(b, 0, h, nullptr, out);
   return LEGO_OK;
 }

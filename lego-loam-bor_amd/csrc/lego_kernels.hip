@@ -443,7 +443,7 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
     B.orient[s * 4 + 1] = eo;
     B.orient[s * 4 + 2] = od;
     B.orient[s * 4 + 3] = (float)(fmax >= 0);
-    B.state[s].proj_status = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
+    B.fe_state[2 * s] = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
   }
 }
 
@@ -627,7 +627,7 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
     B.orient[s * 4 + 1] = eo;
     B.orient[s * 4 + 2] = od;
     B.orient[s * 4 + 3] = (float)(fmax >= 0);
-    B.state[s].proj_status = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
+    B.fe_state[2 * s] = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
   }
 }
 
@@ -937,7 +937,7 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   int32_t* __restrict__ ring_end = B.ring_end + (size_t)s * V;
   // adjustOutlierCloud (fa.cpp:1273-1283) runs in publishCloudsLast, i.e. not on the
   // initialisation scan (:1414-1416): the state read here is the one FeatureAssociation will see
-  const bool swap_axes = B.state[s].fe_scans > 0;  // not the initialisation scan (:1414-1416)
+  const bool swap_axes = B.fe_state[2 * s + 1] > 0;  // not the initialisation scan (:1414-1416)
   auto cell_label = [&](int c, int& lab, bool& gnd) {
     const int v = parent[c];
     gnd = v == SEG_GND;
@@ -1359,7 +1359,7 @@ __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
   float4* outlier_fa = B.outlier_fa + (size_t)s * VH;
   int32_t* ring_start = B.ring_start + (size_t)s * V;
   int32_t* ring_end = B.ring_end + (size_t)s * V;
-  const bool swap_axes = B.state[s].fe_scans > 0;  // not the initialisation scan (:1414-1416)
+  const bool swap_axes = B.fe_state[2 * s + 1] > 0;  // not the initialisation scan (:1414-1416)
   const int4 b0 = sw_tile_base(B, s, &base);
   int kseg = b0.y, kout = b0.z;
   for (int u = 0; u < 4; ++u) {
@@ -1468,7 +1468,7 @@ __global__ __launch_bounds__(kNT) void k_fa_prep(LgParams P, LgBufs B) {
     const int nout = cnt[CNT_OUTLIER];
     const float4* __restrict__ outl = B.outlier + (size_t)s * VH;
     float4* __restrict__ outa = B.outlier_fa + (size_t)s * VH;
-    const bool swap_axes = B.state[s].fe_scans > 0;  // not the initialisation scan (:1414-1416)  // not on the initialisation scan (:1414-1416)
+    const bool swap_axes = B.fe_state[2 * s + 1] > 0;  // not the initialisation scan (:1414-1416)  // not on the initialisation scan (:1414-1416)
     for (int k = tid; k < nout; k += nt) {
       const float4 p = outl[k];
       outa[k] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;
@@ -2704,7 +2704,7 @@ __global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
     cnt[CNT_STATUS] = status;
     int32_t* fc = B.fcnt + ((size_t)P.par * P.S + s) * 4;  // k_lm's copy, half P.par
     fc[0] = a[0]; fc[1] = a[1]; fc[2] = a[2]; fc[3] = status;
-    B.state[s].fe_scans += 1;  // read by the next scan's front end (adjustOutlierCloud)
+    B.fe_state[2 * s + 1] += 1;  // read by the next scan's front end (adjustOutlierCloud)
   }
   __syncthreads();
   // feature clouds into half P.par: k_lm of this scan may run after the next scan's k_concat
