@@ -32,10 +32,11 @@ NAMES = {0: "x:load+sort seg", 1: "x:sharp greedy", 2: "x:flat greedy", 3: "x:le
 def main():
     S = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     order = int(sys.argv[2]) if len(sys.argv) > 2 else 1  # voxel_tie_order (bench default 1)
+    kind = sys.argv[3] if len(sys.argv) > 3 else "vlp16"
     steps = 4
-    params = L.params_vlp16(voxel_tie_order=order)
-    cfg = A.synth_cfg("vlp16")
-    cap = 16 * 1800
+    params = (L.params_vlp16 if kind == "vlp16" else L.params_hdl64)(voxel_tie_order=order)
+    cfg = A.synth_cfg(kind)
+    cap = params.num_vertical_scans * params.num_horizontal_scans
     seqs = np.repeat(np.arange(S)[None, :], steps, 0).reshape(-1)
     scans = np.repeat(np.arange(steps)[:, None], S, 1).reshape(-1)
     pts, cnt = A.synth_batch(cfg, seqs, scans, nthreads=16)
@@ -66,7 +67,7 @@ def main():
 
     print("heap-sort fallbacks %d per step" % (prof[24] / nsteps))
     print("LM solves per scan: surf %.2f corner %.2f" % (prof[44] / nsteps / S, prof[45] / nsteps / S))
-    V = 16
+    V = params.num_vertical_scans
     print("per-ring extract wave cycles (mean / max over streams), ring 63 = first pass:")
     for r in list(range(V)) + [63]:
         if prof[128 + r]:
