@@ -36,6 +36,8 @@ extern "C" {
 #define LEGO_ENOTSUP    -4   /* configuration not supported (e.g. fp_mode != 0)           */
 #define LEGO_EEMPTY     -5   /* empty input cloud (reference: UB in findStartEndAngle)    */
 
+#define LEGO_MAX_POINTS ((1 << 28) - 1)  /* points of one input cloud (larger: LEGO_EINVAL) */
+
 /* ---- per-scan status bits reported by the association stage ------------------- */
 #define LEGO_ST_INIT            0x001  /* first scan: checkSystemInitialization (fa.cpp:1181-1209)   */
 #define LEGO_ST_LM_SKIPPED      0x002  /* Last clouds too small, LM skipped (fa.cpp:1214)            */

@@ -281,7 +281,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   *out = nullptr;
   int rc = lego_params_validate(p);
   if (rc != LEGO_OK) return rc;
-  if (n_streams < 1 || max_points < 1) return LEGO_EINVAL;
+  if (n_streams < 1 || max_points < 1 || max_points > LEGO_MAX_POINTS) return LEGO_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return LEGO_EDEVICE;
   if (hipSetDevice(device) != hipSuccess) return LEGO_EDEVICE;
@@ -884,7 +884,7 @@ void lego_ctx_destroy(lego_ctx* ctx) { delete ctx; }
 
 int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step, int32_t ox, int32_t oy, int32_t oz,
                        lego_projection_out* out) {
-  if (!c || (!points && n > 0) || n < 0 || step < 12 || ox < 0 || oy < 0 || oz < 0 || ox + 4 > step ||
+  if (!c || (!points && n > 0) || n < 0 || n > LEGO_MAX_POINTS || step < 12 || ox < 0 || oy < 0 || oz < 0 || ox + 4 > step ||
       oy + 4 > step || oz + 4 > step)
     return LEGO_EINVAL;
   lego_batch* b = c->b;
