@@ -1,0 +1,76 @@
+/*
+ * lego_s2m.h — C-ABI of the MI355X-native scan-to-map LM (MapOptimization's scan2MapOptimization).
+ *
+ * Drop-in boundary for the optimisation core of the reference's mapping thread:
+ *   MapOptimization::scan2MapOptimization  (LeGO-LOAM/src/mapOptmization.cpp:1315-1332)
+ *   MapOptimization::cornerOptimization    (:1028-1134)  kNN-5 line fit, point-to-line residuals
+ *   MapOptimization::surfOptimization      (:1136-1197)  kNN-5 plane fit (5x3 QR), point-to-plane
+ *   MapOptimization::LMOptimization        (:1199-1312)  6x6 normal equations, QR solve, degeneracy
+ * with the members they read and write (mapOptimization.h:200-226): transformTobeMapped[6] and
+ * isDegenerate (persisting from call to call, as the member does).  The caller keeps the rest of the
+ * mapping thread (transformAssociateToMap, key-frame selection, map assembly and VoxelGrid, GTSAM):
+ * it hands over, per problem, the four clouds scan2MapOptimization works on:
+ *   corner      laserCloudCornerLastDS      (the scan's corner features, downsampled, lidar frame)
+ *   surf        laserCloudSurfTotalLastDS   (surf + outlier features, downsampled, lidar frame)
+ *   corner_map  laserCloudCornerFromMapDS   (the surrounding map's corner cloud, map frame)
+ *   surf_map    laserCloudSurfFromMapDS     (the surrounding map's surf cloud, map frame)
+ * Points are lego_point (pcl::PointXYZI, 16 B; lego_frontend.h).  The kd-trees the reference builds
+ * over the two map clouds (:1317-1318) are replaced by per-problem hash grids built on the device.
+ *
+ * Many independent problems (one per mapping sequence) run in one launch, one workgroup each.  Plain
+ * C, plain pointers and sizes; every entry point returns LEGO_OK (0) or a negative LEGO_E* code
+ * (lego_frontend.h) and never throws.  There is no CPU fallback: without a usable HIP device
+ * lego_s2m_create returns LEGO_EDEVICE.
+ */
+#ifndef LEGO_S2M_H
+#define LEGO_S2M_H
+
+#include <stdint.h>
+
+#include "lego_frontend.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* info[4] of a problem: [0] 1 if the optimisation ran (:1316: corner map > 10 and surf map > 100
+ * points), [1] LM iterations run (<= 10), [2] correspondences of the last iteration
+ * (laserCloudOri size), [3] status bits below. */
+#define LEGO_S2M_ST_KNN_TIE     0x01  /* equal distances among a query's 6 nearest (kd-tree visit order unpinned) */
+#define LEGO_S2M_ST_DEGENERATE  0x02  /* iteration 0: largest eigenvalue of AtA < 100 (:1267-1285)        */
+#define LEGO_S2M_ST_FEW         0x04  /* an iteration had < 50 correspondences (:1208: no update)           */
+#define LEGO_S2M_ST_CONVERGED   0x08  /* LMOptimization returned true (:1308) before the 10th iteration     */
+#define LEGO_S2M_ST_SKIPPED     0x10  /* the map gate of :1316 failed: transform and state untouched        */
+
+/* Device-side batch: array i of problem p is base_i[off_i[p] .. off_i[p] + n_i[p]).  All pointers are
+ * DEVICE pointers (offsets int64, counts int32, one entry per problem). */
+typedef struct lego_s2m_io {
+  const lego_point* corner;      const int64_t* corner_off;     const int32_t* corner_n;
+  const lego_point* surf;        const int64_t* surf_off;       const int32_t* surf_n;
+  const lego_point* corner_map;  const int64_t* corner_map_off; const int32_t* corner_map_n;
+  const lego_point* surf_map;    const int64_t* surf_map_off;   const int32_t* surf_map_n;
+  float*   transform;   /* [n][6] transformTobeMapped: initial guess in, optimised pose out     */
+  int32_t* degenerate;  /* [n]    isDegenerate, in and out (mapOptimization.h:210)              */
+  int32_t* info;        /* [n][4] out, see above                                                */
+} lego_s2m_io;
+
+typedef struct lego_s2m lego_s2m;
+
+/* Scratch for up to max_problems problems whose map clouds hold up to max_map_points points each. */
+int  lego_s2m_create(int32_t device, int32_t max_problems, int32_t max_map_points, lego_s2m** out);
+void lego_s2m_destroy(lego_s2m* m);
+/* scan2MapOptimization of n problems, asynchronous on hip_stream (NULL = default).  LEGO_EINVAL when
+ * n is outside [1, max_problems]; a problem whose map cloud exceeds max_map_points gets status
+ * LEGO_S2M_ST_SKIPPED and info[0] = -1. */
+int  lego_s2m_run(lego_s2m* m, int32_t n, const lego_s2m_io* io, void* hip_stream);
+/* One problem from host clouds (blocking): the reference's per-scan call.  transform[6] and
+ * *degenerate are read and written; info[4] is written. */
+int  lego_s2m_run_host(lego_s2m* m, const lego_point* corner, int32_t n_corner, const lego_point* surf,
+                       int32_t n_surf, const lego_point* corner_map, int32_t n_corner_map,
+                       const lego_point* surf_map, int32_t n_surf_map, float* transform, int32_t* degenerate,
+                       int32_t* info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LEGO_S2M_H */

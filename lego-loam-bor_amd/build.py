@@ -1,6 +1,6 @@
 """Build the in-tree native libraries (no JIT cache: the .so files travel with the repo snapshot).
 
-  liblego_frontend.so  product: HIP kernels for gfx950 + C-ABI (include/lego_frontend.h)
+  liblego_frontend.so  product: HIP kernels for gfx950 + C-ABI (include/lego_frontend.h, include/lego_s2m.h)
   liblego_synth.so     synthetic VLP-16 / HDL-64E sweep generator (tests / bench input)
 
 Usage: python lego-loam-bor_amd/build.py [--force]
@@ -16,7 +16,7 @@ REPO = os.path.dirname(HERE)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("LEGO_OFFLOAD_ARCH", "gfx950")
 
-FRONTEND_SRC = ["lego_kernels.hip", "lego_frontend.hip"]
+FRONTEND_SRC = ["lego_kernels.hip", "lego_frontend.hip", "lego_s2m.hip"]
 FRONTEND_DEPS = FRONTEND_SRC + ["lego_device.h", "lego_libm.h", "lego_introsort.h"]
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "--offload-arch=" + ARCH,
              # numerics contract: no FMA contraction, IEEE division/sqrt
@@ -33,7 +33,8 @@ def _stale(target, deps):
 
 def build_frontend(force=False, profile=False):
     target = os.path.join(OUT, "liblego_frontend_prof.so" if profile else "liblego_frontend.so")
-    deps = [os.path.join(CSRC, f) for f in FRONTEND_DEPS] + [os.path.join(REPO, "include", "lego_frontend.h")]
+    deps = [os.path.join(CSRC, f) for f in FRONTEND_DEPS] + [os.path.join(REPO, "include", h)
+                                                          for h in ("lego_frontend.h", "lego_s2m.h")]
     if force or _stale(target, deps):
         cmd = [HIPCC] + HIP_FLAGS + (["-DLG_PROFILE"] if profile else []) + \
             [os.path.join(CSRC, f) for f in FRONTEND_SRC] + ["-o", target]

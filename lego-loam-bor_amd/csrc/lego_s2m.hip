@@ -1,0 +1,848 @@
+// lego_s2m.hip — scan-to-map LM on gfx950: MapOptimization::scan2MapOptimization
+// (LeGO-LOAM/src/mapOptmization.cpp:1315-1332) and what it calls, behind include/lego_s2m.h.
+//
+// One workgroup per problem (one mapping sequence's current scan against its surrounding map):
+//   1. hash grids over the two map clouds (replacing kdtreeCornerFromMap / kdtreeSurfFromMap,
+//      :1317-1318): cells of 1.01 m, so the 1 m ball the reference's kNN-5 gate admits (:1036, :1144)
+//      lies in the 27 cells around the query's; buckets hold points by a hash of the cell, each point
+//      tagged with its packed cell so the search skips colliding cells;
+//   2. up to 10 iterations (:1320-1328), each one pass over all queries (corner then surf, one lane a
+//      query): pointAssociateToMap, exact kNN-5 of the 1 m ball by (distance, index), the line fit
+//      (3x3 symmetric eigen solver, :1037-1131) or the plane fit (5x3 QR, :1145-1194), and the
+//      query's row of the normal equations accumulated in double; a block reduction; thread 0 solves
+//      the 6x6 system (QR, :1260), decides degeneracy at iteration 0 (:1262-1286) and convergence
+//      (:1294-1311).
+// Numerics follow oracle/s2m_oracle.cpp operation for operation (-ffp-contract=off; the Eigen pieces
+// are the same restatements), except the normal equations' double sums, whose order differs.
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <new>
+
+#include "../../include/lego_s2m.h"
+#include "lego_device.h"
+
+using namespace lg;
+
+namespace {
+
+constexpr int S2M_THREADS = 1024;
+constexpr int S2M_NB_MAX = 65536;  // hash buckets per map cloud (power of two)
+constexpr float S2M_CELL = 1.01f;  // cell edge: >= the 1 m kNN gate plus rounding
+constexpr int S2M_DIM = 1024;      // cells per axis a packed cell can hold (10 bits)
+
+LG_DEVICE int lane_id() { return threadIdx.x & 63; }
+LG_DEVICE int wave_id() { return threadIdx.x >> 6; }
+
+struct S2mScratch {  // per problem, per map cloud
+  int* start;        // [S2M_NB_MAX + 1] bucket ends after the build
+  float4* pts;       // [max_map_points] x, y, z, packed cell
+  int* idx;          // [max_map_points] index in the caller's cloud
+  float4* rows;      // [max_map_points][2] (corner scratch only) the queries' LM rows of an iteration
+};
+
+// ---- restated Eigen pieces (oracle/s2m_oracle.cpp) ------------------------------------------------
+LG_DEVICE float hypot_e(float x, float y) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  float p, qp;
+  if (ax > ay) { p = ax; qp = ay / p; }
+  else { p = ay; qp = ax / p; }
+  if (p == 0.f) return 0.f;
+  return p * sqrtf(1.f + qp * qp);
+}
+
+LG_DEVICE void givens(float p, float q, float& c, float& s) {
+  if (q == 0.f) {
+    c = p < 0.f ? -1.f : 1.f;
+    s = 0.f;
+  } else if (p == 0.f) {
+    c = 0.f;
+    s = q < 0.f ? 1.f : -1.f;
+  } else if (fabsf(p) > fabsf(q)) {
+    const float t = q / p;
+    float u = sqrtf(1.f + t * t);
+    if (p < 0.f) u = -u;
+    c = 1.f / u;
+    s = -t * c;
+  } else {
+    const float t = p / q;
+    float u = sqrtf(1.f + t * t);
+    if (q < 0.f) u = -u;
+    s = -1.f / u;
+    c = -t * s;
+  }
+}
+
+// SelfAdjointEigenSolver<Matrix3f> (Eigen 3.3.4): ascending eigenvalues, V column j = eigenvector j.
+// (Every array index is a compile-time constant after unrolling, so the state stays in registers.)
+LG_DEVICE void eig3(const float A[9], float ev[3], float V[9]) {
+  float m[9] = {A[0], 0.f, 0.f, A[3], A[4], 0.f, A[6], A[7], A[8]};
+  float scale = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) scale = fmaxf(scale, fabsf(m[k]));
+  if (scale == 0.f) scale = 1.f;
+  m[0] /= scale; m[3] /= scale; m[4] /= scale; m[6] /= scale; m[7] /= scale; m[8] /= scale;
+  float d[3], e[3];
+  e[2] = 0.f;
+  d[0] = m[0];
+  const float v1norm2 = m[6] * m[6];
+  if (v1norm2 <= FLT_MIN) {
+    d[1] = m[4]; d[2] = m[8]; e[0] = m[3]; e[1] = m[7];
+    V[0] = 1.f; V[1] = 0.f; V[2] = 0.f; V[3] = 0.f; V[4] = 1.f; V[5] = 0.f; V[6] = 0.f; V[7] = 0.f; V[8] = 1.f;
+  } else {
+    const float beta = sqrtf(m[3] * m[3] + v1norm2);
+    const float invBeta = 1.f / beta;
+    const float m01 = m[3] * invBeta, m02 = m[6] * invBeta;
+    const float q = 2.f * m01 * m[7] + m02 * (m[8] - m[4]);
+    d[1] = m[4] + m02 * q;
+    d[2] = m[8] - m02 * q;
+    e[0] = beta;
+    e[1] = m[7] - m01 * q;
+    V[0] = 1.f; V[1] = 0.f; V[2] = 0.f; V[3] = 0.f; V[4] = m01; V[5] = m02; V[6] = 0.f; V[7] = m02; V[8] = -m01;
+  }
+  // computeFromTridiagonal_impl (maxIterations 30, n = 3): end, start in {0, 1, 2}
+  int end = 2, start = 0, iter = 0;
+  const float precision = 2.f * FLT_EPSILON;
+  bool ok = true;
+  while (end > 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (i >= start && i < end &&
+          (fabsf(e[i]) <= (fabsf(d[i]) + fabsf(d[i + 1])) * precision || fabsf(e[i]) <= FLT_MIN))
+        e[i] = 0.f;
+    if (end == 2 && e[1] == 0.f) end = 1;
+    if (end == 1 && e[0] == 0.f) end = 0;
+    if (end <= 0) break;
+    iter++;
+    if (iter > 90) { ok = false; break; }
+    start = end - 1;
+    if (start == 1 && e[0] != 0.f) start = 0;
+    // tridiagonal_qr_step: Wilkinson shift
+    const float dE = end == 2 ? d[2] : d[1], dE1 = end == 2 ? d[1] : d[0], ee = end == 2 ? e[1] : e[0];
+    const float td = (dE1 - dE) * 0.5f;
+    float mu = dE;
+    if (td == 0.f) {
+      mu -= fabsf(ee);
+    } else {
+      const float e2 = ee * ee;
+      const float h = hypot_e(td, ee);
+      if (e2 == 0.f) mu -= (ee / (td + (td > 0.f ? 1.f : -1.f))) * (ee / h);
+      else mu -= e2 / (td + (td > 0.f ? h : -h));
+    }
+    float x = (start == 0 ? d[0] : d[1]) - mu, z = start == 0 ? e[0] : e[1];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k < start || k >= end) continue;
+      float c, s;
+      givens(x, z, c, s);
+      const float sdk = s * d[k] + c * e[k];
+      const float dkp1 = s * e[k] + c * d[k + 1];
+      d[k] = c * (c * d[k] - s * e[k]) - s * (c * e[k] - s * d[k + 1]);
+      d[k + 1] = s * sdk + c * dkp1;
+      e[k] = c * sdk - s * dkp1;
+      if (k > start) e[k - 1 >= 0 ? k - 1 : 0] = c * e[k - 1 >= 0 ? k - 1 : 0] - s * z;
+      x = e[k];
+      if (k < end - 1) {
+        z = -s * e[k + 1];
+        e[k + 1] = c * e[k + 1];
+      }
+      if (!(c == 1.f && s == 0.f))
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const float xi = V[r * 3 + k], yi = V[r * 3 + k + 1];
+          V[r * 3 + k] = c * xi - s * yi;
+          V[r * 3 + k + 1] = s * xi + c * yi;
+        }
+    }
+  }
+  if (ok) {  // ascending: the first minimum of d[i..2] to position i, columns swapped with it
+    int k = 0;
+    float best = d[0];
+    if (d[1] < best) { best = d[1]; k = 1; }
+    if (d[2] < best) { best = d[2]; k = 2; }
+    if (k == 1) {
+      const float t = d[0]; d[0] = d[1]; d[1] = t;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) { const float v = V[r * 3]; V[r * 3] = V[r * 3 + 1]; V[r * 3 + 1] = v; }
+    } else if (k == 2) {
+      const float t = d[0]; d[0] = d[2]; d[2] = t;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) { const float v = V[r * 3]; V[r * 3] = V[r * 3 + 2]; V[r * 3 + 2] = v; }
+    }
+    if (d[2] < d[1]) {
+      const float t = d[1]; d[1] = d[2]; d[2] = t;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) { const float v = V[r * 3 + 1]; V[r * 3 + 1] = V[r * 3 + 2]; V[r * 3 + 2] = v; }
+    }
+  }
+  ev[0] = d[0] * scale; ev[1] = d[1] * scale; ev[2] = d[2] * scale;
+}
+
+// ColPivHouseholderQR<Matrix<float, M, N>>::solve (M >= N), fully unrolled
+template <int M, int N>
+LG_DEVICE void qr_solve(const float* A_in, const float* b_in, float* x) {
+  float A[M * N];
+#pragma unroll
+  for (int k = 0; k < M * N; ++k) A[k] = A_in[k];
+  const float eps = FLT_EPSILON;
+  float nu[N], nd[N], hc[N];
+  int perm[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < M; ++r) s += A[r * N + k] * A[r * N + k];
+    nu[k] = nd[k] = sqrtf(s);
+    perm[k] = k;
+  }
+  float maxn = 0.f;
+#pragma unroll
+  for (int k = 0; k < N; ++k) maxn = fmaxf(maxn, nu[k]);
+  const float th_help = (maxn * eps) * (maxn * eps) / (float)M;
+  const float ndt = sqrtf(eps);
+  int nzp = N;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    int bc = k;
+    float bv = nu[k];
+#pragma unroll
+    for (int j = k + 1; j < N; ++j)
+      if (nu[j] > bv) { bv = nu[j]; bc = j; }
+    const float bsq = bv * bv;
+    if (nzp == N && bsq < th_help * (float)(M - k)) nzp = k;
+#pragma unroll
+    for (int j = k + 1; j < N; ++j)
+      if (j == bc) {
+#pragma unroll
+        for (int r = 0; r < M; ++r) { const float t = A[r * N + k]; A[r * N + k] = A[r * N + j]; A[r * N + j] = t; }
+        float t = nu[k]; nu[k] = nu[j]; nu[j] = t;
+        t = nd[k]; nd[k] = nd[j]; nd[j] = t;
+        const int p = perm[k]; perm[k] = perm[j]; perm[j] = p;
+      }
+    float tail = 0.f;
+#pragma unroll
+    for (int r = k + 1; r < M; ++r) tail += A[r * N + k] * A[r * N + k];
+    const float c0 = A[k * N + k];
+    float tau, beta;
+    if (tail <= FLT_MIN) {
+      tau = 0.f;
+      beta = c0;
+#pragma unroll
+      for (int r = k + 1; r < M; ++r) A[r * N + k] = 0.f;
+    } else {
+      beta = sqrtf(c0 * c0 + tail);
+      if (c0 >= 0.f) beta = -beta;
+#pragma unroll
+      for (int r = k + 1; r < M; ++r) A[r * N + k] = A[r * N + k] / (c0 - beta);
+      tau = (beta - c0) / beta;
+    }
+    hc[k] = tau;
+    A[k * N + k] = beta;
+    if (tau != 0.f)
+#pragma unroll
+      for (int j = k + 1; j < N; ++j) {
+        float t = A[k * N + j];
+#pragma unroll
+        for (int r = k + 1; r < M; ++r) t += A[r * N + k] * A[r * N + j];
+        A[k * N + j] -= tau * t;
+#pragma unroll
+        for (int r = k + 1; r < M; ++r) A[r * N + j] -= tau * A[r * N + k] * t;
+      }
+#pragma unroll
+    for (int j = k + 1; j < N; ++j) {
+      if (nu[j] != 0.f) {
+        float t = fabsf(A[k * N + j]) / nu[j];
+        t = (1.f + t) * (1.f - t);
+        if (t < 0.f) t = 0.f;
+        const float q = nu[j] / nd[j];
+        const float t2 = t * q * q;
+        if (t2 <= ndt) {
+          float s = 0.f;
+#pragma unroll
+          for (int r = k + 1; r < M; ++r) s += A[r * N + j] * A[r * N + j];
+          nd[j] = sqrtf(s);
+          nu[j] = nd[j];
+        } else {
+          nu[j] *= sqrtf(t);
+        }
+      }
+    }
+  }
+  float c[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) c[k] = b_in[k];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if (k >= nzp || hc[k] == 0.f) continue;
+    float t = c[k];
+#pragma unroll
+    for (int r = k + 1; r < M; ++r) t += A[r * N + k] * c[r];
+    c[k] -= hc[k] * t;
+#pragma unroll
+    for (int r = k + 1; r < M; ++r) c[r] -= hc[k] * A[r * N + k] * t;
+  }
+  float y[N];
+#pragma unroll
+  for (int i = N - 1; i >= 0; --i) {
+    y[i] = 0.f;
+    if (i >= nzp) continue;
+    float t = c[i];
+#pragma unroll
+    for (int j = i + 1; j < N; ++j)
+      if (j < nzp) t -= A[i * N + j] * y[j];
+    y[i] = t / A[i * N + i];
+  }
+#pragma unroll
+  for (int o = 0; o < N; ++o) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (perm[i] == o) v = y[i];
+    x[o] = v;
+  }
+}
+
+// largest eigenvalue of a symmetric 6x6 < 100 (:1267-1285); Rayleigh / Gershgorin bounds first
+__device__ __attribute__((noinline)) bool lmax6_below(const float* A, double thr) {
+  double dmax = -1e300, gmax = -1e300;
+  for (int i = 0; i < 6; ++i) {
+    double g = 0.0;
+    for (int j = 0; j < 6; ++j) g += fabs((double)A[i * 6 + j]);
+    dmax = fmax(dmax, (double)A[i * 6 + i]);
+    gmax = fmax(gmax, g);
+  }
+  if (dmax >= thr) return false;  // lambda_max >= max a_ii
+  if (gmax < thr) return true;    // lambda_max <= max row sum
+  double a[36];
+  for (int k = 0; k < 36; ++k) a[k] = A[k];
+  for (int sweep = 0; sweep < 50; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < 6; ++p)
+      for (int q = p + 1; q < 6; ++q) off += a[p * 6 + q] * a[p * 6 + q];
+    if (off < 1e-30) break;
+    for (int p = 0; p < 6; ++p)
+      for (int q = p + 1; q < 6; ++q) {
+        const double apq = a[p * 6 + q];
+        if (apq == 0.0) continue;
+        const double th = (a[q * 6 + q] - a[p * 6 + p]) / (2.0 * apq);
+        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < 6; ++k) {
+          const double akp = a[k * 6 + p], akq = a[k * 6 + q];
+          a[k * 6 + p] = c * akp - s * akq;
+          a[k * 6 + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < 6; ++k) {
+          const double apk = a[p * 6 + k], aqk = a[q * 6 + k];
+          a[p * 6 + k] = c * apk - s * aqk;
+          a[q * 6 + k] = s * apk + c * aqk;
+        }
+      }
+  }
+  double m = a[0];
+  for (int k = 1; k < 6; ++k) m = fmax(m, a[k * 6 + k]);
+  return m < thr;
+}
+
+// ---- hash grid -------------------------------------------------------------------------------------
+LG_DEVICE int cell_of(float v, float mn) { return (int)floorf((v - mn) / S2M_CELL); }
+LG_DEVICE int pack_cell(int cx, int cy, int cz) { return (cz << 20) | (cy << 10) | cx; }
+LG_DEVICE int bucket_of(int packed, int lg_nb) { return (int)(((unsigned)packed * 2654435761u) >> (32 - lg_nb)); }
+
+struct GridInfo {
+  float mn[3];
+  int lg_nb;
+  int ok;  // every cell fits the packing
+};
+
+LG_DEVICE float block_min(float v, float* red) {
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+  __syncthreads();
+  if (lane_id() == 0) red[wave_id()] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int w = 1; w < S2M_THREADS / 64; ++w) r = fminf(r, red[w]);
+  return r;
+}
+
+// Build one map cloud's grid (whole workgroup).  Afterwards start[b] = end of bucket b.
+LG_DEVICE void build_grid(const float4* __restrict__ cloud, int n, const S2mScratch& G, GridInfo& gi, float* red,
+                          int* flag) {
+  const int tid = threadIdx.x;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int j = tid; j < n; j += S2M_THREADS) {
+    const float4 p = cloud[j];
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  float lo[3], hi[3];
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = block_min(mn[a], red);
+    hi[a] = -block_min(-mx[a], red);
+  }
+  int lg = 8;
+  while (lg < 16 && (1 << lg) < n) ++lg;
+  const int nb = 1 << lg;
+  bool fits = true;
+  for (int a = 0; a < 3; ++a) fits = fits && (n == 0 || cell_of(hi[a], lo[a]) < S2M_DIM);
+  if (tid == 0) {
+    for (int a = 0; a < 3; ++a) gi.mn[a] = lo[a];
+    gi.lg_nb = lg;
+    gi.ok = fits ? 1 : 0;
+  }
+  for (int b = tid; b <= nb; b += S2M_THREADS) G.start[b] = 0;
+  __syncthreads();
+  if (!gi.ok) return;
+  for (int j = tid; j < n; j += S2M_THREADS) {
+    const float4 p = cloud[j];
+    const int pk = pack_cell(cell_of(p.x, lo[0]), cell_of(p.y, lo[1]), cell_of(p.z, lo[2]));
+    atomicAdd(&G.start[bucket_of(pk, lg)], 1);
+  }
+  __syncthreads();
+  // exclusive scan of the counts: a chunk per thread, then the chunk sums in thread 0 (nb <= 65536)
+  const int per = (nb + S2M_THREADS - 1) / S2M_THREADS;
+  const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+  int local = 0;
+  for (int b = b0; b < b1; ++b) local += G.start[b];
+  flag[tid] = local;
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int t = 0; t < S2M_THREADS; ++t) { const int v = flag[t]; flag[t] = run; run += v; }
+  }
+  __syncthreads();
+  int run = flag[tid];
+  for (int b = b0; b < b1; ++b) { const int c = G.start[b]; G.start[b] = run; run += c; }
+  __syncthreads();
+  for (int j = tid; j < n; j += S2M_THREADS) {
+    const float4 p = cloud[j];
+    const int pk = pack_cell(cell_of(p.x, lo[0]), cell_of(p.y, lo[1]), cell_of(p.z, lo[2]));
+    const int slot = atomicAdd(&G.start[bucket_of(pk, lg)], 1);
+    G.pts[slot] = make_float4(p.x, p.y, p.z, __int_as_float(pk));
+    G.idx[slot] = j;
+  }
+  __syncthreads();
+}
+
+// kNN-5 of q inside the 1 m ball by (distance, index): true when 5 points are closer than 1 (the
+// reference's pointSearchSqDis[4] < 1.0); slot[] index the grid's points; tie = equal distances
+// among the 6 nearest
+LG_DEVICE bool knn5(const S2mScratch& G, const GridInfo& gi, float4 q, int slot[5], bool& tie) {
+  float d[6];
+  int ix[6], sl[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { d[k] = 1.0f; ix[k] = 0x7fffffff; sl[k] = -1; }
+  const int qx = cell_of(q.x, gi.mn[0]), qy = cell_of(q.y, gi.mn[1]), qz = cell_of(q.z, gi.mn[2]);
+  for (int dz = -1; dz <= 1; ++dz)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int cx = qx + dx, cy = qy + dy, cz = qz + dz;
+        if (cx < 0 || cx >= S2M_DIM || cy < 0 || cy >= S2M_DIM || cz < 0 || cz >= S2M_DIM) continue;
+        const int pk = pack_cell(cx, cy, cz);
+        const int b = bucket_of(pk, gi.lg_nb);
+        const int e = G.start[b];
+        for (int j = b == 0 ? 0 : G.start[b - 1]; j < e; ++j) {
+          const float4 p = G.pts[j];
+          if (__float_as_int(p.w) != pk) continue;
+          const float ex = q.x - p.x, ey = q.y - p.y, ez = q.z - p.z;
+          const float dd = ex * ex + ey * ey + ez * ez;  // nanoflann L2_Simple_Adaptor order
+          if (!(dd < 1.0f)) continue;
+          const int id = G.idx[j];
+          if (!(dd < d[5] || (dd == d[5] && id < ix[5]))) continue;
+          d[5] = dd; ix[5] = id; sl[5] = j;
+#pragma unroll
+          for (int k = 5; k > 0; --k) {
+            if (d[k] < d[k - 1] || (d[k] == d[k - 1] && ix[k] < ix[k - 1])) {
+              float td = d[k]; d[k] = d[k - 1]; d[k - 1] = td;
+              int t = ix[k]; ix[k] = ix[k - 1]; ix[k - 1] = t;
+              t = sl[k]; sl[k] = sl[k - 1]; sl[k - 1] = t;
+            }
+          }
+        }
+      }
+  tie = false;
+  if (!(sl[4] >= 0)) return false;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    slot[k] = sl[k];
+    if (sl[k + 1] >= 0 && d[k] == d[k + 1]) tie = true;
+  }
+  return true;
+}
+
+struct Trig { float cRoll, sRoll, cPitch, sPitch, cYaw, sYaw, tX, tY, tZ; };
+
+// pointAssociateToMap (:412-426)
+LG_DEVICE float4 associate(const Trig& T, float4 pi) {
+  const float x1 = T.cYaw * pi.x - T.sYaw * pi.y;
+  const float y1 = T.sYaw * pi.x + T.cYaw * pi.y;
+  const float z1 = pi.z;
+  const float x2 = x1;
+  const float y2 = T.cRoll * y1 - T.sRoll * z1;
+  const float z2 = T.sRoll * y1 + T.cRoll * z1;
+  return make_float4(T.cPitch * x2 + T.sPitch * z2 + T.tX, y2 + T.tY, -T.sPitch * x2 + T.cPitch * z2 + T.tZ, pi.w);
+}
+
+// cornerOptimization's per-point body (:1037-1131)
+LG_DEVICE bool corner_coeff(const float4* nb, float4 sel, float4& coeff) {
+  float cx = 0, cy = 0, cz = 0;
+  for (int j = 0; j < 5; j++) { cx += nb[j].x; cy += nb[j].y; cz += nb[j].z; }
+  cx /= 5; cy /= 5; cz /= 5;
+  float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+  for (int j = 0; j < 5; j++) {
+    const float ax = nb[j].x - cx, ay = nb[j].y - cy, az = nb[j].z - cz;
+    a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+    a22 += ay * ay; a23 += ay * az; a33 += az * az;
+  }
+  a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+  const float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33};
+  float D[3], V[9];
+  eig3(A1, D, V);
+  if (!(D[2] > 3 * D[1])) return false;
+  const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+  const float x1 = (float)((double)cx + 0.1 * (double)V[0]), y1 = (float)((double)cy + 0.1 * (double)V[1]),
+              z1 = (float)((double)cz + 0.1 * (double)V[2]);
+  const float x2 = (float)((double)cx - 0.1 * (double)V[0]), y2 = (float)((double)cy - 0.1 * (double)V[1]),
+              z2 = (float)((double)cz - 0.1 * (double)V[2]);
+  const float m1 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+  const float m2 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+  const float m3 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+  const float a012 = sqrtf(m1 * m1 + m2 * m2 + m3 * m3);
+  const float l12 = sqrtf((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+  const float la = ((y1 - y2) * m1 + (z1 - z2) * m2) / a012 / l12;
+  const float lb = -((x1 - x2) * m1 - (z1 - z2) * m3) / a012 / l12;
+  const float lc = -((x1 - x2) * m2 + (y1 - y2) * m3) / a012 / l12;
+  const float ld2 = a012 / l12;
+  const float s = (float)(1.0 - 0.9 * (double)fabsf(ld2));
+  coeff = make_float4(s * la, s * lb, s * lc, s * ld2);
+  return (double)s > 0.1;
+}
+
+// surfOptimization's per-point body (:1145-1194)
+LG_DEVICE bool surf_coeff(const float4* nb, float4 sel, float4& coeff) {
+  float A0[15], B0[5], X0[3];
+  for (int j = 0; j < 5; j++) {
+    A0[j * 3 + 0] = nb[j].x; A0[j * 3 + 1] = nb[j].y; A0[j * 3 + 2] = nb[j].z;
+    B0[j] = -1.f;
+  }
+  qr_solve<5, 3>(A0, B0, X0);
+  float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+  const float ps = sqrtf(pa * pa + pb * pb + pc * pc);
+  pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+  for (int j = 0; j < 5; j++)
+    if ((double)fabsf(pa * nb[j].x + pb * nb[j].y + pc * nb[j].z + pd) > 0.2) return false;
+  const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+  const float s = (float)(1.0 - 0.9 * (double)fabsf(pd2) / (double)sqrtf(sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
+  coeff = make_float4(s * pa, s * pb, s * pc, s * pd2);
+  return (double)s > 0.1;
+}
+
+// One query of cornerOptimization / surfOptimization (:1030-1133, :1138-1196) and its
+// LMOptimization row (:1219-1256): r0 = (arx, ary, arz, coeff.x), r1 = (coeff.y, coeff.z,
+// -coeff.intensity, 1), or r1.w = 0 when the point is not selected.
+struct QueryRow {
+  float4 r0, r1;
+  int st;
+};
+__device__ __attribute__((noinline)) QueryRow query_row(bool is_corner, float4 ori, Trig T, S2mScratch G,
+                                                        GridInfo gi) {
+  QueryRow out;
+  out.r0 = make_float4(0.f, 0.f, 0.f, 0.f);
+  out.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
+  out.st = 0;
+  const float4 sel = associate(T, ori);
+  int sl[5];
+  bool tie = false;
+  if (!knn5(G, gi, sel, sl, tie)) return out;
+  if (tie) out.st |= LEGO_S2M_ST_KNN_TIE;
+  float4 nb[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) nb[j] = G.pts[sl[j]];
+  float4 c;
+  if (!(is_corner ? corner_coeff(nb, sel, c) : surf_coeff(nb, sel, c))) return out;
+  const float srx = T.sRoll, crx = T.cRoll, sry = T.sPitch, cry = T.cPitch, srz = T.sYaw, crz = T.cYaw;
+  const float arx = (crx * sry * srz * ori.x + crx * crz * sry * ori.y - srx * sry * ori.z) * c.x +
+                    (-srx * srz * ori.x - crz * srx * ori.y - crx * ori.z) * c.y +
+                    (crx * cry * srz * ori.x + crx * cry * crz * ori.y - cry * srx * ori.z) * c.z;
+  const float ary = ((cry * srx * srz - crz * sry) * ori.x + (sry * srz + cry * crz * srx) * ori.y + crx * cry * ori.z) * c.x +
+                    ((-cry * crz - srx * sry * srz) * ori.x + (cry * srz - crz * srx * sry) * ori.y - crx * sry * ori.z) * c.z;
+  const float arz = ((crz * srx * sry - cry * srz) * ori.x + (-cry * crz - srx * sry * srz) * ori.y) * c.x +
+                    (crx * crz * ori.x - crx * srz * ori.y) * c.y +
+                    ((sry * srz + cry * crz * srx) * ori.x + (crz * sry - cry * srx * srz) * ori.y) * c.z;
+  out.r0 = make_float4(arx, ary, arz, c.x);
+  out.r1 = make_float4(c.y, c.z, -c.w, 1.f);
+  return out;
+}
+
+struct S2mLds {
+  float red[S2M_THREADS / 64];
+  int scan[S2M_THREADS];
+  double acc[S2M_THREADS / 64][28];
+  GridInfo gc, gs;
+  float t[6];
+  Trig T;
+  int flag, status, iters, nsel, degenerate;
+};
+
+// LMOptimization's solve (:1257-1311) on the reduced normal equations (thread 0)
+__device__ __attribute__((noinline)) void lm_solve(S2mLds& L, int iterCount) {
+  double s[28];
+  for (int k = 0; k < 28; ++k) {
+    s[k] = 0.0;
+    for (int w = 0; w < S2M_THREADS / 64; ++w) s[k] += L.acc[w][k];
+  }
+  const int nsel = (int)s[27];
+  L.iters = iterCount + 1;
+  L.nsel = nsel;
+  bool conv = false;
+  if (nsel < 50) {
+    L.status |= LEGO_S2M_ST_FEW;
+  } else {
+    float A[36], Bv[6], X[6];
+    int k = 0;
+    for (int r = 0; r < 6; ++r)
+      for (int j = r; j < 6; ++j) { A[r * 6 + j] = A[j * 6 + r] = (float)s[k]; ++k; }
+    for (int r = 0; r < 6; ++r) Bv[r] = (float)s[21 + r];
+    qr_solve<6, 6>(A, Bv, X);
+    if (iterCount == 0) {
+      L.degenerate = lmax6_below(A, 100.0) ? 1 : 0;
+      if (L.degenerate) L.status |= LEGO_S2M_ST_DEGENERATE;
+    }
+    if (L.degenerate)
+      for (int j = 0; j < 6; ++j) X[j] = 0.f;  // matP = 0 (see oracle/s2m_oracle.cpp)
+    for (int j = 0; j < 6; ++j) L.t[j] += X[j];
+    const double r0 = (double)(X[0] * 57.29578f), r1 = (double)(X[1] * 57.29578f), r2 = (double)(X[2] * 57.29578f);
+    const double t0 = (double)(X[3] * 100), t1 = (double)(X[4] * 100), t2 = (double)(X[5] * 100);
+    const float deltaR = (float)sqrt(r0 * r0 + r1 * r1 + r2 * r2);
+    const float deltaT = (float)sqrt(t0 * t0 + t1 * t1 + t2 * t2);
+    conv = (double)deltaR < 0.05 && (double)deltaT < 0.05;
+    if (conv) L.status |= LEGO_S2M_ST_CONVERGED;
+  }
+  L.flag = conv ? 1 : 0;
+}
+
+__global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch* scratch, int max_map) {
+  __shared__ S2mLds L;
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const float4* corner = (const float4*)io.corner + io.corner_off[p];
+  const float4* surf = (const float4*)io.surf + io.surf_off[p];
+  const float4* cmap = (const float4*)io.corner_map + io.corner_map_off[p];
+  const float4* smap = (const float4*)io.surf_map + io.surf_map_off[p];
+  const int nc = io.corner_n[p], ns = io.surf_n[p], ncm = io.corner_map_n[p], nsm = io.surf_map_n[p];
+  int* info = io.info + 4 * p;
+  if (!(ncm > 10 && nsm > 100)) {  // :1316
+    if (tid == 0) { info[0] = 0; info[1] = 0; info[2] = 0; info[3] = LEGO_S2M_ST_SKIPPED; }
+    return;
+  }
+  if (ncm > max_map || nsm > max_map || nc < 0 || ns < 0 || nc + ns > max_map) {
+    if (tid == 0) { info[0] = -1; info[1] = 0; info[2] = 0; info[3] = LEGO_S2M_ST_SKIPPED; }
+    return;
+  }
+  const S2mScratch Gc = scratch[2 * p], Gs = scratch[2 * p + 1];
+  build_grid(cmap, ncm, Gc, L.gc, L.red, L.scan);
+  build_grid(smap, nsm, Gs, L.gs, L.red, L.scan);
+  if (tid == 0) {
+    for (int k = 0; k < 6; ++k) L.t[k] = io.transform[6 * p + k];
+    L.degenerate = io.degenerate[p];
+    L.status = 0;
+    L.iters = 0;
+    L.nsel = 0;
+    L.flag = 0;
+  }
+  __syncthreads();
+  if (!L.gc.ok || !L.gs.ok) {  // a map wider than 1024 cells (1 km) on an axis
+    if (tid == 0) { info[0] = -1; info[1] = 0; info[2] = 0; info[3] = LEGO_S2M_ST_SKIPPED; }
+    return;
+  }
+  const GridInfo gc = L.gc, gs = L.gs;
+  for (int iterCount = 0; iterCount < 10; iterCount++) {
+    if (tid == 0) {  // updatePointAssociateToMapSinCos (:397-410); LMOptimization's trig is the same
+      const float* t = L.t;
+      L.T = Trig{cosf_g(t[0]), sinf_g(t[0]), cosf_g(t[1]), sinf_g(t[1]), cosf_g(t[2]), sinf_g(t[2]), t[3], t[4], t[5]};
+    }
+    __syncthreads();
+    const Trig T = L.T;
+    // queries: each lane writes its query's LM row (or a zero flag) to the rows scratch
+    for (int q = tid; q < nc + ns; q += S2M_THREADS) {
+      const bool is_corner = q < nc;
+      const float4 ori = is_corner ? corner[q] : surf[q - nc];
+      const QueryRow r = query_row(is_corner, ori, T, is_corner ? Gc : Gs, is_corner ? gc : gs);
+      Gc.rows[2 * q] = r.r0;
+      Gc.rows[2 * q + 1] = r.r1;
+      if (r.st) atomicOr(&L.status, r.st);
+    }
+    __syncthreads();
+    // the normal equations (AtA upper triangle, AtB, count) in two passes of 14 double sums over the
+    // rows (register budget), each reduced over the wave and then per wave into LDS
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      double acc[14];
+#pragma unroll
+      for (int k = 0; k < 14; ++k) acc[k] = 0.0;
+      for (int q = tid; q < nc + ns; q += S2M_THREADS) {
+        const float4 r1 = Gc.rows[2 * q + 1];
+        if (r1.w == 0.f) continue;
+        const float4 r0 = Gc.rows[2 * q];
+        const float a[6] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y};
+        const float b = r1.z;
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+#pragma unroll
+          for (int j = r; j < 6; ++j) {
+            if (k >= 14 * half && k < 14 * half + 14) acc[k - 14 * half] += (double)(a[r] * a[j]);
+            ++k;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+          if (21 + r >= 14 * half && 21 + r < 14 * half + 14) acc[21 + r - 14 * half] += (double)(a[r] * b);
+        if (half == 1) acc[13] += 1.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 14; ++k)
+        for (int o = 32; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o);
+      if (lane_id() == 0)
+        for (int k = 0; k < 14; ++k) L.acc[wave_id()][14 * half + k] = acc[k];
+    }
+    __syncthreads();
+    if (tid == 0) lm_solve(L, iterCount);
+    __syncthreads();
+    if (L.flag) break;
+  }
+  if (tid == 0) {
+    for (int k = 0; k < 6; ++k) io.transform[6 * p + k] = L.t[k];
+    io.degenerate[p] = L.degenerate;
+    info[0] = 1;
+    info[1] = L.iters;
+    info[2] = L.nsel;
+    info[3] = L.status;
+  }
+}
+
+}  // namespace
+
+struct lego_s2m {
+  int device = 0;
+  int max_problems = 0, max_map = 0;
+  S2mScratch* d_scratch = nullptr;
+  void* d_mem = nullptr;
+  // host-call staging
+  lego_point* d_clouds = nullptr;
+  size_t cloud_cap = 0;
+  int64_t* d_meta = nullptr;  // 4 offsets + 4 counts (int32 after the offsets) + transform/degenerate/info
+};
+
+extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max_map_points, lego_s2m** out) {
+  if (!out) return LEGO_EINVAL;
+  *out = nullptr;
+  if (max_problems < 1 || max_map_points < 1 || max_map_points > LEGO_MAX_POINTS) return LEGO_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return LEGO_EDEVICE;
+  if (hipSetDevice(device) != hipSuccess) return LEGO_EDEVICE;
+  lego_s2m* m = new (std::nothrow) lego_s2m();
+  if (!m) return LEGO_ENOMEM;
+  m->device = device;
+  m->max_problems = max_problems;
+  m->max_map = max_map_points;
+  // per problem and map cloud: bucket table, points, indices
+  const size_t tab = (size_t)(S2M_NB_MAX + 1) * 4, pts = (size_t)max_map_points * 16, idx = (size_t)max_map_points * 4;
+  const size_t rows = (size_t)max_map_points * 32;
+  const size_t per = ((tab + 255) & ~(size_t)255) + pts + ((idx + 255) & ~(size_t)255) + rows;
+  if (hipMalloc(&m->d_mem, per * 2 * max_problems) != hipSuccess ||
+      hipMalloc((void**)&m->d_scratch, sizeof(S2mScratch) * 2 * max_problems) != hipSuccess ||
+      hipMalloc((void**)&m->d_meta, 256) != hipSuccess) {
+    lego_s2m_destroy(m);
+    return LEGO_ENOMEM;
+  }
+  S2mScratch* h = new (std::nothrow) S2mScratch[2 * max_problems];
+  if (!h) { lego_s2m_destroy(m); return LEGO_ENOMEM; }
+  char* base = (char*)m->d_mem;
+  for (int k = 0; k < 2 * max_problems; ++k) {
+    char* b = base + per * k;
+    h[k].start = (int*)b;
+    h[k].pts = (float4*)(b + ((tab + 255) & ~(size_t)255));
+    h[k].idx = (int*)(b + ((tab + 255) & ~(size_t)255) + pts);
+    h[k].rows = (float4*)(b + ((tab + 255) & ~(size_t)255) + pts + ((idx + 255) & ~(size_t)255));
+  }
+  const bool ok = hipMemcpy(m->d_scratch, h, sizeof(S2mScratch) * 2 * max_problems, hipMemcpyHostToDevice) == hipSuccess;
+  delete[] h;
+  if (!ok) { lego_s2m_destroy(m); return LEGO_EDEVICE; }
+  *out = m;
+  return LEGO_OK;
+}
+
+extern "C" void lego_s2m_destroy(lego_s2m* m) {
+  if (!m) return;
+  hipSetDevice(m->device);
+  hipDeviceSynchronize();
+  if (m->d_mem) hipFree(m->d_mem);
+  if (m->d_scratch) hipFree(m->d_scratch);
+  if (m->d_clouds) hipFree(m->d_clouds);
+  if (m->d_meta) hipFree(m->d_meta);
+  delete m;
+}
+
+extern "C" int lego_s2m_run(lego_s2m* m, int32_t n, const lego_s2m_io* io, void* hip_stream) {
+  if (!m || !io || n < 1 || n > m->max_problems) return LEGO_EINVAL;
+  if (!io->corner || !io->corner_off || !io->corner_n || !io->surf || !io->surf_off || !io->surf_n ||
+      !io->corner_map || !io->corner_map_off || !io->corner_map_n || !io->surf_map || !io->surf_map_off ||
+      !io->surf_map_n || !io->transform || !io->degenerate || !io->info)
+    return LEGO_EINVAL;
+  if (hipSetDevice(m->device) != hipSuccess) return LEGO_EDEVICE;
+  hipLaunchKernelGGL(k_s2m, dim3(n), dim3(S2M_THREADS), 0, (hipStream_t)hip_stream, *io, m->d_scratch, m->max_map);
+  return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+}
+
+extern "C" int lego_s2m_run_host(lego_s2m* m, const lego_point* corner, int32_t n_corner, const lego_point* surf,
+                                 int32_t n_surf, const lego_point* corner_map, int32_t n_corner_map,
+                                 const lego_point* surf_map, int32_t n_surf_map, float* transform, int32_t* degenerate,
+                                 int32_t* info) {
+  if (!m || !transform || !degenerate || !info || n_corner < 0 || n_surf < 0 || n_corner_map < 0 || n_surf_map < 0 ||
+      (n_corner && !corner) || (n_surf && !surf) || (n_corner_map && !corner_map) || (n_surf_map && !surf_map))
+    return LEGO_EINVAL;
+  if (hipSetDevice(m->device) != hipSuccess) return LEGO_EDEVICE;
+  const size_t total = (size_t)n_corner + n_surf + n_corner_map + n_surf_map;
+  if (total > m->cloud_cap) {
+    if (m->d_clouds) hipFree(m->d_clouds);
+    m->d_clouds = nullptr;
+    m->cloud_cap = 0;
+    if (hipMalloc((void**)&m->d_clouds, (total ? total : 1) * sizeof(lego_point)) != hipSuccess) return LEGO_ENOMEM;
+    m->cloud_cap = total;
+  }
+  const lego_point* src[4] = {corner, surf, corner_map, surf_map};
+  const int32_t cnt[4] = {n_corner, n_surf, n_corner_map, n_surf_map};
+  // meta: off[4] (int64), cnt[4] (int32), transform[6] (float), degenerate (int32), info[4] (int32)
+  struct Meta { int64_t off[4]; int32_t n[4]; float t[6]; int32_t dg; int32_t info[4]; } h;
+  int64_t o = 0;
+  for (int k = 0; k < 4; ++k) {
+    h.off[k] = o;
+    h.n[k] = cnt[k];
+    if (cnt[k] && hipMemcpy(m->d_clouds + o, src[k], (size_t)cnt[k] * sizeof(lego_point), hipMemcpyHostToDevice) != hipSuccess)
+      return LEGO_EDEVICE;
+    o += cnt[k];
+  }
+  for (int k = 0; k < 6; ++k) h.t[k] = transform[k];
+  h.dg = *degenerate;
+  for (int k = 0; k < 4; ++k) h.info[k] = 0;
+  if (hipMemcpy(m->d_meta, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) return LEGO_EDEVICE;
+  Meta* dm = (Meta*)m->d_meta;
+  lego_s2m_io io;
+  io.corner = m->d_clouds; io.corner_off = &dm->off[0]; io.corner_n = &dm->n[0];
+  io.surf = m->d_clouds; io.surf_off = &dm->off[1]; io.surf_n = &dm->n[1];
+  io.corner_map = m->d_clouds; io.corner_map_off = &dm->off[2]; io.corner_map_n = &dm->n[2];
+  io.surf_map = m->d_clouds; io.surf_map_off = &dm->off[3]; io.surf_map_n = &dm->n[3];
+  io.transform = dm->t;
+  io.degenerate = &dm->dg;
+  io.info = dm->info;
+  int rc = lego_s2m_run(m, 1, &io, nullptr);
+  if (rc) return rc;
+  if (hipMemcpy(&h, m->d_meta, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
+  for (int k = 0; k < 6; ++k) transform[k] = h.t[k];
+  *degenerate = h.dg;
+  for (int k = 0; k < 4; ++k) info[k] = h.info[k];
+  return LEGO_OK;
+}

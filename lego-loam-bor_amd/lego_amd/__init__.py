@@ -7,6 +7,7 @@ constructors raise.
   Frontend  — one sequence: cloud_handler() (ImageProjection::cloudHandler) and
               feature_association() (one FeatureAssociation::runFeatureAssociation iteration).
   Batch     — S independent sequences advanced one scan per step on device-resident input.
+  ScanToMap — MapOptimization::scan2MapOptimization for many problems at once (include/lego_s2m.h).
 """
 import ctypes as C
 import os
@@ -21,6 +22,13 @@ P = C.POINTER
 _lib = None
 
 
+class LegoS2mIo(C.Structure):
+    """lego_s2m_io (include/lego_s2m.h): device pointers of a batch of scan-to-map problems."""
+    _fields_ = [(n, C.c_void_p) for c in ("corner", "surf", "corner_map", "surf_map")
+                for n in (c, c + "_off", c + "_n")] + [("transform", C.c_void_p), ("degenerate", C.c_void_p),
+                                                       ("info", C.c_void_p)]
+
+
 class LegoError(RuntimeError):
     pass
 
@@ -31,6 +39,10 @@ def lib():
     if _lib is None:
         if not os.path.exists(A.LIB_FRONTEND):
             raise LegoError("liblego_frontend.so not built: run python lego-loam-bor_amd/build.py")
+        try:  # torch first: its HIP runtime (loaded RTLD_GLOBAL) then serves this library as well, so the
+            import torch  # noqa: F401  process has one runtime and torch's tensors / streams interoperate
+        except ImportError:
+            pass
         L = C.CDLL(A.LIB_FRONTEND)
         L.lego_abi_version.restype = C.c_int32
         L.lego_params_vlp16.argtypes = [P(LegoParams)]
@@ -61,6 +73,11 @@ def lib():
         L.lego_test_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int32, C.c_int32]
         L.lego_test_libm.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_int32, C.c_int32]
         L.lego_test_project_cells.argtypes = [P(LegoParams), P(C.c_float), C.c_int32, P(C.c_int32), P(C.c_int32)]
+        L.lego_s2m_create.argtypes = [C.c_int32, C.c_int32, C.c_int32, P(C.c_void_p)]
+        L.lego_s2m_destroy.argtypes = [C.c_void_p]
+        L.lego_s2m_run.argtypes = [C.c_void_p, C.c_int32, P(LegoS2mIo), C.c_void_p]
+        L.lego_s2m_run_host.argtypes = [C.c_void_p] + [C.c_void_p, C.c_int32] * 4 + [P(C.c_float), P(C.c_int32),
+                                                                                  P(C.c_int32)]
         _lib = L
     return _lib
 
@@ -208,3 +225,43 @@ class Batch:
         _check(lib().lego_batch_read_poses(self.h, out.ctypes.data_as(P(C.c_float)), st.ctypes.data_as(P(C.c_int32))),
                "lego_batch_read_poses")
         return out, st
+
+
+class ScanToMap:
+    """MapOptimization's scan-to-map LM (scan2MapOptimization, mapOptmization.cpp:1315-1332) on the GPU.
+
+    run_host(): one problem from host clouds, as the reference's mapping thread calls it per scan.
+    run():      many problems from device arrays (lego_s2m_io), one workgroup each.
+    """
+
+    def __init__(self, max_problems=1, max_map_points=200000, device=0):
+        h = C.c_void_p()
+        _check(lib().lego_s2m_create(int(device), int(max_problems), int(max_map_points), C.byref(h)),
+               "lego_s2m_create")
+        self.h = h
+        self.max_problems = int(max_problems)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().lego_s2m_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def run_host(self, corner, surf, corner_map, surf_map, transform, degenerate=0):
+        """Returns (transform[6] float32, degenerate, info[4] int32)."""
+        arrs = [np.ascontiguousarray(np.asarray(a, np.float32).reshape(-1, 4)) for a in (corner, surf, corner_map,
+                                                                                          surf_map)]
+        t = np.ascontiguousarray(np.asarray(transform, np.float32).reshape(6).copy())
+        dg = C.c_int32(int(degenerate))
+        info = np.zeros(4, np.int32)
+        args = []
+        for a in arrs:
+            args += [C.c_void_p(a.ctypes.data), len(a)]
+        _check(lib().lego_s2m_run_host(self.h, *args, t.ctypes.data_as(P(C.c_float)), C.byref(dg),
+                                       info.ctypes.data_as(P(C.c_int32))), "lego_s2m_run_host")
+        return t, dg.value, info
+
+    def run(self, n, io, stream=0):
+        """n problems described by a LegoS2mIo of device pointers; asynchronous on `stream`."""
+        _check(lib().lego_s2m_run(self.h, int(n), C.byref(io), C.c_void_p(stream)), "lego_s2m_run")

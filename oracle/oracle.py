@@ -17,7 +17,8 @@ P = C.POINTER
 
 
 def build(force=False):
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "lego_oracle.cpp")):
+    srcs = [os.path.join(HERE, f) for f in ("lego_oracle.cpp", "s2m_oracle.cpp")]
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-C", HERE, "liblego_oracle.so"])
 
 
@@ -97,3 +98,54 @@ def std_sort(keys, vals, is_float):
     v = np.ascontiguousarray(vals, dtype=np.int32).copy()
     lib().oracle_std_sort(k.ctypes.data_as(P(C.c_uint32)), v.ctypes.data_as(P(C.c_int32)), len(k), int(is_float))
     return k, v
+
+
+# ---- scan-to-map LM (oracle/s2m_oracle.cpp) ----------------------------------------------------------
+def _f32(a, cols=4):
+    import numpy as np
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32).reshape(-1, cols))
+
+
+def scan2map(corner, surf, corner_map, surf_map, transform, degenerate=0):
+    """MapOptimization::scan2MapOptimization restated: returns (transform[6], degenerate, info[4])."""
+    import numpy as np
+    L = lib()
+    c, s, cm, sm = (_f32(a) for a in (corner, surf, corner_map, surf_map))
+    t = np.ascontiguousarray(np.asarray(transform, dtype=np.float32).copy())
+    dg = C.c_int32(int(degenerate))
+    info = np.zeros(4, np.int32)
+    fp = lambda a: a.ctypes.data_as(P(C.c_float))  # noqa: E731
+    L.oracle_scan2map(fp(c), len(c), fp(s), len(s), fp(cm), len(cm), fp(sm), len(sm), fp(t), C.byref(dg),
+                      info.ctypes.data_as(P(C.c_int32)))
+    return t, dg.value, info
+
+
+def eig3(A):
+    import numpy as np
+    A = np.ascontiguousarray(np.asarray(A, np.float32).reshape(9))
+    ev = np.zeros(3, np.float32)
+    V = np.zeros(9, np.float32)
+    lib().oracle_eig3(A.ctypes.data_as(P(C.c_float)), ev.ctypes.data_as(P(C.c_float)), V.ctypes.data_as(P(C.c_float)))
+    return ev, V.reshape(3, 3)
+
+
+def qr_solve(A, b):
+    import numpy as np
+    A = np.ascontiguousarray(np.asarray(A, np.float32))
+    b = np.ascontiguousarray(np.asarray(b, np.float32).reshape(-1))
+    x = np.zeros(A.shape[1], np.float32)
+    f = {(5, 3): lib().oracle_qr53, (6, 6): lib().oracle_qr66}[A.shape]
+    f(A.ctypes.data_as(P(C.c_float)), b.ctypes.data_as(P(C.c_float)), x.ctypes.data_as(P(C.c_float)))
+    return x
+
+
+def knn5(cloud, queries):
+    """(indices [n,5], sq dists [n,5], flags [n]: bit 0 = 5th closer than 1, bit 1 = distance tie)."""
+    import numpy as np
+    m, q = _f32(cloud), _f32(queries)
+    ind = np.zeros((len(q), 5), np.int32)
+    d = np.zeros((len(q), 5), np.float32)
+    fl = np.zeros(len(q), np.int32)
+    lib().oracle_knn5(m.ctypes.data_as(P(C.c_float)), len(m), q.ctypes.data_as(P(C.c_float)), len(q),
+                      ind.ctypes.data_as(P(C.c_int32)), d.ctypes.data_as(P(C.c_float)), fl.ctypes.data_as(P(C.c_int32)))
+    return ind, d, fl

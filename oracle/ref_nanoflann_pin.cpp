@@ -4,11 +4,11 @@
 //
 // Builds the index exactly as nanoflann_pcl.h:100-138 does (KDTreeSingleIndexAdaptor<
 // SO3_Adaptor<float, Adaptor>, Adaptor, 3, int>, default leaf_max_size 10, bbox computed by
-// nanoflann) and queries it as nearestKSearch(k = 1) does (:141-152: KNNResultSet<float,int>(1),
-// default SearchParams).
+// nanoflann) and queries it as nearestKSearch(k) does (:141-152: KNNResultSet<float,int>(k), default
+// SearchParams); k = argv[1], 1 if absent (FeatureAssociation's 1-NN; MapOptimization uses k = 5).
 //
 // stdin:  int32 n_cloud, n_cloud x float32[3], int32 n_query, n_query x float32[3]
-// stdout: n_query x (int32 index, float32 sq_dist)
+// stdout: n_query x k x (int32 index, float32 sq_dist), nearest first
 #include <cstdint>
 #include <cstdio>
 #include <vector>
@@ -27,7 +27,11 @@ typedef nanoflann::KDTreeSingleIndexAdaptor<nanoflann::SO3_Adaptor<float, Adapto
 
 static bool rd(void* p, size_t n) { return fread(p, 1, n, stdin) == n; }
 
-int main() {
+#include <cstdlib>
+
+int main(int argc, char** argv) {
+  const int k = argc > 1 ? std::atoi(argv[1]) : 1;
+  if (k < 1) return 1;
   int32_t n = 0, m = 0;
   Adaptor a;
   if (!rd(&n, 4)) return 1;
@@ -39,14 +43,16 @@ int main() {
   Tree tree(3, a);
   tree.buildIndex();
   for (int i = 0; i < m; ++i) {
-    int idx = -1;
-    float d = 0.f;
-    nanoflann::KNNResultSet<float, int> rs(1);
-    rs.init(&idx, &d);
+    std::vector<int> idx(k, -1);
+    std::vector<float> d(k, 0.f);
+    nanoflann::KNNResultSet<float, int> rs(k);
+    rs.init(idx.data(), d.data());
     tree.findNeighbors(rs, &q[(size_t)i * 3], nanoflann::SearchParams());
-    int32_t oi = idx;
-    fwrite(&oi, 4, 1, stdout);
-    fwrite(&d, 4, 1, stdout);
+    for (int j = 0; j < k; ++j) {
+      int32_t oi = idx[j];
+      fwrite(&oi, 4, 1, stdout);
+      fwrite(&d[j], 4, 1, stdout);
+    }
   }
   return 0;
 }

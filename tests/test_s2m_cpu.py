@@ -1,0 +1,155 @@
+"""CPU tests of the scan-to-map oracle (oracle/s2m_oracle.cpp) and of the C-ABI surface of lego_s2m.h.
+
+The oracle restates MapOptimization::scan2MapOptimization (mapOptmization.cpp:1315-1332); the GPU
+path (tests/test_gpu_s2m.py) is checked against it.  Here: its restated pieces on their own
+(kNN-5 pinned against the reference's vendored nanoflann; the Eigen restatements against numpy
+double-precision answers), and whole problems built from the FA oracle's AssociationOut records.
+"""
+import ctypes as C
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from lego_amd import _abi as A
+from lego_amd import mapping as M
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def frames():
+    """AssociationOut records of one synthetic VLP-16 sequence (FA oracle)."""
+    import lego_amd as LA
+    orc = O.Oracle(LA.params_vlp16())
+    cfg = A.synth_cfg("vlp16")
+    out = []
+    for k in range(8):
+        orc.cloud_handler(A.synth_scan(cfg, 1, k))
+        out.append(orc.feature_association())
+    return out
+
+
+def test_eig3_restatement_is_an_eigendecomposition():
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        X = rng.normal(size=(5, 3)).astype(np.float32) * rng.uniform(0.01, 3.0, size=3).astype(np.float32)
+        A3 = np.cov(X.T, bias=True).astype(np.float32)
+        ev, V = O.eig3(A3)
+        ref = np.linalg.eigvalsh(A3.astype(np.float64))
+        assert np.all(np.diff(ev) >= 0)  # ascending, as SelfAdjointEigenSolver
+        np.testing.assert_allclose(ev, ref, rtol=1e-4, atol=1e-6 * max(1.0, ref[-1]))
+        np.testing.assert_allclose(V.T @ V, np.eye(3), atol=2e-6)
+        np.testing.assert_allclose(A3 @ V, V * ev, atol=2e-5 * max(1.0, ref[-1]))
+    # diagonal and already-tridiagonal inputs take the v1norm2 <= min branch
+    ev, V = O.eig3(np.diag([3.0, 1.0, 2.0]).astype(np.float32))
+    np.testing.assert_array_equal(ev, [1.0, 2.0, 3.0])
+    np.testing.assert_array_equal(np.abs(V), np.array([[0, 0, 1], [1, 0, 0], [0, 1, 0]], np.float32))
+
+
+def test_qr_restatement_solves():
+    rng = np.random.default_rng(4)
+    for _ in range(100):
+        A5 = rng.normal(size=(5, 3)).astype(np.float32)
+        b5 = -np.ones(5, np.float32)
+        ref = np.linalg.lstsq(A5.astype(np.float64), b5.astype(np.float64), rcond=None)[0]
+        np.testing.assert_allclose(O.qr_solve(A5, b5), ref, rtol=1e-4, atol=1e-5)
+        B = rng.normal(size=(8, 6)).astype(np.float32)
+        A6 = (B.T @ B).astype(np.float32)
+        b6 = rng.normal(size=6).astype(np.float32)
+        ref = np.linalg.solve(A6.astype(np.float64), b6.astype(np.float64))
+        np.testing.assert_allclose(O.qr_solve(A6, b6), ref, rtol=2e-3, atol=2e-3 * np.abs(ref).max())
+    # rank-deficient plane fit (collinear points): the pivots below threshold give zeros, no NaN
+    A5 = np.array([[1, 2, 3], [2, 4, 6], [3, 6, 9], [4, 8, 12], [5, 10, 15]], np.float32)
+    x = O.qr_solve(A5, -np.ones(5, np.float32))
+    assert np.all(np.isfinite(x))
+
+
+def _brute_knn5(cloud, q):
+    d = ((q[:, None, 0] - cloud[None, :, 0]) ** 2 + (q[:, None, 1] - cloud[None, :, 1]) ** 2) + (q[:, None, 2] - cloud[None, :, 2]) ** 2
+    order = np.lexsort((np.broadcast_to(np.arange(len(cloud)), d.shape), d), axis=1)[:, :6]
+    return order, np.take_along_axis(d, order, axis=1)
+
+
+def test_knn5_matches_brute_force(frames):
+    pr = M.build_problem(frames, 6)
+    cloud = pr["surf_map"]
+    rng = np.random.default_rng(5)
+    q = np.concatenate([cloud[rng.integers(0, len(cloud), 300)] + rng.normal(0, 0.2, (300, 4)).astype(np.float32),
+                        rng.uniform(-40, 40, (50, 4)).astype(np.float32)]).astype(np.float32)
+    ind, dist, fl = O.knn5(cloud, q)
+    bo, bd = _brute_knn5(cloud.astype(np.float32), q.astype(np.float32))
+    ok = bd[:, 4] < 1.0
+    np.testing.assert_array_equal((fl & 1) != 0, ok)
+    assert ok.sum() > 100
+    np.testing.assert_array_equal(ind[ok], bo[ok, :5])
+    assert np.array_equal(dist[ok].view(np.int32), bd[ok, :5].astype(np.float32).view(np.int32))
+    # a duplicated point: equal distances are flagged as a tie, order by index
+    _, d0 = _brute_knn5(cloud[:500], cloud[:500])
+    i = int(np.argmax(d0[:, 5] < 1.0))
+    assert d0[i, 5] < 1.0
+    dup = np.concatenate([cloud, cloud[i:i + 1]])
+    ind, dist, fl = O.knn5(dup, cloud[i:i + 1])
+    assert fl[0] == 3 and ind[0, 0] == i and ind[0, 1] == len(cloud)
+
+
+def test_knn5_pin_nanoflann(frames):
+    """The oracle's kNN-5 equals the reference's vendored nanoflann 1.3.0 nearestKSearch(k = 5) (built
+    from /root/reference into oracle/_ref) wherever the 6 nearest distances are distinct."""
+    if not os.path.exists("/root/reference/LeGO-LOAM/include/lego_loam/nanoflann.hpp"):
+        pytest.skip("reference sources not mounted here")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "ref"])
+    exe = os.path.join(REPO, "oracle", "_ref", "nanoflann_pin")
+    pr = M.build_problem(frames, 6)
+    rng = np.random.default_rng(6)
+    for cloud, scan in ((pr["surf_map"], pr["surf"]), (pr["corner_map"], pr["corner"])):
+        q = M.associate_to_map(scan, pr["transform"])[:600]
+        q = np.concatenate([q, cloud[rng.integers(0, len(cloud), 200)] + rng.normal(0, 0.1, (200, 4)).astype(np.float32)])
+        xyz = np.ascontiguousarray(cloud[:, :3], np.float32)
+        qq = np.ascontiguousarray(q[:, :3], np.float32)
+        blob = struct.pack("<i", len(xyz)) + xyz.tobytes() + struct.pack("<i", len(qq)) + qq.tobytes()
+        out = subprocess.run([exe, "5"], input=blob, stdout=subprocess.PIPE, check=True).stdout
+        res = np.frombuffer(out, dtype=np.dtype([("i", "<i4"), ("d", "<f4")])).reshape(len(qq), 5)
+        ind, dist, fl = O.knn5(cloud, q)
+        use = ((fl & 1) != 0) & ((fl & 2) == 0)
+        assert use.sum() > 100
+        np.testing.assert_array_equal(ind[use], res["i"][use])
+        assert np.array_equal(dist[use].view(np.int32), res["d"][use].view(np.int32))
+        # the gate: nanoflann's 5th distance < 1.0 exactly where the oracle found 5 in the ball
+        np.testing.assert_array_equal((fl & 1) != 0, res["d"][:, 4] < 1.0)
+
+
+def test_scan2map_oracle_converges(frames):
+    for k in (3, 7):
+        pr = M.build_problem(frames, k)
+        t, dg, info = O.scan2map(pr["corner"], pr["surf"], pr["corner_map"], pr["surf_map"], pr["transform"])
+        assert info[0] == 1 and 1 <= info[1] <= 10 and info[2] > 1000
+        assert info[3] & 0x08  # LEGO_S2M_ST_CONVERGED
+        assert dg == 0
+        assert np.all(np.isfinite(t))
+        # the perturbed guess is pulled back toward the sequence's odometry
+        assert np.abs(t - frames[k]["transform_sum"]).sum() < np.abs(pr["transform"] - frames[k]["transform_sum"]).sum()
+
+
+def test_scan2map_oracle_gates(frames):
+    pr = M.build_problem(frames, 5)
+    # :1316 map gate: corner map <= 10 points -> nothing runs, transform untouched
+    t, dg, info = O.scan2map(pr["corner"], pr["surf"], pr["corner_map"][:10], pr["surf_map"], pr["transform"])
+    assert info[0] == 0 and info[3] == 0x10 and np.array_equal(t, pr["transform"])
+    # :1208 fewer than 50 correspondences: no update in any iteration
+    t, dg, info = O.scan2map(pr["corner"][:5], pr["surf"][:20], pr["corner_map"], pr["surf_map"], pr["transform"])
+    assert info[0] == 1 and info[1] == 10 and info[3] & 0x04 and np.array_equal(t, pr["transform"])
+
+
+def test_s2m_abi_exports():
+    """liblego_frontend.so exports every entry point include/lego_s2m.h declares (no GPU needed)."""
+    import re
+    hdr = open(os.path.join(REPO, "include", "lego_s2m.h")).read()
+    names = set(re.findall(r"\b(lego_s2m_\w+)\s*\(", hdr))
+    assert names == {"lego_s2m_create", "lego_s2m_destroy", "lego_s2m_run", "lego_s2m_run_host"}
+    lib = C.CDLL(A.LIB_FRONTEND)
+    for n in names:
+        assert hasattr(lib, n), n
