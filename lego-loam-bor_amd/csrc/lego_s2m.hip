@@ -348,6 +348,13 @@ __device__ __attribute__((noinline)) bool lmax6_below(const float* A, double thr
 }
 
 // ---- hash grid -------------------------------------------------------------------------------------
+// the 27 cells around a query: offset (dx, dy, dz) + 1 packed 2 bits an axis, by |dx| + |dy| + |dz|
+__constant__ unsigned char c_s2m_order[27] = {
+    21,                                   // own cell (1, 1, 1)
+    20, 22, 17, 25, 5, 37,                // faces
+    16, 18, 24, 26, 4, 6, 36, 38, 1, 9, 33, 41,  // edges
+    0, 2, 8, 10, 32, 34, 40, 42};         // corners
+
 LG_DEVICE int cell_of(float v, float mn) { return (int)floorf((v - mn) / S2M_CELL); }
 LG_DEVICE int pack_cell(int cx, int cy, int cz) { return (cz << 20) | (cy << 10) | cx; }
 LG_DEVICE int bucket_of(int packed, int lg_nb) { return (int)(((unsigned)packed * 2654435761u) >> (32 - lg_nb)); }
@@ -434,35 +441,85 @@ LG_DEVICE bool knn5(const S2mScratch& G, const GridInfo& gi, float4 q, int slot[
   float d[6];
   int ix[6], sl[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) { d[k] = 1.0f; ix[k] = 0x7fffffff; sl[k] = -1; }
+  for (int k = 0; k < 6; ++k) { d[k] = 1.0f; ix[k] = -1; sl[k] = -1; }
   const int qx = cell_of(q.x, gi.mn[0]), qy = cell_of(q.y, gi.mn[1]), qz = cell_of(q.z, gi.mn[2]);
-  for (int dz = -1; dz <= 1; ++dz)
-    for (int dy = -1; dy <= 1; ++dy)
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int cx = qx + dx, cy = qy + dy, cz = qz + dz;
-        if (cx < 0 || cx >= S2M_DIM || cy < 0 || cy >= S2M_DIM || cz < 0 || cz >= S2M_DIM) continue;
-        const int pk = pack_cell(cx, cy, cz);
-        const int b = bucket_of(pk, gi.lg_nb);
-        const int e = G.start[b];
-        for (int j = b == 0 ? 0 : G.start[b - 1]; j < e; ++j) {
-          const float4 p = G.pts[j];
-          if (__float_as_int(p.w) != pk) continue;
-          const float ex = q.x - p.x, ey = q.y - p.y, ez = q.z - p.z;
-          const float dd = ex * ex + ey * ey + ez * ez;  // nanoflann L2_Simple_Adaptor order
-          if (!(dd < 1.0f)) continue;
-          const int id = G.idx[j];
-          if (!(dd < d[5] || (dd == d[5] && id < ix[5]))) continue;
-          d[5] = dd; ix[5] = id; sl[5] = j;
+  const float qv[3] = {q.x, q.y, q.z};
+  const int qc[3] = {qx, qy, qz};
+  // candidates ordered by (distance, index in the caller's cloud); the index is loaded only to break
+  // an exact distance tie (ix = -1: not loaded yet), so the common path has no dependent load
+  auto idx_of = [&](int k) {
+    if (ix[k] < 0) ix[k] = G.idx[sl[k]];
+    return ix[k];
+  };
+  auto consider = [&](const float4 p, int j, int pk) {
+    if (__float_as_int(p.w) != pk) return;  // another cell in the bucket
+    const float ex = q.x - p.x, ey = q.y - p.y, ez = q.z - p.z;
+    const float dd = ex * ex + ey * ey + ez * ez;  // nanoflann L2_Simple_Adaptor order
+    if (!(dd <= d[5]) || !(dd < 1.0f)) return;
+    int id = -1;
+    if (dd == d[5]) {
+      id = G.idx[j];
+      if (!(sl[5] < 0 || id < idx_of(5))) return;
+    }
+    d[5] = dd; ix[5] = id; sl[5] = j;
 #pragma unroll
-          for (int k = 5; k > 0; --k) {
-            if (d[k] < d[k - 1] || (d[k] == d[k - 1] && ix[k] < ix[k - 1])) {
-              float td = d[k]; d[k] = d[k - 1]; d[k - 1] = td;
-              int t = ix[k]; ix[k] = ix[k - 1]; ix[k - 1] = t;
-              t = sl[k]; sl[k] = sl[k - 1]; sl[k - 1] = t;
-            }
-          }
-        }
+    for (int k = 5; k > 0; --k) {
+      bool sw = d[k] < d[k - 1];
+      if (d[k] == d[k - 1] && sl[k - 1] >= 0) sw = idx_of(k) < idx_of(k - 1);
+      if (sw) {
+        float td = d[k]; d[k] = d[k - 1]; d[k - 1] = td;
+        int t = ix[k]; ix[k] = ix[k - 1]; ix[k - 1] = t;
+        t = sl[k]; sl[k] = sl[k - 1]; sl[k - 1] = t;
       }
+    }
+  };
+  // the query's cell, then its 6 faces, 12 edges and 8 corners (offsets packed 2 bits per axis); a
+  // neighbour whose box (shrunk by 1 mm against the cell assignment's rounding) lies farther than the
+  // current 6th distance holds no point that could enter the 6 nearest or tie them.  The next cell's
+  // bucket range is loaded while the current cell's points are.
+  auto cell_at = [&](int i, int cc[3]) {  // i-th cell in ring order; false if outside the packing
+    const int o = c_s2m_order[i];
+    cc[0] = qx + ((o & 3) - 1); cc[1] = qy + (((o >> 2) & 3) - 1); cc[2] = qz + (((o >> 4) & 3) - 1);
+    return cc[0] >= 0 && cc[0] < S2M_DIM && cc[1] >= 0 && cc[1] < S2M_DIM && cc[2] >= 0 && cc[2] < S2M_DIM;
+  };
+  auto range_of = [&](int i, int& b0, int& b1, int& pk) {
+    int cc[3];
+    if (!cell_at(i, cc)) { b0 = b1 = 0; pk = -1; return; }
+    pk = pack_cell(cc[0], cc[1], cc[2]);
+    const int b = bucket_of(pk, gi.lg_nb);
+    b1 = G.start[b];
+    b0 = b == 0 ? 0 : G.start[b - 1];
+  };
+  int n0, n1, npk;
+  range_of(0, n0, n1, npk);
+  for (int i = 0; i < 27; ++i) {
+    const int b0 = n0, b1 = n1, pk = npk;
+    if (i + 1 < 27) range_of(i + 1, n0, n1, npk);
+    if (pk < 0 || b0 >= b1) continue;
+    if (i > 0) {
+      int cc[3];
+      cell_at(i, cc);
+      float lb = 0.f;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        if (cc[a] == qc[a]) continue;
+        const float lo = gi.mn[a] + (float)cc[a] * S2M_CELL, hi = lo + S2M_CELL;
+        float e = fmaxf(fmaxf(lo - qv[a], qv[a] - hi), 0.f);
+        e = fmaxf(e - 1e-3f, 0.f);
+        lb += e * e;
+      }
+      if (lb > d[5]) continue;
+    }
+    int j = b0;
+    for (; j + 3 < b1; j += 4) {  // 4 loads in flight
+      float4 p4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p4[u] = G.pts[j + u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) consider(p4[u], j + u, pk);
+    }
+    for (; j < b1; ++j) consider(G.pts[j], j, pk);
+  }
   tie = false;
   if (!(sl[4] >= 0)) return false;
 #pragma unroll
@@ -557,6 +614,7 @@ __device__ __attribute__((noinline)) QueryRow query_row(bool is_corner, float4 o
   int sl[5];
   bool tie = false;
   if (!knn5(G, gi, sel, sl, tie)) return out;
+
   if (tie) out.st |= LEGO_S2M_ST_KNN_TIE;
   float4 nb[5];
 #pragma unroll
