@@ -348,13 +348,6 @@ __device__ __attribute__((noinline)) bool lmax6_below(const float* A, double thr
 }
 
 // ---- hash grid -------------------------------------------------------------------------------------
-// the 27 cells around a query: offset (dx, dy, dz) + 1 packed 2 bits an axis, by |dx| + |dy| + |dz|
-__constant__ unsigned char c_s2m_order[27] = {
-    21,                                   // own cell (1, 1, 1)
-    20, 22, 17, 25, 5, 37,                // faces
-    16, 18, 24, 26, 4, 6, 36, 38, 1, 9, 33, 41,  // edges
-    0, 2, 8, 10, 32, 34, 40, 42};         // corners
-
 LG_DEVICE int cell_of(float v, float mn) { return (int)floorf((v - mn) / S2M_CELL); }
 LG_DEVICE int pack_cell(int cx, int cy, int cz) { return (cz << 20) | (cy << 10) | cx; }
 LG_DEVICE int bucket_of(int packed, int lg_nb) { return (int)(((unsigned)packed * 2654435761u) >> (32 - lg_nb)); }
@@ -473,53 +466,41 @@ LG_DEVICE bool knn5(const S2mScratch& G, const GridInfo& gi, float4 q, int slot[
       }
     }
   };
-  // the query's cell, then its 6 faces, 12 edges and 8 corners (offsets packed 2 bits per axis); a
-  // neighbour whose box (shrunk by 1 mm against the cell assignment's rounding) lies farther than the
-  // current 6th distance holds no point that could enter the 6 nearest or tie them.  The next cell's
-  // bucket range is loaded while the current cell's points are.
-  auto cell_at = [&](int i, int cc[3]) {  // i-th cell in ring order; false if outside the packing
-    const int o = c_s2m_order[i];
-    cc[0] = qx + ((o & 3) - 1); cc[1] = qy + (((o >> 2) & 3) - 1); cc[2] = qz + (((o >> 4) & 3) - 1);
-    return cc[0] >= 0 && cc[0] < S2M_DIM && cc[1] >= 0 && cc[1] < S2M_DIM && cc[2] >= 0 && cc[2] < S2M_DIM;
-  };
-  auto range_of = [&](int i, int& b0, int& b1, int& pk) {
-    int cc[3];
-    if (!cell_at(i, cc)) { b0 = b1 = 0; pk = -1; return; }
-    pk = pack_cell(cc[0], cc[1], cc[2]);
-    const int b = bucket_of(pk, gi.lg_nb);
-    b1 = G.start[b];
-    b0 = b == 0 ? 0 : G.start[b - 1];
-  };
-  int n0, n1, npk;
-  range_of(0, n0, n1, npk);
-  for (int i = 0; i < 27; ++i) {
-    const int b0 = n0, b1 = n1, pk = npk;
-    if (i + 1 < 27) range_of(i + 1, n0, n1, npk);
-    if (pk < 0 || b0 >= b1) continue;
-    if (i > 0) {
-      int cc[3];
-      cell_at(i, cc);
-      float lb = 0.f;
+  // the query's cell, then its faces, edges and corners; a neighbour whose box (shrunk by 1 mm
+  // against the cell assignment's rounding) lies farther than the current 6th distance holds no
+  // point that could enter the 6 nearest or tie them
+  for (int ring = 0; ring <= 3; ++ring)
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (abs(dx) + abs(dy) + abs(dz) != ring) continue;
+          const int cc[3] = {qx + dx, qy + dy, qz + dz};
+          if (cc[0] < 0 || cc[0] >= S2M_DIM || cc[1] < 0 || cc[1] >= S2M_DIM || cc[2] < 0 || cc[2] >= S2M_DIM) continue;
+          if (ring > 0) {
+            float lb = 0.f;
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        if (cc[a] == qc[a]) continue;
-        const float lo = gi.mn[a] + (float)cc[a] * S2M_CELL, hi = lo + S2M_CELL;
-        float e = fmaxf(fmaxf(lo - qv[a], qv[a] - hi), 0.f);
-        e = fmaxf(e - 1e-3f, 0.f);
-        lb += e * e;
-      }
-      if (lb > d[5]) continue;
-    }
-    int j = b0;
-    for (; j + 3 < b1; j += 4) {  // 4 loads in flight
-      float4 p4[4];
+            for (int a = 0; a < 3; ++a) {
+              if (cc[a] == qc[a]) continue;
+              const float lo = gi.mn[a] + (float)cc[a] * S2M_CELL, hi = lo + S2M_CELL;
+              float e = fmaxf(fmaxf(lo - qv[a], qv[a] - hi), 0.f);
+              e = fmaxf(e - 1e-3f, 0.f);
+              lb += e * e;
+            }
+            if (lb > d[5]) continue;
+          }
+          const int pk = pack_cell(cc[0], cc[1], cc[2]);
+          const int b = bucket_of(pk, gi.lg_nb);
+          const int e = G.start[b];
+          int j = b == 0 ? 0 : G.start[b - 1];
+          for (; j + 3 < e; j += 4) {  // 4 loads in flight
+            float4 p4[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) p4[u] = G.pts[j + u];
+            for (int u = 0; u < 4; ++u) p4[u] = G.pts[j + u];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) consider(p4[u], j + u, pk);
-    }
-    for (; j < b1; ++j) consider(G.pts[j], j, pk);
-  }
+            for (int u = 0; u < 4; ++u) consider(p4[u], j + u, pk);
+          }
+          for (; j < e; ++j) consider(G.pts[j], j, pk);
+        }
   tie = false;
   if (!(sl[4] >= 0)) return false;
 #pragma unroll
