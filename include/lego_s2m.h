@@ -70,6 +70,38 @@ int  lego_s2m_run_host(lego_s2m* m, const lego_point* corner, int32_t n_corner, 
                        const lego_point* surf_map, int32_t n_surf_map, float* transform, int32_t* degenerate,
                        int32_t* info);
 
+/* ---- map-side cloud preparation ------------------------------------------------
+ * The clouds scan2MapOptimization consumes are built by extractSurroundingKeyFrames (:857-996) and
+ * downsampleCurrentScan (:999-1026) from two operations, batched here over n clouds (device arrays,
+ * asynchronous on hip_stream):
+ *   lego_map_transform  transformPointCloud (:443-473): part p of the input rotated / translated by
+ *                       pose[p] = (roll, pitch, yaw, x, y, z) of its key frame (PointTypePose), written
+ *                       at out + out_off[p] (parts written next to each other concatenate: the `+=`
+ *                       of :909-913 / :982-986);
+ *   lego_map_voxel      pcl::VoxelGrid<PointXYZI>::filter (PCL 1.7/1.8 applyFilter; leaves :71-78) of
+ *                       cloud c with leaf[c]: one centroid per occupied leaf in ascending leaf order,
+ *                       each the float sum of its points in input order (std::stable_sort's tie order,
+ *                       lego_params.voxel_tie_order = 1) divided by their count.  status[c] =
+ *                       LEGO_ST_VOXEL_OVERFLOW when the leaf indices would overflow int32 (PCL's warning
+ *                       path: the cloud is copied unfiltered).  Clouds hold at most max_map_points
+ *                       points (larger: out_n = -1). */
+typedef struct lego_map_transform_io {
+  const lego_point* in;  const int64_t* in_off;  const int32_t* in_n;
+  const float* pose;     /* [n][6] roll, pitch, yaw, x, y, z */
+  lego_point* out;       const int64_t* out_off;
+} lego_map_transform_io;
+typedef struct lego_map_voxel_io {
+  const lego_point* in;  const int64_t* in_off;  const int32_t* in_n;
+  const float* leaf;     /* [n] */
+  lego_point* out;       const int64_t* out_off; /* room for in_n[c] points */
+  int32_t* out_n;        /* [n] */
+  int32_t* status;       /* [n] */
+} lego_map_voxel_io;
+int  lego_map_transform(lego_s2m* m, int32_t n, const lego_map_transform_io* io, void* hip_stream);
+/* scratch for the call's n clouds of max_map_points each is allocated on first use (and regrown for a
+ * larger n, after a device synchronize) */
+int  lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* io, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

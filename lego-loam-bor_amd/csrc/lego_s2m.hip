@@ -15,12 +15,15 @@
 // Numerics follow oracle/s2m_oracle.cpp operation for operation (-ffp-contract=off; the Eigen pieces
 // are the same restatements), except the normal equations' double sums, whose order differs.
 #include <float.h>
+#include <string.h>  // (before rocprim, whose texture iterator uses memset)
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
 
 #include <new>
+
+#include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "../../include/lego_s2m.h"
 #include "lego_device.h"
@@ -762,6 +765,148 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch*
   }
 }
 
+
+// ---- map-side cloud preparation -------------------------------------------------------------------
+// transformPointCloud (:443-473) of part p (blockIdx.y) by its key pose
+__global__ __launch_bounds__(256) void k_map_transform(lego_map_transform_io io) {
+  const int p = blockIdx.y;
+  __shared__ float tr[9];
+  if (threadIdx.x == 0) {  // updateTransformPointCloudSinCos (:428-441): float cos / sin
+    const float* q = io.pose + 6 * p;
+    tr[0] = cosf_g(q[0]); tr[1] = sinf_g(q[0]); tr[2] = cosf_g(q[1]); tr[3] = sinf_g(q[1]);
+    tr[4] = cosf_g(q[2]); tr[5] = sinf_g(q[2]); tr[6] = q[3]; tr[7] = q[4]; tr[8] = q[5];
+  }
+  __syncthreads();
+  const float ctRoll = tr[0], stRoll = tr[1], ctPitch = tr[2], stPitch = tr[3], ctYaw = tr[4], stYaw = tr[5];
+  const float4* in = (const float4*)io.in + io.in_off[p];
+  float4* out = (float4*)io.out + io.out_off[p];
+  const int n = io.in_n[p];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const float4 f = in[i];
+    const float x1 = ctYaw * f.x - stYaw * f.y;
+    const float y1 = stYaw * f.x + ctYaw * f.y;
+    const float z1 = f.z;
+    const float x2 = x1;
+    const float y2 = ctRoll * y1 - stRoll * z1;
+    const float z2 = stRoll * y1 + ctRoll * z1;
+    out[i] = make_float4(ctPitch * x2 + stPitch * z2 + tr[6], y2 + tr[7], -stPitch * x2 + ctPitch * z2 + tr[8], f.w);
+  }
+}
+
+LG_DEVICE int block_excl_scan(int v, int* red, int& total) {
+  const int lane = lane_id(), w = wave_id();
+  int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  __syncthreads();
+  if (lane == 63) red[w] = x;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int k = 0; k < S2M_THREADS / 64; ++k) {
+    if (k < w) off += red[k];
+    tot += red[k];
+  }
+  total = tot;
+  return off + x - v;
+}
+
+// VoxelGrid, part 1 (PCL applyFilter up to the sort): bounds, leaf indices, the cloud's sort segment
+__global__ __launch_bounds__(S2M_THREADS) void k_vox_keys(lego_map_voxel_io io, unsigned* keys, unsigned* vals,
+                                                          int* seg_b, int* seg_e, int* ovf, int cap) {
+  __shared__ float red[S2M_THREADS / 64];
+  __shared__ int sh[8];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int n = io.in_n[c];
+  const float4* in = (const float4*)io.in + io.in_off[c];
+  if (n > cap || n < 0) {
+    if (tid == 0) { seg_b[c] = seg_e[c] = c * cap; ovf[c] = -1; }
+    return;
+  }
+  const float inv = 1.0f / io.leaf[c];  // inverse_leaf_size_
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = tid; i < n; i += S2M_THREADS) {  // getMinMax3D
+    const float4 p = in[i];
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  float lo[3], hi[3];
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = block_min(mn[a], red);
+    hi[a] = -block_min(-mx[a], red);
+  }
+  if (tid == 0) {
+    const long long dx = (long long)((hi[0] - lo[0]) * inv) + 1, dy = (long long)((hi[1] - lo[1]) * inv) + 1,
+                    dz = (long long)((hi[2] - lo[2]) * inv) + 1;
+    const int bad = n > 0 && dx * dy * dz > 2147483647LL;
+    int min_b[3], div_b[3];
+    for (int a = 0; a < 3; ++a) {
+      min_b[a] = (int)floorf(lo[a] * inv);
+      div_b[a] = (int)floorf(hi[a] * inv) - min_b[a] + 1;
+    }
+    sh[0] = min_b[0]; sh[1] = min_b[1]; sh[2] = min_b[2];
+    sh[3] = div_b[0]; sh[4] = div_b[0] * div_b[1];
+    sh[5] = bad;
+    seg_b[c] = c * cap;
+    seg_e[c] = c * cap + (bad ? 0 : n);
+    ovf[c] = bad;
+  }
+  __syncthreads();
+  if (sh[5]) return;
+  const float mb0 = (float)sh[0], mb1 = (float)sh[1], mb2 = (float)sh[2];
+  const int m1 = sh[3], m2 = sh[4];
+  unsigned* k = keys + (size_t)c * cap;
+  unsigned* v = vals + (size_t)c * cap;
+  for (int i = tid; i < n; i += S2M_THREADS) {
+    const float4 p = in[i];
+    const int i0 = (int)(floorf(p.x * inv) - mb0), i1 = (int)(floorf(p.y * inv) - mb1), i2 = (int)(floorf(p.z * inv) - mb2);
+    k[i] = (unsigned)(i0 + i1 * m1 + i2 * m2);
+    v[i] = (unsigned)i;
+  }
+}
+
+// VoxelGrid, part 2: one centroid per run of equal leaf index in the (stably) sorted keys
+__global__ __launch_bounds__(S2M_THREADS) void k_vox_reduce(lego_map_voxel_io io, const unsigned* keys,
+                                                            const unsigned* vals, const int* ovf, int cap) {
+  __shared__ int red[S2M_THREADS / 64];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int n = io.in_n[c];
+  const float4* in = (const float4*)io.in + io.in_off[c];
+  float4* out = (float4*)io.out + io.out_off[c];
+  if (ovf[c] < 0) {
+    if (tid == 0) { io.out_n[c] = -1; io.status[c] = 0; }
+    return;
+  }
+  if (ovf[c]) {  // PCL: "Leaf size is too small ... Integer indices would overflow": output = input
+    for (int i = tid; i < n; i += S2M_THREADS) out[i] = in[i];
+    if (tid == 0) { io.out_n[c] = n; io.status[c] = LEGO_ST_VOXEL_OVERFLOW; }
+    return;
+  }
+  const unsigned* k = keys + (size_t)c * cap;
+  const unsigned* v = vals + (size_t)c * cap;
+  int base = 0;
+  for (int t0 = 0; t0 < n; t0 += S2M_THREADS) {
+    const int i = t0 + tid;
+    const bool head = i < n && (i == 0 || k[i] != k[i - 1]);
+    int total;
+    const int slot = base + block_excl_scan(head ? 1 : 0, red, total);
+    if (head) {  // CentroidPoint: float sums in sorted order, / count
+      float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+      int j = i;
+      const unsigned key = k[i];
+      for (; j < n && k[j] == key; ++j) {
+        const float4 p = in[v[j]];
+        sx += p.x; sy += p.y; sz += p.z; si += p.w;
+      }
+      const float cnt = (float)(j - i);
+      out[slot] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+    }
+    base += total;
+  }
+  if (tid == 0) { io.out_n[c] = base; io.status[c] = 0; }
+}
+
 }  // namespace
 
 struct lego_s2m {
@@ -773,6 +918,13 @@ struct lego_s2m {
   lego_point* d_clouds = nullptr;
   size_t cloud_cap = 0;
   int64_t* d_meta = nullptr;  // 4 offsets + 4 counts (int32 after the offsets) + transform/degenerate/info
+  // VoxelGrid scratch, for vox_clouds clouds of up to max_map points: keys / values in and sorted, the
+  // clouds' sort segments and overflow flags, rocprim's temporary storage
+  int vox_clouds = 0;
+  unsigned *d_keys = nullptr, *d_vals = nullptr, *d_keys2 = nullptr, *d_vals2 = nullptr;
+  int *d_seg = nullptr, *d_ovf = nullptr;
+  void* d_sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
 };
 
 extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max_map_points, lego_s2m** out) {
@@ -822,6 +974,9 @@ extern "C" void lego_s2m_destroy(lego_s2m* m) {
   if (m->d_scratch) hipFree(m->d_scratch);
   if (m->d_clouds) hipFree(m->d_clouds);
   if (m->d_meta) hipFree(m->d_meta);
+  for (void* p : {(void*)m->d_keys, (void*)m->d_vals, (void*)m->d_keys2, (void*)m->d_vals2, (void*)m->d_seg,
+                  (void*)m->d_ovf, m->d_sort_tmp})
+    if (p) hipFree(p);
   delete m;
 }
 
@@ -884,4 +1039,59 @@ extern "C" int lego_s2m_run_host(lego_s2m* m, const lego_point* corner, int32_t 
   *degenerate = h.dg;
   for (int k = 0; k < 4; ++k) info[k] = h.info[k];
   return LEGO_OK;
+}
+
+extern "C" int lego_map_transform(lego_s2m* m, int32_t n, const lego_map_transform_io* io, void* hip_stream) {
+  if (!m || !io || n < 1 || !io->in || !io->in_off || !io->in_n || !io->pose || !io->out || !io->out_off)
+    return LEGO_EINVAL;
+  if (hipSetDevice(m->device) != hipSuccess) return LEGO_EDEVICE;
+  hipLaunchKernelGGL(k_map_transform, dim3(16, n), dim3(256), 0, (hipStream_t)hip_stream, *io);
+  return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+}
+
+extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* io, void* hip_stream) {
+  if (!m || !io || n < 1 || !io->in || !io->in_off || !io->in_n || !io->leaf ||
+      !io->out || !io->out_off || !io->out_n || !io->status)
+    return LEGO_EINVAL;
+  if (hipSetDevice(m->device) != hipSuccess) return LEGO_EDEVICE;
+  const int cap = m->max_map;
+  if (n > m->vox_clouds) {  // scratch for n clouds of up to max_map_points (grows, never shrinks)
+    const int nc = n;
+    const size_t e = (size_t)nc * cap;
+    if (e >= (1ull << 32)) return LEGO_EINVAL;
+    size_t tmp = 0;
+    if (rocprim::segmented_radix_sort_pairs((void*)nullptr, tmp, (unsigned*)nullptr, (unsigned*)nullptr,
+                                            (unsigned*)nullptr, (unsigned*)nullptr, (unsigned)e, (unsigned)nc,
+                                            (int*)nullptr, (int*)nullptr, 0, 32) != hipSuccess)
+      return LEGO_EDEVICE;
+    hipDeviceSynchronize();  // earlier calls may still use the old scratch
+    for (void* p : {(void*)m->d_keys, (void*)m->d_vals, (void*)m->d_keys2, (void*)m->d_vals2, (void*)m->d_seg,
+                    (void*)m->d_ovf, m->d_sort_tmp})
+      if (p) hipFree(p);
+    m->d_keys = m->d_vals = m->d_keys2 = m->d_vals2 = nullptr;
+    m->d_seg = m->d_ovf = nullptr;
+    m->d_sort_tmp = nullptr;
+    m->vox_clouds = 0;
+    if (hipMalloc((void**)&m->d_keys, e * 4) != hipSuccess || hipMalloc((void**)&m->d_vals, e * 4) != hipSuccess ||
+        hipMalloc((void**)&m->d_keys2, e * 4) != hipSuccess || hipMalloc((void**)&m->d_vals2, e * 4) != hipSuccess ||
+        hipMalloc((void**)&m->d_seg, (size_t)nc * 2 * 4) != hipSuccess ||
+        hipMalloc((void**)&m->d_ovf, (size_t)nc * 4) != hipSuccess || hipMalloc(&m->d_sort_tmp, tmp) != hipSuccess)
+      return LEGO_ENOMEM;
+    m->sort_tmp_bytes = tmp;
+    m->vox_clouds = nc;
+  }
+  hipStream_t st = (hipStream_t)hip_stream;
+  int* seg_b = m->d_seg;
+  int* seg_e = m->d_seg + m->vox_clouds;
+  hipLaunchKernelGGL(k_vox_keys, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys, m->d_vals, seg_b, seg_e, m->d_ovf,
+                     cap);
+  if (hipGetLastError() != hipSuccess) return LEGO_EDEVICE;
+  // stable LSD radix sort of every cloud's (leaf index, point index) pairs: std::stable_sort's order
+  size_t tmp = m->sort_tmp_bytes;
+  if (rocprim::segmented_radix_sort_pairs(m->d_sort_tmp, tmp, m->d_keys, m->d_keys2, m->d_vals, m->d_vals2,
+                                          (unsigned)((size_t)n * cap), (unsigned)n, seg_b, seg_e, 0, 32, st) !=
+      hipSuccess)
+    return LEGO_EDEVICE;
+  hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys2, m->d_vals2, m->d_ovf, cap);
+  return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }

@@ -22,6 +22,16 @@ P = C.POINTER
 _lib = None
 
 
+class LegoMapTransformIo(C.Structure):
+    """lego_map_transform_io (include/lego_s2m.h)."""
+    _fields_ = [(n, C.c_void_p) for n in ("in_", "in_off", "in_n", "pose", "out", "out_off")]
+
+
+class LegoMapVoxelIo(C.Structure):
+    """lego_map_voxel_io (include/lego_s2m.h)."""
+    _fields_ = [(n, C.c_void_p) for n in ("in_", "in_off", "in_n", "leaf", "out", "out_off", "out_n", "status")]
+
+
 class LegoS2mIo(C.Structure):
     """lego_s2m_io (include/lego_s2m.h): device pointers of a batch of scan-to-map problems."""
     _fields_ = [(n, C.c_void_p) for c in ("corner", "surf", "corner_map", "surf_map")
@@ -78,6 +88,8 @@ def lib():
         L.lego_s2m_run.argtypes = [C.c_void_p, C.c_int32, P(LegoS2mIo), C.c_void_p]
         L.lego_s2m_run_host.argtypes = [C.c_void_p] + [C.c_void_p, C.c_int32] * 4 + [P(C.c_float), P(C.c_int32),
                                                                                   P(C.c_int32)]
+        L.lego_map_transform.argtypes = [C.c_void_p, C.c_int32, P(LegoMapTransformIo), C.c_void_p]
+        L.lego_map_voxel.argtypes = [C.c_void_p, C.c_int32, P(LegoMapVoxelIo), C.c_void_p]
         _lib = L
     return _lib
 
@@ -265,3 +277,11 @@ class ScanToMap:
     def run(self, n, io, stream=0):
         """n problems described by a LegoS2mIo of device pointers; asynchronous on `stream`."""
         _check(lib().lego_s2m_run(self.h, int(n), C.byref(io), C.c_void_p(stream)), "lego_s2m_run")
+
+    def map_transform(self, n, io, stream=0):
+        """transformPointCloud of n parts (LegoMapTransformIo of device pointers); asynchronous."""
+        _check(lib().lego_map_transform(self.h, int(n), C.byref(io), C.c_void_p(stream)), "lego_map_transform")
+
+    def map_voxel(self, n, io, stream=0):
+        """pcl::VoxelGrid::filter of n clouds (LegoMapVoxelIo of device pointers); asynchronous."""
+        _check(lib().lego_map_voxel(self.h, int(n), C.byref(io), C.c_void_p(stream)), "lego_map_voxel")

@@ -79,3 +79,148 @@ def build_problem(frames, k, n_keys=10, perturb=(0.002, 0.002, 0.004, 0.03, 0.01
     t0 = np.asarray(f["transform_sum"], np.float32) + np.asarray(perturb, np.float32)
     return {"corner": corner, "surf": surf, "corner_map": corner_map, "surf_map": surf_map,
             "transform": t0.astype(np.float32)}
+
+
+# ---- the same preparation on the GPU (lego_map_transform / lego_map_voxel) ---------------------------
+SCAN_CLOUDS = ("corner", "surf", "corner_map", "surf_map")
+
+
+def _parts(frames, k, n_keys):
+    """The clouds build_problem assembles, as (key-frame parts, current-scan clouds)."""
+    lo = max(0, k - n_keys)
+    corner_parts = [(frames[j]["corner_last"], frames[j]["transform_sum"]) for j in range(lo, k)]
+    surf_parts = []
+    for j in range(lo, k):  # per key frame: its surf cloud, then its outlier cloud (:909-913, :982-986)
+        surf_parts += [(frames[j]["surf_last"], frames[j]["transform_sum"]),
+                       (frames[j]["outlier_last"], frames[j]["transform_sum"])]
+    f = frames[k]
+    return corner_parts, surf_parts, (f["corner_last"], f["surf_last"], f["outlier_last"])
+
+
+def prepare_gpu(s2m, sequences, k, n_keys=10, perturb=(0.002, 0.002, 0.004, 0.03, 0.01, 0.03), stream=0,
+                events=None):
+    """GPU version of build_problem for many sequences at once: the scan-to-map problem of scan k of
+    every sequence (a list of AssociationOut-like records per sequence), built on the device with
+    lego_map_transform (key frames into the map frame, concatenated) and lego_map_voxel (the
+    reference's leaves; downsampleCurrentScan's surf total = VoxelGrid(VoxelGrid(surf) ++
+    VoxelGrid(outlier))).  Two launches of each, one host read of the first VoxelGrid's counts.
+
+    Returns (io, keep, transform, degenerate, info, views): a LegoS2mIo for ScanToMap.run, the tensors
+    behind it, the transform / degenerate / info tensors it points at, and the VoxelGrid outputs
+    (for tests).  events = (start, end) torch.cuda.Events are recorded around the device work (after the
+    key frames' upload; including the count read between the two VoxelGrid launches).
+    """
+    import torch
+    from . import LegoMapTransformIo, LegoMapVoxelIo, LegoS2mIo
+    P_ = len(sequences)
+    dev = "cuda"
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float32).reshape(-1, 4))  # noqa: E731
+
+    # 1. key-frame parts of every problem: corner map parts, then surf map parts
+    cparts, sparts, scans = zip(*[_parts(seq, k, n_keys) for seq in sequences])
+    parts = [(f32(c), t) for pp in cparts for (c, t) in pp] + [(f32(c), t) for pp in sparts for (c, t) in pp]
+    n_c = [sum(len(f32(c)) for c, _ in pp) for pp in cparts]
+    n_s = [sum(len(f32(c)) for c, _ in pp) for pp in sparts]
+    sizes = np.array([len(a) for a, _ in parts], np.int32)
+    in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    raw = torch.from_numpy(np.concatenate([a for a, _ in parts]) if len(parts) else np.zeros((1, 4), np.float32)).to(dev)
+    poses = torch.from_numpy(np.stack([np.asarray(t, np.float32) for _, t in parts])).to(dev)
+    # concatenated outputs: problem p's corner map raw cloud, then (after all of them) surf map raw clouds
+    map_raw = torch.empty((max(1, int(sizes.sum())), 4), dtype=torch.float32, device=dev)
+    keep = [raw, poses, map_raw]
+    t_io = LegoMapTransformIo()
+    t_in_off = torch.from_numpy(in_off).to(dev)
+    t_in_n = torch.from_numpy(sizes).to(dev)
+    keep += [t_in_off, t_in_n]
+    t_io.in_, t_io.in_off, t_io.in_n, t_io.pose = raw.data_ptr(), t_in_off.data_ptr(), t_in_n.data_ptr(), poses.data_ptr()
+    t_io.out, t_io.out_off = map_raw.data_ptr(), t_in_off.data_ptr()  # parts land next to each other
+    sc = [f32(x) for tri in scans for x in tri]  # per problem: corner, surf, outlier
+    scan_raw = torch.from_numpy(np.concatenate(sc) if sc else np.zeros((1, 4), np.float32)).to(dev)
+    sc_n = np.array([len(a) for a in sc], np.int32)
+    if events is not None:
+        events[0].record()
+    s2m.map_transform(len(parts), t_io, stream)
+
+    # 2. VoxelGrid: corner maps (0.2), surf maps (0.4), the scans' corner (0.2), surf (0.4), outlier (0.4)
+    sc_off = np.concatenate([[0], np.cumsum(sc_n)[:-1]]).astype(np.int64)
+    # the voxel inputs as (base tensor, offset) pairs: map clouds live in map_raw, scans in scan_raw
+    c_off = np.concatenate([[0], np.cumsum(n_c)[:-1]]).astype(np.int64)
+    s_off = int(sum(n_c)) + np.concatenate([[0], np.cumsum(n_s)[:-1]]).astype(np.int64)
+    # one input base for the launch: map_raw ++ scan_raw
+    both = torch.cat([map_raw[:int(sizes.sum())], scan_raw[:int(sc_n.sum())]]) if sizes.sum() or sc_n.sum() \
+        else torch.zeros((1, 4), dtype=torch.float32, device=dev)
+    base_sc = int(sizes.sum())
+    v_off = np.concatenate([c_off, s_off, base_sc + sc_off]).astype(np.int64)
+    v_n = np.concatenate([n_c, n_s, sc_n]).astype(np.int32)
+    leaf = np.concatenate([np.full(P_, 0.2), np.full(P_, 0.4),
+                           np.tile(np.array([0.2, 0.4, 0.4]), P_)]).astype(np.float32)
+    nv = len(v_n)
+    v_out = torch.empty((max(1, int(v_n.sum())), 4), dtype=torch.float32, device=dev)
+    out_off = np.concatenate([[0], np.cumsum(v_n)[:-1]]).astype(np.int64)
+    tens = {n: torch.from_numpy(a).to(dev) for n, a in (("off", v_off), ("n", v_n), ("leaf", leaf), ("oo", out_off))}
+    out_n = torch.zeros(nv, dtype=torch.int32, device=dev)
+    status = torch.zeros(nv, dtype=torch.int32, device=dev)
+    keep += [scan_raw, both, v_out, out_n, status] + list(tens.values())
+    v_io = LegoMapVoxelIo()
+    v_io.in_, v_io.in_off, v_io.in_n, v_io.leaf = both.data_ptr(), tens["off"].data_ptr(), tens["n"].data_ptr(), \
+        tens["leaf"].data_ptr()
+    v_io.out, v_io.out_off, v_io.out_n, v_io.status = v_out.data_ptr(), tens["oo"].data_ptr(), out_n.data_ptr(), \
+        status.data_ptr()
+    s2m.map_voxel(nv, v_io, stream)
+    on = out_n.cpu().numpy()  # the one host read: where the surf total clouds start
+
+    # 3. surf total = VoxelGrid(surf DS ++ outlier DS) of each scan (leaf 0.4)
+    i_sd = 2 * P_ + 3 * np.arange(P_) + 1  # the scans' surf DS entries; outlier DS follows each
+    tot_n = (on[i_sd] + on[i_sd + 1]).astype(np.int32)
+    tot_off = np.concatenate([[0], np.cumsum(tot_n)[:-1]]).astype(np.int64)
+    tot_raw = torch.empty((max(1, int(tot_n.sum())), 4), dtype=torch.float32, device=dev)
+    # concatenation by the identity transform (cos 0 = 1, sin 0 = 0: every coordinate copied exactly)
+    cat_in_off = np.stack([out_off[i_sd], out_off[i_sd + 1]], 1).reshape(-1).astype(np.int64)
+    cat_n = np.stack([on[i_sd], on[i_sd + 1]], 1).reshape(-1).astype(np.int32)
+    cat_out_off = np.stack([tot_off, tot_off + on[i_sd]], 1).reshape(-1).astype(np.int64)
+    ident = torch.zeros((2 * P_, 6), dtype=torch.float32, device=dev)
+    ct = {n: torch.from_numpy(a).to(dev) for n, a in (("io", cat_in_off), ("n", cat_n), ("oo", cat_out_off))}
+    keep += [tot_raw, ident] + list(ct.values())
+    c_io = LegoMapTransformIo()
+    c_io.in_, c_io.in_off, c_io.in_n, c_io.pose = v_out.data_ptr(), ct["io"].data_ptr(), ct["n"].data_ptr(), \
+        ident.data_ptr()
+    c_io.out, c_io.out_off = tot_raw.data_ptr(), ct["oo"].data_ptr()
+    s2m.map_transform(2 * P_, c_io, stream)
+    t2 = {n: torch.from_numpy(a).to(dev) for n, a in (("off", tot_off), ("n", tot_n),
+                                                       ("leaf", np.full(P_, 0.4, np.float32)))}
+    tot_out = torch.empty_like(tot_raw)
+    tot_on = torch.zeros(P_, dtype=torch.int32, device=dev)
+    tot_st = torch.zeros(P_, dtype=torch.int32, device=dev)
+    keep += [tot_out, tot_on, tot_st] + list(t2.values())
+    v2 = LegoMapVoxelIo()
+    v2.in_, v2.in_off, v2.in_n, v2.leaf = tot_raw.data_ptr(), t2["off"].data_ptr(), t2["n"].data_ptr(), \
+        t2["leaf"].data_ptr()
+    v2.out, v2.out_off, v2.out_n, v2.status = tot_out.data_ptr(), t2["off"].data_ptr(), tot_on.data_ptr(), \
+        tot_st.data_ptr()
+    s2m.map_voxel(P_, v2, stream)
+    if events is not None:
+        events[1].record()
+
+    # 4. the scan-to-map io: corner map / surf map / scan corner from the first VoxelGrid, surf total from the second
+    oo = torch.from_numpy(out_off).to(dev)
+    keep.append(oo)
+    io = LegoS2mIo()
+    co, cn = oo[2 * P_::3].contiguous(), out_n[2 * P_::3].contiguous()
+    keep += [co, cn]
+    io.corner, io.corner_off, io.corner_n = v_out.data_ptr(), co.data_ptr(), cn.data_ptr()
+    io.surf, io.surf_off, io.surf_n = tot_out.data_ptr(), t2["off"].data_ptr(), tot_on.data_ptr()
+    cmo, cmn = oo[:P_].contiguous(), out_n[:P_].contiguous()
+    smo, smn = oo[P_:2 * P_].contiguous(), out_n[P_:2 * P_].contiguous()
+    keep += [cmo, cmn, smo, smn]
+    io.corner_map, io.corner_map_off, io.corner_map_n = v_out.data_ptr(), cmo.data_ptr(), cmn.data_ptr()
+    io.surf_map, io.surf_map_off, io.surf_map_n = v_out.data_ptr(), smo.data_ptr(), smn.data_ptr()
+    t0 = np.stack([np.asarray(seq[k]["transform_sum"], np.float32) + np.asarray(perturb, np.float32)
+                   for seq in sequences]).astype(np.float32)
+    tr = torch.from_numpy(t0).to(dev)
+    dg = torch.zeros(P_, dtype=torch.int32, device=dev)
+    info = torch.zeros((P_, 4), dtype=torch.int32, device=dev)
+    keep += [tr, dg, info]
+    io.transform, io.degenerate, io.info = tr.data_ptr(), dg.data_ptr(), info.data_ptr()
+    views = {"v_out": v_out, "out_off": out_off, "out_n": out_n, "tot_out": tot_out, "tot_off": tot_off,
+             "tot_n": tot_on, "status": status, "tot_status": tot_st}
+    return io, keep, tr, dg, info, views

@@ -1295,4 +1295,16 @@ int oracle_std_sort(uint32_t* keys, int32_t* vals, int n, int is_float) {
 float oracle_atan2f(float y, float x) { return atan2f(y, x); }
 float oracle_asinf(float x) { return asinf(x); }
 
+// pcl::VoxelGrid<PointXYZI>::filter (the restatement above) of one cloud: out needs room for n points.
+// stable: std::stable_sort's tie order (voxel_tie_order 1) instead of std::sort's.  Returns the status
+// bits (LEGO_ST_VOXEL_OVERFLOW) and the output size in *n_out.
+int oracle_voxel_grid(const float* in, int n, float leaf, int stable, float* out, int* n_out) {
+  std::vector<Pt> v((size_t)n), o;
+  std::memcpy(v.data(), in, (size_t)n * sizeof(Pt));
+  const int st = voxel_grid(v, leaf, o, stable != 0);
+  std::memcpy(out, o.data(), o.size() * sizeof(Pt));
+  *n_out = (int)o.size();
+  return st;
+}
+
 }  // extern "C"

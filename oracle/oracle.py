@@ -149,3 +149,27 @@ def knn5(cloud, queries):
     lib().oracle_knn5(m.ctypes.data_as(P(C.c_float)), len(m), q.ctypes.data_as(P(C.c_float)), len(q),
                       ind.ctypes.data_as(P(C.c_int32)), d.ctypes.data_as(P(C.c_float)), fl.ctypes.data_as(P(C.c_int32)))
     return ind, d, fl
+
+
+def voxel_grid(points, leaf, stable=True):
+    """pcl::VoxelGrid::filter restated (oracle/lego_oracle.cpp): (output (M, 4) float32, status bits)."""
+    import numpy as np
+    p = _f32(points)
+    out = np.zeros((max(len(p), 1), 4), np.float32)
+    n_out = C.c_int(0)
+    L = lib()
+    L.oracle_voxel_grid.restype = C.c_int
+    st = L.oracle_voxel_grid(p.ctypes.data_as(P(C.c_float)), len(p), C.c_float(leaf), int(bool(stable)),
+                             out.ctypes.data_as(P(C.c_float)), C.byref(n_out))
+    return out[:n_out.value].copy(), st
+
+
+def transform_cloud(points, pose):
+    """MapOptimization::transformPointCloud restated: pose = (roll, pitch, yaw, x, y, z)."""
+    import numpy as np
+    p = _f32(points)
+    out = np.zeros_like(p)
+    q = np.ascontiguousarray(np.asarray(pose, np.float32).reshape(6))
+    lib().oracle_transform_cloud(p.ctypes.data_as(P(C.c_float)), len(p), q.ctypes.data_as(P(C.c_float)),
+                                 out.ctypes.data_as(P(C.c_float)))
+    return out

@@ -538,3 +538,25 @@ extern "C" int oracle_knn5(const float* map, int n_map, const float* q, int n_q,
   }
   return 0;
 }
+
+// MapOptimization::transformPointCloud (:428-473) with the key pose (roll, pitch, yaw, x, y, z)
+extern "C" void oracle_transform_cloud(const float* in, int n, const float* pose, float* out) {
+  const float ctRoll = std::cos(pose[0]), stRoll = std::sin(pose[0]);
+  const float ctPitch = std::cos(pose[1]), stPitch = std::sin(pose[1]);
+  const float ctYaw = std::cos(pose[2]), stYaw = std::sin(pose[2]);
+  const float tInX = pose[3], tInY = pose[4], tInZ = pose[5];
+  for (int i = 0; i < n; ++i) {
+    const float* f = in + 4 * i;
+    const float x1 = ctYaw * f[0] - stYaw * f[1];
+    const float y1 = stYaw * f[0] + ctYaw * f[1];
+    const float z1 = f[2];
+    const float x2 = x1;
+    const float y2 = ctRoll * y1 - stRoll * z1;
+    const float z2 = stRoll * y1 + ctRoll * z1;
+    float* t = out + 4 * i;
+    t[0] = ctPitch * x2 + stPitch * z2 + tInX;
+    t[1] = y2 + tInY;
+    t[2] = -stPitch * x2 + ctPitch * z2 + tInZ;
+    t[3] = f[3];
+  }
+}

@@ -148,8 +148,34 @@ def test_s2m_abi_exports():
     """liblego_frontend.so exports every entry point include/lego_s2m.h declares (no GPU needed)."""
     import re
     hdr = open(os.path.join(REPO, "include", "lego_s2m.h")).read()
-    names = set(re.findall(r"\b(lego_s2m_\w+)\s*\(", hdr))
-    assert names == {"lego_s2m_create", "lego_s2m_destroy", "lego_s2m_run", "lego_s2m_run_host"}
+    names = set(re.findall(r"\b(lego_(?:s2m|map)_\w+)\s*\(", hdr))
+    assert names == {"lego_s2m_create", "lego_s2m_destroy", "lego_s2m_run", "lego_s2m_run_host", "lego_map_transform",
+                     "lego_map_voxel"}
     lib = C.CDLL(A.LIB_FRONTEND)
     for n in names:
         assert hasattr(lib, n), n
+
+
+def test_voxel_grid_stable_oracle_matches_python():
+    """The oracle's VoxelGrid with std::stable_sort's tie order (the map-side order) against a direct
+    Python restatement of PCL's applyFilter: float32 leaf indices, float32 sums in point order."""
+    rng = np.random.default_rng(13)
+    pts = np.concatenate([rng.uniform(-3, 3, (400, 4)), np.repeat(rng.uniform(-3, 3, (30, 4)), 5, axis=0)]).astype(np.float32)
+    rng.shuffle(pts)
+    for leaf in (0.2, 0.4, 1.0):
+        got, st = O.voxel_grid(pts, leaf, stable=True)
+        inv = np.float32(1.0) / np.float32(leaf)
+        mn, mx = pts[:, :3].min(0), pts[:, :3].max(0)
+        min_b = np.floor(mn * inv).astype(np.int64)
+        div = np.floor(mx * inv).astype(np.int64) - min_b + 1
+        ijk = (np.floor(pts[:, :3] * inv) - min_b.astype(np.float32)).astype(np.int64)
+        key = ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]
+        out = []
+        for kv in np.unique(key):
+            s_ = np.zeros(4, np.float32)
+            idx = np.flatnonzero(key == kv)
+            for i in idx:
+                s_ = (s_ + pts[i]).astype(np.float32)
+            out.append((s_ / np.float32(len(idx))).astype(np.float32))
+        ref = np.array(out, np.float32)
+        assert st == 0 and np.array_equal(got.view(np.int32), ref.view(np.int32)), leaf

@@ -6,7 +6,8 @@ clouds, transformSum) build its scan-to-map problem for scan K-1 (lego_amd.mappi
 the previous up-to-10 scans as the surrounding map, the reference's VoxelGrid leaves).  All S
 problems run in one lego_s2m_run launch; the timed region is R launches on device-resident inputs,
 bracketed by hipEvents on the launch stream.  The CPU baseline runs the oracle (oracle/s2m_oracle.cpp,
-single thread) on a sample of the same problems, which also gives the parity figure.
+single thread) on a sample of the same problems, which also gives the parity figure.  The map-side
+preparation (lego_map_transform / lego_map_voxel through lego_amd.mapping.prepare_gpu) is timed too.
 
   python tools/bench_s2m.py [--streams 256] [--scans 8] [--reps 20] [--cpu-sample 16]
 """
@@ -87,6 +88,28 @@ def main():
         total += ev0.elapsed_time(ev1)
     ms = total / args.reps
     t_gpu, dg_gpu, info_gpu = tr.cpu().numpy(), dg.cpu().numpy(), info.cpu().numpy()
+
+    # map-side preparation on the GPU (lego_map_transform + lego_map_voxel, mapping.prepare_gpu): the
+    # same problems assembled from the sequences' records, timed end to end (host uploads of the key
+    # frames, the kernels, one read of the VoxelGrid counts)
+    m.close()
+    m = LA.ScanToMap(max_problems=S, max_map_points=max(max_map, 8 * 12000 + 4000), device=0)
+    seqs = [frames[s] for s in range(S)]
+    M.prepare_gpu(m, seqs, K - 1)  # warm-up (allocates the VoxelGrid scratch)
+    torch.cuda.synchronize()
+    prep, prep_dev_ms = [], []
+    for _ in range(3):
+        t1 = time.time()
+        evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        pio, pkeep, ptr, pdg, pinfo, _v = M.prepare_gpu(m, seqs, K - 1, events=evs)
+        torch.cuda.synchronize()
+        prep.append(time.time() - t1)
+        prep_dev_ms.append(evs[0].elapsed_time(evs[1]))
+    prep_ms = 1e3 * min(prep)
+    prep_d = min(prep_dev_ms)
+    m.run(S, pio, stream.cuda_stream)
+    torch.cuda.synchronize()
+    prep_dev = float(np.abs(ptr.cpu().numpy() - t_gpu).max())  # GPU-prepared (stable VoxelGrid) vs numpy-prepared
     m.close()
 
     # CPU oracle on a sample of the same problems (single thread): baseline and parity
@@ -99,6 +122,16 @@ def main():
         t_ref, _, info_ref = O.scan2map(pr["corner"], pr["surf"], pr["corner_map"], pr["surf_map"], pr["transform"])
         dev.append(float(np.abs(t_ref - t_gpu[i]).max()))
     cpu_s = (time.time() - t1) / n_cpu
+    # the map-side preparation on the CPU: the oracle's transformPointCloud + VoxelGrid (stable order)
+    t1 = time.time()
+    for i in range(n_cpu):
+        cparts, sparts, (c, s_, o) = M._parts(frames[i], K - 1, 10)
+        vg = lambda x, leaf: O.voxel_grid(x, leaf, stable=True)[0]  # noqa: E731
+        vg(np.concatenate([O.transform_cloud(x, t) for x, t in cparts]), 0.2)
+        vg(np.concatenate([O.transform_cloud(x, t) for x, t in sparts]), 0.4)
+        vg(c, 0.2)
+        vg(np.concatenate([vg(s_, 0.4), vg(o, 0.4)]), 0.4)
+    cpu_prep_s = (time.time() - t1) / n_cpu
     out = {
         "metric": "scan-to-map problems/s (MapOptimization::scan2MapOptimization, <= 10 LM iterations each)",
         "value": round(S / (ms * 1e-3), 1), "unit": "problems/s", "n_gpus": 1, "ms_per_launch": round(ms, 4),
@@ -111,6 +144,15 @@ def main():
                          "sample": "%d of the same problems, oracle/s2m_oracle.cpp (grid kNN-5), single thread" % n_cpu},
         "parity": {"max_abs_transform_diff": max(dev), "tolerance": 1e-4, "sample": n_cpu},
         "input_gen_s": round(t_gen, 1),
+        "map_prep": {"device_ms": round(prep_d, 3), "problems_per_s": round(S / (prep_d * 1e-3), 1),
+                     "end_to_end_ms": round(prep_ms, 3),
+                     "note": "lego_map_transform + lego_map_voxel for all problems (two of each, one count read in "
+                             "between), hipEvents around the device work; end_to_end adds the Python assembly and "
+                             "host upload of the key frames (mapping.prepare_gpu)",
+                     "max_abs_transform_diff_vs_numpy_prepared": prep_dev,
+                     "cpu_baseline": {"value": round(1.0 / cpu_prep_s, 1), "unit": "problems/s", "cores": 1,
+                                      "kind": "port", "sample": "the same %d problems: oracle transform_cloud + "
+                                      "voxel_grid (stable), single thread" % n_cpu}},
     }
     line = json.dumps(out)
     print(line)
