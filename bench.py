@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--kind", default="vlp16", choices=["vlp16", "hdl64"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (rank 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the all-cores CPU variant (one sequence per thread; the box's CPU share)")
     ap.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (test rehearsal)")
     ap.add_argument("--groups", type=int, default=1, help="stream slices launched on separate HIP streams")
@@ -84,8 +86,56 @@ def cpu_baseline(params, cfg, pts, counts, budget_s):
             break
     return {"value": round(n_scans / t_sum, 2), "unit": "scans/s", "cores": 1, "kind": "port",
             "sample": "%d sequences x %d scans (scan 0 excluded) of the benchmark's own inputs, single thread, "
-                      "host %s" % (n_seq, nsteps - 1, platform.processor() or platform.machine()),
+                      "host %s" % (n_seq, nsteps - 1, cpu_model()),
             "ms_per_scan": round(1e3 * t_sum / max(n_scans, 1), 3)}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline_threads(params, cfg, pts, counts, budget_s, threads):
+    """The same oracle throughput with one sequence per host thread (SURVEY 8(d)'s all-cores variant):
+    `threads` Python threads, each running whole sequences through its own oracle instance (the ctypes
+    calls release the GIL), until the time budget is spent; scans of all threads / wall time."""
+    import threading
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    nsteps, S = counts.shape
+    lock = threading.Lock()
+    state = {"next": 0, "scans": 0}
+    t_start = time.time()
+
+    def worker():
+        while True:
+            with lock:
+                s = state["next"]
+                if s >= S or time.time() - t_start > budget_s:
+                    return
+                state["next"] += 1
+            orc = O.Oracle(params)
+            n = 0
+            for k in range(nsteps):
+                orc.cloud_handler(pts[k, s, :counts[k, s]])
+                orc.feature_association()
+                n += 1
+            with lock:
+                state["scans"] += n
+    ts = [threading.Thread(target=worker) for _ in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    wall = time.time() - t_start
+    return {"value": round(state["scans"] / wall, 1), "unit": "scans/s", "cores": threads, "kind": "port",
+            "sample": "%d sequences x %d scans, one sequence per thread, %d threads, host %s" % (
+                state["next"], nsteps, threads, cpu_model())}
 
 
 def pmc_traffic(args, S, kernels):
@@ -260,6 +310,9 @@ def main():
         params_ref = (L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64)(voxel_tie_order=0)
         out["cpu_baseline"] = cpu_baseline(params_ref, cfg, host_pts, host_cnt, args.cpu_seconds)
         out["speedup_vs_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
+        if args.cpu_threads > 1:
+            out["cpu_baseline_threads"] = cpu_baseline_threads(params_ref, cfg, host_pts, host_cnt, args.cpu_seconds,
+                                                               args.cpu_threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
