@@ -11,6 +11,10 @@
 //                               channel) spawns the worker thread; dtor sends an empty item and joins
 //                               (featureAssociation.cpp:87-94); every mapping_frequency_divider-th
 //                               odometry cycle sends an AssociationOut (:1431-1448)
+//   ScanToMapOptimization       mapOptimization.h / mapOptmization.cpp:1315-1332: scan2MapOptimization
+//                               with the members it owns (transformTobeMapped, isDegenerate), over
+//                               lego_s2m.h; the rest of MapOptimization (key frames, GTSAM, loop
+//                               closure) stays with the caller
 // Each stage owns its own GPU context (lego_ctx); all compute runs in the HIP kernels of
 // liblego_frontend.so.  Header-only; link with -llego_frontend.  Errors throw lego_amd::Error
 // (the C-ABI itself never throws).
@@ -27,6 +31,7 @@
 #include <vector>
 
 #include "lego_frontend.h"
+#include "lego_s2m.h"
 
 namespace lego_amd {
 
@@ -250,6 +255,46 @@ class FeatureAssociation {
   int _status = 0;
   int _n = 0;
   std::string _error;
+};
+
+// MapOptimization's scan-to-map LM.  transformTobeMapped / isDegenerate are the reference's members
+// (mapOptimization.h:208-210, 226): set transformTobeMapped (transformAssociateToMap) before the call,
+// read it after; isDegenerate carries over between calls as the member does.
+class ScanToMapOptimization {
+ public:
+  explicit ScanToMapOptimization(int device = 0, int max_map_points = 200000) {
+    check(lego_s2m_create(device, 1, max_map_points, &_m), "lego_s2m_create");
+  }
+  ~ScanToMapOptimization() { lego_s2m_destroy(_m); }
+  ScanToMapOptimization(const ScanToMapOptimization&) = delete;
+  ScanToMapOptimization& operator=(const ScanToMapOptimization&) = delete;
+
+  float transformTobeMapped[6] = {0, 0, 0, 0, 0, 0};
+  bool isDegenerate = false;
+
+  struct Info {
+    bool ran;        // the :1316 gate passed (false: transform untouched, transformUpdate not due)
+    int iterations;  // LMOptimization calls (<= 10)
+    int correspondences;
+    int status;      // LEGO_S2M_ST_*
+  };
+  // scan2MapOptimization (:1315-1332) on laserCloudCornerLastDS, laserCloudSurfTotalLastDS and the
+  // surrounding map's laserCloudCornerFromMapDS / laserCloudSurfFromMapDS
+  Info scan2MapOptimization(const std::vector<lego_point>& cornerLastDS, const std::vector<lego_point>& surfTotalLastDS,
+                            const std::vector<lego_point>& cornerFromMapDS,
+                            const std::vector<lego_point>& surfFromMapDS) {
+    int32_t dg = isDegenerate ? 1 : 0, info[4];
+    check(lego_s2m_run_host(_m, cornerLastDS.data(), (int32_t)cornerLastDS.size(), surfTotalLastDS.data(),
+                            (int32_t)surfTotalLastDS.size(), cornerFromMapDS.data(), (int32_t)cornerFromMapDS.size(),
+                            surfFromMapDS.data(), (int32_t)surfFromMapDS.size(), transformTobeMapped, &dg, info),
+          "lego_s2m_run_host");
+    if (info[0] < 0) throw Error("scan2MapOptimization: a map cloud exceeds max_map_points", LEGO_EINVAL);
+    isDegenerate = dg != 0;
+    return Info{info[0] == 1, info[1], info[2], info[3]};
+  }
+
+ private:
+  lego_s2m* _m = nullptr;
 };
 
 }  // namespace lego_amd

@@ -85,3 +85,58 @@ def test_rosbag_replay_equals_direct_replay(gpu, tmp_path):
         outs.append(r.stdout.strip())
     assert outs[0] == outs[1]
     assert outs[0].startswith("cycles 5 ")
+
+
+S2M_EXE = os.path.join(REPO, "examples", "scan2map")
+
+
+def _write_problem(path, pr):
+    with open(path, "wb") as f:
+        for name in ("corner", "surf", "corner_map", "surf_map"):
+            a = np.ascontiguousarray(pr[name], dtype=np.float32).reshape(-1, 4)
+            f.write(struct.pack("<i", a.shape[0]))
+            f.write(a.tobytes())
+        f.write(np.asarray(pr["transform"], np.float32).tobytes())
+
+
+def _problem():
+    import oracle as O
+    import make_golden as MG
+    from lego_amd import mapping as M
+    orc = O.Oracle(MG.params_for("vlp16"))
+    cfg = A.synth_cfg("vlp16")
+    frames = []
+    for k in range(5):
+        orc.cloud_handler(A.synth_scan(cfg, 13, k))
+        frames.append(orc.feature_association())
+    return M.build_problem(frames, 4)
+
+
+def test_scan2map_mirror_fails_loudly_without_device(tmp_path):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "scan2map"])
+    import lego_amd
+    if lego_amd.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    f = tmp_path / "p.bin"
+    _write_problem(str(f), _problem())
+    r = subprocess.run([S2M_EXE, str(f)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, universal_newlines=True)
+    assert r.returncode == 1 and "rc=-3" in r.stderr
+
+
+@pytest.mark.gpu
+def test_scan2map_mirror_matches_oracle(gpu, tmp_path):
+    """ScanToMapOptimization (the C++ mirror of MapOptimization's LM members and scan2MapOptimization)
+    reproduces the oracle's optimised transformTobeMapped."""
+    import oracle as O
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "scan2map"])
+    pr = _problem()
+    f = tmp_path / "p.bin"
+    _write_problem(str(f), pr)
+    r = subprocess.run([S2M_EXE, str(f), "0"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, universal_newlines=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    tok = r.stdout.split()
+    t = np.array([float(x) for x in tok[1:7]], np.float32)
+    t_ref, dg_ref, info_ref = O.scan2map(pr["corner"], pr["surf"], pr["corner_map"], pr["surf_map"], pr["transform"])
+    np.testing.assert_allclose(t, t_ref, atol=Hs.TF_TOL, rtol=0)
+    assert int(tok[8]) == dg_ref and int(tok[10]) == info_ref[0] and int(tok[12]) == info_ref[1]
