@@ -373,7 +373,7 @@ LG_DEVICE float block_min(float v, float* red) {
 
 // Build one map cloud's grid (whole workgroup).  Afterwards start[b] = end of bucket b.
 LG_DEVICE void build_grid(const float4* __restrict__ cloud, int n, const S2mScratch& G, GridInfo& gi, float* red,
-                          int* flag) {
+                          int* flag, int max_lg) {
   const int tid = threadIdx.x;
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
   for (int j = tid; j < n; j += S2M_THREADS) {
@@ -387,7 +387,7 @@ LG_DEVICE void build_grid(const float4* __restrict__ cloud, int n, const S2mScra
     hi[a] = -block_min(-mx[a], red);
   }
   int lg = 8;
-  while (lg < 16 && (1 << lg) < n) ++lg;
+  while (lg < max_lg && (1 << lg) < n) ++lg;
   const int nb = 1 << lg;
   bool fits = true;
   for (int a = 0; a < 3; ++a) fits = fits && (n == 0 || cell_of(hi[a], lo[a]) < S2M_DIM);
@@ -619,7 +619,11 @@ __device__ __attribute__((noinline)) QueryRow query_row(bool is_corner, float4 o
   return out;
 }
 
+constexpr int S2M_LG_SURF = 14, S2M_LG_CORNER = 13;  // bucket tables held in LDS: 64 KB + 32 KB
+
 struct S2mLds {
+  int tab_s[(1 << S2M_LG_SURF) + 1];    // the surf map's bucket ends (the grid's only dependent lookup)
+  int tab_c[(1 << S2M_LG_CORNER) + 1];  // the corner map's
   float red[S2M_THREADS / 64];
   int scan[S2M_THREADS];
   double acc[S2M_THREADS / 64][28];
@@ -683,9 +687,11 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch*
     if (tid == 0) { info[0] = -1; info[1] = 0; info[2] = 0; info[3] = LEGO_S2M_ST_SKIPPED; }
     return;
   }
-  const S2mScratch Gc = scratch[2 * p], Gs = scratch[2 * p + 1];
-  build_grid(cmap, ncm, Gc, L.gc, L.red, L.scan);
-  build_grid(smap, nsm, Gs, L.gs, L.red, L.scan);
+  S2mScratch Gc = scratch[2 * p], Gs = scratch[2 * p + 1];
+  Gc.start = L.tab_c;  // bucket tables in LDS, points in HBM
+  Gs.start = L.tab_s;
+  build_grid(cmap, ncm, Gc, L.gc, L.red, L.scan, S2M_LG_CORNER);
+  build_grid(smap, nsm, Gs, L.gs, L.red, L.scan, S2M_LG_SURF);
   if (tid == 0) {
     for (int k = 0; k < 6; ++k) L.t[k] = io.transform[6 * p + k];
     L.degenerate = io.degenerate[p];
