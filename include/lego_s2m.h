@@ -19,7 +19,9 @@
  *
  * Many independent problems (one per mapping sequence) run in one launch, one workgroup each.  Plain
  * C, plain pointers and sizes; every entry point returns LEGO_OK (0) or a negative LEGO_E* code
- * (lego_frontend.h) and never throws.  There is no CPU fallback: without a usable HIP device
+ * (lego_frontend.h) and never throws.  A lego_s2m object (its scratch) serves one call at a time:
+ * calls on different streams must be ordered by the caller, as the reference's single mapping
+ * thread orders them.  There is no CPU fallback: without a usable HIP device
  * lego_s2m_create returns LEGO_EDEVICE.
  */
 #ifndef LEGO_S2M_H
