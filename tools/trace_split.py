@@ -1,33 +1,51 @@
-"""Per-kernel duration summary from a rocprofv3 kernel trace, split by launch size.
+"""Per-kernel duration summary from a rocprofv3 kernel trace of bench.py, split by bench phase.
 
-  python tools/trace_split.py run_kernel_trace.csv OUT.csv
+  python tools/trace_split.py run_kernel_trace.csv OUT.csv [--steps K] [--warmup W]
 
-bench.py launches every stage twice per step size: the timed steps as `--groups` slices (S/groups
-scans per launch) and the per-stage timing pass as one launch of all S scans.  rocprofv3's
---stats file averages both; this split lets the full-S launches be compared with bench.py's
-per-launch stage times (stages_ms, roofline.launch_ms).
+bench.py runs the W + K steps twice: first the throughput pass (the timed region; with lag 1 and one
+slice, k_publish / k_lm run on an internal stream concurrently with the next scan's front end, so a
+kernel's duration there includes sharing the GPU), then the per-stage timing pass (one stream, stages
+in sequence) whose last K launches give bench.py's stages_ms and roofline.launch_ms.  rocprofv3's
+--stats file averages both passes; this split reports them apart, so the timing pass can be compared
+with the bench line.  Launches are assigned to the passes in time order, per kernel (each kernel runs
+once per step in each pass).
 """
+import argparse
 import collections
 import csv
-import sys
 
 
 def main():
-    src, out = sys.argv[1], sys.argv[2]
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("out")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    a = ap.parse_args()
+    per = a.steps + a.warmup
     acc = collections.defaultdict(list)
-    for r in csv.DictReader(open(src)):
+    for r in csv.DictReader(open(a.trace)):
         name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
-        if name.startswith("__amd"):
+        if name.startswith("__amd") or "rocprim" in name:
             continue
         grid = int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1)
-        acc[(name, grid)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    with open(out, "w", newline="") as f:
+        acc[(name, grid)].append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    rows = []
+    for (name, grid), v in sorted(acc.items()):
+        v.sort()
+        d = [x for _, x in v]
+        if len(d) == 2 * per:  # throughput pass, then the timing pass (measured: its last K)
+            parts = (("throughput_pass", d[a.warmup:per]), ("timing_pass", d[per + a.warmup:]))
+        else:
+            parts = (("all", d),)
+        for phase, x in parts:
+            rows.append([name, grid, phase, len(x), round(sum(x) / len(x), 2), round(min(x), 2), round(max(x), 2)])
+    with open(a.out, "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["kernel", "workgroups", "calls", "avg_us", "min_us", "max_us"])
-        for (name, grid), v in sorted(acc.items()):
-            w.writerow([name, grid, len(v), round(sum(v) / len(v), 2), round(min(v), 2), round(max(v), 2)])
-            print("%-24s wg=%6d calls=%3d avg %9.2f us  min %9.2f  max %9.2f" % (
-                name, grid, len(v), sum(v) / len(v), min(v), max(v)))
+        w.writerow(["kernel", "workgroups", "phase", "calls", "avg_us", "min_us", "max_us"])
+        for r in rows:
+            w.writerow(r)
+            print("%-24s wg=%6d %-16s calls=%3d avg %9.2f us  min %9.2f  max %9.2f" % tuple(r))
 
 
 if __name__ == "__main__":
