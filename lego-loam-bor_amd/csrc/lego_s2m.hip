@@ -891,24 +891,40 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vox_reduce(lego_map_voxel_io io
   }
   const unsigned* k = keys + (size_t)c * cap;
   const unsigned* v = vals + (size_t)c * cap;
+  __shared__ float4 tp[S2M_THREADS];   // the tile's points in sorted order (gathered together)
+  __shared__ unsigned tk[S2M_THREADS + 1];
   int base = 0;
   for (int t0 = 0; t0 < n; t0 += S2M_THREADS) {
     const int i = t0 + tid;
-    const bool head = i < n && (i == 0 || k[i] != k[i - 1]);
+    const int m = min(S2M_THREADS, n - t0);
+    if (i < n) {
+      tk[tid] = k[i];
+      tp[tid] = in[v[i]];
+    }
+    if (tid == 0) tk[S2M_THREADS] = t0 > 0 ? k[t0 - 1] : 0u;
+    __syncthreads();
+    const bool head = i < n && (i == 0 || tk[tid] != (tid == 0 ? tk[S2M_THREADS] : tk[tid - 1]));
     int total;
     const int slot = base + block_excl_scan(head ? 1 : 0, red, total);
     if (head) {  // CentroidPoint: float sums in sorted order, / count
       float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-      int j = i;
-      const unsigned key = k[i];
-      for (; j < n && k[j] == key; ++j) {
-        const float4 p = in[v[j]];
+      const unsigned key = tk[tid];
+      int j = tid;
+      for (; j < m && tk[j] == key; ++j) {
+        const float4 p = tp[j];
         sx += p.x; sy += p.y; sz += p.z; si += p.w;
       }
-      const float cnt = (float)(j - i);
+      int g = t0 + j;  // a run that continues past the tile
+      if (j == m)
+        for (; g < n && k[g] == key; ++g) {
+          const float4 p = in[v[g]];
+          sx += p.x; sy += p.y; sz += p.z; si += p.w;
+        }
+      const float cnt = (float)(g - i);
       out[slot] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
     }
     base += total;
+    __syncthreads();  // the tile's LDS is reused
   }
   if (tid == 0) { io.out_n[c] = base; io.status[c] = 0; }
 }
