@@ -110,21 +110,32 @@ def prepare_gpu(s2m, sequences, k, n_keys=10, perturb=(0.002, 0.002, 0.004, 0.03
     (for tests).  events = (start, end) torch.cuda.Events are recorded around the device work (after the
     key frames' upload; including the count read between the two VoxelGrid launches).
     """
+    cparts, sparts, scans = zip(*[_parts(seq, k, n_keys) for seq in sequences])
+    t0 = np.stack([np.asarray(seq[k]["transform_sum"], np.float32) + np.asarray(perturb, np.float32)
+                   for seq in sequences]).astype(np.float32)
+    return prepare_parts_gpu(s2m, cparts, sparts, scans, t0, stream=stream, events=events)
+
+
+def prepare_parts_gpu(s2m, cparts, sparts, scans, t0, degenerate=None, stream=0, events=None):
+    """prepare_gpu on explicit inputs, per problem p: cparts[p] / sparts[p] = [(cloud, key pose), ...]
+    (the surrounding key frames' corner clouds; their surf and outlier clouds, frame by frame), scans[p]
+    = (corner, surf, outlier) of the current scan, t0[p] = transformTobeMapped before the optimisation,
+    degenerate[p] = isDegenerate."""
     import torch
     from . import LegoMapTransformIo, LegoMapVoxelIo, LegoS2mIo
-    P_ = len(sequences)
+    P_ = len(scans)
     dev = "cuda"
     f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float32).reshape(-1, 4))  # noqa: E731
 
     # 1. key-frame parts of every problem: corner map parts, then surf map parts
-    cparts, sparts, scans = zip(*[_parts(seq, k, n_keys) for seq in sequences])
     parts = [(f32(c), t) for pp in cparts for (c, t) in pp] + [(f32(c), t) for pp in sparts for (c, t) in pp]
     n_c = [sum(len(f32(c)) for c, _ in pp) for pp in cparts]
     n_s = [sum(len(f32(c)) for c, _ in pp) for pp in sparts]
     sizes = np.array([len(a) for a, _ in parts], np.int32)
     in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     raw = torch.from_numpy(np.concatenate([a for a, _ in parts]) if len(parts) else np.zeros((1, 4), np.float32)).to(dev)
-    poses = torch.from_numpy(np.stack([np.asarray(t, np.float32) for _, t in parts])).to(dev)
+    poses = torch.from_numpy(np.stack([np.asarray(t, np.float32) for _, t in parts]) if parts
+                             else np.zeros((1, 6), np.float32)).to(dev)
     # concatenated outputs: problem p's corner map raw cloud, then (after all of them) surf map raw clouds
     map_raw = torch.empty((max(1, int(sizes.sum())), 4), dtype=torch.float32, device=dev)
     keep = [raw, poses, map_raw]
@@ -139,7 +150,8 @@ def prepare_gpu(s2m, sequences, k, n_keys=10, perturb=(0.002, 0.002, 0.004, 0.03
     sc_n = np.array([len(a) for a in sc], np.int32)
     if events is not None:
         events[0].record()
-    s2m.map_transform(len(parts), t_io, stream)
+    if parts:
+        s2m.map_transform(len(parts), t_io, stream)
 
     # 2. VoxelGrid: corner maps (0.2), surf maps (0.4), the scans' corner (0.2), surf (0.4), outlier (0.4)
     sc_off = np.concatenate([[0], np.cumsum(sc_n)[:-1]]).astype(np.int64)
@@ -214,13 +226,192 @@ def prepare_gpu(s2m, sequences, k, n_keys=10, perturb=(0.002, 0.002, 0.004, 0.03
     keep += [cmo, cmn, smo, smn]
     io.corner_map, io.corner_map_off, io.corner_map_n = v_out.data_ptr(), cmo.data_ptr(), cmn.data_ptr()
     io.surf_map, io.surf_map_off, io.surf_map_n = v_out.data_ptr(), smo.data_ptr(), smn.data_ptr()
-    t0 = np.stack([np.asarray(seq[k]["transform_sum"], np.float32) + np.asarray(perturb, np.float32)
-                   for seq in sequences]).astype(np.float32)
-    tr = torch.from_numpy(t0).to(dev)
-    dg = torch.zeros(P_, dtype=torch.int32, device=dev)
+    tr = torch.from_numpy(np.ascontiguousarray(np.asarray(t0, np.float32).reshape(P_, 6))).to(dev)
+    dg = (torch.from_numpy(np.asarray(degenerate, np.int32)).to(dev) if degenerate is not None
+          else torch.zeros(P_, dtype=torch.int32, device=dev))
     info = torch.zeros((P_, 4), dtype=torch.int32, device=dev)
     keep += [tr, dg, info]
     io.transform, io.degenerate, io.info = tr.data_ptr(), dg.data_ptr(), info.data_ptr()
     views = {"v_out": v_out, "out_off": out_off, "out_n": out_n, "tot_out": tot_out, "tot_off": tot_off,
              "tot_n": tot_on, "status": status, "tot_status": tot_st}
     return io, keep, tr, dg, info, views
+
+
+# ---- MapOptimization's mapping loop around the GPU operations ---------------------------------------
+def _f(x):
+    return np.float32(x)
+
+
+def transform_associate_to_map(tSum, tBef, tAft):
+    """transformAssociateToMap (mapOptmization.cpp:264-387) in float32: the odometry increment since the
+    last mapping step applied to the last mapped pose; returns transformTobeMapped."""
+    S, B, A = [np.asarray(t, np.float32) for t in (tSum, tBef, tAft)]
+    c, s = np.cos, np.sin
+    incre = np.zeros(6, np.float32)
+    x1 = c(S[1]) * (B[3] - S[3]) - s(S[1]) * (B[5] - S[5])
+    y1 = B[4] - S[4]
+    z1 = s(S[1]) * (B[3] - S[3]) + c(S[1]) * (B[5] - S[5])
+    x2 = x1
+    y2 = c(S[0]) * y1 + s(S[0]) * z1
+    z2 = -s(S[0]) * y1 + c(S[0]) * z1
+    incre[3] = c(S[2]) * x2 + s(S[2]) * y2
+    incre[4] = -s(S[2]) * x2 + c(S[2]) * y2
+    incre[5] = z2
+    sbcx, cbcx, sbcy, cbcy, sbcz, cbcz = s(S[0]), c(S[0]), s(S[1]), c(S[1]), s(S[2]), c(S[2])
+    sblx, cblx, sbly, cbly, sblz, cblz = s(B[0]), c(B[0]), s(B[1]), c(B[1]), s(B[2]), c(B[2])
+    salx, calx, saly, caly, salz, calz = s(A[0]), c(A[0]), s(A[1]), c(A[1]), s(A[2]), c(A[2])
+    T = np.zeros(6, np.float32)
+    srx = (-sbcx * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz) -
+           cbcx * sbcy * (calx * calz * (cbly * sblz - cblz * sblx * sbly) - calx * salz * (cbly * cblz + sblx * sbly * sblz) +
+                          cblx * salx * sbly) -
+           cbcx * cbcy * (calx * salz * (cblz * sbly - cbly * sblx * sblz) - calx * calz * (sbly * sblz + cbly * cblz * sblx) +
+                          cblx * cbly * salx))
+    T[0] = -np.arcsin(np.float32(srx))
+    srycrx = (sbcx * (cblx * cblz * (caly * salz - calz * salx * saly) - cblx * sblz * (caly * calz + salx * saly * salz) +
+                      calx * saly * sblx) -
+              cbcx * cbcy * ((caly * calz + salx * saly * salz) * (cblz * sbly - cbly * sblx * sblz) +
+                             (caly * salz - calz * salx * saly) * (sbly * sblz + cbly * cblz * sblx) - calx * cblx * cbly * saly) +
+              cbcx * sbcy * ((caly * calz + salx * saly * salz) * (cbly * cblz + sblx * sbly * sblz) +
+                             (caly * salz - calz * salx * saly) * (cbly * sblz - cblz * sblx * sbly) + calx * cblx * saly * sbly))
+    crycrx = (sbcx * (cblx * sblz * (calz * saly - caly * salx * salz) - cblx * cblz * (saly * salz + caly * calz * salx) +
+                      calx * caly * sblx) +
+              cbcx * cbcy * ((saly * salz + caly * calz * salx) * (sbly * sblz + cbly * cblz * sblx) +
+                             (calz * saly - caly * salx * salz) * (cblz * sbly - cbly * sblx * sblz) + calx * caly * cblx * cbly) -
+              cbcx * sbcy * ((saly * salz + caly * calz * salx) * (cbly * sblz - cblz * sblx * sbly) +
+                             (calz * saly - caly * salx * salz) * (cbly * cblz + sblx * sbly * sblz) - calx * caly * cblx * sbly))
+    T[1] = np.arctan2(np.float32(srycrx / c(T[0])), np.float32(crycrx / c(T[0])))
+    srzcrx = ((cbcz * sbcy - cbcy * sbcx * sbcz) * (calx * salz * (cblz * sbly - cbly * sblx * sblz) -
+                                                    calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx) -
+              (cbcy * cbcz + sbcx * sbcy * sbcz) * (calx * calz * (cbly * sblz - cblz * sblx * sbly) -
+                                                    calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) +
+              cbcx * sbcz * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz))
+    crzcrx = ((cbcy * sbcz - cbcz * sbcx * sbcy) * (calx * calz * (cbly * sblz - cblz * sblx * sbly) -
+                                                    calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) -
+              (sbcy * sbcz + cbcy * cbcz * sbcx) * (calx * salz * (cblz * sbly - cbly * sblx * sblz) -
+                                                    calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx) +
+              cbcx * cbcz * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz))
+    T[2] = np.arctan2(np.float32(srzcrx / c(T[0])), np.float32(crzcrx / c(T[0])))
+    x1 = c(T[2]) * incre[3] - s(T[2]) * incre[4]
+    y1 = s(T[2]) * incre[3] + c(T[2]) * incre[4]
+    z1 = incre[5]
+    x2 = x1
+    y2 = c(T[0]) * y1 - s(T[0]) * z1
+    z2 = s(T[0]) * y1 + c(T[0]) * z1
+    T[3] = A[3] - (c(T[1]) * x2 + s(T[1]) * z2)
+    T[4] = A[4] - y2
+    T[5] = A[5] - (-s(T[1]) * x2 + c(T[1]) * z2)
+    return T
+
+
+def voxel_grid_small(points, leaf):
+    """pcl::VoxelGrid::applyFilter for small clouds on the host (the 1 m key-pose filter, :78, :930-931):
+    float32 leaf indices, float32 sums in point order (stable tie order), ascending leaf order."""
+    p = np.asarray(points, np.float32).reshape(-1, 4)
+    if len(p) == 0:
+        return p.copy()
+    inv = np.float32(1.0) / np.float32(leaf)
+    mn, mx = p[:, :3].min(0), p[:, :3].max(0)
+    min_b = np.floor(mn * inv).astype(np.int64)
+    div = np.floor(mx * inv).astype(np.int64) - min_b + 1
+    ijk = (np.floor(p[:, :3] * inv) - min_b.astype(np.float32)).astype(np.int64)
+    key = ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]
+    out = []
+    for kv in np.unique(key):
+        acc = np.zeros(4, np.float32)
+        idx = np.flatnonzero(key == kv)
+        for i in idx:
+            acc = (acc + p[i]).astype(np.float32)
+        out.append((acc / np.float32(len(idx))).astype(np.float32))
+    return np.array(out, np.float32)
+
+
+class MapSequence:
+    """MapOptimization::run (mapOptmization.cpp:1521-1570) for one sequence, loop closure off (the
+    reference's default, loam_config.yaml:24), host side: transformAssociateToMap,
+    extractSurroundingKeyFrames (:915-995: key poses within 50 m, their 1 m VoxelGrid, the existing
+    key-frame list kept in the reference's order), the inputs of downsampleCurrentScan, and after the
+    scan-to-map LM transformUpdate and saveKeyFramesAndFactor (:1335-1478).  GTSAM is left out: with no
+    loop closure its graph is a chain whose optimum is the inserted pose itself, so the key pose is
+    transformAftMapped (the reference's Rot3 round trip aside).  The clouds' transforms and VoxelGrids
+    and the LM run batched over many sequences (MappingBatch)."""
+
+    RADIUS = 50.0  # surrounding_keyframe_search_radius (loam_config.yaml:27)
+
+    def __init__(self):
+        z = lambda: np.zeros(6, np.float32)  # noqa: E731
+        self.t_sum, self.t_tobe, self.t_bef, self.t_aft = z(), z(), z(), z()
+        self.key_pos = []       # cloudKeyPoses3D: (x, y, z, index)
+        self.key_pose6 = []     # cloudKeyPoses6D as (roll, pitch, yaw, x, y, z)
+        self.key_clouds = []    # (corner DS, surf DS, outlier DS) per key frame, lidar frame
+        self.existing = []      # surroundingExistingKeyPosesID
+        self.cur_pos = np.zeros(3, np.float32)
+        self.prev_pos = np.zeros(3, np.float32)
+        self.degenerate = 0
+        self.cycles = 0
+
+    def begin(self, assoc):
+        """One AssociationOut: returns (corner parts, surf parts, scan clouds, transformTobeMapped)."""
+        self.t_sum = np.asarray(assoc["transform_sum"], np.float32).copy()  # OdometryToTransform (:1540)
+        self.t_tobe = transform_associate_to_map(self.t_sum, self.t_bef, self.t_aft)
+        if self.key_pos:  # extractSurroundingKeyFrames, loop closure off (:915-995)
+            kp = np.array(self.key_pos, np.float32)
+            d = ((kp[:, 0] - self.cur_pos[0]) ** 2 + (kp[:, 1] - self.cur_pos[1]) ** 2) + (kp[:, 2] - self.cur_pos[2]) ** 2
+            sel = np.flatnonzero(d < np.float32(self.RADIUS * self.RADIUS))
+            sel = sel[np.argsort(d[sel], kind="stable")]  # radiusSearch, sorted by distance
+            ds = voxel_grid_small(kp[sel], 1.0)
+            ids = [int(x) for x in ds[:, 3]]
+            self.existing = [i for i in self.existing if i in ids]
+            for i in ids:
+                if i not in self.existing:
+                    self.existing.append(i)
+        corner_parts = [(self.key_clouds[i][0], self.key_pose6[i]) for i in self.existing]
+        surf_parts = []
+        for i in self.existing:
+            surf_parts += [(self.key_clouds[i][1], self.key_pose6[i]), (self.key_clouds[i][2], self.key_pose6[i])]
+        scan = (assoc["corner_last"], assoc["surf_last"], assoc["outlier_last"])
+        return corner_parts, surf_parts, scan, self.t_tobe.copy()
+
+    def end(self, transform, degenerate, info, scan_ds):
+        """After the LM: scan_ds = (corner DS, surf DS, outlier DS) of the current scan."""
+        self.t_tobe = np.asarray(transform, np.float32).copy()
+        self.degenerate = int(degenerate)
+        if info[0] == 1:  # transformUpdate (:389-395), inside scan2MapOptimization's gate
+            self.t_bef = self.t_sum.copy()
+            self.t_aft = self.t_tobe.copy()
+        # saveKeyFramesAndFactor (:1335-1478) without GTSAM
+        self.cur_pos = self.t_aft[3:6].copy()
+        dd = self.prev_pos - self.cur_pos
+        moved = np.sqrt(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]) >= 0.3
+        self.cycles += 1
+        if not moved and self.key_pos:
+            return
+        self.prev_pos = self.cur_pos.copy()
+        # the first key frame is the prior at transformTobeMapped (:1361-1376), later ones the chain's
+        # estimate at transformAftMapped (:1381-1406, :1424-1426)
+        pose = (self.t_tobe if not self.key_pos else self.t_aft).copy()
+        self.key_pos.append((pose[3], pose[4], pose[5], float(len(self.key_pos))))
+        self.key_pose6.append(pose)
+        if len(self.key_pos) > 1:  # :1447-1459
+            self.t_tobe = self.t_aft.copy()
+        self.key_clouds.append(tuple(np.asarray(c, np.float32).reshape(-1, 4).copy() for c in scan_ds))
+
+
+def mapping_step_gpu(s2m, seqs, assocs, stream=0):
+    """One mapping cycle of every sequence in `seqs` (MapSequence) on its AssociationOut: the key
+    frames' transforms and all VoxelGrids (lego_map_transform / lego_map_voxel) and the scan-to-map LM
+    (lego_s2m_run) in batched launches.  Returns the per-sequence (transform, degenerate, info)."""
+    import torch
+    begun = [sq.begin(a) for sq, a in zip(seqs, assocs)]
+    cparts, sparts, scans, t0 = zip(*begun)
+    io, keep, tr, dg, info, v = prepare_parts_gpu(s2m, cparts, sparts, scans, np.stack(t0),
+                                                  degenerate=[sq.degenerate for sq in seqs], stream=stream)
+    s2m.run(len(seqs), io, stream)
+    torch.cuda.synchronize()
+    P_ = len(seqs)
+    vo, oo, on = v["v_out"].cpu().numpy(), v["out_off"], v["out_n"].cpu().numpy()
+    t, d, inf = tr.cpu().numpy(), dg.cpu().numpy(), info.cpu().numpy()
+    for p, sq in enumerate(seqs):
+        b = 2 * P_ + 3 * p  # the scan's corner, surf, outlier DS
+        ds = tuple(vo[oo[b + i]:oo[b + i] + on[b + i]] for i in range(3))
+        sq.end(t[p], d[p], inf[p], ds)
+    return [(t[p], int(d[p]), inf[p]) for p in range(P_)]
