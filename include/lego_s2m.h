@@ -104,6 +104,27 @@ int  lego_map_transform(lego_s2m* m, int32_t n, const lego_map_transform_io* io,
  * larger n, after a device synchronize) */
 int  lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* io, void* hip_stream);
 
+/* ---- MapOptimization's loop body (loop closure off: loam_config.yaml:24) --------------------------------
+ * One mapping sequence: MapOptimization::run (mapOptmization.cpp:1521-1570) per AssociationOut, with the
+ * key frames kept in device memory:
+ *   transformAssociateToMap (:264-387) from transform_sum (OdometryToTransform of the odometry, :1540),
+ *   extractSurroundingKeyFrames (:915-995: key poses within 50 m by distance, their 1 m VoxelGrid, the
+ *     existing key-frame list erased / extended in the reference's order; lego_map_transform + _voxel),
+ *   downsampleCurrentScan (:999-1026), scan2MapOptimization (:1315-1332), transformUpdate (:389-395),
+ *   saveKeyFramesAndFactor (:1335-1478) without GTSAM: with no loop closure the factor graph is a chain
+ *     whose optimum is the pose just inserted (the first key frame at transformTobeMapped, later ones at
+ *     transformAftMapped), so the key poses are those.
+ * lego_mapper_step returns transformAftMapped after the cycle (publishTF's pose, :510-538) and info[4] as
+ * lego_s2m_run's.  A mapper serves one call at a time. */
+typedef struct lego_mapper lego_mapper;
+int  lego_mapper_create(int32_t device, int32_t max_map_points, int64_t max_key_points, lego_mapper** out);
+void lego_mapper_destroy(lego_mapper* m);
+int  lego_mapper_step(lego_mapper* m, const lego_point* corner_last, int32_t n_corner, const lego_point* surf_last,
+                      int32_t n_surf, const lego_point* outlier_last, int32_t n_outlier, const float* transform_sum,
+                      float* transform_aft_mapped, int32_t* info);
+/* key poses so far, (roll, pitch, yaw, x, y, z) each (cloudKeyPoses6D); *n = their count */
+int  lego_mapper_key_poses(const lego_mapper* m, float* out, int32_t cap, int32_t* n);
+
 #ifdef __cplusplus
 }
 #endif

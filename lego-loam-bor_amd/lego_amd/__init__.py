@@ -90,6 +90,11 @@ def lib():
                                                                                   P(C.c_int32)]
         L.lego_map_transform.argtypes = [C.c_void_p, C.c_int32, P(LegoMapTransformIo), C.c_void_p]
         L.lego_map_voxel.argtypes = [C.c_void_p, C.c_int32, P(LegoMapVoxelIo), C.c_void_p]
+        L.lego_mapper_create.argtypes = [C.c_int32, C.c_int32, C.c_int64, P(C.c_void_p)]
+        L.lego_mapper_destroy.argtypes = [C.c_void_p]
+        L.lego_mapper_step.argtypes = [C.c_void_p] + [C.c_void_p, C.c_int32] * 3 + [P(C.c_float), P(C.c_float),
+                                                                                    P(C.c_int32)]
+        L.lego_mapper_key_poses.argtypes = [C.c_void_p, P(C.c_float), C.c_int32, P(C.c_int32)]
         _lib = L
     return _lib
 
@@ -285,3 +290,45 @@ class ScanToMap:
     def map_voxel(self, n, io, stream=0):
         """pcl::VoxelGrid::filter of n clouds (LegoMapVoxelIo of device pointers); asynchronous."""
         _check(lib().lego_map_voxel(self.h, int(n), C.byref(io), C.c_void_p(stream)), "lego_map_voxel")
+
+
+class Mapper:
+    """MapOptimization's mapping thread (mapOptmization.cpp:1521-1570, loop closure off) for one
+    sequence: step() takes one AssociationOut's clouds and transformSum and returns transformAftMapped;
+    the key frames' downsampled clouds stay in device memory (lego_mapper_*, include/lego_s2m.h)."""
+
+    def __init__(self, max_map_points=200000, max_key_points=50_000_000, device=0):
+        h = C.c_void_p()
+        _check(lib().lego_mapper_create(int(device), int(max_map_points), int(max_key_points), C.byref(h)),
+               "lego_mapper_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().lego_mapper_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def step(self, corner_last, surf_last, outlier_last, transform_sum):
+        """Returns (transformAftMapped[6] float32, info[4] int32: iterations-gate / LM status as lego_s2m)."""
+        arrs = [np.ascontiguousarray(np.asarray(a, np.float32).reshape(-1, 4)) for a in (corner_last, surf_last,
+                                                                                          outlier_last)]
+        ts = np.ascontiguousarray(np.asarray(transform_sum, np.float32).reshape(6))
+        out = np.zeros(6, np.float32)
+        info = np.zeros(4, np.int32)
+        args = []
+        for a in arrs:
+            args += [C.c_void_p(a.ctypes.data), len(a)]
+        _check(lib().lego_mapper_step(self.h, *args, ts.ctypes.data_as(P(C.c_float)), out.ctypes.data_as(P(C.c_float)),
+                                      info.ctypes.data_as(P(C.c_int32))), "lego_mapper_step")
+        return out, info
+
+    def key_poses(self):
+        """cloudKeyPoses6D as an (n, 6) float32 array of (roll, pitch, yaw, x, y, z)."""
+        n = C.c_int32()
+        _check(lib().lego_mapper_key_poses(self.h, None, 0, C.byref(n)), "lego_mapper_key_poses")
+        out = np.zeros((max(n.value, 1), 6), np.float32)
+        _check(lib().lego_mapper_key_poses(self.h, out.ctypes.data_as(P(C.c_float)), n.value, C.byref(n)),
+               "lego_mapper_key_poses")
+        return out[:n.value]

@@ -381,7 +381,7 @@ class MapSequence:
         # saveKeyFramesAndFactor (:1335-1478) without GTSAM
         self.cur_pos = self.t_aft[3:6].copy()
         dd = self.prev_pos - self.cur_pos
-        moved = np.sqrt(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]) >= 0.3
+        moved = float(np.sqrt(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2])) >= 0.3  # float distance vs double 0.3
         self.cycles += 1
         if not moved and self.key_pos:
             return

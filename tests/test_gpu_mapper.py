@@ -1,0 +1,49 @@
+"""The native mapping thread (lego_mapper_*, Mapper) against MapSequence around the oracle's operations.
+
+lego_mapper_step is MapOptimization::run's loop body (mapOptmization.cpp:1521-1570, loop closure off)
+with the host logic in C++ and the key frames' clouds in device memory; MapSequence +
+mapping_step_oracle is the same loop in Python over the CPU restatements.  Per cycle the
+transformAftMapped must agree within 1e-4, the LM gate / iteration counts exactly, and the key poses
+at the end within 1e-4.
+"""
+import numpy as np
+import pytest
+
+from lego_amd import mapping as M
+from test_gpu_mapping_loop import _emitted, mapping_step_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seq", [3, 8])
+def test_mapper_matches_oracle_loop(gpu, seq):
+    import lego_amd as LA
+    stream = _emitted(seq, 31)
+    assert len(stream) >= 5
+    mp = LA.Mapper(max_map_points=150000, max_key_points=4_000_000, device=gpu)
+    r = M.MapSequence()
+    ran = 0
+    for k, a in enumerate(stream):
+        tg, ig = mp.step(a["corner_last"], a["surf_last"], a["outlier_last"], a["transform_sum"])
+        (_, _, ir), = mapping_step_oracle([r], [a])
+        assert np.abs(tg - r.t_aft).max() <= 1e-4, (k, tg, r.t_aft)
+        assert ig[0] == ir[0] and ig[1] == ir[1], (k, ig, ir)
+        ran += int(ig[0] == 1)
+    kp = mp.key_poses()
+    assert kp.shape == (len(r.key_pose6), 6)
+    assert np.abs(kp - np.array(r.key_pose6)).max() <= 1e-4
+    mp.close()
+    assert ran >= len(stream) - 1
+    assert len(kp) >= 3
+
+
+def test_mapper_rejects_bad_args(gpu):
+    import lego_amd as LA
+    with pytest.raises(LA.LegoError):
+        LA.Mapper(max_map_points=0, device=gpu)
+    mp = LA.Mapper(max_map_points=1000, max_key_points=10000, device=gpu)
+    big = np.zeros((1001, 4), np.float32)
+    with pytest.raises(LA.LegoError):
+        mp.step(big, big[:1], big[:1], np.zeros(6, np.float32))
+    assert mp.key_poses().shape == (0, 6)
+    mp.close()
