@@ -213,7 +213,8 @@ int  lego_batch_wide(const lego_batch* b);
 /* Evaluate the device libm restatement on host arrays: which = 0 asinf(a), 1 atan2f(a, b),
  * 2 atanf(a), 3 sqrtf(a), 4 a / b.  Lets tests compare gfx950 results with the host's glibc.
  * which = 5 / 6: groundRemoval's pair test atan2f(dZ = a, r = b) <= 10 deg (mount 0) as k_project
- * decides it (polynomial with a margin, glibc-faithful fallback) / by the glibc-faithful path only. */
+ * decides it (polynomial with a margin, glibc-faithful fallback) / by the glibc-faithful path only.
+ * which = 7 / 8: sinf(a) / cosf(a) (the LM trig). */
 int  lego_test_libm(const float* a, const float* b, float* out, int32_t n, int32_t which);
 /* Sort (key, val) pairs by key with the device's wave-parallel std::sort emulation (n <= 2048);
  * keys are uint32 (is_float 0) or float bit patterns (1); is_float 2 runs k_extract's segment

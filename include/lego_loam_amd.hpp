@@ -20,6 +20,7 @@
 // (the C-ABI itself never throws).
 #pragma once
 
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -295,6 +296,41 @@ class ScanToMapOptimization {
 
  private:
   lego_s2m* _m = nullptr;
+};
+
+// MapOptimization's mapping thread, loop closure off (mapOptmization.cpp:1521-1570): run() is one
+// pass of its loop on one AssociationOut (laserCloudCornerLast / SurfLast / OutlierLast, transformSum),
+// the key frames' clouds kept on the GPU.  transformAftMapped is the reference's member after the pass.
+class MapOptimization {
+ public:
+  explicit MapOptimization(int device = 0, int max_map_points = 200000, int64_t max_key_points = 50000000) {
+    check(lego_mapper_create(device, max_map_points, max_key_points, &_m), "lego_mapper_create");
+  }
+  ~MapOptimization() { lego_mapper_destroy(_m); }
+  MapOptimization(const MapOptimization&) = delete;
+  MapOptimization& operator=(const MapOptimization&) = delete;
+
+  float transformAftMapped[6] = {0, 0, 0, 0, 0, 0};
+
+  ScanToMapOptimization::Info run(const std::vector<lego_point>& cornerLast, const std::vector<lego_point>& surfLast,
+                                  const std::vector<lego_point>& outlierLast, const float transformSum[6]) {
+    int32_t info[4];
+    check(lego_mapper_step(_m, cornerLast.data(), (int32_t)cornerLast.size(), surfLast.data(), (int32_t)surfLast.size(),
+                           outlierLast.data(), (int32_t)outlierLast.size(), transformSum, transformAftMapped, info),
+          "lego_mapper_step");
+    return ScanToMapOptimization::Info{info[0] == 1, info[1], info[2], info[3]};
+  }
+  // cloudKeyPoses6D: (roll, pitch, yaw, x, y, z) per key frame
+  std::vector<std::array<float, 6>> keyPoses() const {
+    int32_t n = 0;
+    check(lego_mapper_key_poses(_m, nullptr, 0, &n), "lego_mapper_key_poses");
+    std::vector<std::array<float, 6>> out(n);
+    if (n) check(lego_mapper_key_poses(_m, out[0].data(), n, &n), "lego_mapper_key_poses");
+    return out;
+  }
+
+ private:
+  lego_mapper* _m = nullptr;
 };
 
 }  // namespace lego_amd

@@ -124,6 +124,14 @@ int  lego_mapper_step(lego_mapper* m, const lego_point* corner_last, int32_t n_c
                       float* transform_aft_mapped, int32_t* info);
 /* key poses so far, (roll, pitch, yaw, x, y, z) each (cloudKeyPoses6D); *n = their count */
 int  lego_mapper_key_poses(const lego_mapper* m, float* out, int32_t cap, int32_t* n);
+/* test hook (not for the mapping path): cap the LM iterations of later runs at max_iters (the product's 10
+ * restored by passing 10) and copy problem p's LM rows of its last iteration, 8 floats a query (arx, ary,
+ * arz, coeff x, y, z, -coeff intensity, 1 if selected else 0), into out[8 * nq] */
+int  lego_test_s2m_debug(lego_s2m* m, int32_t max_iters, int32_t p, int32_t nq, float* out);
+/* transformAssociateToMap (mapOptmization.cpp:264-387) on the host, float with the float libm (no device
+ * needed): transformTobeMapped from transformSum / transformBefMapped / transformAftMapped. */
+int  lego_map_associate(const float* transform_sum, const float* transform_bef_mapped, const float* transform_aft_mapped,
+                        float* transform_tobe_mapped);
 
 #ifdef __cplusplus
 }

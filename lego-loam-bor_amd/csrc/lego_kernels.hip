@@ -4176,6 +4176,8 @@ __global__ void k_libm_test(const float* a, const float* b, float* out, int n, i
   else if (which == 3) r = sqrtf(a[i]);
   else if (which == 4) r = a[i] / b[i];
   else if (which == 5) r = ground_pair(a[i], b[i], 0.f) ? 1.f : 0.f;                       // fast + exact
+  else if (which == 7) r = sinf_g(a[i]);
+  else if (which == 8) r = cosf_g(a[i]);
   else r = (double)atan2f_g(a[i], b[i]) <= 10 * DEG_TO_RAD_D ? 1.f : 0.f;                  // exact only
   out[i] = r;
 }

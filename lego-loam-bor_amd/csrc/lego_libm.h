@@ -142,43 +142,70 @@ LG_LIBM float asinf_g(float x) {
   return (hx > 0) ? t : -t;
 }
 
-// sinf/cosf: double evaluation rounded once (glibc's own sinf/cosf differ on ~1e-3 of inputs;
-// they are used only inside the LM, which is parity-checked within 1e-4).  For |x| <= pi/4 (every
-// LM angle in practice) a Taylor polynomial in double: truncation < 1e-19 relative, a few double
-// ulps of rounding, so the float result is the rounded true value except within ~1e-15 of a float
-// rounding boundary; larger |x| goes to the library's double sin/cos.
-LG_LIBM double sin_poly_d(double x) {
-  const double x2 = x * x;
-  double p = 1.0 / 355687428096000.0;
-  p = __builtin_fma(p, x2, -1.0 / 1307674368000.0);
-  p = __builtin_fma(p, x2, 1.0 / 6227020800.0);
-  p = __builtin_fma(p, x2, -1.0 / 39916800.0);
-  p = __builtin_fma(p, x2, 1.0 / 362880.0);
-  p = __builtin_fma(p, x2, -1.0 / 5040.0);
-  p = __builtin_fma(p, x2, 1.0 / 120.0);
-  p = __builtin_fma(p, x2, -1.0 / 6.0);
-  return __builtin_fma(x * x2, p, x);
+// ---- glibc 2.35 sinf / cosf (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h, sincosf_data.c) --
+// The x86-64 build the reference links runs the FMA ifunc variant (sysdeps/x86_64/fpu/multiarch/
+// s_sinf-fma.c) on any AVX2/FMA host: the polynomial's a + b * c steps and the range reduction's
+// x - n * pi/2 are fused there, so they are __builtin_fma here.  Bit-exact with the host's sinf / cosf
+// for every float in [-120, 120] (checked exhaustively, tests/native/trig_check.cpp); beyond 120 rad
+// (never an LM angle) glibc's large-argument reduction is not restated: float(sin(double x)) instead.
+struct SinCosTab {
+  double c0, c1, c2, c3, c4, s1, s2, s3;
+};
+LG_LIBM SinCosTab sincos_tab(bool second) {  // __sincosf_table[0] / [1]: [1] negates the cosine terms
+  const double k = second ? -1.0 : 1.0;
+  return SinCosTab{k * 0x1p0, k * -0x1.ffffffd0c621cp-2, k * 0x1.55553e1068f19p-5, k * -0x1.6c087e89a359dp-10,
+                   k * 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
 }
-LG_LIBM double cos_poly_d(double x) {
-  const double x2 = x * x;
-  double p = -1.0 / 6402373705728000.0;
-  p = __builtin_fma(p, x2, 1.0 / 20922789888000.0);
-  p = __builtin_fma(p, x2, -1.0 / 87178291200.0);
-  p = __builtin_fma(p, x2, 1.0 / 479001600.0);
-  p = __builtin_fma(p, x2, -1.0 / 3628800.0);
-  p = __builtin_fma(p, x2, 1.0 / 40320.0);
-  p = __builtin_fma(p, x2, -1.0 / 720.0);
-  p = __builtin_fma(p, x2, 1.0 / 24.0);
-  p = __builtin_fma(p, x2, -0.5);
-  return __builtin_fma(x2, p, 1.0);
+// sinf_poly: n even -> sin(x), odd -> cos(x) (table [1]: -cos(x))
+LG_LIBM float sincos_poly(double x, double x2, const SinCosTab& p, int n) {
+  if ((n & 1) == 0) {
+    const double x3 = x * x2;
+    const double s1 = __builtin_fma(x2, p.s3, p.s2);
+    const double x7 = x3 * x2;
+    const double s = __builtin_fma(x3, p.s1, x);
+    return (float)__builtin_fma(x7, s1, s);
+  }
+  const double x4 = x2 * x2;
+  const double c2 = __builtin_fma(x2, p.c4, p.c3);
+  const double c1 = __builtin_fma(x2, p.c1, p.c0);
+  const double x6 = x4 * x2;
+  const double c = __builtin_fma(x4, p.c2, c1);
+  return (float)__builtin_fma(x6, c2, c);
 }
-LG_LIBM float sinf_g(float x) {
-  const double d = (double)x;
-  return (float)(__builtin_fabs(d) <= 0.78539816 ? sin_poly_d(d) : sin(d));
+LG_LIBM uint32_t abstop12(float x) { return (fbits(x) >> 20) & 0x7ff; }
+// reduce_fast: n = nearest multiple of pi/2 (fixed point, 2/pi * 2^24), x - n * pi/2
+LG_LIBM double sincos_reduce(double x, int& n) {
+  const double r = x * 0x1.45f306dc9c883p+23;
+  n = ((int32_t)r + 0x800000) >> 24;
+  return __builtin_fma(-(double)n, 0x1.921fb54442d18p0, x);
 }
-LG_LIBM float cosf_g(float x) {
-  const double d = (double)x;
-  return (float)(__builtin_fabs(d) <= 0.78539816 ? cos_poly_d(d) : cos(d));
+LG_LIBM float sinf_g(float y) {
+  const double x = (double)y;
+  if (abstop12(y) < abstop12(0x1.921fb6p-1f)) {
+    if (abstop12(y) < abstop12(0x1p-12f)) return y;
+    return sincos_poly(x, x * x, sincos_tab(false), 0);
+  }
+  if (abstop12(y) < abstop12(120.0f)) {
+    int n;
+    const double r = sincos_reduce(x, n);
+    const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;  // sign[] = {1, -1, -1, 1}
+    return sincos_poly(r * sg, r * r, sincos_tab((n & 2) != 0), n);
+  }
+  return (float)sin(x);
+}
+LG_LIBM float cosf_g(float y) {
+  const double x = (double)y;
+  if (abstop12(y) < abstop12(0x1.921fb6p-1f)) {
+    if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
+    return sincos_poly(x, x * x, sincos_tab(false), 1);
+  }
+  if (abstop12(y) < abstop12(120.0f)) {
+    int n;
+    const double r = sincos_reduce(x, n);
+    const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
+    return sincos_poly(r * sg, r * r, sincos_tab((n & 2) != 0), n ^ 1);
+  }
+  return (float)cos(x);
 }
 
 LG_LIBM bool isfinite_f(float x) { return (fbits(x) & 0x7f800000u) != 0x7f800000u; }

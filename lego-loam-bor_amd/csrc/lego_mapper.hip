@@ -204,6 +204,13 @@ extern "C" int lego_mapper_create(int32_t device, int32_t max_map_points, int64_
   return LEGO_OK;
 }
 
+extern "C" int lego_map_associate(const float* transform_sum, const float* transform_bef_mapped,
+                                  const float* transform_aft_mapped, float* transform_tobe_mapped) {
+  if (!transform_sum || !transform_bef_mapped || !transform_aft_mapped || !transform_tobe_mapped) return LEGO_EINVAL;
+  associate_to_map(transform_sum, transform_bef_mapped, transform_aft_mapped, transform_tobe_mapped);
+  return LEGO_OK;
+}
+
 extern "C" int lego_mapper_key_poses(const lego_mapper* m, float* out, int32_t cap, int32_t* n) {
   if (!m || !n || (cap > 0 && !out)) return LEGO_EINVAL;
   *n = (int32_t)m->kf.size();
@@ -340,6 +347,7 @@ extern "C" int lego_mapper_step(lego_mapper* m, const lego_point* corner_last, i
   MCHECK(hipMemcpy(m->t_tobe, m->d_t, sizeof(m->t_tobe), hipMemcpyDeviceToHost));
   MCHECK(hipMemcpy(&m->degenerate, m->d_dg, sizeof(int32_t), hipMemcpyDeviceToHost));
   MCHECK(hipMemcpy(info, m->d_info, 4 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (info[0] < 0) return LEGO_EINVAL;  // a cloud over max_map_points (lego_s2m_run's gate)
   if (info[0] == 1) {  // transformUpdate (:389-395)
     memcpy(m->t_bef, m->t_sum, sizeof(m->t_sum));
     memcpy(m->t_aft, m->t_tobe, sizeof(m->t_tobe));

@@ -23,6 +23,7 @@
 
 #include <new>
 
+#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "../../include/lego_s2m.h"
@@ -35,7 +36,8 @@ namespace {
 constexpr int S2M_THREADS = 1024;
 constexpr int S2M_NB_MAX = 65536;  // hash buckets per map cloud (power of two)
 constexpr float S2M_CELL = 1.01f;  // cell edge: >= the 1 m kNN gate plus rounding
-constexpr int S2M_DIM = 1024;      // cells per axis a packed cell can hold (10 bits)
+constexpr int S2M_DIM = 1024;
+constexpr size_t S2M_WIDE_MAX = (size_t)8 << 20;  // few-clouds VoxelGrid layout: n * max_map_points <= this      // cells per axis a packed cell can hold (10 bits)
 
 LG_DEVICE int lane_id() { return threadIdx.x & 63; }
 LG_DEVICE int wave_id() { return threadIdx.x >> 6; }
@@ -670,7 +672,8 @@ __device__ __attribute__((noinline)) void lm_solve(S2mLds& L, int iterCount) {
   L.flag = conv ? 1 : 0;
 }
 
-__global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch* scratch, int max_map) {
+__global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch* scratch, int max_map,
+                                                     int max_iters) {
   __shared__ S2mLds L;
   const int p = blockIdx.x, tid = threadIdx.x;
   const float4* corner = (const float4*)io.corner + io.corner_off[p];
@@ -706,7 +709,7 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch*
     return;
   }
   const GridInfo gc = L.gc, gs = L.gs;
-  for (int iterCount = 0; iterCount < 10; iterCount++) {
+  for (int iterCount = 0; iterCount < max_iters; iterCount++) {
     if (tid == 0) {  // updatePointAssociateToMapSinCos (:397-410); LMOptimization's trig is the same
       const float* t = L.t;
       L.T = Trig{cosf_g(t[0]), sinf_g(t[0]), cosf_g(t[1]), sinf_g(t[1]), cosf_g(t[2]), sinf_g(t[2]), t[3], t[4], t[5]};
@@ -819,8 +822,18 @@ LG_DEVICE int block_excl_scan(int v, int* red, int& total) {
 }
 
 // VoxelGrid, part 1 (PCL applyFilter up to the sort): bounds, leaf indices, the cloud's sort segment
+// k64 != nullptr: the few-clouds layout for one device-wide sort, 64-bit keys (cloud << 32 | leaf index)
+// with every slot past the cloud's points padded by (n_clouds << 32), which sorts after all clouds
+LG_DEVICE void vox_pad(unsigned long long* k64, unsigned* vals, int c, int from, int cap, int n_clouds) {
+  for (int i = from + (int)threadIdx.x; i < cap; i += S2M_THREADS) {
+    k64[(size_t)c * cap + i] = (unsigned long long)n_clouds << 32;
+    vals[(size_t)c * cap + i] = 0u;
+  }
+}
+
 __global__ __launch_bounds__(S2M_THREADS) void k_vox_keys(lego_map_voxel_io io, unsigned* keys, unsigned* vals,
-                                                          int* seg_b, int* seg_e, int* ovf, int cap) {
+                                                          int* seg_b, int* seg_e, int* ovf, int cap,
+                                                          unsigned long long* k64, int n_clouds) {
   __shared__ float red[S2M_THREADS / 64];
   __shared__ int sh[8];
   const int c = blockIdx.x, tid = threadIdx.x;
@@ -828,6 +841,7 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vox_keys(lego_map_voxel_io io, 
   const float4* in = (const float4*)io.in + io.in_off[c];
   if (n > cap || n < 0) {
     if (tid == 0) { seg_b[c] = seg_e[c] = c * cap; ovf[c] = -1; }
+    if (k64) vox_pad(k64, vals, c, 0, cap, n_clouds);
     return;
   }
   const float inv = 1.0f / io.leaf[c];  // inverse_leaf_size_
@@ -859,22 +873,40 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vox_keys(lego_map_voxel_io io, 
     ovf[c] = bad;
   }
   __syncthreads();
-  if (sh[5]) return;
+  if (sh[5]) {
+    if (k64) vox_pad(k64, vals, c, 0, cap, n_clouds);
+    return;
+  }
   const float mb0 = (float)sh[0], mb1 = (float)sh[1], mb2 = (float)sh[2];
   const int m1 = sh[3], m2 = sh[4];
   unsigned* k = keys + (size_t)c * cap;
   unsigned* v = vals + (size_t)c * cap;
+  const unsigned long long khi = (unsigned long long)c << 32;
   for (int i = tid; i < n; i += S2M_THREADS) {
     const float4 p = in[i];
     const int i0 = (int)(floorf(p.x * inv) - mb0), i1 = (int)(floorf(p.y * inv) - mb1), i2 = (int)(floorf(p.z * inv) - mb2);
-    k[i] = (unsigned)(i0 + i1 * m1 + i2 * m2);
+    const unsigned key = (unsigned)(i0 + i1 * m1 + i2 * m2);
+    if (k64)
+      k64[(size_t)c * cap + i] = khi | key;
+    else
+      k[i] = key;
     v[i] = (unsigned)i;
   }
+  if (k64) vox_pad(k64, vals, c, n, cap, n_clouds);
 }
 
+struct KeyView {
+  const unsigned* p;
+  int ks;
+  LG_DEVICE unsigned operator[](int i) const { return p[(size_t)i * ks]; }
+};
+
 // VoxelGrid, part 2: one centroid per run of equal leaf index in the (stably) sorted keys
+// ks = 1: keys / vals per cloud at c * cap (segmented sort); ks = 2: the low words of the few-clouds
+// layout's sorted 64-bit keys, cloud c's entries after those of the clouds before it
 __global__ __launch_bounds__(S2M_THREADS) void k_vox_reduce(lego_map_voxel_io io, const unsigned* keys,
-                                                            const unsigned* vals, const int* ovf, int cap) {
+                                                            const unsigned* vals, const int* ovf, int cap,
+                                                            const int* seg_b, const int* seg_e, int ks) {
   __shared__ int red[S2M_THREADS / 64];
   const int c = blockIdx.x, tid = threadIdx.x;
   const int n = io.in_n[c];
@@ -889,8 +921,13 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vox_reduce(lego_map_voxel_io io
     if (tid == 0) { io.out_n[c] = n; io.status[c] = LEGO_ST_VOXEL_OVERFLOW; }
     return;
   }
-  const unsigned* k = keys + (size_t)c * cap;
-  const unsigned* v = vals + (size_t)c * cap;
+  size_t start = (size_t)c * cap;
+  if (ks == 2) {
+    start = 0;
+    for (int q = 0; q < c; ++q) start += (size_t)(seg_e[q] - seg_b[q]);
+  }
+  const KeyView k{keys + start * ks, ks};
+  const unsigned* v = vals + start;
   __shared__ float4 tp[S2M_THREADS];   // the tile's points in sorted order (gathered together)
   __shared__ unsigned tk[S2M_THREADS + 1];
   int base = 0;
@@ -934,6 +971,7 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vox_reduce(lego_map_voxel_io io
 struct lego_s2m {
   int device = 0;
   int max_problems = 0, max_map = 0;
+  int max_iters = 10;  // :1320; lego_test_s2m_debug lowers it
   S2mScratch* d_scratch = nullptr;
   void* d_mem = nullptr;
   // host-call staging
@@ -947,6 +985,13 @@ struct lego_s2m {
   int *d_seg = nullptr, *d_ovf = nullptr;
   void* d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
+  // few-clouds layout (n * max_map <= S2M_WIDE_MAX): 64-bit keys in / sorted, values in / sorted
+  unsigned long long *d_k64 = nullptr, *d_k64b = nullptr;
+  unsigned *d_wv = nullptr, *d_wv2 = nullptr;
+  int *d_wseg = nullptr, *d_wovf = nullptr;
+  void* d_wide_tmp = nullptr;
+  size_t wide_tmp_bytes = 0;
+  int wide_clouds = 0;
 };
 
 extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max_map_points, lego_s2m** out) {
@@ -997,7 +1042,8 @@ extern "C" void lego_s2m_destroy(lego_s2m* m) {
   if (m->d_clouds) hipFree(m->d_clouds);
   if (m->d_meta) hipFree(m->d_meta);
   for (void* p : {(void*)m->d_keys, (void*)m->d_vals, (void*)m->d_keys2, (void*)m->d_vals2, (void*)m->d_seg,
-                  (void*)m->d_ovf, m->d_sort_tmp})
+                  (void*)m->d_ovf, m->d_sort_tmp, (void*)m->d_k64, (void*)m->d_k64b, (void*)m->d_wv, (void*)m->d_wv2,
+                  (void*)m->d_wseg, (void*)m->d_wovf, m->d_wide_tmp})
     if (p) hipFree(p);
   delete m;
 }
@@ -1009,7 +1055,8 @@ extern "C" int lego_s2m_run(lego_s2m* m, int32_t n, const lego_s2m_io* io, void*
       !io->surf_map_n || !io->transform || !io->degenerate || !io->info)
     return LEGO_EINVAL;
   if (hipSetDevice(m->device) != hipSuccess) return LEGO_EDEVICE;
-  hipLaunchKernelGGL(k_s2m, dim3(n), dim3(S2M_THREADS), 0, (hipStream_t)hip_stream, *io, m->d_scratch, m->max_map);
+  hipLaunchKernelGGL(k_s2m, dim3(n), dim3(S2M_THREADS), 0, (hipStream_t)hip_stream, *io, m->d_scratch, m->max_map,
+                     m->max_iters);
   return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }
 
@@ -1077,6 +1124,48 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
     return LEGO_EINVAL;
   if (hipSetDevice(m->device) != hipSuccess) return LEGO_EDEVICE;
   const int cap = m->max_map;
+  hipStream_t st = (hipStream_t)hip_stream;
+  if ((size_t)n * cap <= S2M_WIDE_MAX && n < 64) {
+    // few clouds (the mapping thread's five): one device-wide stable radix sort over all of them instead
+    // of rocPRIM's segmented sort, which gives each cloud a single workgroup
+    if (n > m->wide_clouds) {
+      const size_t e = (size_t)n * cap;
+      size_t tmp = 0;
+      if (rocprim::radix_sort_pairs((void*)nullptr, tmp, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                    (unsigned*)nullptr, (unsigned*)nullptr, e, 0, 38) != hipSuccess)
+        return LEGO_EDEVICE;
+      hipDeviceSynchronize();
+      for (void* p : {(void*)m->d_k64, (void*)m->d_k64b, (void*)m->d_wv, (void*)m->d_wv2, (void*)m->d_wseg,
+                      (void*)m->d_wovf, m->d_wide_tmp})
+        if (p) hipFree(p);
+      m->d_k64 = m->d_k64b = nullptr;
+      m->d_wv = m->d_wv2 = nullptr;
+      m->d_wseg = m->d_wovf = nullptr;
+      m->d_wide_tmp = nullptr;
+      m->wide_clouds = 0;
+      if (hipMalloc((void**)&m->d_k64, e * 8) != hipSuccess || hipMalloc((void**)&m->d_k64b, e * 8) != hipSuccess ||
+          hipMalloc((void**)&m->d_wv, e * 4) != hipSuccess || hipMalloc((void**)&m->d_wv2, e * 4) != hipSuccess ||
+          hipMalloc((void**)&m->d_wseg, (size_t)n * 2 * 4) != hipSuccess ||
+          hipMalloc((void**)&m->d_wovf, (size_t)n * 4) != hipSuccess || hipMalloc(&m->d_wide_tmp, tmp) != hipSuccess)
+        return LEGO_ENOMEM;
+      m->wide_tmp_bytes = tmp;
+      m->wide_clouds = n;
+    }
+    int* wb = m->d_wseg;
+    int* we = m->d_wseg + m->wide_clouds;
+    hipLaunchKernelGGL(k_vox_keys, dim3(n), dim3(S2M_THREADS), 0, st, *io, nullptr, m->d_wv, wb, we, m->d_wovf, cap,
+                       m->d_k64, n);
+    if (hipGetLastError() != hipSuccess) return LEGO_EDEVICE;
+    int bits = 32;
+    while ((1 << (bits - 32)) <= n) ++bits;  // the cloud index and the pad value n
+    size_t tmp = m->wide_tmp_bytes;
+    if (rocprim::radix_sort_pairs(m->d_wide_tmp, tmp, m->d_k64, m->d_k64b, m->d_wv, m->d_wv2, (size_t)n * cap, 0, bits,
+                                  st) != hipSuccess)
+      return LEGO_EDEVICE;
+    hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, (const unsigned*)m->d_k64b, m->d_wv2,
+                       m->d_wovf, cap, wb, we, 2);
+    return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+  }
   if (n > m->vox_clouds) {  // scratch for n clouds of up to max_map_points (grows, never shrinks)
     const int nc = n;
     const size_t e = (size_t)nc * cap;
@@ -1102,11 +1191,10 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
     m->sort_tmp_bytes = tmp;
     m->vox_clouds = nc;
   }
-  hipStream_t st = (hipStream_t)hip_stream;
   int* seg_b = m->d_seg;
   int* seg_e = m->d_seg + m->vox_clouds;
   hipLaunchKernelGGL(k_vox_keys, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys, m->d_vals, seg_b, seg_e, m->d_ovf,
-                     cap);
+                     cap, nullptr, n);
   if (hipGetLastError() != hipSuccess) return LEGO_EDEVICE;
   // stable LSD radix sort of every cloud's (leaf index, point index) pairs: std::stable_sort's order
   size_t tmp = m->sort_tmp_bytes;
@@ -1114,6 +1202,24 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
                                           (unsigned)((size_t)n * cap), (unsigned)n, seg_b, seg_e, 0, 32, st) !=
       hipSuccess)
     return LEGO_EDEVICE;
-  hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys2, m->d_vals2, m->d_ovf, cap);
+  hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys2, m->d_vals2, m->d_ovf, cap, seg_b,
+                     seg_e, 1);
   return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }
+
+// test hook: the LM iteration cap (10 in the product), and the LM rows of problem p's last iteration
+// (per query: arx, ary, arz, coeff.x, coeff.y, coeff.z, -coeff.intensity, selected) into out[8 * nq]
+extern "C" int lego_test_s2m_debug(lego_s2m* m, int32_t max_iters, int32_t p, int32_t nq, float* out) {
+  if (!m || max_iters < 1 || max_iters > 10 || p < 0 || p >= m->max_problems || nq < 0 || nq > m->max_map ||
+      (nq && !out))
+    return LEGO_EINVAL;
+  m->max_iters = max_iters;
+  if (!nq) return LEGO_OK;
+  if (hipSetDevice(m->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  S2mScratch g;
+  if (hipMemcpy(&g, m->d_scratch + 2 * p, sizeof(g), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(out, g.rows, (size_t)nq * 32, hipMemcpyDeviceToHost) != hipSuccess)
+    return LEGO_EDEVICE;
+  return LEGO_OK;
+}
+

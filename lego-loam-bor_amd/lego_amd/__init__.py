@@ -95,6 +95,7 @@ def lib():
         L.lego_mapper_step.argtypes = [C.c_void_p] + [C.c_void_p, C.c_int32] * 3 + [P(C.c_float), P(C.c_float),
                                                                                     P(C.c_int32)]
         L.lego_mapper_key_poses.argtypes = [C.c_void_p, P(C.c_float), C.c_int32, P(C.c_int32)]
+        L.lego_map_associate.argtypes = [P(C.c_float)] * 4
         _lib = L
     return _lib
 

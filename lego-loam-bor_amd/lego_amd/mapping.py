@@ -238,68 +238,16 @@ def prepare_parts_gpu(s2m, cparts, sparts, scans, t0, degenerate=None, stream=0,
 
 
 # ---- MapOptimization's mapping loop around the GPU operations ---------------------------------------
-def _f(x):
-    return np.float32(x)
-
-
 def transform_associate_to_map(tSum, tBef, tAft):
-    """transformAssociateToMap (mapOptmization.cpp:264-387) in float32: the odometry increment since the
-    last mapping step applied to the last mapped pose; returns transformTobeMapped."""
-    S, B, A = [np.asarray(t, np.float32) for t in (tSum, tBef, tAft)]
-    c, s = np.cos, np.sin
-    incre = np.zeros(6, np.float32)
-    x1 = c(S[1]) * (B[3] - S[3]) - s(S[1]) * (B[5] - S[5])
-    y1 = B[4] - S[4]
-    z1 = s(S[1]) * (B[3] - S[3]) + c(S[1]) * (B[5] - S[5])
-    x2 = x1
-    y2 = c(S[0]) * y1 + s(S[0]) * z1
-    z2 = -s(S[0]) * y1 + c(S[0]) * z1
-    incre[3] = c(S[2]) * x2 + s(S[2]) * y2
-    incre[4] = -s(S[2]) * x2 + c(S[2]) * y2
-    incre[5] = z2
-    sbcx, cbcx, sbcy, cbcy, sbcz, cbcz = s(S[0]), c(S[0]), s(S[1]), c(S[1]), s(S[2]), c(S[2])
-    sblx, cblx, sbly, cbly, sblz, cblz = s(B[0]), c(B[0]), s(B[1]), c(B[1]), s(B[2]), c(B[2])
-    salx, calx, saly, caly, salz, calz = s(A[0]), c(A[0]), s(A[1]), c(A[1]), s(A[2]), c(A[2])
+    """transformAssociateToMap (mapOptmization.cpp:264-387): the odometry increment since the last mapping
+    step applied to the last mapped pose; returns transformTobeMapped.  Runs in the product library
+    (lego_map_associate: float, the float libm the reference's build calls)."""
+    import ctypes as C
+    import lego_amd as LA
+    S, B, A = [np.ascontiguousarray(np.asarray(t, np.float32).reshape(6)) for t in (tSum, tBef, tAft)]
     T = np.zeros(6, np.float32)
-    srx = (-sbcx * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz) -
-           cbcx * sbcy * (calx * calz * (cbly * sblz - cblz * sblx * sbly) - calx * salz * (cbly * cblz + sblx * sbly * sblz) +
-                          cblx * salx * sbly) -
-           cbcx * cbcy * (calx * salz * (cblz * sbly - cbly * sblx * sblz) - calx * calz * (sbly * sblz + cbly * cblz * sblx) +
-                          cblx * cbly * salx))
-    T[0] = -np.arcsin(np.float32(srx))
-    srycrx = (sbcx * (cblx * cblz * (caly * salz - calz * salx * saly) - cblx * sblz * (caly * calz + salx * saly * salz) +
-                      calx * saly * sblx) -
-              cbcx * cbcy * ((caly * calz + salx * saly * salz) * (cblz * sbly - cbly * sblx * sblz) +
-                             (caly * salz - calz * salx * saly) * (sbly * sblz + cbly * cblz * sblx) - calx * cblx * cbly * saly) +
-              cbcx * sbcy * ((caly * calz + salx * saly * salz) * (cbly * cblz + sblx * sbly * sblz) +
-                             (caly * salz - calz * salx * saly) * (cbly * sblz - cblz * sblx * sbly) + calx * cblx * saly * sbly))
-    crycrx = (sbcx * (cblx * sblz * (calz * saly - caly * salx * salz) - cblx * cblz * (saly * salz + caly * calz * salx) +
-                      calx * caly * sblx) +
-              cbcx * cbcy * ((saly * salz + caly * calz * salx) * (sbly * sblz + cbly * cblz * sblx) +
-                             (calz * saly - caly * salx * salz) * (cblz * sbly - cbly * sblx * sblz) + calx * caly * cblx * cbly) -
-              cbcx * sbcy * ((saly * salz + caly * calz * salx) * (cbly * sblz - cblz * sblx * sbly) +
-                             (calz * saly - caly * salx * salz) * (cbly * cblz + sblx * sbly * sblz) - calx * caly * cblx * sbly))
-    T[1] = np.arctan2(np.float32(srycrx / c(T[0])), np.float32(crycrx / c(T[0])))
-    srzcrx = ((cbcz * sbcy - cbcy * sbcx * sbcz) * (calx * salz * (cblz * sbly - cbly * sblx * sblz) -
-                                                    calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx) -
-              (cbcy * cbcz + sbcx * sbcy * sbcz) * (calx * calz * (cbly * sblz - cblz * sblx * sbly) -
-                                                    calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) +
-              cbcx * sbcz * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz))
-    crzcrx = ((cbcy * sbcz - cbcz * sbcx * sbcy) * (calx * calz * (cbly * sblz - cblz * sblx * sbly) -
-                                                    calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) -
-              (sbcy * sbcz + cbcy * cbcz * sbcx) * (calx * salz * (cblz * sbly - cbly * sblx * sblz) -
-                                                    calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx) +
-              cbcx * cbcz * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz))
-    T[2] = np.arctan2(np.float32(srzcrx / c(T[0])), np.float32(crzcrx / c(T[0])))
-    x1 = c(T[2]) * incre[3] - s(T[2]) * incre[4]
-    y1 = s(T[2]) * incre[3] + c(T[2]) * incre[4]
-    z1 = incre[5]
-    x2 = x1
-    y2 = c(T[0]) * y1 - s(T[0]) * z1
-    z2 = s(T[0]) * y1 + c(T[0]) * z1
-    T[3] = A[3] - (c(T[1]) * x2 + s(T[1]) * z2)
-    T[4] = A[4] - y2
-    T[5] = A[5] - (-s(T[1]) * x2 + c(T[1]) * z2)
+    fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))  # noqa: E731
+    LA._check(LA.lib().lego_map_associate(fp(S), fp(B), fp(A), fp(T)), "lego_map_associate")
     return T
 
 
@@ -337,7 +285,8 @@ class MapSequence:
 
     RADIUS = 50.0  # surrounding_keyframe_search_radius (loam_config.yaml:27)
 
-    def __init__(self):
+    def __init__(self, associate=None):
+        self._associate = associate or transform_associate_to_map  # tests pass the oracle's
         z = lambda: np.zeros(6, np.float32)  # noqa: E731
         self.t_sum, self.t_tobe, self.t_bef, self.t_aft = z(), z(), z(), z()
         self.key_pos = []       # cloudKeyPoses3D: (x, y, z, index)
@@ -352,7 +301,7 @@ class MapSequence:
     def begin(self, assoc):
         """One AssociationOut: returns (corner parts, surf parts, scan clouds, transformTobeMapped)."""
         self.t_sum = np.asarray(assoc["transform_sum"], np.float32).copy()  # OdometryToTransform (:1540)
-        self.t_tobe = transform_associate_to_map(self.t_sum, self.t_bef, self.t_aft)
+        self.t_tobe = self._associate(self.t_sum, self.t_bef, self.t_aft)
         if self.key_pos:  # extractSurroundingKeyFrames, loop closure off (:915-995)
             kp = np.array(self.key_pos, np.float32)
             d = ((kp[:, 0] - self.cur_pos[0]) ** 2 + (kp[:, 1] - self.cur_pos[1]) ** 2) + (kp[:, 2] - self.cur_pos[2]) ** 2

@@ -164,6 +164,32 @@ def voxel_grid(points, leaf, stable=True):
     return out[:n_out.value].copy(), st
 
 
+def scan2map_debug(corner, surf, corner_map, surf_map, transform, degenerate=0, max_iters=10):
+    """scan2map with at most max_iters LM iterations; also returns the last iteration's rows (8 floats a
+    query, lego_test_s2m_debug's layout)."""
+    import numpy as np
+    arrs = [_f32(a) for a in (corner, surf, corner_map, surf_map)]
+    t = np.ascontiguousarray(np.asarray(transform, np.float32).reshape(6).copy())
+    dg = C.c_int32(int(degenerate))
+    info = np.zeros(4, np.int32)
+    rows = np.zeros((len(arrs[0]) + len(arrs[1]), 8), np.float32)
+    args = []
+    for a in arrs:
+        args += [a.ctypes.data_as(P(C.c_float)), len(a)]
+    lib().oracle_scan2map_debug(*args, t.ctypes.data_as(P(C.c_float)), C.byref(dg), info.ctypes.data_as(P(C.c_int32)),
+                                int(max_iters), rows.ctypes.data_as(P(C.c_float)))
+    return t, dg.value, info, rows
+
+
+def associate_to_map(t_sum, t_bef, t_aft):
+    """MapOptimization::transformAssociateToMap restated (mapOptmization.cpp:264-387): transformTobeMapped."""
+    import numpy as np
+    a = [np.ascontiguousarray(np.asarray(t, np.float32).reshape(6)) for t in (t_sum, t_bef, t_aft)]
+    out = np.zeros(6, np.float32)
+    lib().oracle_associate_to_map(*[x.ctypes.data_as(P(C.c_float)) for x in a + [out]])
+    return out
+
+
 def transform_cloud(points, pose):
     """MapOptimization::transformPointCloud restated: pose = (roll, pitch, yaw, x, y, z)."""
     import numpy as np

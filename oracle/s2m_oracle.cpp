@@ -21,7 +21,8 @@
 //         component of each eigenvector;
 //       ColPivHouseholderQR<Matrix<float,5,3>> / <Matrix<float,6,6>> (:1153, :1260): restated in
 //         float with sequential sums;
-//       matAt * matA (:1258): float products summed in double, rounded to float (the FA LM's model);
+//       matAt * matA (:1258): float products summed in double, rounded to float (the FA LM's model),
+//         in the product's fixed summation order (see lm_step);
 //       SelfAdjointEigenSolver<Matrix<float,6,6>> (:1267): only "largest eigenvalue < 100" is used
 //         (the ascending order makes :1275-1284 zero every row exactly then), by cyclic Jacobi in
 //         double.
@@ -417,35 +418,69 @@ struct State {
   bool degenerate;
 };
 
-// LMOptimization (:1199-1312); true = converged
-static bool lm_step(State& S, const std::vector<Pt>& ori, const std::vector<Pt>& coeffs, int iterCount) {
-  const float srx = std::sin(S.t[0]), crx = std::cos(S.t[0]);
-  const float sry = std::sin(S.t[1]), cry = std::cos(S.t[1]);
-  const float srz = std::sin(S.t[2]), crz = std::cos(S.t[2]);
+// one LM row (:1219-1256): matA = (arx, ary, arz, coeff x, y, z), matB = -coeff intensity
+static void lm_row(const Trig& T, const Pt& p, const Pt& c, float out[7]) {
+  const float srx = T.sRoll, crx = T.cRoll, sry = T.sPitch, cry = T.cPitch, srz = T.sYaw, crz = T.cYaw;
+  const float arx = (crx * sry * srz * p.x + crx * crz * sry * p.y - srx * sry * p.z) * c.x +
+                    (-srx * srz * p.x - crz * srx * p.y - crx * p.z) * c.y +
+                    (crx * cry * srz * p.x + crx * cry * crz * p.y - cry * srx * p.z) * c.z;
+  const float ary = ((cry * srx * srz - crz * sry) * p.x + (sry * srz + cry * crz * srx) * p.y + crx * cry * p.z) * c.x +
+                    ((-cry * crz - srx * sry * srz) * p.x + (cry * srz - crz * srx * sry) * p.y - crx * sry * p.z) * c.z;
+  const float arz = ((crz * srx * sry - cry * srz) * p.x + (-cry * crz - srx * sry * srz) * p.y) * c.x +
+                    (crx * crz * p.x - crx * srz * p.y) * c.y +
+                    ((sry * srz + cry * crz * srx) * p.x + (crz * sry - cry * srx * srz) * p.y) * c.z;
+  const float row[7] = {arx, ary, arz, c.x, c.y, c.z, -c.i};  // matA row, matB entry (:1246-1256)
+  std::memcpy(out, row, sizeof(row));
+}
+
+// matAt * matA and matAt * matB (:1258-1259) in a fixed order: row q (its query index: corners first,
+// then surfs) adds its float products, widened to double, into lane q % 1024's partial sums in
+// increasing q; each 64-lane group reduces by xor butterflies (offsets 32, 16, .., 1) and the 16 group
+// sums add in group order.  This is the order of the product's k_s2m (one lane per query, wave
+// shuffles, a per-wave table); Eigen's float GEMM order cannot be restated without Eigen, and any
+// fixed order is the reference's sum up to rounding.  out: 21 upper-triangle AtA entries, then 6 AtB.
+static void normal_equations(const std::vector<float>& rows, const std::vector<int>& qidx, double out[27]) {
+  constexpr int LANES = 1024, W = 64;
+  std::vector<double> part((size_t)LANES * 27, 0.0);
+  for (size_t i = 0; i < qidx.size(); ++i) {
+    const float* a = &rows[7 * i];
+    const float b = a[6];
+    double* p = &part[(size_t)(qidx[i] % LANES) * 27];
+    int k = 0;
+    for (int r = 0; r < 6; ++r)
+      for (int j = r; j < 6; ++j) p[k++] += (double)(a[r] * a[j]);
+    for (int r = 0; r < 6; ++r) p[21 + r] += (double)(a[r] * b);
+  }
+  for (int k = 0; k < 27; ++k) {
+    double s = 0.0;
+    for (int w = 0; w < LANES / W; ++w) {
+      double v[W], t[W];
+      for (int l = 0; l < W; ++l) v[l] = part[(size_t)(w * W + l) * 27 + k];
+      for (int o = W / 2; o > 0; o >>= 1) {
+        for (int l = 0; l < W; ++l) t[l] = v[l] + v[l ^ o];
+        std::memcpy(v, t, sizeof(v));
+      }
+      s += v[0];
+    }
+    out[k] = s;
+  }
+}
+
+// LMOptimization (:1199-1312); true = converged.  qidx: each selected row's query index.
+static bool lm_step(State& S, const std::vector<Pt>& ori, const std::vector<Pt>& coeffs, const std::vector<int>& qidx,
+                    int iterCount) {
   const int n = (int)ori.size();
   if (n < 50) return false;
-  double AtA[36] = {0}, Atb[6] = {0};
-  for (int i = 0; i < n; i++) {
-    const Pt& p = ori[i];
-    const Pt& c = coeffs[i];
-    const float arx = (crx * sry * srz * p.x + crx * crz * sry * p.y - srx * sry * p.z) * c.x +
-                      (-srx * srz * p.x - crz * srx * p.y - crx * p.z) * c.y +
-                      (crx * cry * srz * p.x + crx * cry * crz * p.y - cry * srx * p.z) * c.z;
-    const float ary = ((cry * srx * srz - crz * sry) * p.x + (sry * srz + cry * crz * srx) * p.y + crx * cry * p.z) * c.x +
-                      ((-cry * crz - srx * sry * srz) * p.x + (cry * srz - crz * srx * sry) * p.y - crx * sry * p.z) * c.z;
-    const float arz = ((crz * srx * sry - cry * srz) * p.x + (-cry * crz - srx * sry * srz) * p.y) * c.x +
-                      (crx * crz * p.x - crx * srz * p.y) * c.y +
-                      ((sry * srz + cry * crz * srx) * p.x + (crz * sry - cry * srx * srz) * p.y) * c.z;
-    const float a[6] = {arx, ary, arz, c.x, c.y, c.z};
-    const float b = -c.i;
-    for (int r = 0; r < 6; ++r) {
-      for (int k = 0; k < 6; ++k) AtA[r * 6 + k] += (double)(a[r] * a[k]);
-      Atb[r] += (double)(a[r] * b);
-    }
-  }
+  std::vector<float> rows((size_t)7 * n);
+  const Trig T = trig_of(S.t);
+  for (int i = 0; i < n; i++) lm_row(T, ori[i], coeffs[i], &rows[(size_t)7 * i]);
+  double ne[27];
+  normal_equations(rows, qidx, ne);
   float A[36], B[6], X[6];
-  for (int k = 0; k < 36; ++k) A[k] = (float)AtA[k];
-  for (int k = 0; k < 6; ++k) B[k] = (float)Atb[k];
+  int k = 0;
+  for (int r = 0; r < 6; ++r)
+    for (int j = r; j < 6; ++j, ++k) A[r * 6 + j] = A[j * 6 + r] = (float)ne[k];
+  for (int r = 0; r < 6; ++r) B[r] = (float)ne[21 + r];
   qr_solve<6, 6>(A, B, X);
   if (iterCount == 0) S.degenerate = lmax6(A) < 100.0;  // :1262-1286 (see header)
   if (S.degenerate)
@@ -459,9 +494,9 @@ static bool lm_step(State& S, const std::vector<Pt>& ori, const std::vector<Pt>&
 
 }  // namespace s2m
 
-extern "C" int oracle_scan2map(const float* corner, int n_corner, const float* surf, int n_surf, const float* corner_map,
-                               int n_corner_map, const float* surf_map, int n_surf_map, float* transform,
-                               int32_t* degenerate, int32_t* info) {
+static int scan2map(const float* corner, int n_corner, const float* surf, int n_surf, const float* corner_map,
+                    int n_corner_map, const float* surf_map, int n_surf_map, float* transform, int32_t* degenerate,
+                    int32_t* info, int max_iters, float* rows_out) {
   using namespace s2m;
   info[0] = 0; info[1] = 0; info[2] = 0; info[3] = 0;
   if (!(n_corner_map > 10 && n_surf_map > 100)) {  // :1316
@@ -480,9 +515,11 @@ extern "C" int oracle_scan2map(const float* corner, int n_corner, const float* s
   S.degenerate = *degenerate != 0;
   int status = 0, iters = 0, nsel = 0;
   std::vector<Pt> ori, coeffs;
-  for (int iterCount = 0; iterCount < 10; iterCount++) {
+  std::vector<int> qidx;
+  for (int iterCount = 0; iterCount < max_iters; iterCount++) {
     ori.clear();
     coeffs.clear();
+    qidx.clear();
     const Trig T = trig_of(S.t);
     for (int i = 0; i < n_corner; i++) {  // cornerOptimization (:1028-1134)
       const Pt sel = associate(T, cs[i]);
@@ -492,7 +529,7 @@ extern "C" int oracle_scan2map(const float* corner, int n_corner, const float* s
       if (!gc.knn5(sel, ind, d, tie)) continue;
       if (tie) status |= LEGO_S2M_ST_KNN_TIE;
       Pt c;
-      if (corner_coeff(cm, ind, sel, c)) { ori.push_back(cs[i]); coeffs.push_back(c); }
+      if (corner_coeff(cm, ind, sel, c)) { ori.push_back(cs[i]); coeffs.push_back(c); qidx.push_back(i); }
     }
     for (int i = 0; i < n_surf; i++) {  // surfOptimization (:1136-1197)
       const Pt sel = associate(T, ss[i]);
@@ -502,12 +539,23 @@ extern "C" int oracle_scan2map(const float* corner, int n_corner, const float* s
       if (!gs.knn5(sel, ind, d, tie)) continue;
       if (tie) status |= LEGO_S2M_ST_KNN_TIE;
       Pt c;
-      if (surf_coeff(sm, ind, sel, c)) { ori.push_back(ss[i]); coeffs.push_back(c); }
+      if (surf_coeff(sm, ind, sel, c)) { ori.push_back(ss[i]); coeffs.push_back(c); qidx.push_back(n_corner + i); }
     }
     iters = iterCount + 1;
     nsel = (int)ori.size();
     if (nsel < 50) status |= LEGO_S2M_ST_FEW;
-    const bool conv = lm_step(S, ori, coeffs, iterCount);
+    if (rows_out) {  // the debug view: this iteration's rows in the product's layout
+      std::memset(rows_out, 0, sizeof(float) * 8 * (size_t)(n_corner + n_surf));
+      const Trig T0 = trig_of(S.t);
+      for (size_t i = 0; i < ori.size(); ++i) {
+        float r[7];
+        lm_row(T0, ori[i], coeffs[i], r);
+        float* o = rows_out + 8 * (size_t)qidx[i];
+        std::memcpy(o, r, sizeof(r));
+        o[7] = 1.f;
+      }
+    }
+    const bool conv = lm_step(S, ori, coeffs, qidx, iterCount);
     if (iterCount == 0 && S.degenerate && nsel >= 50) status |= LEGO_S2M_ST_DEGENERATE;
     if (conv) {
       status |= LEGO_S2M_ST_CONVERGED;
@@ -521,6 +569,22 @@ extern "C" int oracle_scan2map(const float* corner, int n_corner, const float* s
   info[2] = nsel;
   info[3] = status;
   return 0;
+}
+
+extern "C" int oracle_scan2map(const float* corner, int n_corner, const float* surf, int n_surf, const float* corner_map,
+                               int n_corner_map, const float* surf_map, int n_surf_map, float* transform,
+                               int32_t* degenerate, int32_t* info) {
+  return scan2map(corner, n_corner, surf, n_surf, corner_map, n_corner_map, surf_map, n_surf_map, transform, degenerate,
+                  info, 10, nullptr);
+}
+
+// debug view: at most max_iters LM iterations, the last iteration's rows as lego_test_s2m_debug's
+extern "C" int oracle_scan2map_debug(const float* corner, int n_corner, const float* surf, int n_surf,
+                                     const float* corner_map, int n_corner_map, const float* surf_map, int n_surf_map,
+                                     float* transform, int32_t* degenerate, int32_t* info, int max_iters,
+                                     float* rows_out) {
+  return scan2map(corner, n_corner, surf, n_surf, corner_map, n_corner_map, surf_map, n_surf_map, transform, degenerate,
+                  info, max_iters, rows_out);
 }
 
 // test hooks: the restated Eigen pieces and the kNN on their own
@@ -559,4 +623,57 @@ extern "C" void oracle_transform_cloud(const float* in, int n, const float* pose
     t[2] = -stPitch * x2 + ctPitch * z2 + tInZ;
     t[3] = f[3];
   }
+}
+
+// MapOptimization::transformAssociateToMap (mapOptmization.cpp:264-387): transformSum S, transformBefMapped
+// B, transformAftMapped A -> transformTobeMapped T.  float throughout, the float libm overloads.
+extern "C" void oracle_associate_to_map(const float* S, const float* B, const float* A, float* T) {
+  using std::cos;
+  using std::sin;
+  float inc[6] = {0, 0, 0, 0, 0, 0};
+  {
+    const float x1 = cos(S[1]) * (B[3] - S[3]) - sin(S[1]) * (B[5] - S[5]);
+    const float y1 = B[4] - S[4];
+    const float z1 = sin(S[1]) * (B[3] - S[3]) + cos(S[1]) * (B[5] - S[5]);
+    const float y2 = cos(S[0]) * y1 + sin(S[0]) * z1;
+    const float z2 = -sin(S[0]) * y1 + cos(S[0]) * z1;
+    inc[3] = cos(S[2]) * x1 + sin(S[2]) * y2;
+    inc[4] = -sin(S[2]) * x1 + cos(S[2]) * y2;
+    inc[5] = z2;
+  }
+  const float sbcx = sin(S[0]), cbcx = cos(S[0]), sbcy = sin(S[1]), cbcy = cos(S[1]), sbcz = sin(S[2]), cbcz = cos(S[2]);
+  const float sblx = sin(B[0]), cblx = cos(B[0]), sbly = sin(B[1]), cbly = cos(B[1]), sblz = sin(B[2]), cblz = cos(B[2]);
+  const float salx = sin(A[0]), calx = cos(A[0]), saly = sin(A[1]), caly = cos(A[1]), salz = sin(A[2]), calz = cos(A[2]);
+  // products shared by the three angle expressions
+  const float p1 = salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz;
+  const float p2 = calx * calz * (cbly * sblz - cblz * sblx * sbly) - calx * salz * (cbly * cblz + sblx * sbly * sblz) +
+                   cblx * salx * sbly;
+  const float p3 = calx * salz * (cblz * sbly - cbly * sblx * sblz) - calx * calz * (sbly * sblz + cbly * cblz * sblx) +
+                   cblx * cbly * salx;
+  const float srx = -sbcx * p1 - cbcx * sbcy * p2 - cbcx * cbcy * p3;
+  T[0] = -std::asin(srx);
+  const float q1 = caly * calz + salx * saly * salz, q2 = caly * salz - calz * salx * saly;
+  const float q3 = saly * salz + caly * calz * salx, q4 = calz * saly - caly * salx * salz;
+  const float srycrx = sbcx * (cblx * cblz * q2 - cblx * sblz * q1 + calx * saly * sblx) -
+                       cbcx * cbcy * (q1 * (cblz * sbly - cbly * sblx * sblz) + q2 * (sbly * sblz + cbly * cblz * sblx) -
+                                      calx * cblx * cbly * saly) +
+                       cbcx * sbcy * (q1 * (cbly * cblz + sblx * sbly * sblz) + q2 * (cbly * sblz - cblz * sblx * sbly) +
+                                      calx * cblx * saly * sbly);
+  const float crycrx = sbcx * (cblx * sblz * q4 - cblx * cblz * q3 + calx * caly * sblx) +
+                       cbcx * cbcy * (q3 * (sbly * sblz + cbly * cblz * sblx) + q4 * (cblz * sbly - cbly * sblx * sblz) +
+                                      calx * caly * cblx * cbly) -
+                       cbcx * sbcy * (q3 * (cbly * sblz - cblz * sblx * sbly) + q4 * (cbly * cblz + sblx * sbly * sblz) -
+                                      calx * caly * cblx * sbly);
+  T[1] = std::atan2(srycrx / cos(T[0]), crycrx / cos(T[0]));
+  const float srzcrx = (cbcz * sbcy - cbcy * sbcx * sbcz) * p3 - (cbcy * cbcz + sbcx * sbcy * sbcz) * p2 + cbcx * sbcz * p1;
+  const float crzcrx = (cbcy * sbcz - cbcz * sbcx * sbcy) * p2 - (sbcy * sbcz + cbcy * cbcz * sbcx) * p3 + cbcx * cbcz * p1;
+  T[2] = std::atan2(srzcrx / cos(T[0]), crzcrx / cos(T[0]));
+  const float x1 = cos(T[2]) * inc[3] - sin(T[2]) * inc[4];
+  const float y1 = sin(T[2]) * inc[3] + cos(T[2]) * inc[4];
+  const float z1 = inc[5];
+  const float y2 = cos(T[0]) * y1 - sin(T[0]) * z1;
+  const float z2 = sin(T[0]) * y1 + cos(T[0]) * z1;
+  T[3] = A[3] - (cos(T[1]) * x1 + sin(T[1]) * z2);
+  T[4] = A[4] - y2;
+  T[5] = A[5] - (-sin(T[1]) * x1 + cos(T[1]) * z2);
 }

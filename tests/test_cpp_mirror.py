@@ -140,3 +140,53 @@ def test_scan2map_mirror_matches_oracle(gpu, tmp_path):
     t_ref, dg_ref, info_ref = O.scan2map(pr["corner"], pr["surf"], pr["corner_map"], pr["surf_map"], pr["transform"])
     np.testing.assert_allclose(t, t_ref, atol=Hs.TF_TOL, rtol=0)
     assert int(tok[8]) == dg_ref and int(tok[10]) == info_ref[0] and int(tok[12]) == info_ref[1]
+
+
+MAP_EXE = os.path.join(REPO, "examples", "mapping")
+
+
+def _write_cycles(path, assocs):
+    with open(path, "wb") as f:
+        f.write(struct.pack("<i", len(assocs)))
+        for a in assocs:
+            for name in ("corner_last", "surf_last", "outlier_last"):
+                x = np.ascontiguousarray(a[name], dtype=np.float32).reshape(-1, 4)
+                f.write(struct.pack("<i", x.shape[0]))
+                f.write(x.tobytes())
+            f.write(np.asarray(a["transform_sum"], np.float32).tobytes())
+
+
+def test_mapping_mirror_fails_loudly_without_device(tmp_path):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "mapping"])
+    import lego_amd
+    if lego_amd.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    f = tmp_path / "c.bin"
+    _write_cycles(str(f), [])
+    r = subprocess.run([MAP_EXE, str(f)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, universal_newlines=True)
+    assert r.returncode == 1 and "rc=-3" in r.stderr
+
+
+@pytest.mark.gpu
+def test_mapping_mirror_matches_oracle_loop(gpu, tmp_path):
+    """MapOptimization (the C++ mirror of the mapping thread) reproduces the oracle loop's
+    transformAftMapped every cycle and its key-frame count."""
+    from lego_amd import mapping as M
+    from test_gpu_mapping_loop import _emitted, mapping_step_oracle
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "mapping"])
+    assocs = _emitted(6, 26)
+    f = tmp_path / "c.bin"
+    _write_cycles(str(f), assocs)
+    r = subprocess.run([MAP_EXE, str(f), "0"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, universal_newlines=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == len(assocs) + 1
+    import oracle as O
+    sq = M.MapSequence(associate=O.associate_to_map)
+    for a, line in zip(assocs, lines):
+        (_, _, info), = mapping_step_oracle([sq], [a])
+        tok = line.split()
+        np.testing.assert_allclose(np.array([float(x) for x in tok[1:7]], np.float32), sq.t_aft, atol=1e-4, rtol=0)
+        assert int(tok[8]) == int(info[0] == 1) and int(tok[10]) == info[1]
+    assert lines[-1] == "keys %d" % len(sq.key_pose6)

@@ -78,6 +78,21 @@ def test_voxel_matches_oracle(s2m, sequences):
             assert np.array_equal(o.view(np.int32), ref.view(np.int32)), (leaf, len(c))
 
 
+def test_voxel_both_sort_layouts(s2m, sequences):
+    """Few clouds take one device-wide radix sort (64-bit cloud|leaf keys), many clouds rocPRIM's
+    segmented sort; the same clouds through both give the oracle's output."""
+    fr = sequences[1]
+    rng = np.random.default_rng(17)
+    base = [fr[4]["corner_last"], fr[4]["surf_last"], np.zeros((0, 4), np.float32),
+            np.repeat(rng.uniform(-1, 1, (30, 4)).astype(np.float32), 7, axis=0)]
+    many = base + [rng.uniform(-5, 5, (int(rng.integers(0, 300)), 4)).astype(np.float32) for _ in range(66)]
+    for clouds in (base, many):  # 4 clouds: device-wide; 70 clouds: segmented
+        got = _gpu_voxel(s2m, clouds, [0.4] * len(clouds))
+        for c, (o, on, st) in zip(clouds, got):
+            ref, rst = O.voxel_grid(c, 0.4, stable=True)
+            assert st == rst and on == len(ref) and np.array_equal(o.view(np.int32), ref.view(np.int32)), len(clouds)
+
+
 def test_voxel_limits(s2m):
     rng = np.random.default_rng(12)
     wide = rng.uniform(-1000, 1000, (2000, 4)).astype(np.float32)  # 1e-3 leaves: indices overflow int32

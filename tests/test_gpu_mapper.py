@@ -2,13 +2,15 @@
 
 lego_mapper_step is MapOptimization::run's loop body (mapOptmization.cpp:1521-1570, loop closure off)
 with the host logic in C++ and the key frames' clouds in device memory; MapSequence +
-mapping_step_oracle is the same loop in Python over the CPU restatements.  Per cycle the
-transformAftMapped must agree within 1e-4, the LM gate / iteration counts exactly, and the key poses
-at the end within 1e-4.
+mapping_step_oracle is the same loop in Python over the CPU restatements.  Bar: north_star's 1e-4 on
+transformAftMapped; measured bit-identical (the device's sinf / cosf restate the host glibc's and the
+normal equations are summed in the oracle's order), so the test asserts identical bits every cycle,
+identical LM gate / iteration / correspondence counts and identical key poses.
 """
 import numpy as np
 import pytest
 
+import oracle as O
 from lego_amd import mapping as M
 from test_gpu_mapping_loop import _emitted, mapping_step_oracle
 
@@ -18,20 +20,20 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("seq", [3, 8])
 def test_mapper_matches_oracle_loop(gpu, seq):
     import lego_amd as LA
-    stream = _emitted(seq, 31)
+    stream = _emitted(seq, 61)
     assert len(stream) >= 5
     mp = LA.Mapper(max_map_points=150000, max_key_points=4_000_000, device=gpu)
-    r = M.MapSequence()
+    r = M.MapSequence(associate=O.associate_to_map)
     ran = 0
     for k, a in enumerate(stream):
         tg, ig = mp.step(a["corner_last"], a["surf_last"], a["outlier_last"], a["transform_sum"])
         (_, _, ir), = mapping_step_oracle([r], [a])
-        assert np.abs(tg - r.t_aft).max() <= 1e-4, (k, tg, r.t_aft)
-        assert ig[0] == ir[0] and ig[1] == ir[1], (k, ig, ir)
+        assert np.array_equal(tg.view(np.int32), r.t_aft.view(np.int32)), (k, tg, r.t_aft)
+        assert np.array_equal(ig, ir), (k, ig, ir)
         ran += int(ig[0] == 1)
     kp = mp.key_poses()
     assert kp.shape == (len(r.key_pose6), 6)
-    assert np.abs(kp - np.array(r.key_pose6)).max() <= 1e-4
+    assert np.array_equal(kp.view(np.int32), np.array(r.key_pose6, np.float32).view(np.int32))
     mp.close()
     assert ran >= len(stream) - 1
     assert len(kp) >= 3

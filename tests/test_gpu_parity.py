@@ -54,7 +54,7 @@ def assert_scan_parity(k, pg, pr, fg, fr, tf_tol=Hs.TF_TOL):
 
 
 def test_device_libm_matches_glibc(gpu):
-    """gfx950 asinf/atan2f/atanf restatement and IEEE sqrt/div equal the host glibc bit for bit."""
+    """gfx950 asinf/atan2f/atanf/sinf/cosf restatements and IEEE sqrt/div equal the host glibc bit for bit."""
     rng = np.random.default_rng(1)
     n = 1 << 21
     a = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32)
@@ -62,7 +62,7 @@ def test_device_libm_matches_glibc(gpu):
     u = rng.uniform(-1, 1, n).astype(np.float32)
     xy = rng.uniform(-100, 100, (2, n)).astype(np.float32)
     libm = C.CDLL("libm.so.6")
-    for f in ("asinf", "atanf", "sqrtf"):
+    for f in ("asinf", "atanf", "sqrtf", "sinf", "cosf"):
         getattr(libm, f).restype = C.c_float
         getattr(libm, f).argtypes = [C.c_float]
     libm.atan2f.restype = C.c_float
@@ -77,7 +77,9 @@ def test_device_libm_matches_glibc(gpu):
 
     cases = [(u, u, 0, lambda x, y: libm.asinf(x)), (a, a, 0, lambda x, y: libm.asinf(x)),
              (xy[0], xy[1], 1, lambda x, y: libm.atan2f(x, y)), (a, b, 1, lambda x, y: libm.atan2f(x, y)),
-             (a, a, 2, lambda x, y: libm.atanf(x)), (np.abs(a), a, 3, lambda x, y: libm.sqrtf(x))]
+             (a, a, 2, lambda x, y: libm.atanf(x)), (np.abs(a), a, 3, lambda x, y: libm.sqrtf(x)),
+             (xy[0], xy[1], 7, lambda x, y: libm.sinf(x)), (xy[1], xy[0], 8, lambda x, y: libm.cosf(x)),
+             (u, u, 7, lambda x, y: libm.sinf(x)), (u, u, 8, lambda x, y: libm.cosf(x))]
     for x, y, which, ref in cases:
         got = dev(np.ascontiguousarray(x), np.ascontiguousarray(y), which)
         idx = rng.choice(len(x), 20000, replace=False)  # host glibc reference on a sample (ctypes is slow)

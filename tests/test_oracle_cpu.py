@@ -211,8 +211,9 @@ def test_introsort_depth_limit_inputs(tmp_path):
     assert rc == 0, out
 
 
-def test_lm_trig_polynomial(tmp_path):
-    """The LM's sinf/cosf fast path equals float(sin(double x)) except in double-rounding corner cases."""
+def test_lm_trig_matches_glibc(tmp_path):
+    """The device's sinf/cosf (glibc 2.35's algorithm, FMA variant) equal the host's glibc bit for bit on
+    every 101st float in [-120, 120] (tools: stride 1 is the exhaustive check)."""
     rc, out = _compile_and_run(os.path.join(REPO, "tests", "native", "trig_check.cpp"), str(tmp_path / "tc"), ["101"])
     assert rc == 0, out
 

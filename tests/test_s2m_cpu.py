@@ -148,9 +148,12 @@ def test_s2m_abi_exports():
     """liblego_frontend.so exports every entry point include/lego_s2m.h declares (no GPU needed)."""
     import re
     hdr = open(os.path.join(REPO, "include", "lego_s2m.h")).read()
-    names = set(re.findall(r"\b(lego_(?:s2m|map)_\w+)\s*\(", hdr))
+    names = set(re.findall(r"\b(lego_(?:s2m|map|mapper)_\w+)\s*\(", hdr))
     assert names == {"lego_s2m_create", "lego_s2m_destroy", "lego_s2m_run", "lego_s2m_run_host", "lego_map_transform",
-                     "lego_map_voxel"}
+                     "lego_map_voxel", "lego_map_associate", "lego_mapper_create", "lego_mapper_destroy",
+                     "lego_mapper_step", "lego_mapper_key_poses"}
+    assert "lego_test_s2m_debug" in hdr
+    names.add("lego_test_s2m_debug")
     lib = C.CDLL(A.LIB_FRONTEND)
     for n in names:
         assert hasattr(lib, n), n
@@ -179,3 +182,19 @@ def test_voxel_grid_stable_oracle_matches_python():
             out.append((s_ / np.float32(len(idx))).astype(np.float32))
         ref = np.array(out, np.float32)
         assert st == 0 and np.array_equal(got.view(np.int32), ref.view(np.int32)), leaf
+
+
+def test_associate_to_map_matches_oracle():
+    """transformAssociateToMap: the product's host function (lego_map_associate, used by the mapping
+    loop) bit-exact to the oracle's restatement (float, the float libm) on random poses."""
+    from lego_amd import mapping as M
+    rng = np.random.default_rng(21)
+    for _ in range(300):
+        t = rng.uniform(-1, 1, (3, 6)).astype(np.float32)
+        t[:, 3:] *= 50
+        got = M.transform_associate_to_map(t[0], t[1], t[2])
+        ref = O.associate_to_map(t[0], t[1], t[2])
+        assert np.array_equal(got.view(np.int32), ref.view(np.int32)), (t, got, ref)
+    z = np.zeros(6, np.float32)
+    assert np.array_equal(M.transform_associate_to_map(z, z, z), z)
+
