@@ -2,7 +2,9 @@
 // without ROS: ImageProjection on the caller thread, FeatureAssociation on its own thread, joined by
 // a blocking Channel<ProjectionOut>; AssociationOut goes to a non-blocking channel (live mode).
 //
-//   replay_pipeline <scans.bin | file.bag> [device] [topic]
+//   replay_pipeline <scans.bin | file.bag> [device] [topic] [--mapping]
+// --mapping: MapOptimization on its own thread behind a blocking Channel<AssociationOut> (main.cpp's
+// rosbag mode, use_rosbag = true) and a second line "mapping cycles <n> keys <k> aft x y z qx qy qz qw".
 // scans.bin: int32 nscans, then per scan: int32 n, n x (float x, y, z, intensity).
 // file.bag: a ROS bag v2.0; every sensor_msgs/PointCloud2 on `topic` (default /velodyne_points,
 // the reference's pointCloudTopic, utility.h:28) is decoded zero-copy (lego_rosbag.hpp) and replayed
@@ -10,6 +12,7 @@
 // Prints one line per run: "cycles <n> status <bits> position x y z orientation x y z w".
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -17,6 +20,14 @@
 #include "lego_rosbag.hpp"
 
 int main(int argc, char** argv) {
+  bool mapping = false;
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--mapping") {
+      mapping = true;
+      for (int j = i; j + 1 < argc; ++j) argv[j] = argv[j + 1];
+      --argc;
+      break;
+    }
   if (argc < 2) {
     std::fprintf(stderr, "usage: %s scans.bin|file.bag [device] [topic]\n", argv[0]);
     return 2;
@@ -43,11 +54,14 @@ int main(int argc, char** argv) {
   using namespace lego_amd;
   lego_params params = vlp16_params();
   Channel<ProjectionOut> projection_out_channel(true);
-  Channel<AssociationOut> association_out_channel(false);
+  Channel<AssociationOut> association_out_channel(mapping);  // main.cpp:38: blocking in rosbag mode
   Odometry odom;
-  int status = 0, cycles = 0;
+  int status = 0, cycles = 0, map_cycles = 0, keys = 0;
+  Odometry aft;
   try {
     ImageProjection IP(params, projection_out_channel, device);
+    std::unique_ptr<MapOptimization> MO;
+    if (mapping) MO.reset(new MapOptimization(association_out_channel, device, 200000, 20000000));
     FeatureAssociation FA(params, projection_out_channel, association_out_channel, device);
     int nscans = 0;
     if (is_bag) {  // rosbag replay loop (main.cpp:62-76)
@@ -76,6 +90,16 @@ int main(int argc, char** argv) {
     odom = FA.last_odometry();
     status = FA.last_status();
     cycles = FA.cycles();
+    if (MO) {
+      MO->finish();  // every AssociationOut FA sent has been through the mapping loop
+      if (!MO->error().empty()) {
+        std::fprintf(stderr, "%s\n", MO->error().c_str());
+        return 1;
+      }
+      map_cycles = MO->cycles();
+      keys = (int)MO->keyPoses().size();
+      aft = MO->aft_mapped();
+    }
   } catch (const Error& e) {
     std::fprintf(stderr, "error: %s\n", e.what());
     return 1;
@@ -86,5 +110,9 @@ int main(int argc, char** argv) {
   std::printf("cycles %d status %d position %.9g %.9g %.9g orientation %.9g %.9g %.9g %.9g\n", cycles, status,
               odom.position[0], odom.position[1], odom.position[2], odom.orientation[0], odom.orientation[1],
               odom.orientation[2], odom.orientation[3]);
+  if (mapping)
+    std::printf("mapping cycles %d keys %d aft %.9g %.9g %.9g %.9g %.9g %.9g %.9g\n", map_cycles, keys, aft.position[0],
+                aft.position[1], aft.position[2], aft.orientation[0], aft.orientation[1], aft.orientation[2],
+                aft.orientation[3]);
   return 0;
 }

@@ -22,6 +22,7 @@
 
 #include <array>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstdint>
 #include <mutex>
@@ -298,22 +299,26 @@ class ScanToMapOptimization {
   lego_s2m* _m = nullptr;
 };
 
-// MapOptimization's mapping thread, loop closure off (mapOptmization.cpp:1521-1570): run() is one
-// pass of its loop on one AssociationOut (laserCloudCornerLast / SurfLast / OutlierLast, transformSum),
-// the key frames' clouds kept on the GPU.  transformAftMapped is the reference's member after the pass.
-class MapOptimization {
+// One pass of MapOptimization's mapping loop, loop closure off (mapOptmization.cpp:1521-1570), per call:
+// OdometryToTransform, transformAssociateToMap, extractSurroundingKeyFrames, downsampleCurrentScan,
+// scan2MapOptimization, saveKeyFramesAndFactor, with the key frames' clouds kept on the GPU.
+// transformAftMapped is the reference's member after the pass.
+class Mapper {
  public:
-  explicit MapOptimization(int device = 0, int max_map_points = 200000, int64_t max_key_points = 50000000) {
+  explicit Mapper(int device = 0, int max_map_points = 200000, int64_t max_key_points = 50000000) {
     check(lego_mapper_create(device, max_map_points, max_key_points, &_m), "lego_mapper_create");
   }
-  ~MapOptimization() { lego_mapper_destroy(_m); }
-  MapOptimization(const MapOptimization&) = delete;
-  MapOptimization& operator=(const MapOptimization&) = delete;
+  ~Mapper() { lego_mapper_destroy(_m); }
+  Mapper(const Mapper&) = delete;
+  Mapper& operator=(const Mapper&) = delete;
 
   float transformAftMapped[6] = {0, 0, 0, 0, 0, 0};
 
-  ScanToMapOptimization::Info run(const std::vector<lego_point>& cornerLast, const std::vector<lego_point>& surfLast,
-                                  const std::vector<lego_point>& outlierLast, const float transformSum[6]) {
+  ScanToMapOptimization::Info run(const Cloud& cornerLast, const Cloud& surfLast, const Cloud& outlierLast,
+                                  const Odometry& laserOdometry) {
+    float transformSum[6];
+    check(lego_map_odometry_to_transform(laserOdometry.orientation, laserOdometry.position, transformSum),
+          "lego_map_odometry_to_transform");  // OdometryToTransform (:1540)
     int32_t info[4];
     check(lego_mapper_step(_m, cornerLast.data(), (int32_t)cornerLast.size(), surfLast.data(), (int32_t)surfLast.size(),
                            outlierLast.data(), (int32_t)outlierLast.size(), transformSum, transformAftMapped, info),
@@ -331,6 +336,89 @@ class MapOptimization {
 
  private:
   lego_mapper* _m = nullptr;
+};
+
+// publishTF's /aft_mapped_to_init pose (mapOptmization.cpp:510-522): tf::createQuaternionMsgFromRollPitchYaw
+// in double, as FeatureAssociation::publishOdometry
+inline Odometry aft_mapped_odometry(const float t[6], double stamp) {
+  const double roll = t[2], pitch = -(double)t[0], yaw = -(double)t[1];
+  const double hy = yaw * 0.5, hp = pitch * 0.5, hr = roll * 0.5;
+  const double cy = std::cos(hy), sy = std::sin(hy), cp = std::cos(hp), sp = std::sin(hp), cr = std::cos(hr),
+               sr = std::sin(hr);
+  const double qx = sr * cp * cy - cr * sp * sy, qy = cr * sp * cy + sr * cp * sy;
+  const double qz = cr * cp * sy - sr * sp * cy, qw = cr * cp * cy + sr * sp * sy;
+  Odometry o;
+  o.stamp = stamp;
+  o.orientation[0] = -qy;
+  o.orientation[1] = -qz;
+  o.orientation[2] = qx;
+  o.orientation[3] = qw;
+  for (int k = 0; k < 3; ++k) o.position[k] = t[3 + k];
+  return o;
+}
+
+// mapOptimization.h's surface: the constructor starts the mapping thread on input_channel (the
+// AssociationOut channel FeatureAssociation feeds, main.cpp:38-45); the destructor sends the empty item
+// and joins (:126-129).  Loop closure and the global-map publisher are not built (loop closure off).
+class MapOptimization {
+ public:
+  MapOptimization(Channel<AssociationOut>& input_channel, int device = 0, int max_map_points = 200000,
+                  int64_t max_key_points = 50000000)
+      : _mapper(device, max_map_points, max_key_points), _input_channel(input_channel) {
+    _run_thread = std::thread(&MapOptimization::run, this);
+  }
+  ~MapOptimization() { finish(); }
+  // the destructor's hand-off: the empty item after everything already sent, then join (idempotent)
+  void finish() {
+    if (!_run_thread.joinable()) return;
+    _input_channel.send(AssociationOut());
+    _run_thread.join();
+  }
+  MapOptimization(const MapOptimization&) = delete;
+  MapOptimization& operator=(const MapOptimization&) = delete;
+
+  Odometry aft_mapped() {  // the last /aft_mapped_to_init
+    std::lock_guard<std::mutex> g(_mtx);
+    return _aft;
+  }
+  int cycles() {
+    std::lock_guard<std::mutex> g(_mtx);
+    return _n;
+  }
+  std::string error() {
+    std::lock_guard<std::mutex> g(_mtx);
+    return _error;
+  }
+  std::vector<std::array<float, 6>> keyPoses() {
+    std::lock_guard<std::mutex> g(_mtx);
+    return _mapper.keyPoses();
+  }
+
+ private:
+  void run() {  // :1521-1570
+    while (true) {
+      AssociationOut association;
+      _input_channel.receive(association);
+      if (!association.valid) break;
+      std::lock_guard<std::mutex> g(_mtx);
+      try {
+        _mapper.run(association.cloud_corner_last, association.cloud_surf_last, association.cloud_outlier_last,
+                    association.laser_odometry);
+        _aft = aft_mapped_odometry(_mapper.transformAftMapped, association.laser_odometry.stamp);  // publishTF
+      } catch (const Error& e) {
+        _error = e.what();
+      }
+      ++_n;
+    }
+  }
+
+  Mapper _mapper;
+  Channel<AssociationOut>& _input_channel;
+  std::thread _run_thread;
+  std::mutex _mtx;
+  Odometry _aft;
+  int _n = 0;
+  std::string _error;
 };
 
 }  // namespace lego_amd

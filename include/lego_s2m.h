@@ -128,6 +128,10 @@ int  lego_mapper_key_poses(const lego_mapper* m, float* out, int32_t cap, int32_
  * restored by passing 10) and copy problem p's LM rows of its last iteration, 8 floats a query (arx, ary,
  * arz, coeff x, y, z, -coeff intensity, 1 if selected else 0), into out[8 * nq] */
 int  lego_test_s2m_debug(lego_s2m* m, int32_t max_iters, int32_t p, int32_t nq, float* out);
+/* OdometryToTransform (utility.h:96-110) on the host: the mapping thread's transformSum from the
+ * /laser_odom_to_init message (orientation x, y, z, w; position x, y, z), through tf's getRPY in double
+ * (lego_association_out.odom_orientation / odom_position are that message). */
+int  lego_map_odometry_to_transform(const double* orientation, const double* position, float* transform);
 /* transformAssociateToMap (mapOptmization.cpp:264-387) on the host, float with the float libm (no device
  * needed): transformTobeMapped from transformSum / transformBefMapped / transformAftMapped. */
 int  lego_map_associate(const float* transform_sum, const float* transform_bef_mapped, const float* transform_aft_mapped,

@@ -204,6 +204,43 @@ extern "C" int lego_mapper_create(int32_t device, int32_t max_map_points, int64_
   return LEGO_OK;
 }
 
+// OdometryToTransform (utility.h:96-110): the mapping thread's transformSum from the odometry message,
+// through tf::Matrix3x3(tf::Quaternion(q.z, -q.x, -q.y, q.w)).getRPY (tf/LinearMath/Matrix3x3.h:
+// setRotation, getEulerYPR with solution 1) in double, then transform = (-pitch, -yaw, roll, position).
+extern "C" int lego_map_odometry_to_transform(const double* orientation, const double* position, float* transform) {
+  if (!orientation || !position || !transform) return LEGO_EINVAL;
+  const double qx = orientation[2], qy = -orientation[0], qz = -orientation[1], qw = orientation[3];
+  const double d = qx * qx + qy * qy + qz * qz + qw * qw;  // Quaternion::length2
+  const double s = 2.0 / d;
+  const double xs = qx * s, ys = qy * s, zs = qz * s;
+  const double wx = qw * xs, wy = qw * ys, wz = qw * zs;
+  const double xx = qx * xs, xy = qx * ys, xz = qx * zs;
+  const double yy = qy * ys, yz = qy * zs, zz = qz * zs;
+  const double m00 = 1.0 - (yy + zz), m10 = xy + wz;
+  const double m20 = xz - wy, m21 = yz + wx, m22 = 1.0 - (xx + yy);
+  double roll, pitch, yaw;
+  if (fabs(m20) >= 1) {  // gimbal lock
+    yaw = 0;
+    const double delta = atan2(m21, m22);
+    pitch = m20 < 0 ? 3.1415926535897932384626433832795029 / 2.0 : -3.1415926535897932384626433832795029 / 2.0;
+    roll = delta;
+  } else {
+    double a = m20;  // tfAsin clamps to [-1, 1]
+    if (a < -1) a = -1;
+    if (a > 1) a = 1;
+    pitch = -asin(a);
+    roll = atan2(m21 / cos(pitch), m22 / cos(pitch));
+    yaw = atan2(m10 / cos(pitch), m00 / cos(pitch));
+  }
+  transform[0] = (float)-pitch;
+  transform[1] = (float)-yaw;
+  transform[2] = (float)roll;
+  transform[3] = (float)position[0];
+  transform[4] = (float)position[1];
+  transform[5] = (float)position[2];
+  return LEGO_OK;
+}
+
 extern "C" int lego_map_associate(const float* transform_sum, const float* transform_bef_mapped,
                                   const float* transform_aft_mapped, float* transform_tobe_mapped) {
   if (!transform_sum || !transform_bef_mapped || !transform_aft_mapped || !transform_tobe_mapped) return LEGO_EINVAL;

@@ -96,6 +96,7 @@ def lib():
                                                                                     P(C.c_int32)]
         L.lego_mapper_key_poses.argtypes = [C.c_void_p, P(C.c_float), C.c_int32, P(C.c_int32)]
         L.lego_map_associate.argtypes = [P(C.c_float)] * 4
+        L.lego_map_odometry_to_transform.argtypes = [P(C.c_double), P(C.c_double), P(C.c_float)]
         _lib = L
     return _lib
 
@@ -312,7 +313,9 @@ class Mapper:
     __del__ = close
 
     def step(self, corner_last, surf_last, outlier_last, transform_sum):
-        """Returns (transformAftMapped[6] float32, info[4] int32: iterations-gate / LM status as lego_s2m)."""
+        """transform_sum: the mapping thread's transformSum (OdometryToTransform of the odometry message,
+        lego_amd.mapping.odometry_to_transform).  Returns (transformAftMapped[6] float32, info[4] int32 as
+        lego_s2m_run's)."""
         arrs = [np.ascontiguousarray(np.asarray(a, np.float32).reshape(-1, 4)) for a in (corner_last, surf_last,
                                                                                           outlier_last)]
         ts = np.ascontiguousarray(np.asarray(transform_sum, np.float32).reshape(6))

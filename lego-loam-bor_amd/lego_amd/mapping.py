@@ -238,6 +238,22 @@ def prepare_parts_gpu(s2m, cparts, sparts, scans, t0, degenerate=None, stream=0,
 
 
 # ---- MapOptimization's mapping loop around the GPU operations ---------------------------------------
+def odometry_to_transform(orientation, position):
+    """OdometryToTransform (utility.h:96-110): the mapping thread's transformSum from the odometry
+    message (AssociationOut.laser_odometry: orientation x, y, z, w and position; the assoc dicts'
+    odom_orientation / odom_position), through tf's getRPY in double.  Product library
+    (lego_map_odometry_to_transform)."""
+    import ctypes as C
+    import lego_amd as LA
+    q = np.ascontiguousarray(np.asarray(orientation, np.float64).reshape(4))
+    p = np.ascontiguousarray(np.asarray(position, np.float64).reshape(3))
+    t = np.zeros(6, np.float32)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    LA._check(LA.lib().lego_map_odometry_to_transform(dp(q), dp(p), t.ctypes.data_as(C.POINTER(C.c_float))),
+              "lego_map_odometry_to_transform")
+    return t
+
+
 def transform_associate_to_map(tSum, tBef, tAft):
     """transformAssociateToMap (mapOptmization.cpp:264-387): the odometry increment since the last mapping
     step applied to the last mapped pose; returns transformTobeMapped.  Runs in the product library
@@ -285,8 +301,9 @@ class MapSequence:
 
     RADIUS = 50.0  # surrounding_keyframe_search_radius (loam_config.yaml:27)
 
-    def __init__(self, associate=None):
+    def __init__(self, associate=None, odometry=None):
         self._associate = associate or transform_associate_to_map  # tests pass the oracle's
+        self._odometry = odometry or odometry_to_transform
         z = lambda: np.zeros(6, np.float32)  # noqa: E731
         self.t_sum, self.t_tobe, self.t_bef, self.t_aft = z(), z(), z(), z()
         self.key_pos = []       # cloudKeyPoses3D: (x, y, z, index)
@@ -300,7 +317,7 @@ class MapSequence:
 
     def begin(self, assoc):
         """One AssociationOut: returns (corner parts, surf parts, scan clouds, transformTobeMapped)."""
-        self.t_sum = np.asarray(assoc["transform_sum"], np.float32).copy()  # OdometryToTransform (:1540)
+        self.t_sum = self._odometry(assoc["odom_orientation"], assoc["odom_position"])  # OdometryToTransform (:1540)
         self.t_tobe = self._associate(self.t_sum, self.t_bef, self.t_aft)
         if self.key_pos:  # extractSurroundingKeyFrames, loop closure off (:915-995)
             kp = np.array(self.key_pos, np.float32)

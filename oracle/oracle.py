@@ -181,6 +181,17 @@ def scan2map_debug(corner, surf, corner_map, surf_map, transform, degenerate=0, 
     return t, dg.value, info, rows
 
 
+def odometry_to_transform(orientation, position):
+    """OdometryToTransform restated (utility.h:96-110): transformSum from the odometry message."""
+    import numpy as np
+    q = np.ascontiguousarray(np.asarray(orientation, np.float64).reshape(4))
+    p = np.ascontiguousarray(np.asarray(position, np.float64).reshape(3))
+    t = np.zeros(6, np.float32)
+    lib().oracle_odometry_to_transform(q.ctypes.data_as(P(C.c_double)), p.ctypes.data_as(P(C.c_double)),
+                                       t.ctypes.data_as(P(C.c_float)))
+    return t
+
+
 def associate_to_map(t_sum, t_bef, t_aft):
     """MapOptimization::transformAssociateToMap restated (mapOptmization.cpp:264-387): transformTobeMapped."""
     import numpy as np

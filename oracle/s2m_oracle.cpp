@@ -677,3 +677,42 @@ extern "C" void oracle_associate_to_map(const float* S, const float* B, const fl
   T[4] = A[4] - y2;
   T[5] = A[5] - (-sin(T[1]) * x1 + cos(T[1]) * z2);
 }
+
+// OdometryToTransform (utility.h:96-110): the mapping thread's transformSum from the odometry message,
+// through tf::Matrix3x3(tf::Quaternion(q.z, -q.x, -q.y, q.w)).getRPY (tf/LinearMath/Matrix3x3.h:
+// setRotation, getEulerYPR with solution 1) in double, then transform = (-pitch, -yaw, roll, position).
+extern "C" void oracle_odometry_to_transform(const double* orientation, const double* position, float* transform) {
+  using std::asin;
+  using std::atan2;
+  using std::cos;
+  using std::fabs;
+  const double qx = orientation[2], qy = -orientation[0], qz = -orientation[1], qw = orientation[3];
+  const double d = qx * qx + qy * qy + qz * qz + qw * qw;  // Quaternion::length2
+  const double s = 2.0 / d;
+  const double xs = qx * s, ys = qy * s, zs = qz * s;
+  const double wx = qw * xs, wy = qw * ys, wz = qw * zs;
+  const double xx = qx * xs, xy = qx * ys, xz = qx * zs;
+  const double yy = qy * ys, yz = qy * zs, zz = qz * zs;
+  const double m00 = 1.0 - (yy + zz), m10 = xy + wz;
+  const double m20 = xz - wy, m21 = yz + wx, m22 = 1.0 - (xx + yy);
+  double roll, pitch, yaw;
+  if (fabs(m20) >= 1) {  // gimbal lock
+    yaw = 0;
+    const double delta = atan2(m21, m22);
+    pitch = m20 < 0 ? 3.1415926535897932384626433832795029 / 2.0 : -3.1415926535897932384626433832795029 / 2.0;
+    roll = delta;
+  } else {
+    double a = m20;  // tfAsin clamps to [-1, 1]
+    if (a < -1) a = -1;
+    if (a > 1) a = 1;
+    pitch = -asin(a);
+    roll = atan2(m21 / cos(pitch), m22 / cos(pitch));
+    yaw = atan2(m10 / cos(pitch), m00 / cos(pitch));
+  }
+  transform[0] = (float)-pitch;
+  transform[1] = (float)-yaw;
+  transform[2] = (float)roll;
+  transform[3] = (float)position[0];
+  transform[4] = (float)position[1];
+  transform[5] = (float)position[2];
+}

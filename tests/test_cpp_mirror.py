@@ -153,7 +153,8 @@ def _write_cycles(path, assocs):
                 x = np.ascontiguousarray(a[name], dtype=np.float32).reshape(-1, 4)
                 f.write(struct.pack("<i", x.shape[0]))
                 f.write(x.tobytes())
-            f.write(np.asarray(a["transform_sum"], np.float32).tobytes())
+            f.write(np.asarray(a["odom_orientation"], np.float64).tobytes())
+            f.write(np.asarray(a["odom_position"], np.float64).tobytes())
 
 
 def test_mapping_mirror_fails_loudly_without_device(tmp_path):
@@ -183,10 +184,42 @@ def test_mapping_mirror_matches_oracle_loop(gpu, tmp_path):
     lines = r.stdout.strip().splitlines()
     assert len(lines) == len(assocs) + 1
     import oracle as O
-    sq = M.MapSequence(associate=O.associate_to_map)
+    sq = M.MapSequence(associate=O.associate_to_map, odometry=O.odometry_to_transform)
     for a, line in zip(assocs, lines):
         (_, _, info), = mapping_step_oracle([sq], [a])
         tok = line.split()
         np.testing.assert_allclose(np.array([float(x) for x in tok[1:7]], np.float32), sq.t_aft, atol=1e-4, rtol=0)
         assert int(tok[8]) == int(info[0] == 1) and int(tok[10]) == info[1]
     assert lines[-1] == "keys %d" % len(sq.key_pose6)
+
+
+@pytest.mark.gpu
+def test_pipeline_with_mapping_thread_matches_oracle(gpu, tmp_path):
+    """main.cpp's topology with the mapping thread (replay_pipeline --mapping: ImageProjection ->
+    FeatureAssociation thread -> blocking Channel<AssociationOut> -> MapOptimization thread) against the
+    oracle front end and the oracle mapping loop on the same sweeps: every emitted AssociationOut is
+    mapped, the same key frames, and the last /aft_mapped_to_init within 1e-4."""
+    import oracle as O
+    import make_golden as MG
+    from lego_amd import mapping as M
+    from test_gpu_mapping_loop import mapping_step_oracle
+    build()
+    cfg = A.synth_cfg("vlp16")
+    scans = [A.synth_scan(cfg, 6, k) for k in range(26)]
+    f = tmp_path / "s.bin"
+    write_scans(str(f), scans)
+    r = subprocess.run([EXE, str(f), "0", "--mapping"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       universal_newlines=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    line = [x for x in r.stdout.splitlines() if x.startswith("mapping ")][0].split()
+    orc = O.Oracle(MG.params_for("vlp16"))
+    sq = M.MapSequence(associate=O.associate_to_map, odometry=O.odometry_to_transform)
+    emitted = 0
+    for p in scans:
+        orc.cloud_handler(p)
+        a = orc.feature_association()
+        if a["status"] & 0x080:
+            mapping_step_oracle([sq], [a])
+            emitted += 1
+    assert emitted >= 4 and int(line[2]) == emitted and int(line[4]) == len(sq.key_pose6)
+    np.testing.assert_allclose(np.array([float(x) for x in line[6:9]]), sq.t_aft[3:6], atol=1e-4, rtol=0)

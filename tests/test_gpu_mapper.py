@@ -23,10 +23,11 @@ def test_mapper_matches_oracle_loop(gpu, seq):
     stream = _emitted(seq, 61)
     assert len(stream) >= 5
     mp = LA.Mapper(max_map_points=150000, max_key_points=4_000_000, device=gpu)
-    r = M.MapSequence(associate=O.associate_to_map)
+    r = M.MapSequence(associate=O.associate_to_map, odometry=O.odometry_to_transform)
     ran = 0
     for k, a in enumerate(stream):
-        tg, ig = mp.step(a["corner_last"], a["surf_last"], a["outlier_last"], a["transform_sum"])
+        tg, ig = mp.step(a["corner_last"], a["surf_last"], a["outlier_last"],
+                             M.odometry_to_transform(a["odom_orientation"], a["odom_position"]))
         (_, _, ir), = mapping_step_oracle([r], [a])
         assert np.array_equal(tg.view(np.int32), r.t_aft.view(np.int32)), (k, tg, r.t_aft)
         assert np.array_equal(ig, ir), (k, ig, ir)

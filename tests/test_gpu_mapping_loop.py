@@ -56,7 +56,7 @@ def test_mapping_loop_matches_oracle(gpu):
     assert n >= 5
     s2m = LA.ScanToMap(max_problems=len(streams), max_map_points=150000, device=gpu)
     g = [M.MapSequence() for _ in streams]
-    r = [M.MapSequence(associate=O.associate_to_map) for _ in streams]
+    r = [M.MapSequence(associate=O.associate_to_map, odometry=O.odometry_to_transform) for _ in streams]
     ran = 0
     for k in range(n):
         out_g = M.mapping_step_gpu(s2m, g, [s[k] for s in streams])

@@ -150,7 +150,8 @@ def test_s2m_abi_exports():
     hdr = open(os.path.join(REPO, "include", "lego_s2m.h")).read()
     names = set(re.findall(r"\b(lego_(?:s2m|map|mapper)_\w+)\s*\(", hdr))
     assert names == {"lego_s2m_create", "lego_s2m_destroy", "lego_s2m_run", "lego_s2m_run_host", "lego_map_transform",
-                     "lego_map_voxel", "lego_map_associate", "lego_mapper_create", "lego_mapper_destroy",
+                     "lego_map_voxel", "lego_map_associate", "lego_map_odometry_to_transform", "lego_mapper_create",
+                     "lego_mapper_destroy",
                      "lego_mapper_step", "lego_mapper_key_poses"}
     assert "lego_test_s2m_debug" in hdr
     names.add("lego_test_s2m_debug")
@@ -198,3 +199,28 @@ def test_associate_to_map_matches_oracle():
     z = np.zeros(6, np.float32)
     assert np.array_equal(M.transform_associate_to_map(z, z, z), z)
 
+
+
+def test_odometry_to_transform_matches_oracle():
+    """OdometryToTransform (utility.h:96-110): the product's host function (lego_map_odometry_to_transform,
+    the mapping thread's transformSum) bit-exact to the oracle's restatement of tf's getRPY, including
+    gimbal-locked and non-unit quaternions; and it inverts publishOdometry's quaternion to within float
+    rounding."""
+    from lego_amd import mapping as M
+    rng = np.random.default_rng(23)
+    qs = list(rng.normal(size=(400, 4)))
+    for r, p, y in rng.uniform(-1.5, 1.5, (200, 3)):  # publishOdometry's quaternion of transformSum
+        hy, hp, hr = -y * 0.5, -r * 0.5, p * 0.5  # roll = t[2], pitch = -t[0], yaw = -t[1]
+        cy, sy, cp, sp, cr, sr = np.cos(hy), np.sin(hy), np.cos(hp), np.sin(hp), np.cos(hr), np.sin(hr)
+        qx, qy = sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy
+        qz, qw = cr * cp * sy - sr * sp * cy, cr * cp * cy + sr * sp * sy
+        q = np.array([-qy, -qz, qx, qw])
+        qs.append(q)
+        t = M.odometry_to_transform(q, [1.0, 2.0, 3.0])
+        assert np.allclose(t, [r, y, p, 1, 2, 3], atol=2e-6), (r, p, y, t)
+    qs += [np.array([0.0, 0.0, np.sqrt(0.5), np.sqrt(0.5)]), np.array([0.5, 0.5, 0.5, 0.5]),
+           np.array([0.0, 0.0, 0.0, 1.0])]
+    for q in qs:
+        pos = rng.normal(size=3) * 100
+        got, ref = M.odometry_to_transform(q, pos), O.odometry_to_transform(q, pos)
+        assert np.array_equal(got.view(np.int32), ref.view(np.int32)), (q, got, ref)

@@ -54,7 +54,8 @@ def main():
         ms, poses, ran, infos = [], [], 0, []
         for a in assocs:
             t0 = time.perf_counter()
-            t, info = mp.step(a["corner_last"], a["surf_last"], a["outlier_last"], a["transform_sum"])
+            t, info = mp.step(a["corner_last"], a["surf_last"], a["outlier_last"],
+                             M.odometry_to_transform(a["odom_orientation"], a["odom_position"]))
             ms.append((time.perf_counter() - t0) * 1e3)
             poses.append(t)
             infos.append(info.copy())
@@ -66,7 +67,7 @@ def main():
     ms, poses, ran, keys, infos = best
 
     import oracle as O
-    sq = M.MapSequence(associate=O.associate_to_map)
+    sq = M.MapSequence(associate=O.associate_to_map, odometry=O.odometry_to_transform)
     from test_gpu_mapping_loop import mapping_step_oracle
     cpu_ms, dmax, per_cycle = [], 0.0, []
     for a, t, ig in zip(assocs, poses, infos):
