@@ -124,6 +124,11 @@ int  lego_mapper_step(lego_mapper* m, const lego_point* corner_last, int32_t n_c
                       float* transform_aft_mapped, int32_t* info);
 /* key poses so far, (roll, pitch, yaw, x, y, z) each (cloudKeyPoses6D); *n = their count */
 int  lego_mapper_key_poses(const lego_mapper* m, float* out, int32_t cap, int32_t* n);
+/* Launch layout of lego_s2m_run: 0 = one 1024-thread workgroup a problem (throughput: hundreds of
+ * problems), 1 = latency (a problem's grids built by two workgroups, each LM iteration's queries spread
+ * over up to 256 / n workgroups, normal equations and solve in one; 21 launches), -1 (default) = latency
+ * for n <= 16.  Results are identical. */
+int  lego_s2m_set_layout(lego_s2m* m, int32_t layout);
 /* test hook (not for the mapping path): cap the LM iterations of later runs at max_iters (the product's 10
  * restored by passing 10) and copy problem p's LM rows of its last iteration, 8 floats a query (arx, ary,
  * arz, coeff x, y, z, -coeff intensity, 1 if selected else 0), into out[8 * nq] */

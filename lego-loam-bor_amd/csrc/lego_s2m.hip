@@ -23,6 +23,8 @@
 
 #include <new>
 
+#include <algorithm>
+
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
@@ -37,6 +39,7 @@ constexpr int S2M_THREADS = 1024;
 constexpr int S2M_NB_MAX = 65536;  // hash buckets per map cloud (power of two)
 constexpr float S2M_CELL = 1.01f;  // cell edge: >= the 1 m kNN gate plus rounding
 constexpr int S2M_DIM = 1024;
+constexpr int S2M_LATENCY_MAX = 16;  // lego_s2m_run: up to this many problems take the latency layout
 constexpr size_t S2M_WIDE_MAX = (size_t)8 << 20;  // few-clouds VoxelGrid layout: n * max_map_points <= this      // cells per axis a packed cell can hold (10 bits)
 
 LG_DEVICE int lane_id() { return threadIdx.x & 63; }
@@ -635,6 +638,56 @@ struct S2mLds {
   int flag, status, iters, nsel, degenerate;
 };
 
+// The normal equations (AtA upper triangle, AtB, count) over the rows of nq queries in two passes of 14
+// double sums (register budget): lane tid sums rows q = tid, tid + 1024, ... in increasing q, loading R
+// rows at a time (all in flight together; the second pass finds them in cache); each pass is reduced over
+// the wave by xor butterflies and then per wave into L.acc (lm_solve adds the 16 wave sums in order).
+// The oracle's normal_equations restates this order.
+__device__ __attribute__((noinline)) void normal_equations(S2mLds& L, const float4* rows, int nq) {
+  const int tid = threadIdx.x;
+  constexpr int R = 4;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    double acc[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) acc[k] = 0.0;
+    for (int base = 0; base < nq; base += R * S2M_THREADS) {
+      float4 r0[R], r1[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int q = base + u * S2M_THREADS + tid;
+        const int qq = q < nq ? q : 0;
+        r0[u] = rows[2 * qq];
+        r1[u] = rows[2 * qq + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        if (base + u * S2M_THREADS + tid >= nq || r1[u].w == 0.f) continue;
+        const float a[6] = {r0[u].x, r0[u].y, r0[u].z, r0[u].w, r1[u].x, r1[u].y};
+        const float b = r1[u].z;
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+#pragma unroll
+          for (int j = r; j < 6; ++j) {
+            if (k >= 14 * half && k < 14 * half + 14) acc[k - 14 * half] += (double)(a[r] * a[j]);
+            ++k;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+          if (21 + r >= 14 * half && 21 + r < 14 * half + 14) acc[21 + r - 14 * half] += (double)(a[r] * b);
+        if (half == 1) acc[13] += 1.0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 14; ++k)
+      for (int o = 32; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o);
+    if (lane_id() == 0)
+      for (int k = 0; k < 14; ++k) L.acc[wave_id()][14 * half + k] = acc[k];
+  }
+}
+
 // LMOptimization's solve (:1257-1311) on the reduced normal equations (thread 0)
 __device__ __attribute__((noinline)) void lm_solve(S2mLds& L, int iterCount) {
   double s[28];
@@ -726,39 +779,7 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch*
       if (r.st) atomicOr(&L.status, r.st);
     }
     __syncthreads();
-    // the normal equations (AtA upper triangle, AtB, count) in two passes of 14 double sums over the
-    // rows (register budget), each reduced over the wave and then per wave into LDS
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      double acc[14];
-#pragma unroll
-      for (int k = 0; k < 14; ++k) acc[k] = 0.0;
-      for (int q = tid; q < nc + ns; q += S2M_THREADS) {
-        const float4 r1 = Gc.rows[2 * q + 1];
-        if (r1.w == 0.f) continue;
-        const float4 r0 = Gc.rows[2 * q];
-        const float a[6] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y};
-        const float b = r1.z;
-        int k = 0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-#pragma unroll
-          for (int j = r; j < 6; ++j) {
-            if (k >= 14 * half && k < 14 * half + 14) acc[k - 14 * half] += (double)(a[r] * a[j]);
-            ++k;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-          if (21 + r >= 14 * half && 21 + r < 14 * half + 14) acc[21 + r - 14 * half] += (double)(a[r] * b);
-        if (half == 1) acc[13] += 1.0;
-      }
-#pragma unroll
-      for (int k = 0; k < 14; ++k)
-        for (int o = 32; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o);
-      if (lane_id() == 0)
-        for (int k = 0; k < 14; ++k) L.acc[wave_id()][14 * half + k] = acc[k];
-    }
+    normal_equations(L, Gc.rows, nc + ns);
     __syncthreads();
     if (tid == 0) lm_solve(L, iterCount);
     __syncthreads();
@@ -774,6 +795,134 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch*
   }
 }
 
+
+// ---- latency layout (few problems): the same computation over many workgroups a problem -----------
+// k_s2m runs a problem in one workgroup, which suits hundreds of problems; a single mapping sequence
+// would leave all but one CU idle.  Here a problem's grids are built by two workgroups (k_s2m_grid), each
+// LM iteration's queries are spread over gridDim.x workgroups (k_s2m_rows) and one workgroup sums the
+// normal equations in k_s2m's order and solves (k_s2m_solve, the same lm_solve).  The LM state lives in
+// HBM between launches; a converged problem's later launches return at once.  Bit-identical to k_s2m.
+struct S2mState {
+  float t[6];
+  int degenerate, status, iters, nsel, done;
+  GridInfo gc, gs;
+};
+
+LG_DEVICE bool s2m_gates(const lego_s2m_io& io, int p, int max_map, int* info) {  // k_s2m's entry checks
+  const int nc = io.corner_n[p], ns = io.surf_n[p], ncm = io.corner_map_n[p], nsm = io.surf_map_n[p];
+  if (!(ncm > 10 && nsm > 100)) {  // :1316
+    if (info) { info[0] = 0; info[1] = 0; info[2] = 0; info[3] = LEGO_S2M_ST_SKIPPED; }
+    return false;
+  }
+  if (ncm > max_map || nsm > max_map || nc < 0 || ns < 0 || nc + ns > max_map) {
+    if (info) { info[0] = -1; info[1] = 0; info[2] = 0; info[3] = LEGO_S2M_ST_SKIPPED; }
+    return false;
+  }
+  return true;
+}
+
+// grid (2, n): x = 0 the corner map's grid, 1 the surf map's; bucket table copied to HBM
+__global__ __launch_bounds__(S2M_THREADS) void k_s2m_grid(lego_s2m_io io, S2mScratch* scratch, S2mState* st,
+                                                          int max_map) {
+  __shared__ S2mLds L;
+  const int which = blockIdx.x, p = blockIdx.y, tid = threadIdx.x;
+  if (!s2m_gates(io, p, max_map, (which == 0 && tid == 0) ? io.info + 4 * p : nullptr)) {
+    if (which == 0 && tid == 0) st[p].done = 1;
+    return;
+  }
+  S2mScratch G = scratch[2 * p + which];
+  int* tab = which == 0 ? L.tab_c : L.tab_s;
+  G.start = tab;
+  GridInfo& gi = which == 0 ? L.gc : L.gs;
+  if (which == 0)
+    build_grid((const float4*)io.corner_map + io.corner_map_off[p], io.corner_map_n[p], G, gi, L.red, L.scan,
+               S2M_LG_CORNER);
+  else
+    build_grid((const float4*)io.surf_map + io.surf_map_off[p], io.surf_map_n[p], G, gi, L.red, L.scan, S2M_LG_SURF);
+  const int nb = 1 << gi.lg_nb;
+  int* dst = scratch[2 * p + which].start;
+  for (int b = tid; b <= nb; b += S2M_THREADS) dst[b] = tab[b];
+  if (tid == 0) {
+    if (which == 0) {
+      st[p].gc = gi;
+      for (int k = 0; k < 6; ++k) st[p].t[k] = io.transform[6 * p + k];
+      st[p].degenerate = io.degenerate[p];
+      st[p].status = 0;
+      st[p].iters = 0;
+      st[p].nsel = 0;
+      st[p].done = 0;
+    } else {
+      st[p].gs = gi;
+    }
+  }
+}
+
+// grid (G, n): one iteration's LM rows, queries q = blockIdx.x * 1024 + tid, strided by G * 1024
+__global__ __launch_bounds__(S2M_THREADS) void k_s2m_rows(lego_s2m_io io, S2mScratch* scratch, S2mState* st) {
+  __shared__ S2mLds L;
+  const int p = blockIdx.y, tid = threadIdx.x;
+  const S2mState* S = st + p;
+  const int nc = io.corner_n[p], ns = io.surf_n[p];
+  if (S->done || !S->gc.ok || !S->gs.ok || (int)blockIdx.x * S2M_THREADS >= nc + ns) return;
+  const GridInfo gc = S->gc, gs = S->gs;
+  S2mScratch Gc = scratch[2 * p], Gs = scratch[2 * p + 1];
+  for (int b = tid; b <= (1 << gc.lg_nb); b += S2M_THREADS) L.tab_c[b] = Gc.start[b];
+  for (int b = tid; b <= (1 << gs.lg_nb); b += S2M_THREADS) L.tab_s[b] = Gs.start[b];
+  if (tid == 0) {
+    const float* t = S->t;
+    L.T = Trig{cosf_g(t[0]), sinf_g(t[0]), cosf_g(t[1]), sinf_g(t[1]), cosf_g(t[2]), sinf_g(t[2]), t[3], t[4], t[5]};
+    L.status = 0;
+  }
+  __syncthreads();
+  Gc.start = L.tab_c;
+  Gs.start = L.tab_s;
+  const Trig T = L.T;
+  const float4* corner = (const float4*)io.corner + io.corner_off[p];
+  const float4* surf = (const float4*)io.surf + io.surf_off[p];
+  for (int q = blockIdx.x * S2M_THREADS + tid; q < nc + ns; q += gridDim.x * S2M_THREADS) {
+    const bool is_corner = q < nc;
+    const float4 ori = is_corner ? corner[q] : surf[q - nc];
+    const QueryRow r = query_row(is_corner, ori, T, is_corner ? Gc : Gs, is_corner ? gc : gs);
+    Gc.rows[2 * q] = r.r0;
+    Gc.rows[2 * q + 1] = r.r1;
+    if (r.st) atomicOr(&L.status, r.st);
+  }
+  __syncthreads();
+  if (tid == 0 && L.status) atomicOr(&st[p].status, L.status);
+}
+
+// grid (n): one iteration's normal equations and solve; the outputs are written after every iteration
+__global__ __launch_bounds__(S2M_THREADS) void k_s2m_solve(lego_s2m_io io, S2mScratch* scratch, S2mState* st,
+                                                           int iterCount, int max_iters) {
+  __shared__ S2mLds L;
+  const int p = blockIdx.x, tid = threadIdx.x;
+  S2mState* S = st + p;
+  if (S->done) return;
+  int* info = io.info + 4 * p;
+  if (!S->gc.ok || !S->gs.ok) {  // a map wider than 1024 cells (1 km) on an axis
+    __syncthreads();
+    if (tid == 0) { info[0] = -1; info[1] = 0; info[2] = 0; info[3] = LEGO_S2M_ST_SKIPPED; S->done = 1; }
+    return;
+  }
+  normal_equations(L, scratch[2 * p].rows, io.corner_n[p] + io.surf_n[p]);
+  __syncthreads();
+  if (tid == 0) {
+    for (int k = 0; k < 6; ++k) L.t[k] = S->t[k];
+    L.degenerate = S->degenerate;
+    L.status = S->status;
+    lm_solve(L, iterCount);
+    for (int k = 0; k < 6; ++k) S->t[k] = L.t[k];
+    S->degenerate = L.degenerate;
+    S->status = L.status;
+    S->done = (L.flag || iterCount + 1 >= max_iters) ? 1 : 0;
+    for (int k = 0; k < 6; ++k) io.transform[6 * p + k] = L.t[k];
+    io.degenerate[p] = L.degenerate;
+    info[0] = 1;
+    info[1] = L.iters;
+    info[2] = L.nsel;
+    info[3] = L.status;
+  }
+}
 
 // ---- map-side cloud preparation -------------------------------------------------------------------
 // transformPointCloud (:443-473) of part p (blockIdx.y) by its key pose
@@ -972,6 +1121,8 @@ struct lego_s2m {
   int device = 0;
   int max_problems = 0, max_map = 0;
   int max_iters = 10;  // :1320; lego_test_s2m_debug lowers it
+  int layout = -1;     // lego_s2m_set_layout: -1 automatic, 0 a workgroup a problem, 1 latency
+  S2mState* d_state = nullptr;
   S2mScratch* d_scratch = nullptr;
   void* d_mem = nullptr;
   // host-call staging
@@ -1012,7 +1163,8 @@ extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max
   const size_t per = ((tab + 255) & ~(size_t)255) + pts + ((idx + 255) & ~(size_t)255) + rows;
   if (hipMalloc(&m->d_mem, per * 2 * max_problems) != hipSuccess ||
       hipMalloc((void**)&m->d_scratch, sizeof(S2mScratch) * 2 * max_problems) != hipSuccess ||
-      hipMalloc((void**)&m->d_meta, 256) != hipSuccess) {
+      hipMalloc((void**)&m->d_meta, 256) != hipSuccess ||
+      hipMalloc((void**)&m->d_state, sizeof(S2mState) * max_problems) != hipSuccess) {
     lego_s2m_destroy(m);
     return LEGO_ENOMEM;
   }
@@ -1041,6 +1193,7 @@ extern "C" void lego_s2m_destroy(lego_s2m* m) {
   if (m->d_scratch) hipFree(m->d_scratch);
   if (m->d_clouds) hipFree(m->d_clouds);
   if (m->d_meta) hipFree(m->d_meta);
+  if (m->d_state) hipFree(m->d_state);
   for (void* p : {(void*)m->d_keys, (void*)m->d_vals, (void*)m->d_keys2, (void*)m->d_vals2, (void*)m->d_seg,
                   (void*)m->d_ovf, m->d_sort_tmp, (void*)m->d_k64, (void*)m->d_k64b, (void*)m->d_wv, (void*)m->d_wv2,
                   (void*)m->d_wseg, (void*)m->d_wovf, m->d_wide_tmp})
@@ -1055,8 +1208,19 @@ extern "C" int lego_s2m_run(lego_s2m* m, int32_t n, const lego_s2m_io* io, void*
       !io->surf_map_n || !io->transform || !io->degenerate || !io->info)
     return LEGO_EINVAL;
   if (hipSetDevice(m->device) != hipSuccess) return LEGO_EDEVICE;
-  hipLaunchKernelGGL(k_s2m, dim3(n), dim3(S2M_THREADS), 0, (hipStream_t)hip_stream, *io, m->d_scratch, m->max_map,
-                     m->max_iters);
+  hipStream_t st = (hipStream_t)hip_stream;
+  const bool lat = m->layout == 1 || (m->layout < 0 && n <= S2M_LATENCY_MAX);
+  if (!lat) {
+    hipLaunchKernelGGL(k_s2m, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_scratch, m->max_map, m->max_iters);
+    return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+  }
+  // latency layout: enough row workgroups for one query a lane at the largest query count allowed
+  const int g = std::max(1, std::min((m->max_map + S2M_THREADS - 1) / S2M_THREADS, std::max(1, 256 / n)));
+  hipLaunchKernelGGL(k_s2m_grid, dim3(2, n), dim3(S2M_THREADS), 0, st, *io, m->d_scratch, m->d_state, m->max_map);
+  for (int it = 0; it < m->max_iters; ++it) {
+    hipLaunchKernelGGL(k_s2m_rows, dim3(g, n), dim3(S2M_THREADS), 0, st, *io, m->d_scratch, m->d_state);
+    hipLaunchKernelGGL(k_s2m_solve, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_scratch, m->d_state, it, m->max_iters);
+  }
   return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }
 
@@ -1220,6 +1384,12 @@ extern "C" int lego_test_s2m_debug(lego_s2m* m, int32_t max_iters, int32_t p, in
   if (hipMemcpy(&g, m->d_scratch + 2 * p, sizeof(g), hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(out, g.rows, (size_t)nq * 32, hipMemcpyDeviceToHost) != hipSuccess)
     return LEGO_EDEVICE;
+  return LEGO_OK;
+}
+
+extern "C" int lego_s2m_set_layout(lego_s2m* m, int32_t layout) {
+  if (!m || layout < -1 || layout > 1) return LEGO_EINVAL;
+  m->layout = layout;
   return LEGO_OK;
 }
 

@@ -90,6 +90,7 @@ def lib():
                                                                                   P(C.c_int32)]
         L.lego_map_transform.argtypes = [C.c_void_p, C.c_int32, P(LegoMapTransformIo), C.c_void_p]
         L.lego_map_voxel.argtypes = [C.c_void_p, C.c_int32, P(LegoMapVoxelIo), C.c_void_p]
+        L.lego_s2m_set_layout.argtypes = [C.c_void_p, C.c_int32]
         L.lego_mapper_create.argtypes = [C.c_int32, C.c_int32, C.c_int64, P(C.c_void_p)]
         L.lego_mapper_destroy.argtypes = [C.c_void_p]
         L.lego_mapper_step.argtypes = [C.c_void_p] + [C.c_void_p, C.c_int32] * 3 + [P(C.c_float), P(C.c_float),
@@ -284,6 +285,10 @@ class ScanToMap:
     def run(self, n, io, stream=0):
         """n problems described by a LegoS2mIo of device pointers; asynchronous on `stream`."""
         _check(lib().lego_s2m_run(self.h, int(n), C.byref(io), C.c_void_p(stream)), "lego_s2m_run")
+
+    def set_layout(self, layout):
+        """lego_s2m_run's launch layout: 0 a workgroup a problem, 1 latency, -1 automatic (<= 16: latency)."""
+        _check(lib().lego_s2m_set_layout(self.h, int(layout)), "lego_s2m_set_layout")
 
     def map_transform(self, n, io, stream=0):
         """transformPointCloud of n parts (LegoMapTransformIo of device pointers); asynchronous."""

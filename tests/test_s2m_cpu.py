@@ -149,7 +149,8 @@ def test_s2m_abi_exports():
     import re
     hdr = open(os.path.join(REPO, "include", "lego_s2m.h")).read()
     names = set(re.findall(r"\b(lego_(?:s2m|map|mapper)_\w+)\s*\(", hdr))
-    assert names == {"lego_s2m_create", "lego_s2m_destroy", "lego_s2m_run", "lego_s2m_run_host", "lego_map_transform",
+    assert names == {"lego_s2m_create", "lego_s2m_destroy", "lego_s2m_run", "lego_s2m_run_host", "lego_s2m_set_layout",
+                     "lego_map_transform",
                      "lego_map_voxel", "lego_map_associate", "lego_map_odometry_to_transform", "lego_mapper_create",
                      "lego_mapper_destroy",
                      "lego_mapper_step", "lego_mapper_key_poses"}
