@@ -971,18 +971,8 @@ LG_DEVICE int block_excl_scan(int v, int* red, int& total) {
 }
 
 // VoxelGrid, part 1 (PCL applyFilter up to the sort): bounds, leaf indices, the cloud's sort segment
-// k64 != nullptr: the few-clouds layout for one device-wide sort, 64-bit keys (cloud << 32 | leaf index)
-// with every slot past the cloud's points padded by (n_clouds << 32), which sorts after all clouds
-LG_DEVICE void vox_pad(unsigned long long* k64, unsigned* vals, int c, int from, int cap, int n_clouds) {
-  for (int i = from + (int)threadIdx.x; i < cap; i += S2M_THREADS) {
-    k64[(size_t)c * cap + i] = (unsigned long long)n_clouds << 32;
-    vals[(size_t)c * cap + i] = 0u;
-  }
-}
-
 __global__ __launch_bounds__(S2M_THREADS) void k_vox_keys(lego_map_voxel_io io, unsigned* keys, unsigned* vals,
-                                                          int* seg_b, int* seg_e, int* ovf, int cap,
-                                                          unsigned long long* k64, int n_clouds) {
+                                                          int* seg_b, int* seg_e, int* ovf, int cap) {
   __shared__ float red[S2M_THREADS / 64];
   __shared__ int sh[8];
   const int c = blockIdx.x, tid = threadIdx.x;
@@ -990,7 +980,6 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vox_keys(lego_map_voxel_io io, 
   const float4* in = (const float4*)io.in + io.in_off[c];
   if (n > cap || n < 0) {
     if (tid == 0) { seg_b[c] = seg_e[c] = c * cap; ovf[c] = -1; }
-    if (k64) vox_pad(k64, vals, c, 0, cap, n_clouds);
     return;
   }
   const float inv = 1.0f / io.leaf[c];  // inverse_leaf_size_
@@ -1022,40 +1011,22 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vox_keys(lego_map_voxel_io io, 
     ovf[c] = bad;
   }
   __syncthreads();
-  if (sh[5]) {
-    if (k64) vox_pad(k64, vals, c, 0, cap, n_clouds);
-    return;
-  }
+  if (sh[5]) return;
   const float mb0 = (float)sh[0], mb1 = (float)sh[1], mb2 = (float)sh[2];
   const int m1 = sh[3], m2 = sh[4];
   unsigned* k = keys + (size_t)c * cap;
   unsigned* v = vals + (size_t)c * cap;
-  const unsigned long long khi = (unsigned long long)c << 32;
   for (int i = tid; i < n; i += S2M_THREADS) {
     const float4 p = in[i];
     const int i0 = (int)(floorf(p.x * inv) - mb0), i1 = (int)(floorf(p.y * inv) - mb1), i2 = (int)(floorf(p.z * inv) - mb2);
-    const unsigned key = (unsigned)(i0 + i1 * m1 + i2 * m2);
-    if (k64)
-      k64[(size_t)c * cap + i] = khi | key;
-    else
-      k[i] = key;
+    k[i] = (unsigned)(i0 + i1 * m1 + i2 * m2);
     v[i] = (unsigned)i;
   }
-  if (k64) vox_pad(k64, vals, c, n, cap, n_clouds);
 }
 
-struct KeyView {
-  const unsigned* p;
-  int ks;
-  LG_DEVICE unsigned operator[](int i) const { return p[(size_t)i * ks]; }
-};
-
 // VoxelGrid, part 2: one centroid per run of equal leaf index in the (stably) sorted keys
-// ks = 1: keys / vals per cloud at c * cap (segmented sort); ks = 2: the low words of the few-clouds
-// layout's sorted 64-bit keys, cloud c's entries after those of the clouds before it
 __global__ __launch_bounds__(S2M_THREADS) void k_vox_reduce(lego_map_voxel_io io, const unsigned* keys,
-                                                            const unsigned* vals, const int* ovf, int cap,
-                                                            const int* seg_b, const int* seg_e, int ks) {
+                                                            const unsigned* vals, const int* ovf, int cap) {
   __shared__ int red[S2M_THREADS / 64];
   const int c = blockIdx.x, tid = threadIdx.x;
   const int n = io.in_n[c];
@@ -1070,13 +1041,8 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vox_reduce(lego_map_voxel_io io
     if (tid == 0) { io.out_n[c] = n; io.status[c] = LEGO_ST_VOXEL_OVERFLOW; }
     return;
   }
-  size_t start = (size_t)c * cap;
-  if (ks == 2) {
-    start = 0;
-    for (int q = 0; q < c; ++q) start += (size_t)(seg_e[q] - seg_b[q]);
-  }
-  const KeyView k{keys + start * ks, ks};
-  const unsigned* v = vals + start;
+  const unsigned* k = keys + (size_t)c * cap;
+  const unsigned* v = vals + (size_t)c * cap;
   __shared__ float4 tp[S2M_THREADS];   // the tile's points in sorted order (gathered together)
   __shared__ unsigned tk[S2M_THREADS + 1];
   int base = 0;
@@ -1115,6 +1081,157 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vox_reduce(lego_map_voxel_io io
   if (tid == 0) { io.out_n[c] = base; io.status[c] = 0; }
 }
 
+// ---- VoxelGrid for a few large clouds (the mapping thread's five) ----------------------------------
+// One workgroup a cloud (k_vox_keys / segmented sort / k_vox_reduce) leaves most CUs idle when there are
+// five clouds.  Here every stage runs over 1024-point tiles of every cloud: bounds by atomics, 64-bit
+// keys (cloud << 32 | leaf index) at the clouds' compact offsets, one device-wide stable radix sort, head
+// counts per tile, then the centroids, each tile's output slot from the counts of the tiles before it.
+// Same output, bit for bit, as the per-cloud kernels.
+LG_DEVICE int vxf_slots(const lego_map_voxel_io& io, int c, int cap) {  // a cloud's slots in the key arrays
+  const int n = io.in_n[c];
+  return (n < 0 || n > cap) ? 0 : n;
+}
+LG_DEVICE int ord_f(float f) {  // float -> int with the same order
+  const int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7fffffff;
+}
+LG_DEVICE float unord_f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
+
+// grid (tiles, n): bounds[6c..6c+5] = min of ord(x, y, z), min of ~ord(x, y, z) (i.e. the max); 0x7fffffff
+// before the launch
+__global__ __launch_bounds__(S2M_THREADS) void k_vxf_bounds(lego_map_voxel_io io, int* bounds, int cap) {
+  __shared__ float red[S2M_THREADS / 64];
+  const int t = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+  const int n = vxf_slots(io, c, cap);
+  if (t * S2M_THREADS >= n) return;
+  const float4* in = (const float4*)io.in + io.in_off[c];
+  const int i = t * S2M_THREADS + tid;
+  const float4 p = in[i < n ? i : t * S2M_THREADS];
+  float lo[3], hi[3];
+  for (int a = 0; a < 3; ++a) {
+    const float x = a == 0 ? p.x : (a == 1 ? p.y : p.z);
+    lo[a] = block_min(x, red);
+    hi[a] = -block_min(-x, red);
+  }
+  if (tid == 0)
+    for (int a = 0; a < 3; ++a) {
+      atomicMin(&bounds[6 * c + a], ord_f(lo[a]));
+      atomicMin(&bounds[6 * c + 3 + a], ~ord_f(hi[a]));
+    }
+}
+
+// grid (tiles, n): leaf indices of tile t of cloud c at the cloud's compact offset; segments / overflow
+// flags as k_vox_keys (seg_b = compact start, seg_e = seg_b + sorted entries)
+__global__ __launch_bounds__(S2M_THREADS) void k_vxf_keys(lego_map_voxel_io io, const int* bounds,
+                                                          unsigned long long* k64, unsigned* vals, int* seg_b,
+                                                          int* seg_e, int* ovf, int cap, int n_clouds) {
+  const int t = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+  const int n = io.in_n[c];
+  const int ns = vxf_slots(io, c, cap);
+  int base = 0;
+  for (int q = 0; q < c; ++q) base += vxf_slots(io, q, cap);
+  if (n > cap || n < 0) {
+    if (t == 0 && tid == 0) { seg_b[c] = seg_e[c] = base; ovf[c] = -1; }
+    return;
+  }
+  const float inv = 1.0f / io.leaf[c];
+  float lo[3], hi[3];
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = unord_f(bounds[6 * c + a]);
+    hi[a] = unord_f(~bounds[6 * c + 3 + a]);
+  }
+  const long long dx = (long long)((hi[0] - lo[0]) * inv) + 1, dy = (long long)((hi[1] - lo[1]) * inv) + 1,
+                  dz = (long long)((hi[2] - lo[2]) * inv) + 1;
+  const bool bad = n > 0 && dx * dy * dz > 2147483647LL;
+  int min_b[3], div_b[3];
+  for (int a = 0; a < 3; ++a) {
+    min_b[a] = (int)floorf(lo[a] * inv);
+    div_b[a] = (int)floorf(hi[a] * inv) - min_b[a] + 1;
+  }
+  if (t == 0 && tid == 0) {
+    seg_b[c] = base;
+    seg_e[c] = base + (bad ? 0 : n);
+    ovf[c] = bad ? 1 : 0;
+  }
+  const int i = t * S2M_THREADS + tid;
+  if (i >= ns) return;
+  const size_t slot = (size_t)base + i;
+  if (bad) {  // sorts after every cloud's entries; never read
+    k64[slot] = (unsigned long long)n_clouds << 32;
+    vals[slot] = 0u;
+    return;
+  }
+  const float4 p = ((const float4*)io.in + io.in_off[c])[i];
+  const float mb0 = (float)min_b[0], mb1 = (float)min_b[1], mb2 = (float)min_b[2];
+  const int i0 = (int)(floorf(p.x * inv) - mb0), i1 = (int)(floorf(p.y * inv) - mb1), i2 = (int)(floorf(p.z * inv) - mb2);
+  k64[slot] = ((unsigned long long)c << 32) | (unsigned)(i0 + i1 * div_b[0] + i2 * (div_b[0] * div_b[1]));
+  vals[slot] = (unsigned)i;
+}
+
+// sorted entry i of cloud c (start = seg_b[c] in the sorted arrays): its leaf index (the low word)
+LG_DEVICE unsigned vxf_key(const unsigned long long* k, size_t i) { return (unsigned)k[i]; }
+
+// grid (tiles, n): heads (first entry of each leaf's run) per tile of the cloud's sorted entries
+__global__ __launch_bounds__(S2M_THREADS) void k_vxf_heads(const unsigned long long* k, const int* seg_b,
+                                                           const int* seg_e, int* tcount, int tiles) {
+  __shared__ int red[S2M_THREADS / 64];
+  const int t = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+  const int m = seg_e[c] - seg_b[c];
+  if (t * S2M_THREADS >= m) return;
+  const size_t b0 = (size_t)seg_b[c];
+  const int i = t * S2M_THREADS + tid;
+  const bool head = i < m && (i == 0 || vxf_key(k, b0 + i) != vxf_key(k, b0 + i - 1));
+  int total;
+  block_excl_scan(head ? 1 : 0, red, total);
+  if (tid == 0) tcount[c * tiles + t] = total;
+}
+
+// grid (tiles, n): the centroids (CentroidPoint: float sums in sorted order, / count)
+__global__ __launch_bounds__(S2M_THREADS) void k_vxf_emit(lego_map_voxel_io io, const unsigned long long* k,
+                                                          const unsigned* vals, const int* seg_b, const int* seg_e,
+                                                          const int* ovf, const int* tcount, int tiles) {
+  __shared__ int red[S2M_THREADS / 64];
+  const int t = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+  const int n = io.in_n[c];
+  const float4* in = (const float4*)io.in + io.in_off[c];
+  float4* out = (float4*)io.out + io.out_off[c];
+  if (ovf[c] < 0) {
+    if (t == 0 && tid == 0) { io.out_n[c] = -1; io.status[c] = 0; }
+    return;
+  }
+  if (ovf[c]) {  // PCL: "Leaf size is too small ... Integer indices would overflow": output = input
+    const int i = t * S2M_THREADS + tid;
+    if (i < n) out[i] = in[i];
+    if (t == 0 && tid == 0) { io.out_n[c] = n; io.status[c] = LEGO_ST_VOXEL_OVERFLOW; }
+    return;
+  }
+  const int m = seg_e[c] - seg_b[c];
+  if (t == 0 && tid == 0) {
+    int tot = 0;
+    for (int q = 0; q * S2M_THREADS < m; ++q) tot += tcount[c * tiles + q];
+    io.out_n[c] = tot;
+    io.status[c] = 0;
+  }
+  if (t * S2M_THREADS >= m) return;
+  int base = 0;
+  for (int q = 0; q < t; ++q) base += tcount[c * tiles + q];
+  const size_t b0 = (size_t)seg_b[c];
+  const int i = t * S2M_THREADS + tid;
+  const unsigned key = i < m ? vxf_key(k, b0 + i) : 0u;
+  const bool head = i < m && (i == 0 || key != vxf_key(k, b0 + i - 1));
+  int total;
+  const int slot = base + block_excl_scan(head ? 1 : 0, red, total);
+  if (!head) return;
+  float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+  int g = i;
+  for (; g < m && vxf_key(k, b0 + g) == key; ++g) {
+    const float4 p = in[vals[b0 + g]];
+    sx += p.x; sy += p.y; sz += p.z; si += p.w;
+  }
+  const float cnt = (float)(g - i);
+  out[slot] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+}
+
 }  // namespace
 
 struct lego_s2m {
@@ -1139,7 +1256,7 @@ struct lego_s2m {
   // few-clouds layout (n * max_map <= S2M_WIDE_MAX): 64-bit keys in / sorted, values in / sorted
   unsigned long long *d_k64 = nullptr, *d_k64b = nullptr;
   unsigned *d_wv = nullptr, *d_wv2 = nullptr;
-  int *d_wseg = nullptr, *d_wovf = nullptr;
+  int *d_wseg = nullptr, *d_wovf = nullptr, *d_wbounds = nullptr, *d_wtcount = nullptr;
   void* d_wide_tmp = nullptr;
   size_t wide_tmp_bytes = 0;
   int wide_clouds = 0;
@@ -1196,7 +1313,7 @@ extern "C" void lego_s2m_destroy(lego_s2m* m) {
   if (m->d_state) hipFree(m->d_state);
   for (void* p : {(void*)m->d_keys, (void*)m->d_vals, (void*)m->d_keys2, (void*)m->d_vals2, (void*)m->d_seg,
                   (void*)m->d_ovf, m->d_sort_tmp, (void*)m->d_k64, (void*)m->d_k64b, (void*)m->d_wv, (void*)m->d_wv2,
-                  (void*)m->d_wseg, (void*)m->d_wovf, m->d_wide_tmp})
+                  (void*)m->d_wseg, (void*)m->d_wovf, (void*)m->d_wbounds, (void*)m->d_wtcount, m->d_wide_tmp})
     if (p) hipFree(p);
   delete m;
 }
@@ -1290,8 +1407,9 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
   const int cap = m->max_map;
   hipStream_t st = (hipStream_t)hip_stream;
   if ((size_t)n * cap <= S2M_WIDE_MAX && n < 64) {
-    // few clouds (the mapping thread's five): one device-wide stable radix sort over all of them instead
-    // of rocPRIM's segmented sort, which gives each cloud a single workgroup
+    // few clouds (the mapping thread's five): the tiled kernels and one device-wide stable radix sort
+    // over the clouds' points (their counts read back first: this path synchronizes the stream)
+    const int tiles_max = (cap + S2M_THREADS - 1) / S2M_THREADS;
     if (n > m->wide_clouds) {
       const size_t e = (size_t)n * cap;
       size_t tmp = 0;
@@ -1300,34 +1418,56 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
         return LEGO_EDEVICE;
       hipDeviceSynchronize();
       for (void* p : {(void*)m->d_k64, (void*)m->d_k64b, (void*)m->d_wv, (void*)m->d_wv2, (void*)m->d_wseg,
-                      (void*)m->d_wovf, m->d_wide_tmp})
+                      (void*)m->d_wovf, (void*)m->d_wbounds, (void*)m->d_wtcount, m->d_wide_tmp})
         if (p) hipFree(p);
       m->d_k64 = m->d_k64b = nullptr;
       m->d_wv = m->d_wv2 = nullptr;
-      m->d_wseg = m->d_wovf = nullptr;
+      m->d_wseg = m->d_wovf = m->d_wbounds = m->d_wtcount = nullptr;
       m->d_wide_tmp = nullptr;
       m->wide_clouds = 0;
       if (hipMalloc((void**)&m->d_k64, e * 8) != hipSuccess || hipMalloc((void**)&m->d_k64b, e * 8) != hipSuccess ||
           hipMalloc((void**)&m->d_wv, e * 4) != hipSuccess || hipMalloc((void**)&m->d_wv2, e * 4) != hipSuccess ||
           hipMalloc((void**)&m->d_wseg, (size_t)n * 2 * 4) != hipSuccess ||
-          hipMalloc((void**)&m->d_wovf, (size_t)n * 4) != hipSuccess || hipMalloc(&m->d_wide_tmp, tmp) != hipSuccess)
+          hipMalloc((void**)&m->d_wovf, (size_t)n * 4) != hipSuccess ||
+          hipMalloc((void**)&m->d_wbounds, (size_t)n * 6 * 4) != hipSuccess ||
+          hipMalloc((void**)&m->d_wtcount, (size_t)n * tiles_max * 4) != hipSuccess ||
+          hipMalloc(&m->d_wide_tmp, tmp) != hipSuccess)
         return LEGO_ENOMEM;
       m->wide_tmp_bytes = tmp;
       m->wide_clouds = n;
     }
+    int32_t hn[64];
+    if (hipMemcpyAsync(hn, io->in_n, (size_t)n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return LEGO_EDEVICE;
+    size_t total = 0;
+    int tiles = 1;
+    for (int c = 0; c < n; ++c) {
+      const int k = (hn[c] < 0 || hn[c] > cap) ? 0 : hn[c];
+      total += (size_t)k;
+      tiles = std::max(tiles, (k + S2M_THREADS - 1) / S2M_THREADS);
+    }
     int* wb = m->d_wseg;
     int* we = m->d_wseg + m->wide_clouds;
-    hipLaunchKernelGGL(k_vox_keys, dim3(n), dim3(S2M_THREADS), 0, st, *io, nullptr, m->d_wv, wb, we, m->d_wovf, cap,
-                       m->d_k64, n);
+    if (hipMemsetD32Async((hipDeviceptr_t)m->d_wbounds, 0x7fffffff, (size_t)n * 6, st) != hipSuccess)
+      return LEGO_EDEVICE;
+    hipLaunchKernelGGL(k_vxf_bounds, dim3(tiles, n), dim3(S2M_THREADS), 0, st, *io, m->d_wbounds, cap);
+    hipLaunchKernelGGL(k_vxf_keys, dim3(tiles, n), dim3(S2M_THREADS), 0, st, *io, (const int*)m->d_wbounds, m->d_k64,
+                       m->d_wv, wb, we, m->d_wovf, cap, n);
     if (hipGetLastError() != hipSuccess) return LEGO_EDEVICE;
     int bits = 32;
-    while ((1 << (bits - 32)) <= n) ++bits;  // the cloud index and the pad value n
-    size_t tmp = m->wide_tmp_bytes;
-    if (rocprim::radix_sort_pairs(m->d_wide_tmp, tmp, m->d_k64, m->d_k64b, m->d_wv, m->d_wv2, (size_t)n * cap, 0, bits,
-                                  st) != hipSuccess)
-      return LEGO_EDEVICE;
-    hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, (const unsigned*)m->d_k64b, m->d_wv2,
-                       m->d_wovf, cap, wb, we, 2);
+    while ((1 << (bits - 32)) <= n) ++bits;  // the cloud index and the overflowed clouds' n
+    if (total > 0) {
+      size_t tmp = m->wide_tmp_bytes;
+      if (rocprim::radix_sort_pairs(m->d_wide_tmp, tmp, m->d_k64, m->d_k64b, m->d_wv, m->d_wv2, total, 0, bits, st) !=
+          hipSuccess)
+        return LEGO_EDEVICE;
+    }
+    hipLaunchKernelGGL(k_vxf_heads, dim3(tiles, n), dim3(S2M_THREADS), 0, st, (const unsigned long long*)m->d_k64b,
+                       (const int*)wb, (const int*)we, m->d_wtcount, tiles);
+    hipLaunchKernelGGL(k_vxf_emit, dim3(tiles, n), dim3(S2M_THREADS), 0, st, *io, (const unsigned long long*)m->d_k64b,
+                       (const unsigned*)m->d_wv2, (const int*)wb, (const int*)we, (const int*)m->d_wovf,
+                       (const int*)m->d_wtcount, tiles);
     return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
   }
   if (n > m->vox_clouds) {  // scratch for n clouds of up to max_map_points (grows, never shrinks)
@@ -1358,7 +1498,7 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
   int* seg_b = m->d_seg;
   int* seg_e = m->d_seg + m->vox_clouds;
   hipLaunchKernelGGL(k_vox_keys, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys, m->d_vals, seg_b, seg_e, m->d_ovf,
-                     cap, nullptr, n);
+                     cap);
   if (hipGetLastError() != hipSuccess) return LEGO_EDEVICE;
   // stable LSD radix sort of every cloud's (leaf index, point index) pairs: std::stable_sort's order
   size_t tmp = m->sort_tmp_bytes;
@@ -1366,8 +1506,7 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
                                           (unsigned)((size_t)n * cap), (unsigned)n, seg_b, seg_e, 0, 32, st) !=
       hipSuccess)
     return LEGO_EDEVICE;
-  hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys2, m->d_vals2, m->d_ovf, cap, seg_b,
-                     seg_e, 1);
+  hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys2, m->d_vals2, m->d_ovf, cap);
   return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }
 
