@@ -190,6 +190,14 @@ int  lego_batch_reset(lego_batch* b);
  * [4] concat + the pending lessFlat publish, [5] LM (of the previous scan with lag 1; the VoxelGrid
  * overlaps it on an internal stream). */
 int  lego_batch_stage_times(lego_batch* b, float* ms6);
+/* Measurement: the projection and smoothness stages (the HBM-bound pair) launched `reps` times back
+ * to back on the inputs of the batch's last step (the same device arrays), between two events on
+ * hip_stream; *ms_pair = mean milliseconds of one pair.  d_offsets_alt / d_counts_alt (nullable):
+ * another input set in d_points; the projections alternate between the two sets, the last launch on
+ * the step's own.  Idempotent: the batch's results are unchanged.  Synchronises the device first.  bench.py's roofline. */
+int  lego_batch_time_hbm_stages(lego_batch* b, int32_t reps, const lego_point* d_points, const int64_t* d_offsets,
+                                const int32_t* d_counts, const int64_t* d_offsets_alt, const int32_t* d_counts_alt,
+                                void* hip_stream, float* ms_pair);
 /* While timing is enabled, steps run as one slice on the caller's stream (plus the VoxelGrid stream). */
 int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
 /* Split the streams into `groups` (1..LEGO_MAX_GROUPS) slices, each launched on its own internal HIP

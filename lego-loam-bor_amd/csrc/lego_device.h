@@ -19,6 +19,24 @@
 
 #include "lego_libm.h"
 
+// Streaming (non-temporal) vector stores for outputs that no later instruction of the same kernel
+// reads: they do not displace lines the kernel still reads back through L2 (k_project's column pass
+// re-gathers the winning input points).
+LG_DEVICE void st_nt(float* p, float v) { __builtin_nontemporal_store(v, p); }
+LG_DEVICE void st_nt(int* p, int v) { __builtin_nontemporal_store(v, p); }
+LG_DEVICE void st_nt(int8_t* p, int8_t v) { __builtin_nontemporal_store(v, p); }
+LG_DEVICE void st_nt(uint8_t* p, uint8_t v) { __builtin_nontemporal_store(v, p); }
+LG_DEVICE void st_nt(float4* p, float4 v) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, (f4v*)p);
+}
+LG_DEVICE void st_nt(int2* p, int2 v) {
+  typedef int i2v __attribute__((ext_vector_type(2)));
+  const i2v w = {v.x, v.y};
+  __builtin_nontemporal_store(w, (i2v*)p);
+}
+
 
 // ---- shared POD types (host + device) ---------------------------------------------------------
 struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-derived)

@@ -682,6 +682,49 @@ int lego_batch_stage_times(lego_batch* b, float* ms6) {
   return LEGO_OK;
 }
 
+// The HBM-bound pair of stages (projection, then calculateSmoothness / markOccludedPoints) launched
+// `reps` times back to back on the caller's stream between two events, on the inputs of the batch's
+// last step: the mean duration of one pair without the per-stage event gaps.  With a second input
+// set (another step's offsets / counts into the same point array) the projections alternate between
+// the two, ending on the step's own, so no launch re-reads the input its predecessor just read.  Both stages are
+// idempotent on those inputs (k_project rewrites the same images from the same points; k_fa_prep
+// reads only k_segment's output), so the batch's results are unchanged.
+int lego_batch_time_hbm_stages(lego_batch* b, int32_t reps, const lego_point* d_points, const int64_t* d_offsets,
+                               const int32_t* d_counts, const int64_t* d_offsets_alt, const int32_t* d_counts_alt,
+                               void* hip_stream, float* ms_pair) {
+  if (!b || reps < 1 || !d_points || !d_offsets || !d_counts || !ms_pair) return LEGO_EINVAL;
+  if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
+  hipStream_t st = (hipStream_t)hip_stream;
+  int rc = flush_pending(b);
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;  // nothing else on the device
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return LEGO_EDEVICE;
+  if (hipEventCreate(&e1) != hipSuccess) {
+    hipEventDestroy(e0);
+    return LEGO_EDEVICE;
+  }
+  LgParams P = b->P;
+  P.s0 = 0;
+  P.epoch = b->epoch;
+  P.par = b->par;
+  if (hipEventRecord(e0, st) != hipSuccess) rc = LEGO_EDEVICE;
+  for (int r = 0; r < reps && !rc; ++r) {
+    const bool alt = d_offsets_alt && d_counts_alt && ((reps - 1 - r) & 1);  // the last launch: the step's own
+    rc = lg_launch_project(P, b->B, b->S, (const float4*)d_points, alt ? d_offsets_alt : d_offsets,
+                           alt ? d_counts_alt : d_counts, st);
+    if (!rc) rc = lg_launch_fa_prep(P, b->B, b->S, st, false);
+  }
+  if (!rc && hipEventRecord(e1, st) != hipSuccess) rc = LEGO_EDEVICE;
+  float ms = 0.f;
+  if (!rc && hipEventSynchronize(e1) != hipSuccess) rc = LEGO_EDEVICE;
+  if (!rc && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = LEGO_EDEVICE;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (!rc) *ms_pair = ms / reps;
+  return rc;
+}
+
 // Header of stream s (counts, orientation, state) into pinned memory, on st, then wait for it.
 struct ReadHdr {
   int32_t cnt[CNT_N];

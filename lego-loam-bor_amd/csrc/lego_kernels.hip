@@ -303,6 +303,12 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   int* winner = smem + 64;  // LDS image: V*H ints
   const float4* in = pts + offs[s];
   const int n = cnts[s];
+  // the first batch's point loads go out before the LDS image reset (see below)
+  constexpr int kU = 8;
+  const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
+  float3 pk[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) pk[u] = buffer_load_f3(rin, (uint32_t)(tid + u * nt) * 16u);
   PROF_T(t_p0);
   for (int c = tid; c < VH; c += nt) winner[c] = -1;
   __syncthreads();
@@ -315,11 +321,6 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   // queue per wave and take the exact path 64 at a time.
   int* queue = smem + 64 + VH + wave_id() * PQ_CAP;  // PQ_CAP ints per wave
   int qn = 0;
-  constexpr int kU = 8;
-  const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
-  float3 pk[kU];
-#pragma unroll
-  for (int u = 0; u < kU; ++u) pk[u] = buffer_load_f3(rin, (uint32_t)(tid + u * nt) * 16u);
   for (int i0 = tid; i0 < n; i0 += nt * kU) {
     float3 nx[kU];
 #pragma unroll
@@ -410,8 +411,8 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
           r = FLT_MAX;
           q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
         }
-        range[c] = r;
-        cloud[c] = q;
+        st_nt(&range[c], r);  // streaming stores: the input lines stay in L2 for the gathers
+        st_nt(&cloud[c], q);
         if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
           const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
           if (ground_pair(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ), P.mount)) gmask |= (3ull << (i - 1));
@@ -596,8 +597,8 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
           r = FLT_MAX;
           q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
         }
-        range[c] = r;
-        cloud[c] = q;
+        st_nt(&range[c], r);  // streaming stores: the input lines stay in L2 for the gathers
+        st_nt(&cloud[c], q);
         if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
           const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
           if (ground_pair(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ), P.mount)) gmask |= (3ull << (i - 1));

@@ -75,6 +75,8 @@ def lib():
         L.lego_batch_reset.argtypes = [C.c_void_p]
         L.lego_batch_stage_times.argtypes = [C.c_void_p, P(C.c_float)]
         L.lego_batch_set_timing.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_batch_time_hbm_stages.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                 C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_float)]
         L.lego_batch_set_groups.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_lag.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_wide.argtypes = [C.c_void_p, C.c_int32]
@@ -228,6 +230,17 @@ class Batch:
         out = np.zeros((self.S, 7), dtype=np.int32)
         _check(lib().lego_batch_read_counts(self.h, out.ctypes.data_as(P(C.c_int32))), "lego_batch_read_counts")
         return out
+
+    def time_hbm_stages(self, d_points, d_offsets, d_counts, d_offsets_alt=0, d_counts_alt=0, reps=20, stream=0):
+        """Mean ms of one projection + smoothness pair, `reps` launches back to back on the inputs of
+        the last step (the same device arrays; the projections alternate with a second input set when
+        given); the batch's results are unchanged."""
+        ms = C.c_float()
+        _check(lib().lego_batch_time_hbm_stages(self.h, int(reps), C.c_void_p(d_points), C.c_void_p(d_offsets),
+                                                C.c_void_p(d_counts), C.c_void_p(d_offsets_alt or None),
+                                                C.c_void_p(d_counts_alt or None), C.c_void_p(stream), C.byref(ms)),
+               "lego_batch_time_hbm_stages")
+        return ms.value
 
     def stage_times(self):
         ms = (C.c_float * 6)()

@@ -422,6 +422,52 @@ def test_batch_back_to_back_matches_oracle(gpu, groups, lag, alternate, steps):
     b.close()
 
 
+@pytest.mark.parametrize("wide", [0, 1])
+def test_hbm_stage_timing_leaves_results(gpu, wide):
+    """bench.py's roofline timing (k_project + k_fa_prep launched back to back, the projections
+    alternating between two steps' inputs and ending on the last step's) leaves every scan's results
+    as they were, and the next step still matches the oracle."""
+    import torch
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    S, steps = 4, 4
+    cap = params.num_vertical_scans * params.num_horizontal_scans
+    seqs = np.repeat(np.arange(S)[None, :] + 90, steps, 0).reshape(-1)
+    scans = np.repeat(np.arange(steps)[:, None], S, 1).reshape(-1)
+    pts, cnt = A.synth_batch(cfg, seqs, scans)
+    d_pts = torch.from_numpy(pts).cuda()
+    offs = torch.from_numpy((np.arange(S * steps, dtype=np.int64) * cap).reshape(steps, S)).cuda()
+    cnts = torch.from_numpy(cnt.reshape(steps, S).astype(np.int32)).cuda()
+    b = L.Batch(params, S, cap)
+    b.set_wide(wide)
+    st = torch.cuda.current_stream().cuda_stream
+    oracles = [oracle_for(params) for _ in range(S)]
+    for k in range(steps - 1):
+        b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), st)
+        for s in range(S):
+            oracles[s].cloud_handler(pts[k * S + s, :cnt[k * S + s]])
+            oracles[s].feature_association()
+    b.sync()
+    before = [b.read(s) for s in range(S)]
+    k = steps - 2
+    ms = b.time_hbm_stages(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(),
+                           offs[k - 1].data_ptr(), cnts[k - 1].data_ptr(), reps=4, stream=st)
+    assert ms > 0
+    for s in range(S):
+        pg, fg = b.read(s)
+        assert not Hs.diff_report(Hs.PROJ_KEYS, pg, before[s][0])
+        assert not Hs.diff_report(Hs.FEAT_KEYS, fg, before[s][1])
+    k = steps - 1
+    b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), st)
+    b.sync()
+    for s in range(S):
+        pr = oracles[s].cloud_handler(pts[k * S + s, :cnt[k * S + s]])
+        fr = oracles[s].feature_association()
+        pg, fg = b.read(s)
+        assert_scan_parity(k, pg, pr, fg, fr)
+    b.close()
+
+
 def test_edge_inputs(gpu):
     """Empty / all-NaN clouds fail like the oracle; sparse, tiny, colliding and out-of-FOV clouds match."""
     params = L.params_vlp16()

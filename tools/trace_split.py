@@ -5,8 +5,9 @@
 bench.py runs the W + K steps twice: first the throughput pass (the timed region; with lag 1 and one
 slice, k_publish / k_lm run on an internal stream concurrently with the next scan's front end, so a
 kernel's duration there includes sharing the GPU), then the per-stage timing pass (one stream, stages
-in sequence) whose last K launches give bench.py's stages_ms and roofline.launch_ms.  rocprofv3's
---stats file averages both passes; this split reports them apart, so the timing pass can be compared
+in sequence) whose last K launches give bench.py's stages_ms, and for k_project / k_fa_prep the
+roofline pass (R back-to-back pairs, --roofline-reps) that gives roofline.launch_ms.  rocprofv3's
+--stats file averages all passes; this split reports them apart, so the timing pass can be compared
 with the bench line.  Launches are assigned to the passes in time order, per kernel (each kernel runs
 once per step in each pass).
 """
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--roofline-reps", type=int, default=20, help="bench.py's back-to-back roofline launches")
     a = ap.parse_args()
     per = a.steps + a.warmup
     acc = collections.defaultdict(list)
@@ -36,6 +38,9 @@ def main():
         d = [x for _, x in v]
         if len(d) == 2 * per:  # throughput pass, then the timing pass (measured: its last K)
             parts = (("throughput_pass", d[a.warmup:per]), ("timing_pass", d[per + a.warmup:]))
+        elif len(d) == 2 * per + a.roofline_reps:  # + the roofline pass (k_project / k_fa_prep)
+            parts = (("throughput_pass", d[a.warmup:per]), ("timing_pass", d[per + a.warmup:2 * per]),
+                     ("roofline_pass", d[2 * per:]))
         else:
             parts = (("all", d),)
         for phase, x in parts:
