@@ -206,20 +206,39 @@ struct lego_batch {
   }
 };
 
+// Mapped, coherent pinned host memory that kernels write directly (the single-context readback)
+struct Mapped {
+  char* p = nullptr;   // host pointer
+  char* dp = nullptr;  // device pointer to the same memory
+  size_t cap = 0;
+  int alloc(size_t bytes) {
+    if (hipHostMalloc((void**)&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+      p = nullptr;
+      return LEGO_ENOMEM;
+    }
+    if (hipHostGetDevicePointer((void**)&dp, p, 0) != hipSuccess) return LEGO_EDEVICE;
+    cap = bytes;
+    return LEGO_OK;
+  }
+  ~Mapped() {
+    if (p) hipHostFree(p);
+  }
+};
+
 struct lego_ctx {
   lego_batch* b = nullptr;
-  float4* d_pts = nullptr;
+  float4* d_in = nullptr;  // [0]: the point count (int32), [1, cap]: the points
   int64_t* d_off = nullptr;
-  int32_t* d_cnt = nullptr;
   int cap = 0;
-  Pinned h_pts;  // fromROSMsg gather target (pinned: the upload is asynchronous)
-  Pinned h_n;    // the point count, uploaded with the points
+  Pinned h_in;       // fromROSMsg gather target, count first (pinned: one asynchronous upload)
+  Mapped pk_proj;    // ProjectionOut arrays, written by k_pack (layout: proj_layout)
+  Mapped pk_assoc;   // AssociationOut arrays (assoc_layout)
   ~lego_ctx() {
     if (b) {
       hipSetDevice(b->device);
-      if (d_pts) hipFree(d_pts);
+      hipDeviceSynchronize();
+      if (d_in) hipFree(d_in);
       if (d_off) hipFree(d_off);
-      if (d_cnt) hipFree(d_cnt);
       delete b;
     }
   }
@@ -895,6 +914,211 @@ int lego_batch_read_counts(lego_batch* b, int32_t* out) {
   return LEGO_OK;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// single-context readback: one kernel copies every output array of the call (sizes read on the
+// device) straight into mapped pinned host memory, then one wait.  It replaces a header read (four
+// copies and a wait) and a copy per array (each a runtime blit launch, ~5-20 us apart on the
+// timeline of one scan).
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct PackDesc {
+  const char* src;       // device array
+  const int32_t* sel;    // nullable: src += *sel * sel_stride (the Last double buffer)
+  long long sel_stride;
+  char* dst;             // device view of the mapped host region
+  const int32_t* cnt;    // nullable: element count read on the device, capped at `fixed`
+  int32_t fixed;         // element count (or the cap of *cnt)
+  int32_t elem;          // bytes per element
+};
+#define PACK_MAX 16
+struct PackArgs {
+  PackDesc d[PACK_MAX];
+};
+
+__global__ __launch_bounds__(256) void k_pack(PackArgs a) {
+  const PackDesc& d = a.d[blockIdx.y];
+  const long long n = d.cnt ? min(max(*d.cnt, 0), d.fixed) : d.fixed;
+  const char* src = d.src + (d.sel ? (long long)*d.sel * d.sel_stride : 0ll);
+  const size_t bytes = (size_t)n * d.elem;
+  const size_t stride = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool vec = ((((uintptr_t)src) | ((uintptr_t)d.dst)) & 15) == 0;
+  const size_t nv = vec ? bytes / 16 : 0;
+  for (size_t i = t0; i < nv; i += stride) ((uint4*)d.dst)[i] = ((const uint4*)src)[i];
+  for (size_t i = nv * 16 + t0; i < bytes; i += stride) d.dst[i] = src[i];
+}
+
+// Region offsets of a pack buffer (each region 256-byte aligned; sizes at capacity)
+struct PackLayout {
+  size_t off[PACK_MAX];
+  size_t total;
+};
+PackLayout make_layout(const size_t* bytes, int n) {
+  PackLayout L{};
+  size_t o = 0;
+  for (int i = 0; i < n; ++i) {
+    L.off[i] = o;
+    o += (bytes[i] + 255) & ~(size_t)255;
+  }
+  L.total = o;
+  return L;
+}
+// proj: 0 header, 1 segmented, 2 outlier, 3 scan, 4 ring start, 5 ring end, 6 ground flag, 7 col,
+// 8 range (segmented), 9 label, 10 ground, 11 range image
+constexpr int PJ_N = 12;
+PackLayout proj_layout(const LgParams& P) {
+  const size_t VH = P.VH;
+  const size_t b[PJ_N] = {sizeof(ReadHdr), VH * 16, VH * 16, (size_t)P.H * 16, (size_t)P.V * 4, (size_t)P.V * 4,
+                          VH, VH * 4, VH * 4, VH * 4, VH, VH * 4};
+  return make_layout(b, PJ_N);
+}
+// assoc: 0 header, 1 sharp, 2 sharp ind, 3 less sharp, 4 less sharp ind, 5 flat, 6 flat ind,
+// 7 less flat, 8 corner Last, 9 surf Last, 10 outlier Last
+constexpr int AS_N = 11;
+PackLayout assoc_layout(const LgParams& P) {
+  const size_t VH = P.VH, V = P.V;
+  const size_t b[AS_N] = {sizeof(ReadHdr), V * P.cap_sharp * 16, V * P.cap_sharp * 4, V * P.cap_lsharp * 16,
+                          V * P.cap_lsharp * 4, V * P.cap_flat * 16, V * P.cap_flat * 4, VH * 16,
+                          V * P.cap_lsharp * 16, VH * 16, VH * 16};
+  return make_layout(b, AS_N);
+}
+
+// the header's four parts (counts, orientation, front-end state, LgState) of stream s
+int hdr_descs(const lego_batch* b, int s, char* dst, PackDesc* d) {
+  const LgBufs& B = b->B;
+  d[0] = {(const char*)(B.counts + (size_t)s * CNT_N), nullptr, 0, dst + offsetof(ReadHdr, cnt), nullptr,
+          (int32_t)sizeof(int32_t) * CNT_N, 1};
+  d[1] = {(const char*)(B.orient + (size_t)s * 4), nullptr, 0, dst + offsetof(ReadHdr, ori), nullptr, 16, 1};
+  d[2] = {(const char*)(B.fe_state + (size_t)s * 2), nullptr, 0, dst + offsetof(ReadHdr, fe), nullptr, 8, 1};
+  d[3] = {(const char*)(B.state + s), nullptr, 0, dst + offsetof(ReadHdr, S), nullptr, (int32_t)sizeof(LgState), 1};
+  return 4;
+}
+
+int launch_pack(const PackDesc* d, int n, hipStream_t st) {
+  PackArgs a{};
+  for (int i = 0; i < n; ++i) a.d[i] = d[i];
+  hipLaunchKernelGGL(k_pack, dim3(16, n), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+}
+
+// ProjectionOut of stream 0 into c->pk_proj, then one wait; out's arrays point into it
+int pack_proj(lego_ctx* c, lego_projection_out* o, int* fe_status) {
+  lego_batch* b = c->b;
+  const LgParams& P = b->P;
+  const LgBufs& B = b->B;
+  const PackLayout L = proj_layout(P);
+  char* dp = c->pk_proj.dp;
+  const int32_t* cnt = B.counts;
+  const int VH = P.VH;
+  PackDesc d[PACK_MAX];
+  int n = hdr_descs(b, 0, dp + L.off[0], d);
+  d[n++] = {(const char*)B.seg_pts, nullptr, 0, dp + L.off[1], cnt + CNT_M, VH, 16};
+  d[n++] = {(const char*)B.outlier, nullptr, 0, dp + L.off[2], cnt + CNT_OUTLIER, VH, 16};
+  d[n++] = {(const char*)B.scan_msg, nullptr, 0, dp + L.off[3], cnt + CNT_SCAN, P.H, 16};
+  d[n++] = {(const char*)B.ring_start, nullptr, 0, dp + L.off[4], nullptr, P.V, 4};
+  d[n++] = {(const char*)B.ring_end, nullptr, 0, dp + L.off[5], nullptr, P.V, 4};
+  d[n++] = {(const char*)B.seg_ground, nullptr, 0, dp + L.off[6], cnt + CNT_M, VH, 1};
+  d[n++] = {(const char*)B.seg_col, nullptr, 0, dp + L.off[7], cnt + CNT_M, VH, 4};
+  d[n++] = {(const char*)B.seg_range, nullptr, 0, dp + L.off[8], cnt + CNT_M, VH, 4};
+  d[n++] = {(const char*)B.label, nullptr, 0, dp + L.off[9], nullptr, VH, 4};
+  d[n++] = {(const char*)B.ground, nullptr, 0, dp + L.off[10], nullptr, VH, 1};
+  d[n++] = {(const char*)B.range, nullptr, 0, dp + L.off[11], nullptr, VH, 4};
+  if (launch_pack(d, n, nullptr) != LEGO_OK || hipStreamSynchronize(nullptr) != hipSuccess) return LEGO_EDEVICE;
+  char* hp = c->pk_proj.p;
+  const ReadHdr* h = (const ReadHdr*)(hp + L.off[0]);
+  *fe_status = h->fe[0];
+  if (!o) return LEGO_OK;
+  o->n_segmented = h->cnt[CNT_M];
+  o->n_outlier = h->cnt[CNT_OUTLIER];
+  o->n_scan = h->cnt[CNT_SCAN];
+  o->segmented_cloud = (lego_point*)(hp + L.off[1]);
+  o->outlier_cloud = (lego_point*)(hp + L.off[2]);
+  o->scan_msg = (lego_point*)(hp + L.off[3]);
+  o->start_ring_index = (int32_t*)(hp + L.off[4]);
+  o->end_ring_index = (int32_t*)(hp + L.off[5]);
+  o->start_orientation = h->ori[0];
+  o->end_orientation = h->ori[1];
+  o->orientation_diff = h->ori[2];
+  o->segmented_cloud_ground_flag = (uint8_t*)(hp + L.off[6]);
+  o->segmented_cloud_col_ind = (uint32_t*)(hp + L.off[7]);
+  o->segmented_cloud_range = (float*)(hp + L.off[8]);
+  o->label_mat = (int32_t*)(hp + L.off[9]);
+  o->ground_mat = (int8_t*)(hp + L.off[10]);
+  o->range_mat = (float*)(hp + L.off[11]);
+  return LEGO_OK;
+}
+
+// AssociationOut of stream 0 into c->pk_assoc, then one wait
+int pack_assoc(lego_ctx* c, lego_association_out* o) {
+  lego_batch* b = c->b;
+  const LgParams& P = b->P;
+  const LgBufs& B = b->B;
+  const PackLayout L = assoc_layout(P);
+  char* dp = c->pk_assoc.dp;
+  const int32_t* cnt = B.counts;
+  const size_t VH = P.VH, V = P.V;
+  const size_t hs = (size_t)b->last_par;  // the feature half of the last scan (S = 1)
+  const size_t cls = V * P.cap_lsharp;
+  const int32_t* last_buf = (const int32_t*)((const char*)B.state + offsetof(LgState, last_buf));
+  const int32_t* n_cl = (const int32_t*)((const char*)B.state + offsetof(LgState, n_corner_last));
+  const int32_t* n_sl = (const int32_t*)((const char*)B.state + offsetof(LgState, n_surf_last));
+  PackDesc d[PACK_MAX];
+  int n = hdr_descs(b, 0, dp + L.off[0], d);
+  d[n++] = {(const char*)(B.f_sharp + hs * V * P.cap_sharp), nullptr, 0, dp + L.off[1], cnt + CNT_SHARP,
+            (int32_t)(V * P.cap_sharp), 16};
+  d[n++] = {(const char*)(B.f_sharp_ind + hs * V * P.cap_sharp), nullptr, 0, dp + L.off[2], cnt + CNT_SHARP,
+            (int32_t)(V * P.cap_sharp), 4};
+  d[n++] = {(const char*)(B.f_lsharp + hs * V * P.cap_lsharp), nullptr, 0, dp + L.off[3], cnt + CNT_LSHARP,
+            (int32_t)cls, 16};
+  d[n++] = {(const char*)(B.f_lsharp_ind + hs * V * P.cap_lsharp), nullptr, 0, dp + L.off[4], cnt + CNT_LSHARP,
+            (int32_t)cls, 4};
+  d[n++] = {(const char*)(B.f_flat + hs * V * P.cap_flat), nullptr, 0, dp + L.off[5], cnt + CNT_FLAT,
+            (int32_t)(V * P.cap_flat), 16};
+  d[n++] = {(const char*)(B.f_flat_ind + hs * V * P.cap_flat), nullptr, 0, dp + L.off[6], cnt + CNT_FLAT,
+            (int32_t)(V * P.cap_flat), 4};
+  d[n++] = {(const char*)B.f_lflat, nullptr, 0, dp + L.off[7], cnt + CNT_LFLAT, (int32_t)VH, 16};
+  d[n++] = {(const char*)B.corner_last, last_buf, (long long)(cls * 16), dp + L.off[8], n_cl, (int32_t)cls, 16};
+  d[n++] = {(const char*)B.surf_last, last_buf, (long long)(VH * 16), dp + L.off[9], n_sl, (int32_t)VH, 16};
+  d[n++] = {(const char*)B.outlier_fa, nullptr, 0, dp + L.off[10], cnt + CNT_OUTLIER, (int32_t)VH, 16};
+  if (launch_pack(d, n, nullptr) != LEGO_OK || hipStreamSynchronize(nullptr) != hipSuccess) return LEGO_EDEVICE;
+  char* hp = c->pk_assoc.p;
+  const ReadHdr* h = (const ReadHdr*)(hp + L.off[0]);
+  if (!o) return LEGO_OK;
+  const int32_t* k = h->cnt;
+  const LgState& S = h->S;
+  o->status = S.status;
+  o->n_sharp = k[CNT_SHARP];
+  o->n_less_sharp = k[CNT_LSHARP];
+  o->n_flat = k[CNT_FLAT];
+  o->n_less_flat = k[CNT_LFLAT];
+  o->corner_points_sharp = (lego_point*)(hp + L.off[1]);
+  o->sharp_ind = (int32_t*)(hp + L.off[2]);
+  o->corner_points_less_sharp = (lego_point*)(hp + L.off[3]);
+  o->less_sharp_ind = (int32_t*)(hp + L.off[4]);
+  o->surf_points_flat = (lego_point*)(hp + L.off[5]);
+  o->flat_ind = (int32_t*)(hp + L.off[6]);
+  o->surf_points_less_flat = (lego_point*)(hp + L.off[7]);
+  for (int i = 0; i < 6; ++i) {
+    o->transform_cur[i] = S.cur[i];
+    o->transform_sum[i] = S.sum[i];
+  }
+  for (int i = 0; i < 4; ++i) o->odom_orientation[i] = S.quat[i];
+  for (int i = 0; i < 3; ++i) o->odom_position[i] = S.pos[i];
+  o->lm_iter_surf = S.iters_surf;
+  o->lm_iter_corner = S.iters_corner;
+  o->n_corner_last = S.n_corner_last;
+  o->n_surf_last = S.n_surf_last;
+  o->n_outlier_last = k[CNT_OUTLIER];
+  o->cloud_corner_last = (lego_point*)(hp + L.off[8]);
+  o->cloud_surf_last = (lego_point*)(hp + L.off[9]);
+  o->cloud_outlier_last = (lego_point*)(hp + L.off[10]);
+  return LEGO_OK;
+}
+}  // namespace
+
+extern "C" {
+
 // ---------------------------------------------------------------------------------------------
 // single-sequence drop-in
 // ---------------------------------------------------------------------------------------------
@@ -913,9 +1137,14 @@ int lego_ctx_create(const lego_params* p, int32_t device, lego_ctx** out) {
   }
   c->cap = 0;
   if (hipMalloc((void**)&c->d_off, sizeof(int64_t)) != hipSuccess ||
-      hipMalloc((void**)&c->d_cnt, sizeof(int32_t)) != hipSuccess) {
+      hipMalloc((void**)&c->d_in, sizeof(float4)) != hipSuccess) {
     delete c;
     return LEGO_ENOMEM;
+  }
+  if ((rc = c->pk_proj.alloc(proj_layout(c->b->P).total)) != LEGO_OK ||
+      (rc = c->pk_assoc.alloc(assoc_layout(c->b->P).total)) != LEGO_OK) {
+    delete c;
+    return rc;
   }
   int64_t zero = 0;
   hipMemcpy(c->d_off, &zero, sizeof(zero), hipMemcpyHostToDevice);
@@ -932,10 +1161,12 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
     return LEGO_EINVAL;
   lego_batch* b = c->b;
   hipSetDevice(b->device);
-  // fromROSMsg: gather x,y,z from the strided PointCloud2 payload (intensity is not used by the path)
-  float4* hp = c->h_pts.get<float4>(n);
-  int32_t* hn = c->h_n.get<int32_t>(1);
-  if (!hp || !hn) return LEGO_ENOMEM;
+  // fromROSMsg: gather x,y,z from the strided PointCloud2 payload (intensity is not used by the path),
+  // behind the point count: one pinned buffer, one upload
+  float4* hin = c->h_in.get<float4>((size_t)n + 1);
+  if (!hin) return LEGO_ENOMEM;
+  *(int32_t*)hin = n;
+  float4* hp = hin + 1;
   const char* base = (const char*)points;
   for (int i = 0; i < n; ++i) {
     float4 q;
@@ -945,28 +1176,25 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
     q.w = 0.f;
     hp[i] = q;
   }
-  *hn = n;
   if (n > c->cap) {
-    if (c->d_pts) hipFree(c->d_pts);
-    c->d_pts = nullptr;
-    if (hipMalloc((void**)&c->d_pts, (size_t)n * sizeof(float4)) != hipSuccess) return LEGO_ENOMEM;
+    hipStreamSynchronize(nullptr);  // the previous call's kernels may still read d_in (they do not: every
+                                    // call ends with a wait; kept for safety)
+    if (c->d_in) hipFree(c->d_in);
+    c->d_in = nullptr;
+    if (hipMalloc((void**)&c->d_in, ((size_t)n + 1) * sizeof(float4)) != hipSuccess) return LEGO_ENOMEM;
     c->cap = n;
   }
-  // everything in order on the null stream: upload, kernels, then one wait for the header and one
-  // for the output arrays (pinned host buffers throughout)
-  if (n > 0 && hipMemcpyAsync(c->d_pts, hp, (size_t)n * sizeof(float4), hipMemcpyHostToDevice, nullptr) != hipSuccess)
+  // everything in order on the null stream: upload, kernels, the pack into mapped host memory, one wait
+  if (hipMemcpyAsync(c->d_in, hin, ((size_t)n + 1) * sizeof(float4), hipMemcpyHostToDevice, nullptr) != hipSuccess)
     return LEGO_EDEVICE;
-  if (hipMemcpyAsync(c->d_cnt, hn, sizeof(int32_t), hipMemcpyHostToDevice, nullptr) != hipSuccess) return LEGO_EDEVICE;
   int rc = chain_stream(b, nullptr);
   if (rc) return rc;
-  rc = run_projection(b, c->d_pts ? c->d_pts : (const float4*)c->d_off, c->d_off, c->d_cnt, nullptr, 0, 1);
+  rc = run_projection(b, c->d_in + 1, c->d_off, (const int32_t*)c->d_in, nullptr, 0, 1);
   if (rc) return rc;
-  ReadHdr* h = nullptr;
-  rc = read_hdr(b, 0, nullptr, &h);
+  int fe = LEGO_OK;
+  rc = pack_proj(c, out, &fe);
   if (rc) return rc;
-  if (h->fe[0] != LEGO_OK) return h->fe[0];
-  if (out) return read_proj(b, 0, h, nullptr, out);
-  return LEGO_OK;
+  return fe;
 }
 
 static int feature_association(lego_ctx* c, lego_association_out* out, bool distort) {
@@ -982,11 +1210,7 @@ static int feature_association(lego_ctx* c, lego_association_out* out, bool dist
   advance_pipeline(b, false, 1);
   rc = flush_pending(b);
   if (rc) return rc;
-  ReadHdr* h = nullptr;
-  rc = read_hdr(b, 0, nullptr, &h);  // also the wait for the kernels
-  if (rc) return rc;
-  if (out) return read_assoc(b, 0, h, nullptr, out);
-  return LEGO_OK;
+  return pack_assoc(c, out);  // also the wait for the kernels
 }
 
 int lego_feature_association(lego_ctx* c, lego_association_out* out) {

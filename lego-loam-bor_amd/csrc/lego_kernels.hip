@@ -373,86 +373,6 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   int8_t* ground = B.ground + (size_t)s * VH;
   const float qnan = __int_as_float(0x7fc00000);
   const float4* src0 = n > 0 ? in : cloud;  // any readable address for empty cells (value unused)
-#ifdef LG_COLPF
-  // The lane's columns j = tid, tid + nt, ... as a sequence of 8-row chunks; the next chunk's winners
-  // and point gathers are issued before the current chunk is processed, so the gathers of a lane
-  // stay in flight back to back instead of one wait per column.
-  constexpr int kC = 8;
-  const int nchunk = (V + kC - 1) / kC;
-  const int ntask = tid < H ? ((H - 1 - tid) / nt + 1) * nchunk : 0;
-  int wa[kC];
-  float4 pa[kC];
-  auto fetch = [&](int t, int (&w)[kC], float4 (&pk)[kC]) {
-    const int j = tid + (t / nchunk) * nt, i0 = (t % nchunk) * kC;
-#pragma unroll
-    for (int u = 0; u < kC; ++u) w[u] = (i0 + u < V) ? winner[(i0 + u) * H + j] : -1;
-#pragma unroll
-    for (int u = 0; u < kC; ++u) pk[u] = src0[w[u] >= 0 ? w[u] : 0];
-  };
-  if (ntask > 0) fetch(0, wa, pa);
-  unsigned long long gmask = 0ull;
-  float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
-  float prev_r = 0.f;
-  float min_range = 1000.f;
-  int id_min = -1;
-  for (int t = 0; t < ntask; ++t) {
-    int wb[kC];
-    float4 pb[kC];
-    fetch(min(t + 1, ntask - 1), wb, pb);
-    const int j = tid + (t / nchunk) * nt, i0 = (t % nchunk) * kC;
-    const double jfrac = (double)(float)j / 10000.0;
-    if (i0 == 0) {
-      gmask = 0ull;
-      prev = make_float4(0.f, 0.f, 0.f, 0.f);
-      prev_r = 0.f;
-      min_range = 1000.f;
-      id_min = -1;
-    }
-    auto scan = [&](int i, float r, float Z) {  // 2-D scan (:312-330), row i final
-      const int c = i * H + j;
-      const int g = (int)((gmask >> i) & 1ull);
-      ground[c] = (int8_t)g;
-      if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f && r < min_range) {
-        min_range = r;
-        id_min = c;
-      }
-    };
-#pragma unroll
-    for (int u = 0; u < kC; ++u) {
-      const int i = i0 + u;
-      if (i >= V) continue;
-      const int c = i * H + j;
-      float4 q;
-      float r;
-      if (wa[u] >= 0) {
-        const float4 p = pa[u];
-        r = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-        q = make_float4(p.x, p.y, p.z, (float)((double)(float)i + jfrac));
-      } else {
-        r = FLT_MAX;
-        q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
-      }
-      st_nt(&range[c], r);  // streaming stores: the input lines stay in L2 for the gathers
-      st_nt(&cloud[c], q);
-      if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
-        const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
-        if (ground_pair(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ), P.mount)) gmask |= (3ull << (i - 1));
-      }
-      if (i >= 1) scan(i - 1, prev_r, prev.z);
-      prev = q;
-      prev_r = r;
-    }
-    if (i0 + kC >= V) {  // the column's last chunk
-      scan(V - 1, prev_r, prev.z);
-      B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < kC; ++u) {
-      wa[u] = wb[u];
-      pa[u] = pb[u];
-    }
-  }
-#else
   for (int j = tid; j < H; j += nt) {
     unsigned long long gmask = 0ull;
     float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -505,7 +425,6 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
     scan(V - 1, prev_r, prev.z);
     B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
   }
-#endif
   PROF_ADD(23, t_p3);
   if (tid == 0) {  // findStartEndAngle (:234-249)
     for (int w = 1; w < (nt >> 6); ++w) {
