@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (rank 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-reps", type=int, default=20,
-                    help="back-to-back k_project + k_fa_prep pairs timed for the roofline")
+                    help="back-to-back k_project + k_fa_prep4 pairs timed for the roofline")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the all-cores CPU variant (one sequence per thread; the box's CPU share)")
     ap.add_argument("--threads", type=int, default=16, help="host threads for input generation")
@@ -268,7 +268,7 @@ def main():
             m_last = batch.counts()[:, 0].astype(np.float64)  # segmented-cloud sizes M of the last step
     stage /= K
     batch.set_timing(False)
-    # the roofline pair (k_project + k_fa_prep) launched back to back on the last step's inputs: the
+    # the roofline pair (k_project + k_fa_prep4) launched back to back on the last step's inputs: the
     # kernels' own durations, without the per-stage event gaps (which stages_ms keeps)
     k_last = W + K - 1
     k_alt = k_last - 1 if k_last > 0 else k_last  # alternate inputs: no launch re-reads its predecessor's
@@ -281,20 +281,20 @@ def main():
     #   smoothness  B_smooth = 22 M         (read range + colInd; write curvature, picked, label, sort key/index)
     b_proj = S * (16.0 * n_mean + 20.0 * cap)
     b_smooth = 22.0 * float(m_last.sum())
-    t_ms = pair_ms  # k_project + k_fa_prep
+    t_ms = pair_ms  # k_project + k_fa_prep4
     achieved = (b_proj + b_smooth) / (t_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args, S, ("k_project", "k_fa_prep"))
-    roofline = {"kernel": "k_project+k_fa_prep (projection+smoothness)", "bound": "hbm",
+    traffic, traffic_src = pmc_traffic(args, S, ("k_project", "k_fa_prep4"))
+    roofline = {"kernel": "k_project+k_fa_prep4 (projection+smoothness)", "bound": "hbm",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "bytes_per_launch": int(b_proj + b_smooth), "launch_ms": round(t_ms, 4),
-                "launch_ms_source": "%d back-to-back k_project + k_fa_prep pairs between two hipEvents on the "
+                "launch_ms_source": "%d back-to-back k_project + k_fa_prep4 pairs between two hipEvents on the "
                                     "launch stream (projection inputs alternating between the last two steps')"
                                     % args.roofline_reps,
                 "launch_ms_stage_events": round(stage[0] + stage[2], 4),
                 "per_kernel": {"k_project": {"bytes": int(b_proj), "ms": round(stage[0], 4),
                                              "GBps": round(b_proj / (stage[0] * 1e-3) / 1e9, 1)},
-                               "k_fa_prep": {"bytes": int(b_smooth), "ms": round(stage[2], 4),
+                               "k_fa_prep4": {"bytes": int(b_smooth), "ms": round(stage[2], 4),
                                              "GBps": round(b_smooth / (stage[2] * 1e-3) / 1e9, 1)}},
                 "traffic_source": traffic_src,
                 "note": ("%d scans per launch: working set below the 256 MiB Infinity Cache (cache-assisted)" % S

@@ -1168,13 +1168,19 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
   *(int32_t*)hin = n;
   float4* hp = hin + 1;
   const char* base = (const char*)points;
-  for (int i = 0; i < n; ++i) {
-    float4 q;
-    memcpy(&q.x, base + (size_t)i * step + ox, 4);
-    memcpy(&q.y, base + (size_t)i * step + oy, 4);
-    memcpy(&q.z, base + (size_t)i * step + oz, 4);
-    q.w = 0.f;
-    hp[i] = q;
+  if (ox == 0 && oy == 4 && oz == 8 && step == 16) {  // x, y, z, intensity records: the payload as it is
+    if (n > 0) memcpy(hp, base, (size_t)n * 16);       // (the 4th word is never read by the kernels)
+  } else if (ox == 0 && oy == 4 && oz == 8) {  // padded records (PointXYZIR's 32 bytes): 16 bytes each
+    for (int i = 0; i < n; ++i) memcpy(&hp[i], base + (size_t)i * step, 16);
+  } else {
+    for (int i = 0; i < n; ++i) {
+      float4 q;
+      memcpy(&q.x, base + (size_t)i * step + ox, 4);
+      memcpy(&q.y, base + (size_t)i * step + oy, 4);
+      memcpy(&q.z, base + (size_t)i * step + oz, 4);
+      q.w = 0.f;
+      hp[i] = q;
+    }
   }
   if (n > c->cap) {
     hipStreamSynchronize(nullptr);  // the previous call's kernels may still read d_in (they do not: every

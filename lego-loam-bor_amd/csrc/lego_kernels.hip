@@ -1440,10 +1440,9 @@ __global__ __launch_bounds__(1024) void k_sw_finish(LgParams P, LgBufs B, int ti
 // outside [5, M-5) keep their stale value OR the marks, as there).  adjustDistortion and
 // adjustOutlierCloud run in k_segment's epilogue, on the cloud it has just compacted; kDistort
 // runs them here instead, for a ProjectionOut uploaded from the host (lego_feature_association_from).
-// kNT threads a workgroup, FP_TILE = kNT * FP_U positions a tile.  The device-resident path
-// (!kDistort) runs one tile per workgroup, grid (scans, tiles of V*H): ~8 workgroups a scan keep
-// enough loads in flight to stream at HBM rate; kDistort (whole-scan block minimum) loops over the
-// tiles of its scan in one workgroup.
+// kNT threads a workgroup, FP_TILE = kNT * FP_U positions a tile.  The device-resident path runs
+// k_fa_prep4 below (one tile per workgroup, four positions a lane); this template serves kDistort
+// (whole-scan block minimum, looping over the tiles of its scan in one workgroup).
 #define FP_HALO 8
 template <bool kDistort, int kNT>
 __global__ __launch_bounds__(kNT) void k_fa_prep(LgParams P, LgBufs B) {
@@ -1549,6 +1548,141 @@ __global__ __launch_bounds__(kNT) void k_fa_prep(LgParams P, LgBufs B) {
     }
     __syncthreads();
     PROF_ADD(35, t_f3);
+  }
+}
+
+// The device-resident k_fa_prep with four consecutive positions a lane: 16-byte loads of range /
+// column into LDS, the occlusion marks of four positions from one window, the smoothness of four
+// positions from five 16-byte LDS reads, and 16-byte (curvature, sort keys) / 4-byte (picked, label)
+// stores where all four positions lie in [5, M - 5).  Same arithmetic, same order as k_fa_prep.
+// Positions at or beyond M load as 0 (buffer range): no output reads them (marks need i < M - 6,
+// the smoothness k + 5 < M).
+#define FP4_NT 256
+#define FP4_TILE (FP4_NT * 8)
+__global__ __launch_bounds__(FP4_NT) void k_fa_prep4(LgParams P, LgBufs B) {
+  __shared__ __attribute__((aligned(16))) float sr[FP4_TILE + 2 * FP_HALO];
+  __shared__ __attribute__((aligned(16))) uint32_t sc[FP4_TILE + 2 * FP_HALO];
+  __shared__ __attribute__((aligned(16))) uint8_t sf[FP4_TILE + 2 * FP_HALO];
+  const int s = P.s0 + blockIdx.x, tid = threadIdx.x;
+  const int VH = P.VH;
+  const int32_t* cnt = B.counts + (size_t)s * CNT_N;
+  const int M = cnt[CNT_M];
+  const float* __restrict__ r = B.seg_range + (size_t)s * VH;
+  const uint32_t* __restrict__ col = B.seg_col + (size_t)s * VH;
+  float* __restrict__ curv = B.curv + (size_t)s * VH;
+  uint8_t* __restrict__ picked = B.picked + (size_t)s * VH;
+  int8_t* __restrict__ flabel = B.flabel + (size_t)s * VH;
+  int2* __restrict__ smooth = B.smooth + (size_t)s * VH;
+  // k_extract's first pass may move the stale slot 4 while other rings check where it points
+  if (tid == 0 && blockIdx.y == 0) B.fp_sync[2 * s] = smooth[4].y;
+  const int t0 = blockIdx.y * FP4_TILE;
+  if (t0 >= M) return;
+  {  // range / column of [t0 - FP_HALO, t0 + FP4_TILE + FP_HALO) into LDS
+    const __amdgpu_buffer_rsrc_t rr = buffer_rsrc(r, (uint32_t)M * 4u), rc = buffer_rsrc(col, (uint32_t)M * 4u);
+    float4 rv[2];
+    float4 cv[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const uint32_t off = (uint32_t)(t0 + 4 * (tid + g * FP4_NT)) * 4u;
+      rv[g] = buffer_load_f4(rr, off);
+      cv[g] = buffer_load_f4(rc, off);
+    }
+    float rh = 0.f;
+    uint32_t ch = 0u;
+    const int xh = tid < FP_HALO ? tid : FP4_TILE + tid;  // halo slot of this lane (tid < 2 * FP_HALO)
+    if (tid < 2 * FP_HALO) {
+      const int q = min(max(t0 - FP_HALO + xh, 0), M - 1);
+      rh = r[q];
+      ch = col[q];
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int x = FP_HALO + 4 * (tid + g * FP4_NT);
+      *(float4*)&sr[x] = rv[g];
+      *(float4*)&sc[x] = cv[g];
+    }
+    if (tid < 2 * FP_HALO) { sr[xh] = rh; sc[xh] = ch; }
+  }
+  __syncthreads();
+  // markOccludedPoints' per-i conditions (as k_fa_prep) for i in [t0 - 6, t0 + FP4_TILE + 6)
+  auto mark = [&](int x) -> uint32_t {
+    const int i = t0 - FP_HALO + x;
+    uint32_t f = 0;
+    if (i >= 5 && i < M - 6) {
+      const float depth1 = sr[x], depth2 = sr[x + 1];
+      const int columnDiff = abs((int)(sc[x + 1] - sc[x]));
+      if (columnDiff < 10) {
+        if ((double)(depth1 - depth2) > 0.3) f |= 1;
+        else if ((double)(depth2 - depth1) > 0.3) f |= 2;
+      }
+      const float diff1 = fabsf(sr[x - 1] - depth1), diff2 = fabsf(sr[x + 1] - depth1);
+      if ((double)diff1 > 0.02 * (double)depth1 && (double)diff2 > 0.02 * (double)depth1) f |= 4;
+    }
+    return f;
+  };
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int x = FP_HALO + 4 * (tid + g * FP4_NT);
+    const uint32_t w = mark(x) | (mark(x + 1) << 8) | (mark(x + 2) << 16) | (mark(x + 3) << 24);
+    *(uint32_t*)&sf[x] = w;
+  }
+  if (tid < 12) {  // the halo marks: x in [2, FP_HALO) and [FP_HALO + FP4_TILE, FP_HALO + FP4_TILE + 6)
+    const int x = tid < 6 ? 2 + tid : FP_HALO + FP4_TILE + (tid - 6);
+    sf[x] = (uint8_t)mark(x);
+  }
+  __syncthreads();
+  // calculateSmoothness (:200-223) + the marks landing on each k, four positions a lane
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int x = FP_HALO + 4 * (tid + g * FP4_NT);
+    const int k0 = t0 + 4 * (tid + g * FP4_NT);
+    if (k0 > M) break;
+    float w[20];  // sr[x - 8, x + 12)
+    uint8_t m[20];  // sf[x - 8, x + 12)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const float4 v = *(const float4*)&sr[x - 8 + 4 * q];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      const uint32_t f = *(const uint32_t*)&sf[x - 8 + 4 * q];
+      m[4 * q] = f & 255; m[4 * q + 1] = (f >> 8) & 255; m[4 * q + 2] = (f >> 16) & 255; m[4 * q + 3] = f >> 24;
+    }
+    float cvs[4];
+    bool mks[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = 8 + e;  // w[c] = sr[x + e]
+      bool mk = (m[c] & 4) != 0;
+#pragma unroll
+      for (int d = 0; d <= 5; ++d) mk |= (m[c + d] & 1) != 0;   // A(k + d) marks k
+#pragma unroll
+      for (int d = 1; d <= 6; ++d) mk |= (m[c - d] & 2) != 0;   // B(k - d) marks k
+      mks[e] = mk;
+      const float dd = w[c - 5] + w[c - 4] + w[c - 3] + w[c - 2] + w[c - 1] - w[c] * 10 + w[c + 1] + w[c + 2] +
+                       w[c + 3] + w[c + 4] + w[c + 5];
+      cvs[e] = dd * dd;
+    }
+    if (k0 >= 5 && k0 + 3 < M - 5) {  // all four interior: vector stores
+      *(float4*)&curv[k0] = make_float4(cvs[0], cvs[1], cvs[2], cvs[3]);
+      *(uint32_t*)&picked[k0] = (uint32_t)mks[0] | ((uint32_t)mks[1] << 8) | ((uint32_t)mks[2] << 16) |
+                                ((uint32_t)mks[3] << 24);
+      *(uint32_t*)&flabel[k0] = 0u;
+      *(int4*)&smooth[k0] = make_int4(__float_as_int(cvs[0]), k0, __float_as_int(cvs[1]), k0 + 1);
+      *(int4*)&smooth[k0 + 2] = make_int4(__float_as_int(cvs[2]), k0 + 2, __float_as_int(cvs[3]), k0 + 3);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = k0 + e;
+        if (k > M) break;
+        if (k >= 5 && k < M - 5) {
+          curv[k] = cvs[e];
+          picked[k] = mks[e] ? 1 : 0;
+          flabel[k] = 0;
+          smooth[k] = make_int2(__float_as_int(cvs[e]), k);
+        } else if (mks[e]) {
+          picked[k] = 1;
+        }
+      }
+    }
   }
 }
 
@@ -4113,8 +4247,8 @@ int lg_launch_fa_prep(const LgParams& P, const LgBufs& B, int S, hipStream_t st,
   if (distort) {
     hipLaunchKernelGGL((k_fa_prep<true, 1024>), dim3(S), dim3(1024), 0, st, P, B);
   } else {
-    const int tiles = (P.VH + 256 * FP_U - 1) / (256 * FP_U);
-    hipLaunchKernelGGL((k_fa_prep<false, 256>), dim3(S, tiles), dim3(256), 0, st, P, B);
+    const int tiles = (P.VH + FP4_TILE - 1) / FP4_TILE;
+    hipLaunchKernelGGL(k_fa_prep4, dim3(S, tiles), dim3(FP4_NT), 0, st, P, B);
   }
   LG_CHECK_LAUNCH();
   return LEGO_OK;
