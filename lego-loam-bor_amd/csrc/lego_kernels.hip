@@ -457,8 +457,12 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
 // resets every cell it reads); the first / last finite point go to proj_mm by atomicMin / Max.  The
 // image is column-major (cell (i, j) at j * V + i): one firing's lasers are consecutive points and
 // land in consecutive words, so a wave's atomics touch a few cache lines instead of one per lane.
+// kNB batches of 8 points a lane per workgroup: 4 when many scans are in flight (fewer, longer
+// workgroups stream the input with the next batch's loads in flight), 1 for few scans (more
+// workgroups a scan).
 #define PW_NT 256
-#define PW_PTS (PW_NT * 8)
+#define PW_PTS (PW_NT * 8)  // points a batch
+template <int kNB>
 __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                       const int64_t* __restrict__ offs,
                                                       const int32_t* __restrict__ cnts) {
@@ -466,37 +470,47 @@ __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, cons
   const int s = P.s0 + blockIdx.y, tid = threadIdx.x;
   const int V = P.V, H = P.H;
   const int n = cnts[s];
-  const int i0 = blockIdx.x * PW_PTS;
-  if (i0 >= n) return;
+  const int c0 = blockIdx.x * PW_PTS * kNB;
+  if (c0 >= n) return;
   int* winner = B.winner + (size_t)s * P.VH;
   const float4* in = pts + offs[s];
   const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
   int* queue = queue_all + wave_id() * PQ_CAP;
   int qn = 0;
   int fmin = 0x7fffffff, fmax = -1;
-  constexpr int kU = PW_PTS / PW_NT;
+  constexpr int kU = 8;
+  // the batches' loads double-buffered: batch b + 1's go out before batch b is processed
   float3 pk[kU];
 #pragma unroll
-  for (int u = 0; u < kU; ++u) pk[u] = buffer_load_f3(rin, (uint32_t)(i0 + u * PW_NT + tid) * 16u);
+  for (int u = 0; u < kU; ++u) pk[u] = buffer_load_f3(rin, (uint32_t)(c0 + u * PW_NT + tid) * 16u);
+  for (int b = 0; b < kNB; ++b) {
+    const int i0 = c0 + b * kU * PW_NT;
+    if (i0 >= n) break;
+    float3 nx[kU];
 #pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    const int i = i0 + u * PW_NT + tid;
-    const float4 p = make_float4(pk[u].x, pk[u].y, pk[u].z, 0.f);
-    int c = -1;
-    if (i < n && isfinite_f(p.x) && isfinite_f(p.y) && isfinite_f(p.z)) {  // removeNaNFromPointCloud
-      fmin = min(fmin, i);
-      fmax = max(fmax, i);
-      c = P.fast_proj ? proj_cell_fast<true>(P, p)
-                      : cell_cm(proj_cell_exact_ni(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, p), V, H);
-      if (c >= 0) atomicMax(&winner[c], i);
+    for (int u = 0; u < kU; ++u) nx[u] = buffer_load_f3(rin, (uint32_t)(i0 + (kU + u) * PW_NT + tid) * 16u);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * PW_NT + tid;
+      const float4 p = make_float4(pk[u].x, pk[u].y, pk[u].z, 0.f);
+      int c = -1;
+      if (i < n && isfinite_f(p.x) && isfinite_f(p.y) && isfinite_f(p.z)) {  // removeNaNFromPointCloud
+        fmin = min(fmin, i);
+        fmax = max(fmax, i);
+        c = P.fast_proj ? proj_cell_fast<true>(P, p)
+                        : cell_cm(proj_cell_exact_ni(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, p), V, H);
+        if (c >= 0) atomicMax(&winner[c], i);
+      }
+      const unsigned long long amb = __ballot(c == -2);
+      if (c == -2) queue[qn + popc_below(amb)] = i;
+      qn += __popcll(amb);
+      if (qn >= 64) {
+        proj_drain_cm(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue + qn - 64, winner);
+        qn -= 64;
+      }
     }
-    const unsigned long long amb = __ballot(c == -2);
-    if (c == -2) queue[qn + popc_below(amb)] = i;
-    qn += __popcll(amb);
-    if (qn >= 64) {
-      proj_drain_cm(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue + qn - 64, winner);
-      qn -= 64;
-    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) pk[u] = nx[u];
   }
   if (qn > 0) {
     if (lane_id() >= qn) queue[lane_id()] = queue[0];
@@ -513,7 +527,7 @@ __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, cons
 // k_pw_columns: grid (column blocks of PW_NT, scans), one lane per column: the column pass of
 // k_project over the scan's winner image in HBM (each cell read once, then reset to -1), plus
 // labelComponents' initial state for k_sw_*: parent = cell (eligible: not ground, has a return) or
-// -1, component size / row mask 0.  Block (0, s) settles findStartEndAngle from proj_mm.
+// -1, component size / row mask 0 (eligible cells only: no other cell becomes a root).  Block (0, s) settles findStartEndAngle from proj_mm.
 #define PC_NT 128  // columns a workgroup
 __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                       const int64_t* __restrict__ offs,
@@ -567,9 +581,12 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
       const int c = i * H + j;
       const int g = (int)((gmask >> i) & 1ull);
       ground[c] = (int8_t)g;
-      parent[c] = (g != 1 && r != FLT_MAX) ? c : -1;  // _label_mat == 0 (:293-300)
-      ccnt[c] = 0;
-      cmsk[c] = 0ull;
+      const bool elig = g != 1 && r != FLT_MAX;
+      parent[c] = elig ? c : -1;  // _label_mat == 0 (:293-300)
+      if (elig) {  // only roots (eligible cells) ever have their size / row mask read (k_sw_*)
+        ccnt[c] = 0;
+        cmsk[c] = 0ull;
+      }
       if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f && r < min_range) {
         min_range = r;
         id_min = c;
@@ -1224,13 +1241,24 @@ __global__ __launch_bounds__(SW_NT) void k_sw_roots(LgParams P, LgBufs B) {
       r = uf_find(parent, c);  // no hooks any more: plain (L1-cached) reads see valid ancestors
       parent[c] = r;
     }
-    // one atomic per distinct root of the wave (neighbouring cells mostly share a component)
+    // one atomic per distinct root of the wave (neighbouring cells mostly share a component).  The
+    // wave's 64 consecutive cells lie in at most two rows (H >= 64): the non-seed row mask of a root
+    // is two ballots.
     unsigned long long todo = __ballot(r >= 0);
+    const int rowA = __shfl(c, 0) / H;  // (c of lane 0 is the wave's first cell)
+    const bool inA = c / H == rowA;
     while (todo) {
       const int r0 = __shfl(r, __ffsll((long long)todo) - 1);
       const unsigned long long m = __ballot(r == r0);
-      unsigned long long rows = (r == r0 && c != r0) ? (1ull << (c / H)) : 0ull;
-      for (int o = 32; o > 0; o >>= 1) rows |= shfl64(rows, lane ^ o);
+      unsigned long long rows;
+      if (H >= 64) {
+        const unsigned long long ns = __ballot(r == r0 && c != r0);
+        const unsigned long long na = ns & __ballot(inA);
+        rows = (na ? (1ull << rowA) : 0ull) | ((ns & ~na) ? (1ull << (rowA + 1)) : 0ull);
+      } else {
+        rows = (r == r0 && c != r0) ? (1ull << (c / H)) : 0ull;
+        for (int o = 32; o > 0; o >>= 1) rows |= shfl64(rows, lane ^ o);
+      }
       if (lane == __ffsll((long long)m) - 1) {
         atomicAdd(&ccnt[r0], __popcll(m));
         if (rows) atomicOr(&cmsk[r0], rows);
@@ -4206,8 +4234,12 @@ bool lg_lds_segment(const LgParams& P) { return P.V <= 16 && P.VH < 32768; }  //
 int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
                       const int32_t* cnts, hipStream_t st) {
   if (P.wide) {
-    hipLaunchKernelGGL(k_pw_scatter, dim3((P.max_points + PW_PTS - 1) / PW_PTS, S), dim3(PW_NT), 0, st, P, B, pts,
-                       offs, cnts);
+    if (S >= 64)
+      hipLaunchKernelGGL(k_pw_scatter<4>, dim3((P.max_points + 4 * PW_PTS - 1) / (4 * PW_PTS), S), dim3(PW_NT), 0, st,
+                         P, B, pts, offs, cnts);
+    else
+      hipLaunchKernelGGL(k_pw_scatter<1>, dim3((P.max_points + PW_PTS - 1) / PW_PTS, S), dim3(PW_NT), 0, st, P, B,
+                         pts, offs, cnts);
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_pw_columns, dim3((P.H + PC_NT - 1) / PC_NT, S), dim3(PC_NT), 0, st, P, B, pts, offs, cnts);
   } else {  // !wide implies the LDS images fit (lego_batch_set_wide)

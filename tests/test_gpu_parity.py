@@ -468,6 +468,35 @@ def test_hbm_stage_timing_leaves_results(gpu, wide):
     b.close()
 
 
+def test_pointcloud2_layouts(gpu):
+    """lego_cloud_handler's fromROSMsg gather: x,y,z,i records (step 16, copied as they are), padded
+    PointXYZIR-like records (step 32, 16 bytes a point) and a permuted layout (step 24, x,y,z at
+    8,12,16) give the same ProjectionOut, equal to the oracle's."""
+    import ctypes as C
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    pts = np.ascontiguousarray(A.synth_scan(cfg, 3, 1), dtype=np.float32)
+    n = pts.shape[0]
+    rec32 = np.zeros((n, 8), np.float32)
+    rec32[:, :4] = pts
+    rec32[:, 5] = 7.0  # ring / padding words the gather must skip
+    rec24 = np.zeros((n, 6), np.float32)
+    rec24[:, 0] = -1.0
+    rec24[:, 1] = pts[:, 3]
+    rec24[:, 2:5] = pts[:, :3]
+    outs = []
+    for buf, step, off in ((pts, 16, (0, 4, 8)), (rec32, 32, (0, 4, 8)), (rec24, 24, (8, 12, 16))):
+        fe = L.Frontend(params)
+        po = A.LegoProjectionOut()
+        rc = L.lib().lego_cloud_handler(fe.h, buf.ctypes.data, n, step, off[0], off[1], off[2], C.byref(po))
+        assert rc == 0
+        outs.append(A.projection_to_dict(po, params.num_vertical_scans, params.num_horizontal_scans))
+        fe.close()
+    pr = oracle_for(params).cloud_handler(pts)
+    for pg in outs:
+        assert not Hs.diff_report(Hs.PROJ_KEYS, pg, pr)
+
+
 def test_edge_inputs(gpu):
     """Empty / all-NaN clouds fail like the oracle; sparse, tiny, colliding and out-of-FOV clouds match."""
     params = L.params_vlp16()
