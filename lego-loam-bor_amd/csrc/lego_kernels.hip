@@ -1334,45 +1334,50 @@ LG_DEVICE int4 sw_tile_base(const LgBufs& B, int s, int4* sh) {
   return *sh;
 }
 
-// Workgroup-wide exclusive scan of up to three predicates over the tile's cells in raster order
-// (cell cb + u * SW_NT + tid, u = 0..3: the waves own contiguous 64-cell chunks per u).
-LG_DEVICE int sw_tile_scan(bool p, int* wt, int& total) {
-  const unsigned long long m = __ballot(p);
-  if (lane_id() == 0) wt[wave_id()] = __popcll(m);
-  __syncthreads();
-  int before = 0;
-  total = 0;
-  for (int w = 0; w < SW_NT / 64; ++w) {
-    const int v = wt[w];
-    if (w < wave_id()) before += v;
-    total += v;
-  }
-  __syncthreads();
-  return before + popc_below(m);
-}
-
 __global__ __launch_bounds__(SW_NT) void k_sw_rank(LgParams P, LgBufs B) {
   __shared__ int4 base;
-  __shared__ int wt[SW_NT / 64];
+  constexpr int NW = SW_NT / 64;
+  __shared__ int wcnt[4 * NW];
   const int s = P.s0 + blockIdx.y, VH = P.VH;
   const int* parent = B.cc_parent + (size_t)s * VH;
   int* ccnt = B.cc_cnt + (size_t)s * VH;
   const unsigned long long* cmsk = B.cc_mask + (size_t)s * VH;
-  int k = sw_tile_base(B, s, &base).x;
+  const int k0 = sw_tile_base(B, s, &base).x;
+  // the four rounds' loads in flight together, one barrier for the raster-order ranks
+  int c[4];
+  bool root[4], feas[4];
+#pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const int c = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
-    const bool root = c < VH && parent[c] == c;
-    const bool feas = root && sw_feasible(P, ccnt[c], cmsk[c]);
-    int tot;
-    const int o = sw_tile_scan(feas, wt, tot);
-    if (root) ccnt[c] = feas ? k + o + 1 : 999999;  // the root's word now holds its label
+    c[u] = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
+    root[u] = c[u] < VH && parent[c[u]] == c[u];
+  }
+  unsigned long long mf[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    feas[u] = root[u] && sw_feasible(P, ccnt[c[u]], cmsk[c[u]]);
+    mf[u] = __ballot(feas[u]);
+  }
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) wcnt[u * NW + wave_id()] = __popcll(mf[u]);
+  }
+  __syncthreads();
+  int k = k0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    int before = 0, tot = 0;
+    for (int w = 0; w < NW; ++w) {
+      const int v = wcnt[u * NW + w];
+      before += w < wave_id() ? v : 0;
+      tot += v;
+    }
+    if (root[u]) ccnt[c[u]] = feas[u] ? k + before + popc_below(mf[u]) + 1 : 999999;  // the root's word now holds its label
     k += tot;
   }
 }
 
 __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
   __shared__ int4 base;
-  __shared__ int wt[SW_NT / 64];
   const int s = P.s0 + blockIdx.y, V = P.V, H = P.H, VH = P.VH;
   const int* parent = B.cc_parent + (size_t)s * VH;
   const int* clab = B.cc_cnt + (size_t)s * VH;
@@ -1390,42 +1395,76 @@ __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
   int32_t* ring_end = B.ring_end + (size_t)s * V;
   const bool swap_axes = B.fe_state[2 * s + 1] > 0;  // not the initialisation scan (:1414-1416)
   const int4 b0 = sw_tile_base(B, s, &base);
-  int kseg = b0.y, kout = b0.z;
+  // The tile's 4 x SW_NT cells: every load of the four rounds in flight together, then one barrier
+  // for the raster-order offsets of both compactions (wave counts of each round in LDS).
+  __shared__ int wcnt[2 * 4 * (SW_NT / 64)];
+  int c[4], r[4], g[4], lab[4];
+#pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const int c = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
-    const bool in = c < VH;
-    int lab = -1, g = 0;
-    if (in) {
-      const int r = parent[c];
-      lab = r < 0 ? -1 : clab[r];
-      g = ground[c];
-      label[c] = lab;
+    c[u] = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
+    r[u] = c[u] < VH ? parent[c[u]] : -1;
+    g[u] = c[u] < VH ? ground[c[u]] : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) lab[u] = r[u] < 0 ? -1 : clab[r[u]];
+  bool pseg[4], pout[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    pseg[u] = pout[u] = false;
+    if (c[u] < VH) {
+      label[c[u]] = lab[u];
+      sw_classify(P, c[u], lab[u], g[u], pseg[u], pout[u]);
     }
-    bool pseg = false, pout = false;
-    if (in) sw_classify(P, c, lab, g, pseg, pout);
-    int tseg, tout;
-    const int oseg = kseg + sw_tile_scan(pseg, wt, tseg);
-    const int oout = kout + sw_tile_scan(pout, wt, tout);
-    if (in) {
-      const int i = c / H, j = c - i * H;
+  }
+  unsigned long long ms[4], mo[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    ms[u] = __ballot(pseg[u]);
+    mo[u] = __ballot(pout[u]);
+  }
+  constexpr int NW = SW_NT / 64;
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      wcnt[u * NW + wave_id()] = __popcll(ms[u]);
+      wcnt[4 * NW + u * NW + wave_id()] = __popcll(mo[u]);
+    }
+  }
+  __syncthreads();
+  int kseg = b0.y, kout = b0.z;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    int bs = 0, ts = 0, bo = 0, to = 0;
+    for (int w = 0; w < NW; ++w) {
+      const int vs = wcnt[u * NW + w], vo = wcnt[4 * NW + u * NW + w];
+      bs += w < wave_id() ? vs : 0;
+      bo += w < wave_id() ? vo : 0;
+      ts += vs;
+      to += vo;
+    }
+    const int oseg = kseg + bs + popc_below(ms[u]), oout = kout + bo + popc_below(mo[u]);
+    if (c[u] < VH) {
+      const int i = c[u] / H, j = c[u] - i * H;
       if (j == 0) {  // oseg = segmented points before this ring
         ring_start[i] = oseg - 1 + 5;
         if (i > 0) ring_end[i - 1] = oseg - 1 - 5;
       }
-      if (pseg) {
-        seg_pts[oseg] = cloud[c];
-        seg_range[oseg] = range[c];
-        seg_col[oseg] = (uint32_t)j;
-        seg_ground[oseg] = (uint8_t)(g == 1);
-      }
-      if (pout) {
-        const float4 p = cloud[c];
-        outlier[oout] = p;
-        outlier_fa[oout] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;  // adjustOutlierCloud (fa.cpp:1273-1283)
+      if (pseg[u] || pout[u]) {
+        const float4 p = cloud[c[u]];
+        if (pseg[u]) {
+          seg_pts[oseg] = p;
+          seg_range[oseg] = range[c[u]];
+          seg_col[oseg] = (uint32_t)j;
+          seg_ground[oseg] = (uint8_t)(g[u] == 1);
+        }
+        if (pout[u]) {
+          outlier[oout] = p;
+          outlier_fa[oout] = swap_axes ? make_float4(p.y, p.z, p.x, p.w) : p;  // adjustOutlierCloud (fa.cpp:1273-1283)
+        }
       }
     }
-    kseg += tseg;
-    kout += tout;
+    kseg += ts;
+    kout += to;
   }
 }
 
