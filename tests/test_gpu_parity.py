@@ -380,6 +380,38 @@ def test_batch_streams_match_oracle(gpu, groups, wide):
     b.close()
 
 
+@pytest.mark.parametrize("kind,S,steps,every", [("vlp16", 64, 3, 1), ("hdl64", 64, 2, 8)])
+def test_wide_many_streams_match_oracle(gpu, kind, S, steps, every):
+    """The wide layout with many scans in flight (k_pw_scatter's multi-batch workgroups, S >= 64;
+    HDL-64E's bench layout) equals independent oracle runs (every `every`-th stream checked)."""
+    import torch
+    params = L.params_vlp16() if kind == "vlp16" else L.params_hdl64()
+    cfg = A.synth_cfg(kind)
+    cap = params.num_vertical_scans * params.num_horizontal_scans
+    seqs = np.repeat(np.arange(S)[None, :] + 120, steps, 0).reshape(-1)
+    scans = np.repeat(np.arange(steps)[:, None], S, 1).reshape(-1)
+    pts, cnt = A.synth_batch(cfg, seqs, scans)
+    d_pts = torch.from_numpy(pts).cuda()
+    offs = torch.from_numpy((np.arange(S * steps, dtype=np.int64) * cap).reshape(steps, S)).cuda()
+    cnts = torch.from_numpy(cnt.reshape(steps, S).astype(np.int32)).cuda()
+    b = L.Batch(params, S, cap)
+    b.set_wide(1)
+    assert b.wide() == 1
+    for k in range(steps):
+        b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), torch.cuda.current_stream().cuda_stream)
+    b.sync()
+    poses, _ = b.poses()
+    for s in range(0, S, every):
+        orc = oracle_for(params)
+        for k in range(steps):
+            pr = orc.cloud_handler(pts[k * S + s, :cnt[k * S + s]])
+            fr = orc.feature_association()
+        pg, fg = b.read(s)
+        assert_scan_parity(steps - 1, pg, pr, fg, fr)
+        np.testing.assert_allclose(poses[s, 6:], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
+    b.close()
+
+
 @pytest.mark.parametrize("groups,lag,alternate,steps", [(1, 1, False, 6), (3, 1, False, 6), (3, 0, False, 6),
                                                         (2, 1, True, 6), (1, 0, True, 6), (1, 1, False, 2),
                                                         (2, 1, False, 2)])
