@@ -292,6 +292,7 @@ def main():
                                     "launch stream (projection inputs alternating between the last two steps')"
                                     % args.roofline_reps,
                 "launch_ms_stage_events": round(stage[0] + stage[2], 4),
+                "frac_stage_events": round((b_proj + b_smooth) / ((stage[0] + stage[2]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "per_kernel": {"k_project": {"bytes": int(b_proj), "ms": round(stage[0], 4),
                                              "GBps": round(b_proj / (stage[0] * 1e-3) / 1e9, 1)},
                                "k_fa_prep4": {"bytes": int(b_smooth), "ms": round(stage[2], 4),
