@@ -320,7 +320,7 @@ def main():
         "trajectories_gathered": int(traj_all.shape[0]),
         "input_gen_s": round(t_gen, 2),
     }
-    if rank == 0 and not args.no_cpu_baseline:  # the reference's own VoxelGrid order (std::sort)
+    if world == 1 and not args.no_cpu_baseline:  # N = 1 only; the reference's own VoxelGrid order (std::sort)
         params_ref = (L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64)(voxel_tie_order=0)
         out["cpu_baseline"] = cpu_baseline(params_ref, cfg, host_pts, host_cnt, args.cpu_seconds)
         out["speedup_vs_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
