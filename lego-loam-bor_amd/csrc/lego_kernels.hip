@@ -1625,7 +1625,10 @@ __global__ __launch_bounds__(kNT) void k_fa_prep(LgParams P, LgBufs B) {
 // Positions at or beyond M load as 0 (buffer range): no output reads them (marks need i < M - 6,
 // the smoothness k + 5 < M).
 #define FP4_NT 256
-#define FP4_TILE (FP4_NT * 8)
+#ifndef FP4_G
+#define FP4_G 2  // groups of four positions a lane
+#endif
+#define FP4_TILE (FP4_NT * 4 * FP4_G)
 __global__ __launch_bounds__(FP4_NT) void k_fa_prep4(LgParams P, LgBufs B) {
   __shared__ __attribute__((aligned(16))) float sr[FP4_TILE + 2 * FP_HALO];
   __shared__ __attribute__((aligned(16))) uint32_t sc[FP4_TILE + 2 * FP_HALO];
@@ -1646,10 +1649,10 @@ __global__ __launch_bounds__(FP4_NT) void k_fa_prep4(LgParams P, LgBufs B) {
   if (t0 >= M) return;
   {  // range / column of [t0 - FP_HALO, t0 + FP4_TILE + FP_HALO) into LDS
     const __amdgpu_buffer_rsrc_t rr = buffer_rsrc(r, (uint32_t)M * 4u), rc = buffer_rsrc(col, (uint32_t)M * 4u);
-    float4 rv[2];
-    float4 cv[2];
+    float4 rv[FP4_G];
+    float4 cv[FP4_G];
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < FP4_G; ++g) {
       const uint32_t off = (uint32_t)(t0 + 4 * (tid + g * FP4_NT)) * 4u;
       rv[g] = buffer_load_f4(rr, off);
       cv[g] = buffer_load_f4(rc, off);
@@ -1663,7 +1666,7 @@ __global__ __launch_bounds__(FP4_NT) void k_fa_prep4(LgParams P, LgBufs B) {
       ch = col[q];
     }
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < FP4_G; ++g) {
       const int x = FP_HALO + 4 * (tid + g * FP4_NT);
       *(float4*)&sr[x] = rv[g];
       *(float4*)&sc[x] = cv[g];
@@ -1688,7 +1691,7 @@ __global__ __launch_bounds__(FP4_NT) void k_fa_prep4(LgParams P, LgBufs B) {
     return f;
   };
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < FP4_G; ++g) {
     const int x = FP_HALO + 4 * (tid + g * FP4_NT);
     const uint32_t w = mark(x) | (mark(x + 1) << 8) | (mark(x + 2) << 16) | (mark(x + 3) << 24);
     *(uint32_t*)&sf[x] = w;
@@ -1700,7 +1703,7 @@ __global__ __launch_bounds__(FP4_NT) void k_fa_prep4(LgParams P, LgBufs B) {
   __syncthreads();
   // calculateSmoothness (:200-223) + the marks landing on each k, four positions a lane
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < FP4_G; ++g) {
     const int x = FP_HALO + 4 * (tid + g * FP4_NT);
     const int k0 = t0 + 4 * (tid + g * FP4_NT);
     if (k0 > M) break;
