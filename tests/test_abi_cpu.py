@@ -73,6 +73,16 @@ def test_no_cpu_fallback_without_device():
         L.Frontend(p)
 
 
+def test_null_handles_are_rejected():
+    """Entry points given no object fail with LEGO_EINVAL before touching a device (so also here)."""
+    lib = L.lib()
+    ms = C.c_float()
+    assert lib.lego_batch_time_hbm_stages(None, 4, None, None, None, None, None, None, C.byref(ms)) == A.LEGO_EINVAL
+    assert lib.lego_batch_stage_times(None, C.byref(ms)) == A.LEGO_EINVAL
+    assert lib.lego_cloud_handler(None, None, 0, 16, 0, 4, 8, None) == A.LEGO_EINVAL
+    assert lib.lego_feature_association(None, None) == A.LEGO_EINVAL
+
+
 def test_synth_is_deterministic():
     cfg = A.synth_cfg("vlp16")
     a = A.synth_scan(cfg, 3, 5)
