@@ -2980,10 +2980,14 @@ __global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
 // ============================================================================================
 // k_lm: updateTransformation + integrateTransformation + publishOdometry + publishCloudsLast
 // ============================================================================================
+#ifndef LM_THREADS
 #define LM_THREADS 768
+#endif
 #define GRID_MAX 8191  // grid cells (end offsets share LDS with the staged small cloud)
 #define CGRID_MAX 2047  // grid cells over a staged small cloud
+#ifndef LM_MAXQ
 #define LM_MAXQ 1536  // 24 * 64 rings
+#endif
 
 LG_DEVICE float4 transform_to_start(const float4 pi, const float* cur) {  // :388-418
   float s = 10 * (pi.w - (float)(int)pi.w);
