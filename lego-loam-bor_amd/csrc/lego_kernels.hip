@@ -4375,10 +4375,11 @@ int lg_launch_concat(const LgParams& P, const LgBufs& B, int S, hipStream_t st) 
 }
 
 int lg_launch_lm(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  // VLP-16-sized feature sets (<= 384 queries a loop): 512 threads and 66 KB of LDS leave room on the
-  // CU for the next scan's small front-end kernels (256 VLP-16 streams: k_lm 600 -> 526 us, +6 %
-  // scans/s); larger sensors keep 768 threads and LDS for 1,536 queries
-  if (P.V * std::max(P.cap_sharp, P.cap_flat) <= 384)
+  // VLP-16-sized feature sets (<= 384 queries a loop) with many scans in flight: 512 threads and 66 KB
+  // of LDS leave room on the CU for the next scan's small front-end kernels (256 VLP-16 streams: k_lm
+  // 553 -> 515 us, +4 % scans/s).  Few scans in flight (one scan: 2-3 % lower latency) and larger
+  // sensors keep 768 threads (and LDS for 1,536 queries).
+  if (P.V * std::max(P.cap_sharp, P.cap_flat) <= 384 && S > 8)
     hipLaunchKernelGGL((k_lm<512, 384>), dim3(S), dim3(512), 0, st, P, B);
   else
     hipLaunchKernelGGL((k_lm<768, 1536>), dim3(S), dim3(768), 0, st, P, B);
