@@ -33,7 +33,7 @@ extern "C" {
 #define LEGO_EINVAL     -1   /* bad parameter / shape                                   */
 #define LEGO_ENOMEM     -2   /* host or device allocation failed                         */
 #define LEGO_EDEVICE    -3   /* no HIP device / kernel launch or runtime failure          */
-#define LEGO_ENOTSUP    -4   /* configuration not supported (e.g. fp_mode != 0)           */
+#define LEGO_ENOTSUP    -4   /* configuration / build does not support the request         */
 #define LEGO_EEMPTY     -5   /* empty input cloud (reference: UB in findStartEndAngle)    */
 
 #define LEGO_MAX_POINTS ((1 << 28) - 1)  /* points of one input cloud (larger: LEGO_EINVAL) */
@@ -66,9 +66,12 @@ typedef struct lego_params {
   float   surf_threshold;                  /*                                    :20                */
   float   nearest_feature_search_distance; /* m                                  :21                */
   int32_t mapping_frequency_divider;       /*     mapping/...                    :25                */
-  int32_t fp_mode;                         /* libm overload model: 0 = float
-                                              overloads of unqualified sin/cos/atan2 (only mode
-                                              implemented), 1 = double promotion (LEGO_ENOTSUP)  */
+  int32_t fp_mode;                         /* libm overload model of the reference's unqualified
+                                              sin/cos/tan/atan2/asin/sqrt calls on floats (SURVEY
+                                              App. A.1): 0 = float overloads (libstdc++ >= 6's
+                                              <math.h>: Melodic and later), 1 = ::sin(double) etc.,
+                                              rounded where stored to float (GCC 4.8 / 5: the
+                                              Indigo / Kinetic toolchains of README.md:40)          */
   int32_t voxel_tie_order;                 /* order in which PCL VoxelGrid sums the points of one
                                               voxel (featureAssociation.cpp:377-379): PCL sorts
                                               (voxel, point) pairs with std::sort by voxel only, so
@@ -222,8 +225,13 @@ int  lego_batch_wide(const lego_batch* b);
  * 2 atanf(a), 3 sqrtf(a), 4 a / b.  Lets tests compare gfx950 results with the host's glibc.
  * which = 5 / 6: groundRemoval's pair test atan2f(dZ = a, r = b) <= 10 deg (mount 0) as k_project
  * decides it (polynomial with a margin, glibc-faithful fallback) / by the glibc-faithful path only.
- * which = 7 / 8: sinf(a) / cosf(a) (the LM trig). */
+ * which = 7 / 8: sinf(a) / cosf(a) (the LM trig).  which = 9 / 10: the pair test in fp_mode 1 (va =
+ * (float)atan2(double(dZ), sqrt(double(s2)))), fast + exact / exact only; 11: fp_mode 0 exact only.
+ * (5, 6, 9, 10, 11 take s2 = b * b.) */
 int  lego_test_libm(const float* a, const float* b, float* out, int32_t n, int32_t which);
+/* The device's double libm of fp_mode 1 (lego_libm.h, fdlibm): which = 0 sin(a), 1 cos(a), 2 atan2(a, b),
+ * 3 asin(a), 4 sqrt(a), 5 a / b. */
+int  lego_test_libm_d(const double* a, const double* b, double* out, int32_t n, int32_t which);
 /* Sort (key, val) pairs by key with the device's wave-parallel std::sort emulation (n <= 2048);
  * keys are uint32 (is_float 0) or float bit patterns (1); is_float 2 runs k_extract's segment
  * sort (float keys, n <= 512: register sort when keys are distinct, else the emulation). */

@@ -58,6 +58,8 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int S;                                // streams of the batch (staging stride)
   int wide;                             // wide mode: k_pw_* / k_sw_* (many workgroups a scan)
   int max_points;                       // input capacity per scan (wide scatter grid)
+  int fp1;                              // lego_params.fp_mode == 1: unqualified libm calls in double
+  double sinXd, cosXd, sinYd, cosYd;    // fp_mode 1: sin / cos(double(alpha)) of labelComponents (:463)
 };
 
 struct LgState {  // FeatureAssociation members that persist across scans (featureAssociation.h)

@@ -30,8 +30,9 @@ namespace {
 const double DEG_TO_RAD = M_PI / 180.0;  // utility.h:50
 
 // ImageProjection / FeatureAssociation ctor arithmetic with the reference's types
-// (imageProjection.cpp:57-84, featureAssociation.cpp:69-81); glibc float trig for the
-// labelComponents constants (:414, :463), as the reference evaluates them per call.
+// (imageProjection.cpp:57-84, featureAssociation.cpp:69-81); glibc trig for the labelComponents
+// constants (:414, :463), as the reference evaluates them per call: the float overloads (fp_mode 0)
+// or ::tan / ::sin / ::cos in double (fp_mode 1).
 LgParams derive(const lego_params& p) {
   LgParams P;
   memset(&P, 0, sizeof(P));
@@ -49,7 +50,12 @@ LgParams derive(const lego_params& p) {
   float mount = p.sensor_mount_angle;
   mount *= DEG_TO_RAD;
   P.mount = mount;
-  P.theta_thr = tanf(theta);
+  P.fp1 = p.fp_mode == 1;
+  P.theta_thr = P.fp1 ? (float)tan((double)theta) : tanf(theta);
+  P.sinXd = sin((double)P.ang_res_x);
+  P.cosXd = cos((double)P.ang_res_x);
+  P.sinYd = sin((double)P.ang_res_y);
+  P.cosYd = cos((double)P.ang_res_y);
   P.sinX = sinf(P.ang_res_x);
   P.cosX = cosf(P.ang_res_x);
   P.sinY = sinf(P.ang_res_y);
@@ -278,7 +284,7 @@ void lego_params_hdl64(lego_params* p) {
 
 int lego_params_validate(const lego_params* p) {
   if (!p) return LEGO_EINVAL;
-  if (p->fp_mode != 0) return LEGO_ENOTSUP;
+  if (p->fp_mode != 0 && p->fp_mode != 1) return LEGO_EINVAL;
   if (p->voxel_tie_order != 0 && p->voxel_tie_order != 1) return LEGO_EINVAL;
   if (p->num_vertical_scans < 2 || p->num_vertical_scans > 64) return LEGO_EINVAL;
   if (p->num_horizontal_scans < 16 || p->num_horizontal_scans > 2048) return LEGO_EINVAL;

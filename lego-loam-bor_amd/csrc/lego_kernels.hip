@@ -223,23 +223,27 @@ LG_DEVICE int proj_cell_fast(const LgParams& P, float4 p) {
   return kColMajor ? columnIdn * P.V + r0 : r0 * P.H + columnIdn;
 }
 
-// groundRemoval's test (imageProjection.cpp:276-285): (double)(atan2f(dZ, r) - mount) <= 10 deg, r =
-// |(dX, dY, dZ)| >= |dZ|, so the angle lies in [-pi/4, pi/4].  A polynomial atan (error < 1e-6 rad
-// with the reciprocal) decides every pair farther than 1e-5 rad from the threshold; the rest, and
-// r == 0 or NaN (empty cells), take the glibc-faithful atan2f.
-__attribute__((noinline)) __device__ bool ground_pair_exact(float dZ, float r, float mount) {  // one copy
-  const float va = atan2f_g(dZ, r);
+// groundRemoval's test (imageProjection.cpp:276-285): (double)(va - mount) <= 10 deg with va =
+// std::atan2(dZ, sqrt(s2)), s2 = dX*dX + dY*dY + dZ*dZ in float: atan2f(dZ, sqrtf(s2)) with the float
+// overloads (fp_mode 0); with ::sqrt(double) (fp_mode 1) the std::atan2(float, double) overload
+// promotes, va = (float)atan2(double(dZ), sqrt(double(s2))).  r = sqrt(s2) >= |dZ|, so the angle lies
+// in [-pi/4, pi/4].  A polynomial atan (error < 1e-6 rad with the reciprocal) decides every pair
+// farther than 1e-5 rad from the threshold in both models; the rest, and r == 0 or NaN (empty cells),
+// take the glibc-faithful path of the model.
+__attribute__((noinline)) __device__ bool ground_pair_exact(float dZ, float s2, float mount, int fp1) {  // one copy
+  const float va = fp1 ? (float)atan2_d((double)dZ, sqrt((double)s2)) : atan2f_g(dZ, sqrtf(s2));
   return (double)(va - mount) <= 10 * DEG_TO_RAD_D;
 }
-LG_DEVICE bool ground_pair(float dZ, float r, float mount) {
+LG_DEVICE bool ground_pair(float dZ, float s2, float mount, int fp1) {
   const double thr = 10 * DEG_TO_RAD_D;
+  const float r = sqrtf(s2);
   if (r > 0.f && r < FLT_MAX) {
     float h = atan01_poly(fminf(fabsf(dZ) * __builtin_amdgcn_rcpf(r), 1.f));
     const float d = (dZ < 0.f ? -h : h) - mount;
     if (d < (float)thr - 1e-5f) return true;
     if (d > (float)thr + 1e-5f) return false;
   }
-  return ground_pair_exact(dZ, r, mount);
+  return ground_pair_exact(dZ, s2, mount, fp1);
 }
 
 // ============================================================================================
@@ -415,7 +419,7 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
         st_nt(&cloud[c], q);
         if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
           const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
-          if (ground_pair(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ), P.mount)) gmask |= (3ull << (i - 1));
+          if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) gmask |= (3ull << (i - 1));
         }
         if (i >= 1) scan(i - 1, prev_r, prev.z);
         prev = q;
@@ -618,7 +622,7 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
         st_nt(&cloud[c], q);
         if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
           const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
-          if (ground_pair(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ), P.mount)) gmask |= (3ull << (i - 1));
+          if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) gmask |= (3ull << (i - 1));
         }
         if (i >= 1) settle(i - 1, prev_r, prev.z);
         prev = q;
@@ -660,11 +664,21 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
 // member shares it (:469).  Reproduced with lock-free union-find (hook larger root onto smaller:
 // the root is the component minimum = the seed), per-root size and non-seed row mask, and a
 // raster-order block scan over feasible roots.
-LG_DEVICE bool seg_edge(float ra, float rb, float sA, float cA, float thr) {
+// labelComponents' edge test (imageProjection.cpp:457-465) between cells of ranges ra, rb; horiz:
+// alpha = _ang_resolution_X (same row), else _ang_resolution_Y.  tang = d2 * sin(alpha) / (d1 - d2 *
+// cos(alpha)) in float (fp_mode 0) or in double, rounded to the float tang (fp_mode 1).
+LG_DEVICE bool seg_edge(const LgParams& P, float ra, float rb, bool horiz) {
   float d1 = (ra < rb) ? rb : ra;  // std::max(from, this)
   float d2 = (rb < ra) ? rb : ra;  // std::min(from, this)
-  float tang = (d2 * sA / (d1 - d2 * cA));
-  return tang > thr;
+  float tang;
+  if (P.fp1) {
+    const double sA = horiz ? P.sinXd : P.sinYd, cA = horiz ? P.cosXd : P.cosYd;
+    tang = (float)((double)d2 * sA / ((double)d1 - (double)d2 * cA));
+  } else {
+    const float sA = horiz ? P.sinX : P.sinY, cA = horiz ? P.cosX : P.cosY;
+    tang = (d2 * sA / (d1 - d2 * cA));
+  }
+  return tang > P.theta_thr;
 }
 
 template <typename PT>
@@ -796,7 +810,8 @@ LG_DEVICE void distort_segmented(const LgParams& P, const LgBufs& B, int s, int 
 #pragma unroll
     for (int u = 0; u < FP_U; ++u) pk[u] = seg[min(t0 + u * nt + tid, M - 1)];
 #pragma unroll
-    for (int u = 0; u < FP_U; ++u) ori[u] = -atan2f_g(pk[u].y, pk[u].x);  // point.x = y, point.z = x
+    for (int u = 0; u < FP_U; ++u)  // float ori = -atan2(point.x, point.z): point.x = y, point.z = x (:172)
+      ori[u] = P.fp1 ? (float)(-atan2_d((double)pk[u].y, (double)pk[u].x)) : -atan2f_g(pk[u].y, pk[u].x);
     if (h == 0x7fffffff) {
       int hc = 0x7fffffff;
 #pragma unroll
@@ -872,10 +887,10 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
       const int i = c / H, j = c - i * H;
       const bool e0 = seg_eligible(g0[u], r0[u]);
       // the predicate is symmetric in its two ranges (d1 = max, d2 = min), as the BFS's is
-      const bool eu = e0 && i > 0 && seg_eligible(gu[u], ru[u]) && seg_edge(r0[u], ru[u], P.sinY, P.cosY, P.theta_thr);
+      const bool eu = e0 && i > 0 && seg_eligible(gu[u], ru[u]) && seg_edge(P, r0[u], ru[u], false);
       const bool ew = e0 && j == H - 1 && H > 1 && seg_eligible(gw[u], rw[u]) &&
-                      seg_edge(r0[u], rw[u], P.sinX, P.cosX, P.theta_thr);
-      const bool el = e0 && j > 0 && seg_eligible(gl[u], rl[u]) && seg_edge(r0[u], rl[u], P.sinX, P.cosX, P.theta_thr);
+                      seg_edge(P, r0[u], rw[u], true);
+      const bool el = e0 && j > 0 && seg_eligible(gl[u], rl[u]) && seg_edge(P, r0[u], rl[u], true);
       int p0 = c;
       unsigned rest = 0u;  // bit0 up, bit1 wrap, bit2 left: edges left for pass 2
       if (eu) p0 = c - H;
@@ -1181,9 +1196,9 @@ __global__ __launch_bounds__(SW_NT) void k_sw_local(LgParams P, LgBufs B) {
     int tr = -1;
     if (lc + 1 < SW_TC && j + 1 < H) tr = t + 1;
     else if (wrap_local && j == H - 1) tr = lr * SW_TC;  // (i, H-1) -> (i, 0)
-    if (tr >= 0 && lp[tr] >= 0 && seg_edge(r, lrg[tr], P.sinX, P.cosX, P.theta_thr)) uf_unite(lp, t, tr);
+    if (tr >= 0 && lp[tr] >= 0 && seg_edge(P, r, lrg[tr], true)) uf_unite(lp, t, tr);
     const int td = t + SW_TC;
-    if (lr + 1 < SW_TR && i + 1 < V && lp[td] >= 0 && seg_edge(r, lrg[td], P.sinY, P.cosY, P.theta_thr))
+    if (lr + 1 < SW_TR && i + 1 < V && lp[td] >= 0 && seg_edge(P, r, lrg[td], false))
       uf_unite(lp, t, td);
   }
   __syncthreads();
@@ -1223,7 +1238,7 @@ __global__ __launch_bounds__(SW_NT) void k_sw_bound(LgParams P, LgBufs B) {
   }
   if (c < 0) return;
   if (parent[c] < 0 || parent[cn] < 0) return;
-  if (seg_edge(range[c], range[cn], horiz ? P.sinX : P.sinY, horiz ? P.cosX : P.cosY, P.theta_thr))
+  if (seg_edge(P, range[c], range[cn], horiz))
     sw_unite(parent, c, cn);
 }
 
@@ -2984,7 +2999,13 @@ __global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
 #define GRID_MAX 8191  // grid cells (end offsets share LDS with the staged small cloud)
 #define CGRID_MAX 2047  // grid cells over a staged small cloud
 
+// TransformToStart / TransformToEnd (:388-471) in either libm model (Fp<kF1>, lego_libm.h): the
+// unqualified sin / cos on float angles, the expression evaluated in T = float (fp_mode 0) or double
+// (fp_mode 1) and rounded where the reference stores it to float.
+template <bool kF1>
 LG_DEVICE float4 transform_to_start(const float4 pi, const float* cur) {  // :388-418
+  typedef Fp<kF1> F;
+  typedef typename F::T T;
   float s = 10 * (pi.w - (float)(int)pi.w);
   float ry = s * cur[1];
   float rx = s * cur[0];
@@ -2992,25 +3013,30 @@ LG_DEVICE float4 transform_to_start(const float4 pi, const float* cur) {  // :38
   float tx = s * cur[3];
   float ty = s * cur[4];
   float tz = s * cur[5];
-  const float crz = cosf_g(rz), srz = sinf_g(rz), crx = cosf_g(rx), srx = sinf_g(rx), cry = cosf_g(ry),
-              sry = sinf_g(ry);
-  float x1 = crz * (pi.x - tx) + srz * (pi.y - ty);
-  float y1 = -srz * (pi.x - tx) + crz * (pi.y - ty);
+  const T crz = F::cs(rz), srz = F::sn(rz), crx = F::cs(rx), srx = F::sn(rx), cry = F::cs(ry), sry = F::sn(ry);
+  float x1 = crz * (T)(pi.x - tx) + srz * (T)(pi.y - ty);
+  float y1 = -srz * (T)(pi.x - tx) + crz * (T)(pi.y - ty);
   float z1 = (pi.z - tz);
   float x2 = x1;
-  float y2 = crx * y1 + srx * z1;
-  float z2 = -srx * y1 + crx * z1;
-  return make_float4(cry * x2 - sry * z2, y2, sry * x2 + cry * z2, pi.w);
+  float y2 = crx * (T)y1 + srx * (T)z1;
+  float z2 = -srx * (T)y1 + crx * (T)z1;
+  return make_float4((float)(cry * (T)x2 - sry * (T)z2), y2, (float)(sry * (T)x2 + cry * (T)z2), pi.w);
 }
 
 // cos / sin of transformCur's rotation for TransformToEnd's second half (constant per scan)
+template <bool kF1>
 struct EndTrig {
-  float cx, sx, cy, sy, cz, sz;
+  typename Fp<kF1>::T cx, sx, cy, sy, cz, sz;
 };
-LG_DEVICE EndTrig end_trig(const float* cur) {
-  return EndTrig{cosf_g(cur[0]), sinf_g(cur[0]), cosf_g(cur[1]), sinf_g(cur[1]), cosf_g(cur[2]), sinf_g(cur[2])};
+template <bool kF1>
+LG_DEVICE EndTrig<kF1> end_trig(const float* cur) {
+  typedef Fp<kF1> F;
+  return EndTrig<kF1>{F::cs(cur[0]), F::sn(cur[0]), F::cs(cur[1]), F::sn(cur[1]), F::cs(cur[2]), F::sn(cur[2])};
 }
-LG_DEVICE float4 transform_to_end_t(const float4 pi, const float* cur, const EndTrig& E) {  // :422-471
+template <bool kF1>
+LG_DEVICE float4 transform_to_end_t(const float4 pi, const float* cur, const EndTrig<kF1>& E) {  // :422-471
+  typedef Fp<kF1> F;
+  typedef typename F::T T;
   float s = 10 * (pi.w - (float)(int)pi.w);
   float rx = s * cur[0];
   float ry = s * cur[1];
@@ -3018,66 +3044,28 @@ LG_DEVICE float4 transform_to_end_t(const float4 pi, const float* cur, const End
   float tx = s * cur[3];
   float ty = s * cur[4];
   float tz = s * cur[5];
-  float c, sn;
-  c = cosf_g(rz); sn = sinf_g(rz);
-  float x1 = c * (pi.x - tx) + sn * (pi.y - ty);
-  float y1 = -sn * (pi.x - tx) + c * (pi.y - ty);
+  T c, sn;
+  c = F::cs(rz); sn = F::sn(rz);
+  float x1 = c * (T)(pi.x - tx) + sn * (T)(pi.y - ty);
+  float y1 = -sn * (T)(pi.x - tx) + c * (T)(pi.y - ty);
   float z1 = (pi.z - tz);
-  c = cosf_g(rx); sn = sinf_g(rx);
+  c = F::cs(rx); sn = F::sn(rx);
   float x2 = x1;
-  float y2 = c * y1 + sn * z1;
-  float z2 = -sn * y1 + c * z1;
-  c = cosf_g(ry); sn = sinf_g(ry);
-  float x3 = c * x2 - sn * z2;
+  float y2 = c * (T)y1 + sn * (T)z1;
+  float z2 = -sn * (T)y1 + c * (T)z1;
+  c = F::cs(ry); sn = F::sn(ry);
+  float x3 = c * (T)x2 - sn * (T)z2;
   float y3 = y2;
-  float z3 = sn * x2 + c * z2;
+  float z3 = sn * (T)x2 + c * (T)z2;
   tx = cur[3]; ty = cur[4]; tz = cur[5];
-  float x4 = E.cy * x3 + E.sy * z3;
+  float x4 = E.cy * (T)x3 + E.sy * (T)z3;
   float y4 = y3;
-  float z4 = -E.sy * x3 + E.cy * z3;
+  float z4 = -E.sy * (T)x3 + E.cy * (T)z3;
   float x5 = x4;
-  float y5 = E.cx * y4 - E.sx * z4;
-  float z5 = E.sx * y4 + E.cx * z4;
-  float x6 = E.cz * x5 - E.sz * y5 + tx;
-  float y6 = E.sz * x5 + E.cz * y5 + ty;
-  float z6 = z5 + tz;
-  return make_float4(x6, y6, z6, (float)(int)pi.w);
-}
-
-LG_DEVICE float4 transform_to_end(const float4 pi, const float* cur) {  // :422-471
-  float s = 10 * (pi.w - (float)(int)pi.w);
-  float rx = s * cur[0];
-  float ry = s * cur[1];
-  float rz = s * cur[2];
-  float tx = s * cur[3];
-  float ty = s * cur[4];
-  float tz = s * cur[5];
-  float c, sn;
-  c = cosf_g(rz); sn = sinf_g(rz);
-  float x1 = c * (pi.x - tx) + sn * (pi.y - ty);
-  float y1 = -sn * (pi.x - tx) + c * (pi.y - ty);
-  float z1 = (pi.z - tz);
-  c = cosf_g(rx); sn = sinf_g(rx);
-  float x2 = x1;
-  float y2 = c * y1 + sn * z1;
-  float z2 = -sn * y1 + c * z1;
-  c = cosf_g(ry); sn = sinf_g(ry);
-  float x3 = c * x2 - sn * z2;
-  float y3 = y2;
-  float z3 = sn * x2 + c * z2;
-  rx = cur[0]; ry = cur[1]; rz = cur[2];
-  tx = cur[3]; ty = cur[4]; tz = cur[5];
-  c = cosf_g(ry); sn = sinf_g(ry);
-  float x4 = c * x3 + sn * z3;
-  float y4 = y3;
-  float z4 = -sn * x3 + c * z3;
-  c = cosf_g(rx); sn = sinf_g(rx);
-  float x5 = x4;
-  float y5 = c * y4 - sn * z4;
-  float z5 = sn * y4 + c * z4;
-  c = cosf_g(rz); sn = sinf_g(rz);
-  float x6 = c * x5 - sn * y5 + tx;
-  float y6 = sn * x5 + c * y5 + ty;
+  float y5 = E.cx * (T)y4 - E.sx * (T)z4;
+  float z5 = E.sx * (T)y4 + E.cx * (T)z4;
+  float x6 = E.cz * (T)x5 - E.sz * (T)y5 + (T)tx;
+  float y6 = E.sz * (T)x5 + E.cz * (T)y5 + (T)ty;
   float z6 = z5 + tz;
   return make_float4(x6, y6, z6, (float)(int)pi.w);
 }
@@ -3682,10 +3670,12 @@ LG_DEVICE bool lm_solve_reg(float* cur, int& is_degenerate, int& status, const d
 struct LmTrig {
   float srx, crx, sry, cry, srz, crz, tx, ty, tz;
 };
-LG_DEVICE LmTrig lm_trig(const float* cur) {
+template <bool kF1>
+LG_DEVICE LmTrig lm_trig(const float* cur) {  // float srx = sin(transformCur[0]) (:797-802, :939-944)
+  typedef Fp<kF1> F;
   LmTrig t;
-  t.srx = sinf_g(cur[0]); t.crx = cosf_g(cur[0]); t.sry = sinf_g(cur[1]); t.cry = cosf_g(cur[1]);
-  t.srz = sinf_g(cur[2]); t.crz = cosf_g(cur[2]);
+  t.srx = (float)F::sn(cur[0]); t.crx = (float)F::cs(cur[0]); t.sry = (float)F::sn(cur[1]);
+  t.cry = (float)F::cs(cur[1]); t.srz = (float)F::sn(cur[2]); t.crz = (float)F::cs(cur[2]);
   t.tx = cur[3]; t.ty = cur[4]; t.tz = cur[5];
   return t;
 }
@@ -3767,12 +3757,15 @@ LG_DEVICE float4 surf_plane(const float4* last, int i1, int i2, int i3) {
   pa /= ps; pb /= ps; pc /= ps; pd /= ps;
   return make_float4(pa, pb, pc, pd);
 }
+template <bool kF1>
 LG_DEVICE bool surf_coeff_pl(const float4 pl, float4 sel, int iter, float4& cf) {
+  typedef Fp<kF1> F;
+  typedef typename F::T T;
   const float pa = pl.x, pb = pl.y, pc = pl.z, pd = pl.w;
   float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
   float s = 1;
-  if (iter >= 5)
-    s = (float)(1 - 1.8 * (double)fabsf(pd2) / (double)sqrtf(sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
+  if (iter >= 5)  // :761: sqrt(sqrt(float sum)) in T
+    s = (float)(1 - 1.8 * (double)fabsf(pd2) / (double)F::sq(F::sq((T)(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
   if ((double)s > 0.1 && pd2 != 0) {
     cf = make_float4(s * pa, s * pb, s * pc, s * pd2);
     return true;
@@ -3894,7 +3887,7 @@ LG_DEVICE int lds_nn(const float4* last, int nl, float4 q, float r2, bool& tie, 
 // with the updated transform, so wave 0 runs each block of up to 5 iterations on its own
 // (coefficients, a butterfly reduction that leaves the normal equations in every lane, the 3x3 solve
 // in registers) and the workgroup meets once per block instead of three times per iteration.
-template <class Lds>
+template <bool kF1, class Lds>
 LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __restrict__ feat, int nq,
                        const float4* __restrict__ last_g, int nl, bool surf, float4* gp, int& iters) {
   const int tid = threadIdx.x;
@@ -3920,7 +3913,7 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
       float cur[6];
       for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
       PROF_T(t_sel0);
-      for (int q = tid; q < nq; q += (int)blockDim.x) L.sel[q] = transform_to_start(L.featl[q], cur);
+      for (int q = tid; q < nq; q += (int)blockDim.x) L.sel[q] = transform_to_start<kF1>(L.featl[q], cur);
       __syncthreads();
       PROF_ADD(8, t_sel0);
       PROF_T(t_srch0);
@@ -4040,13 +4033,13 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
       bool keep = true;
       for (; it < iter + 5 && it < 25; ++it) {
         PROF_T(t_i0);
-        const LmTrig T = lm_trig(cur);
+        const LmTrig T = lm_trig<kF1>(cur);
         double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (int q = lane; q < nq; q += 64) {
           const float4 po = L.featl[q];
-          const float4 sel = it == iter ? L.sel[q] : transform_to_start(po, cur);
+          const float4 sel = it == iter ? L.sel[q] : transform_to_start<kF1>(po, cur);
           float4 cf;
-          const bool ok = surf ? (L.ind2[q] >= 0 && L.ind3[q] >= 0 && surf_coeff_pl(L.plane[q], sel, it, cf))
+          const bool ok = surf ? (L.ind2[q] >= 0 && L.ind3[q] >= 0 && surf_coeff_pl<kF1>(L.plane[q], sel, it, cf))
                                : corner_coeff(last, L.ind1[q], L.ind2[q], sel, it, cf);
           if (ok) {
             if (surf) accumulate_surf_row(T, po, cf, acc);
@@ -4091,6 +4084,7 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
 // k_lm has just produced (untransformed on the initialisation scan, :1181-1209).  Runs after both
 // k_lm and k_voxel of its scan, before the next scan's k_lm.
 // ============================================================================================
+template <bool kF1>
 __global__ __launch_bounds__(1024) void k_publish(LgParams P, LgBufs B) {
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, VH = P.VH;
@@ -4117,7 +4111,7 @@ __global__ __launch_bounds__(1024) void k_publish(LgParams P, LgBufs B) {
   __syncthreads();
   float c6[6];
   for (int k = 0; k < 6; ++k) c6[k] = cur[k];
-  const EndTrig E = end_trig(c6);
+  const EndTrig<kF1> E = end_trig<kF1>(c6);
   float4* sl = B.surf_last + (size_t)s * 2 * VH + (size_t)nb * VH;
   float4* fl = B.f_lflat + (size_t)s * VH;
   for (int r = wave_id(); r < V; r += nt >> 6) {  // one wave a ring
@@ -4132,7 +4126,7 @@ __global__ __launch_bounds__(1024) void k_publish(LgParams P, LgBufs B) {
         const int t = t0 + 64 * u;
         if (t < n) {
           fl[o + t] = p4[u];
-          sl[o + t] = copy ? p4[u] : transform_to_end_t(p4[u], c6, E);
+          sl[o + t] = copy ? p4[u] : transform_to_end_t<kF1>(p4[u], c6, E);
         }
       }
     }
@@ -4149,7 +4143,7 @@ __global__ __launch_bounds__(1024) void k_publish(LgParams P, LgBufs B) {
   }
 }
 
-template <int kNT, int kMaxQ>
+template <int kNT, int kMaxQ, bool kF1>
 __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
   __shared__ LmLdsT<kMaxQ> L;
   __shared__ LgState S;
@@ -4195,40 +4189,43 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
     if (tid == 0 && S.tree_stale) L.status |= LEGO_ST_STALE_TREE;
     float4* gp = B.grid_pts + (size_t)s * VH;
     PROF_T(t_ls0);
-    lm_loop(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, gp, it_s);
+    lm_loop<kF1>(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, gp, it_s);
     PROF_ADD(17, t_ls0);
     PROF_T(t_lc0);
-    lm_loop(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, gp, it_c);
+    lm_loop<kF1>(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, gp, it_c);
     PROF_ADD(18, t_lc0);
   }
   __syncthreads();
   // integrateTransformation (:1241-1270) + publishOdometry (:1286-1298)
   if (tid == 0) {
+    typedef Fp<kF1> F;
+    typedef typename F::T T;
     const float* cur = L.cur;
     float* sum = S.sum;
     float cx = sum[0], cy = sum[1], cz = sum[2], lx = -cur[0], ly = -cur[1], lz = -cur[2];
-    float clx = cosf_g(lx), slx = sinf_g(lx), cly = cosf_g(ly), sly = sinf_g(ly), clz = cosf_g(lz), slz = sinf_g(lz);
-    float ccx = cosf_g(cx), scx = sinf_g(cx), ccy = cosf_g(cy), scy = sinf_g(cy), ccz = cosf_g(cz), scz = sinf_g(cz);
+    // AccumulateRotation (:474-500)
+    const T clx = F::cs(lx), slx = F::sn(lx), cly = F::cs(ly), sly = F::sn(ly), clz = F::cs(lz), slz = F::sn(lz);
+    const T ccx = F::cs(cx), scx = F::sn(cx), ccy = F::cs(cy), scy = F::sn(cy), ccz = F::cs(cz), scz = F::sn(cz);
     float srx = clx * ccx * sly * scz - ccx * ccz * slx - clx * cly * scx;
-    float ox = -asinf_g(srx);
+    float ox = -F::as(srx);
     float srycrx = slx * (ccy * scz - ccz * scx * scy) + clx * sly * (ccy * ccz + scx * scy * scz) + clx * cly * ccx * scy;
     float crycrx = clx * cly * ccx * ccy - clx * sly * (ccz * scy - ccy * scx * scz) - slx * (scy * scz + ccy * ccz * scx);
-    float cox = cosf_g(ox);
-    float oy = atan2f_g(srycrx / cox, crycrx / cox);
+    const T cox = F::cs(ox);
+    float oy = F::at2((T)srycrx / cox, (T)crycrx / cox);
     float srzcrx = scx * (clz * sly - cly * slx * slz) + ccx * scz * (cly * clz + slx * sly * slz) + clx * ccx * ccz * slz;
     float crzcrx = clx * clz * ccx * ccz - ccx * scz * (cly * slz - clz * slx * sly) - scx * (sly * slz + cly * clz * slx);
-    float oz = atan2f_g(srzcrx / cox, crzcrx / cox);
+    float oz = F::at2((T)srzcrx / cox, (T)crzcrx / cox);
     float rx = ox, ry = oy, rz = oz;
-    float crz_ = cosf_g(rz), srz_ = sinf_g(rz), crx_ = cosf_g(rx), srx_ = sinf_g(rx), cry_ = cosf_g(ry), sry_ = sinf_g(ry);
-    float x1 = crz_ * (cur[3]) - srz_ * (cur[4]);
-    float y1 = srz_ * (cur[3]) + crz_ * (cur[4]);
+    const T crz_ = F::cs(rz), srz_ = F::sn(rz), crx_ = F::cs(rx), srx_ = F::sn(rx), cry_ = F::cs(ry), sry_ = F::sn(ry);
+    float x1 = crz_ * (T)(cur[3]) - srz_ * (T)(cur[4]);
+    float y1 = srz_ * (T)(cur[3]) + crz_ * (T)(cur[4]);
     float z1 = cur[5];
     float x2 = x1;
-    float y2 = crx_ * y1 - srx_ * z1;
-    float z2 = srx_ * y1 + crx_ * z1;
-    float tx = sum[3] - (cry_ * x2 + sry_ * z2);
+    float y2 = crx_ * (T)y1 - srx_ * (T)z1;
+    float z2 = srx_ * (T)y1 + crx_ * (T)z1;
+    float tx = (T)sum[3] - (cry_ * (T)x2 + sry_ * (T)z2);
     float ty = sum[4] - y2;
-    float tz = sum[5] - (-sry_ * x2 + cry_ * z2);
+    float tz = (T)sum[5] - (-sry_ * (T)x2 + cry_ * (T)z2);
     sum[0] = rx; sum[1] = ry; sum[2] = rz; sum[3] = tx; sum[4] = ty; sum[5] = tz;
     for (int k = 0; k < 6; ++k) S.cur[k] = L.cur[k];
     double roll = sum[2], pitch = -(double)sum[0], yaw = -(double)sum[1];
@@ -4251,8 +4248,8 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
     for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
     const int nb = S.last_buf ^ 1;
     float4* cl = corner_base + (size_t)nb * cl_stride;
-    const EndTrig E = end_trig(cur);
-    for (int k = tid; k < n_lsharp; k += (int)blockDim.x) cl[k] = transform_to_end_t(f_lsharp[k], cur, E);
+    const EndTrig<kF1> E = end_trig<kF1>(cur);
+    for (int k = tid; k < n_lsharp; k += (int)blockDim.x) cl[k] = transform_to_end_t<kF1>(f_lsharp[k], cur, E);
   }
   __syncthreads();
   if (tid == 0) {
@@ -4363,7 +4360,10 @@ int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
 }
 
 int lg_launch_publish(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  hipLaunchKernelGGL(k_publish, dim3(S), dim3(1024), 0, st, P, B);
+  if (P.fp1)
+    hipLaunchKernelGGL(k_publish<true>, dim3(S), dim3(1024), 0, st, P, B);
+  else
+    hipLaunchKernelGGL(k_publish<false>, dim3(S), dim3(1024), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
@@ -4379,10 +4379,15 @@ int lg_launch_lm(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   // of LDS leave room on the CU for the next scan's small front-end kernels (256 VLP-16 streams: k_lm
   // 553 -> 515 us, +4 % scans/s).  Few scans in flight (one scan: 2-3 % lower latency) and larger
   // sensors keep 768 threads (and LDS for 1,536 queries).
-  if (P.V * std::max(P.cap_sharp, P.cap_flat) <= 384 && S > 8)
-    hipLaunchKernelGGL((k_lm<512, 384>), dim3(S), dim3(512), 0, st, P, B);
+  const bool small = P.V * std::max(P.cap_sharp, P.cap_flat) <= 384 && S > 8;
+  if (small && !P.fp1)
+    hipLaunchKernelGGL((k_lm<512, 384, false>), dim3(S), dim3(512), 0, st, P, B);
+  else if (small)
+    hipLaunchKernelGGL((k_lm<512, 384, true>), dim3(S), dim3(512), 0, st, P, B);
+  else if (!P.fp1)
+    hipLaunchKernelGGL((k_lm<768, 1536, false>), dim3(S), dim3(768), 0, st, P, B);
   else
-    hipLaunchKernelGGL((k_lm<768, 1536>), dim3(S), dim3(768), 0, st, P, B);
+    hipLaunchKernelGGL((k_lm<768, 1536, true>), dim3(S), dim3(768), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
@@ -4399,10 +4404,12 @@ __global__ void k_libm_test(const float* a, const float* b, float* out, int n, i
   else if (which == 2) r = atanf_g(a[i]);
   else if (which == 3) r = sqrtf(a[i]);
   else if (which == 4) r = a[i] / b[i];
-  else if (which == 5) r = ground_pair(a[i], b[i], 0.f) ? 1.f : 0.f;                       // fast + exact
+  else if (which == 5) r = ground_pair(a[i], b[i] * b[i], 0.f, 0) ? 1.f : 0.f;              // fast + exact
   else if (which == 7) r = sinf_g(a[i]);
   else if (which == 8) r = cosf_g(a[i]);
-  else r = (double)atan2f_g(a[i], b[i]) <= 10 * DEG_TO_RAD_D ? 1.f : 0.f;                  // exact only
+  else if (which == 9) r = ground_pair(a[i], b[i] * b[i], 0.f, 1) ? 1.f : 0.f;              // fp_mode 1
+  else if (which == 10) r = ground_pair_exact(a[i], b[i] * b[i], 0.f, 1) ? 1.f : 0.f;
+  else r = ground_pair_exact(a[i], b[i] * b[i], 0.f, 0) ? 1.f : 0.f;                         // exact only
   out[i] = r;
 }
 
@@ -4452,6 +4459,38 @@ extern "C" int lego_test_libm(const float* h_a, const float* h_b, float* h_out, 
       hipMemcpy(b, h_b, bytes, hipMemcpyHostToDevice) != hipSuccess) rc = LEGO_EDEVICE;
   if (rc == LEGO_OK) {
     hipLaunchKernelGGL(k_libm_test, dim3((n + 255) / 256), dim3(256), 0, 0, a, b, o, n, which);
+    if (hipGetLastError() != hipSuccess || hipMemcpy(h_out, o, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = LEGO_EDEVICE;
+  }
+  hipFree(a); hipFree(b); hipFree(o);
+  return rc;
+}
+
+__global__ void k_libm_d_test(const double* a, const double* b, double* out, int n, int which) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double r;
+  if (which == 0) r = sin_d(a[i]);
+  else if (which == 1) r = cos_d(a[i]);
+  else if (which == 2) r = atan2_d(a[i], b[i]);
+  else if (which == 3) r = asin_d(a[i]);
+  else if (which == 4) r = sqrt(a[i]);
+  else r = a[i] / b[i];
+  out[i] = r;
+}
+
+extern "C" int lego_test_libm_d(const double* h_a, const double* h_b, double* h_out, int32_t n, int32_t which) {
+  if (n <= 0 || !h_a || !h_b || !h_out) return LEGO_EINVAL;
+  double *a = nullptr, *b = nullptr, *o = nullptr;
+  const size_t bytes = (size_t)n * sizeof(double);
+  if (hipMalloc((void**)&a, bytes) != hipSuccess) return LEGO_ENOMEM;
+  if (hipMalloc((void**)&b, bytes) != hipSuccess) { hipFree(a); return LEGO_ENOMEM; }
+  if (hipMalloc((void**)&o, bytes) != hipSuccess) { hipFree(a); hipFree(b); return LEGO_ENOMEM; }
+  int rc = LEGO_OK;
+  if (hipMemcpy(a, h_a, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(b, h_b, bytes, hipMemcpyHostToDevice) != hipSuccess) rc = LEGO_EDEVICE;
+  if (rc == LEGO_OK) {
+    hipLaunchKernelGGL(k_libm_d_test, dim3((n + 255) / 256), dim3(256), 0, 0, a, b, o, n, which);
     if (hipGetLastError() != hipSuccess || hipMemcpy(h_out, o, bytes, hipMemcpyDeviceToHost) != hipSuccess)
       rc = LEGO_EDEVICE;
   }

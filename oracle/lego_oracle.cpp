@@ -43,6 +43,33 @@ const float RAD2DEG = 180.0 / M_PI;              // featureAssociation.cpp:39
 
 typedef lego_point Pt;
 
+// The two libm overload models, selected by lego_params.fp_mode:
+//   Lm<float>  fp_mode 0: unqualified sin(float) etc. resolve to the float overloads (libstdc++ >= 6's
+//              <math.h> wrapper) -> glibc's sinf / cosf / atan2f / asinf / sqrtf;
+//   Lm<double> fp_mode 1: they resolve to ::sin(double) etc. (pre-GCC-6 libstdc++, the ROS Indigo /
+//              Kinetic toolchains of README.md:40): the expression is evaluated in double and rounded
+//              where the reference stores it to float.
+// T is the type the reference's expression is evaluated in.  Explicitly std::-qualified calls
+// (imageProjection.cpp:190,198,237,240) are float in both models.
+template <class T>
+struct Lm;
+template <>
+struct Lm<float> {
+  static float sn(float x) { return sinf(x); }
+  static float cs(float x) { return cosf(x); }
+  static float at2(float y, float x) { return atan2f(y, x); }
+  static float as(float x) { return asinf(x); }
+  static float sq(float x) { return sqrtf(x); }
+};
+template <>
+struct Lm<double> {
+  static double sn(double x) { return sin(x); }
+  static double cs(double x) { return cos(x); }
+  static double at2(double y, double x) { return atan2(y, x); }
+  static double as(double x) { return asin(x); }
+  static double sq(double x) { return sqrt(x); }
+};
+
 Pt nan_point() {  // imageProjection.cpp:109-112 (PCL default ctor: intensity 0)
   Pt p;
   p.x = p.y = p.z = std::numeric_limits<float>::quiet_NaN();
@@ -64,8 +91,11 @@ struct by_value {  // utility.h:58-62
 struct ImageProjection {
   int V, H, G, seg_valid_pt, seg_valid_line;
   float ang_res_x, ang_res_y, ang_bottom, segment_theta, mount;
-  // per-call derived constants of labelComponents (imageProjection.cpp:414,463 — float overloads)
+  // per-call derived constants of labelComponents (imageProjection.cpp:414,463): float overloads
+  // (fp_mode 0) or double (fp_mode 1)
+  bool fp1;
   float theta_thr, sinX, cosX, sinY, cosY;
+  double sinXd, cosXd, sinYd, cosYd;
 
   std::vector<Pt> cloud_in, full_cloud;
   std::vector<float> range_mat;
@@ -98,9 +128,12 @@ struct ImageProjection {
     G = p.ground_scan_index;
     mount = p.sensor_mount_angle;
     mount *= DEG_TO_RAD;                                                      // :84
-    theta_thr = tanf(segment_theta);                                          // :414
+    fp1 = p.fp_mode == 1;
+    theta_thr = fp1 ? (float)tan((double)segment_theta) : tanf(segment_theta);  // :414
     sinX = sinf(ang_res_x); cosX = cosf(ang_res_x);                           // :463 alpha=_ang_resolution_X
     sinY = sinf(ang_res_y); cosY = cosf(ang_res_y);                           // :463 alpha=_ang_resolution_Y
+    sinXd = sin((double)ang_res_x); cosXd = cos((double)ang_res_x);           // fp_mode 1: double sin/cos
+    sinYd = sin((double)ang_res_y); cosYd = cos((double)ang_res_y);
     full_cloud.resize((size_t)V * H);
   }
 
@@ -158,7 +191,10 @@ struct ImageProjection {
         float dX = full_cloud[upperInd].x - full_cloud[lowerInd].x;
         float dY = full_cloud[upperInd].y - full_cloud[lowerInd].y;
         float dZ = full_cloud[upperInd].z - full_cloud[lowerInd].z;
-        float vertical_angle = std::atan2(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ));
+        // std::atan2(float, sqrt(...)): float overloads (fp_mode 0); with ::sqrt(double) the qualified
+        // std::atan2(float, double) promotes to double (fp_mode 1)
+        float vertical_angle = fp1 ? (float)std::atan2((double)dZ, sqrt((double)(dX * dX + dY * dY + dZ * dZ)))
+                                   : std::atan2(dZ, sqrtf(dX * dX + dY * dY + dZ * dZ));
         if ((vertical_angle - mount) <= 10 * DEG_TO_RAD) {
           ground_mat[(size_t)i * H + j] = 1;
           ground_mat[(size_t)(i + 1) * H + j] = 1;
@@ -209,9 +245,16 @@ struct ImageProjection {
         float d1 = std::max(rf, rt);
         float d2 = std::min(rf, rt);
         // alpha = (iter.x() == 0) ? resX : resY; sin/cos(alpha) hoisted (float overloads).
-        float sA = (nb[k][0] == 0) ? sinX : sinY;
-        float cA = (nb[k][0] == 0) ? cosX : cosY;
-        float tang = (d2 * sA / (d1 - d2 * cA));
+        float tang;
+        if (fp1) {  // (d2 * sin(alpha) / (d1 - d2 * cos(alpha))) in double
+          double sA = (nb[k][0] == 0) ? sinXd : sinYd;
+          double cA = (nb[k][0] == 0) ? cosXd : cosYd;
+          tang = (float)((double)d2 * sA / ((double)d1 - (double)d2 * cA));
+        } else {
+          float sA = (nb[k][0] == 0) ? sinX : sinY;
+          float cA = (nb[k][0] == 0) ? cosX : cosY;
+          tang = (d2 * sA / (d1 - d2 * cA));
+        }
         if (tang > theta_thr) {
           q_r.push_back(thisIndX); q_c.push_back(thisIndY);
           label_mat[(size_t)thisIndX * H + thisIndY] = label_count;
@@ -525,6 +568,7 @@ struct FeatureAssociation {
   double quat[4] = {0, 0, 0, 1}, pos[3] = {0, 0, 0};
 
   bool voxel_stable = false;  // lego_params.voxel_tie_order == 1 (std::stable_sort in VoxelGrid)
+  bool fp1 = false;           // lego_params.fp_mode == 1 (double libm overloads)
 
   explicit FeatureAssociation(const lego_params& p) {  // ctor :69-84 + initializationValue :96-157
     V = p.num_vertical_scans;
@@ -534,6 +578,7 @@ struct FeatureAssociation {
     surf_thr = p.surf_threshold;
     map_div = p.mapping_frequency_divider;
     voxel_stable = p.voxel_tie_order == 1;
+    fp1 = p.fp_mode == 1;
     float nearest_dist = p.nearest_feature_search_distance;
     nn_dist_sqr = nearest_dist * nearest_dist;
     const size_t n = (size_t)V * H;
@@ -554,7 +599,7 @@ struct FeatureAssociation {
       point.x = segmented[i].y;
       point.y = segmented[i].z;
       point.z = segmented[i].x;
-      float ori = -atan2f(point.x, point.z);
+      float ori = fp1 ? (float)(-atan2((double)point.x, (double)point.z)) : -atan2f(point.x, point.z);
       if (!halfPassed) {
         if (ori < start_ori - M_PI / 2)
           ori += 2 * M_PI;
@@ -679,7 +724,18 @@ struct FeatureAssociation {
     }
   }
 
-  void TransformToStart(const Pt* pi, Pt* po) {  // :388-418
+  // TransformToStart / TransformToEnd / AccumulateRotation / integrateTransformation: unqualified
+  // sin / cos / asin / atan2 on floats, evaluated in T (Lm<T>, fp_mode) and rounded where stored to float.
+  void TransformToStart(const Pt* pi, Pt* po) {
+    if (fp1) TransformToStartT<double>(pi, po); else TransformToStartT<float>(pi, po);
+  }
+  void TransformToEnd(const Pt* pi, Pt* po) {
+    if (fp1) TransformToEndT<double>(pi, po); else TransformToEndT<float>(pi, po);
+  }
+
+  template <class T>
+  void TransformToStartT(const Pt* pi, Pt* po) {  // :388-418
+    typedef Lm<T> F;
     float s = 10 * (pi->intensity - int(pi->intensity));
     float ry = s * transformCur[1];
     float rx = s * transformCur[0];
@@ -687,19 +743,21 @@ struct FeatureAssociation {
     float tx = s * transformCur[3];
     float ty = s * transformCur[4];
     float tz = s * transformCur[5];
-    float x1 = cosf(rz) * (pi->x - tx) + sinf(rz) * (pi->y - ty);
-    float y1 = -sinf(rz) * (pi->x - tx) + cosf(rz) * (pi->y - ty);
+    float x1 = F::cs(rz) * (T)(pi->x - tx) + F::sn(rz) * (T)(pi->y - ty);
+    float y1 = -F::sn(rz) * (T)(pi->x - tx) + F::cs(rz) * (T)(pi->y - ty);
     float z1 = (pi->z - tz);
     float x2 = x1;
-    float y2 = cosf(rx) * y1 + sinf(rx) * z1;
-    float z2 = -sinf(rx) * y1 + cosf(rx) * z1;
-    po->x = cosf(ry) * x2 - sinf(ry) * z2;
+    float y2 = F::cs(rx) * (T)y1 + F::sn(rx) * (T)z1;
+    float z2 = -F::sn(rx) * (T)y1 + F::cs(rx) * (T)z1;
+    po->x = F::cs(ry) * (T)x2 - F::sn(ry) * (T)z2;
     po->y = y2;
-    po->z = sinf(ry) * x2 + cosf(ry) * z2;
+    po->z = F::sn(ry) * (T)x2 + F::cs(ry) * (T)z2;
     po->intensity = pi->intensity;
   }
 
-  void TransformToEnd(const Pt* pi, Pt* po) {  // :422-471
+  template <class T>
+  void TransformToEndT(const Pt* pi, Pt* po) {  // :422-471
+    typedef Lm<T> F;
     float s = 10 * (pi->intensity - int(pi->intensity));
     float rx = s * transformCur[0];
     float ry = s * transformCur[1];
@@ -707,29 +765,29 @@ struct FeatureAssociation {
     float tx = s * transformCur[3];
     float ty = s * transformCur[4];
     float tz = s * transformCur[5];
-    float x1 = cosf(rz) * (pi->x - tx) + sinf(rz) * (pi->y - ty);
-    float y1 = -sinf(rz) * (pi->x - tx) + cosf(rz) * (pi->y - ty);
+    float x1 = F::cs(rz) * (T)(pi->x - tx) + F::sn(rz) * (T)(pi->y - ty);
+    float y1 = -F::sn(rz) * (T)(pi->x - tx) + F::cs(rz) * (T)(pi->y - ty);
     float z1 = (pi->z - tz);
     float x2 = x1;
-    float y2 = cosf(rx) * y1 + sinf(rx) * z1;
-    float z2 = -sinf(rx) * y1 + cosf(rx) * z1;
-    float x3 = cosf(ry) * x2 - sinf(ry) * z2;
+    float y2 = F::cs(rx) * (T)y1 + F::sn(rx) * (T)z1;
+    float z2 = -F::sn(rx) * (T)y1 + F::cs(rx) * (T)z1;
+    float x3 = F::cs(ry) * (T)x2 - F::sn(ry) * (T)z2;
     float y3 = y2;
-    float z3 = sinf(ry) * x2 + cosf(ry) * z2;
+    float z3 = F::sn(ry) * (T)x2 + F::cs(ry) * (T)z2;
     rx = transformCur[0];
     ry = transformCur[1];
     rz = transformCur[2];
     tx = transformCur[3];
     ty = transformCur[4];
     tz = transformCur[5];
-    float x4 = cosf(ry) * x3 + sinf(ry) * z3;
+    float x4 = F::cs(ry) * (T)x3 + F::sn(ry) * (T)z3;
     float y4 = y3;
-    float z4 = -sinf(ry) * x3 + cosf(ry) * z3;
+    float z4 = -F::sn(ry) * (T)x3 + F::cs(ry) * (T)z3;
     float x5 = x4;
-    float y5 = cosf(rx) * y4 - sinf(rx) * z4;
-    float z5 = sinf(rx) * y4 + cosf(rx) * z4;
-    float x6 = cosf(rz) * x5 - sinf(rz) * y5 + tx;
-    float y6 = sinf(rz) * x5 + cosf(rz) * y5 + ty;
+    float y5 = F::cs(rx) * (T)y4 - F::sn(rx) * (T)z4;
+    float z5 = F::sn(rx) * (T)y4 + F::cs(rx) * (T)z4;
+    float x6 = F::cs(rz) * (T)x5 - F::sn(rz) * (T)y5 + (T)tx;
+    float y6 = F::sn(rz) * (T)x5 + F::cs(rz) * (T)y5 + (T)ty;
     float z6 = z5 + tz;
     po->x = x6;
     po->y = y6;
@@ -737,25 +795,27 @@ struct FeatureAssociation {
     po->intensity = int(pi->intensity);
   }
 
+  template <class T>
   static void AccumulateRotation(float cx, float cy, float cz, float lx, float ly, float lz, float& ox,
                                  float& oy, float& oz) {  // :474-500
-    float srx = cosf(lx) * cosf(cx) * sinf(ly) * sinf(cz) - cosf(cx) * cosf(cz) * sinf(lx) -
-                cosf(lx) * cosf(ly) * sinf(cx);
-    ox = -asinf(srx);
-    float srycrx = sinf(lx) * (cosf(cy) * sinf(cz) - cosf(cz) * sinf(cx) * sinf(cy)) +
-                   cosf(lx) * sinf(ly) * (cosf(cy) * cosf(cz) + sinf(cx) * sinf(cy) * sinf(cz)) +
-                   cosf(lx) * cosf(ly) * cosf(cx) * sinf(cy);
-    float crycrx = cosf(lx) * cosf(ly) * cosf(cx) * cosf(cy) -
-                   cosf(lx) * sinf(ly) * (cosf(cz) * sinf(cy) - cosf(cy) * sinf(cx) * sinf(cz)) -
-                   sinf(lx) * (sinf(cy) * sinf(cz) + cosf(cy) * cosf(cz) * sinf(cx));
-    oy = atan2f(srycrx / cosf(ox), crycrx / cosf(ox));
-    float srzcrx = sinf(cx) * (cosf(lz) * sinf(ly) - cosf(ly) * sinf(lx) * sinf(lz)) +
-                   cosf(cx) * sinf(cz) * (cosf(ly) * cosf(lz) + sinf(lx) * sinf(ly) * sinf(lz)) +
-                   cosf(lx) * cosf(cx) * cosf(cz) * sinf(lz);
-    float crzcrx = cosf(lx) * cosf(lz) * cosf(cx) * cosf(cz) -
-                   cosf(cx) * sinf(cz) * (cosf(ly) * sinf(lz) - cosf(lz) * sinf(lx) * sinf(ly)) -
-                   sinf(cx) * (sinf(ly) * sinf(lz) + cosf(ly) * cosf(lz) * sinf(lx));
-    oz = atan2f(srzcrx / cosf(ox), crzcrx / cosf(ox));
+    typedef Lm<T> F;
+    float srx = F::cs(lx) * F::cs(cx) * F::sn(ly) * F::sn(cz) - F::cs(cx) * F::cs(cz) * F::sn(lx) -
+                F::cs(lx) * F::cs(ly) * F::sn(cx);
+    ox = -F::as(srx);
+    float srycrx = F::sn(lx) * (F::cs(cy) * F::sn(cz) - F::cs(cz) * F::sn(cx) * F::sn(cy)) +
+                   F::cs(lx) * F::sn(ly) * (F::cs(cy) * F::cs(cz) + F::sn(cx) * F::sn(cy) * F::sn(cz)) +
+                   F::cs(lx) * F::cs(ly) * F::cs(cx) * F::sn(cy);
+    float crycrx = F::cs(lx) * F::cs(ly) * F::cs(cx) * F::cs(cy) -
+                   F::cs(lx) * F::sn(ly) * (F::cs(cz) * F::sn(cy) - F::cs(cy) * F::sn(cx) * F::sn(cz)) -
+                   F::sn(lx) * (F::sn(cy) * F::sn(cz) + F::cs(cy) * F::cs(cz) * F::sn(cx));
+    oy = F::at2((T)srycrx / F::cs(ox), (T)crycrx / F::cs(ox));
+    float srzcrx = F::sn(cx) * (F::cs(lz) * F::sn(ly) - F::cs(ly) * F::sn(lx) * F::sn(lz)) +
+                   F::cs(cx) * F::sn(cz) * (F::cs(ly) * F::cs(lz) + F::sn(lx) * F::sn(ly) * F::sn(lz)) +
+                   F::cs(lx) * F::cs(cx) * F::cs(cz) * F::sn(lz);
+    float crzcrx = F::cs(lx) * F::cs(lz) * F::cs(cx) * F::cs(cz) -
+                   F::cs(cx) * F::sn(cz) * (F::cs(ly) * F::sn(lz) - F::cs(lz) * F::sn(lx) * F::sn(ly)) -
+                   F::sn(cx) * (F::sn(ly) * F::sn(lz) + F::cs(ly) * F::cs(lz) * F::sn(lx));
+    oz = F::at2((T)srzcrx / F::cs(ox), (T)crzcrx / F::cs(ox));
   }
 
   // nanoflann KdTreeFLANN::nearestKSearch(k=1) (nanoflann_pcl.h:141-152): exact L2^2 1-NN,
@@ -901,8 +961,10 @@ struct FeatureAssociation {
         float pd2 = pa * pointSel.x + pb * pointSel.y + pc * pointSel.z + pd;
         float s = 1;
         if (iterCount >= 5)
-          s = 1 - 1.8 * fabsf(pd2) /
-                      sqrtf(sqrtf(pointSel.x * pointSel.x + pointSel.y * pointSel.y + pointSel.z * pointSel.z));
+          s = fp1 ? 1 - 1.8 * fabsf(pd2) /
+                            sqrt(sqrt((double)(pointSel.x * pointSel.x + pointSel.y * pointSel.y + pointSel.z * pointSel.z)))
+                  : 1 - 1.8 * fabsf(pd2) /
+                            sqrtf(sqrtf(pointSel.x * pointSel.x + pointSel.y * pointSel.y + pointSel.z * pointSel.z));
         if (s > 0.1 && pd2 != 0) {
           Pt coeff;
           coeff.x = s * pa; coeff.y = s * pb; coeff.z = s * pc; coeff.intensity = s * pd2;
@@ -912,6 +974,10 @@ struct FeatureAssociation {
       }
     }
   }
+
+  // float srx = sin(transformCur[0]) (:797-802, :939-944) in either libm model
+  float lm_sin(float x) const { return fp1 ? (float)sin((double)x) : sinf(x); }
+  float lm_cos(float x) const { return fp1 ? (float)cos((double)x) : cosf(x); }
 
   // AtA / AtB (Eigen GEMM, modelled) + solve + degeneracy; returns x[3]
   void solve_normal(const std::vector<float>& A, const std::vector<float>& B, int iterCount, float x[3]) {
@@ -943,12 +1009,12 @@ struct FeatureAssociation {
 
   bool calculateTransformationSurf(int iterCount) {  // :785-921
     int pointSelNum = (int)laserCloudOri.size();
-    float srx = sinf(transformCur[0]);
-    float crx = cosf(transformCur[0]);
-    float sry = sinf(transformCur[1]);
-    float cry = cosf(transformCur[1]);
-    float srz = sinf(transformCur[2]);
-    float crz = cosf(transformCur[2]);
+    float srx = lm_sin(transformCur[0]);
+    float crx = lm_cos(transformCur[0]);
+    float sry = lm_sin(transformCur[1]);
+    float cry = lm_cos(transformCur[1]);
+    float srz = lm_sin(transformCur[2]);
+    float crz = lm_cos(transformCur[2]);
     float tx = transformCur[3];
     float ty = transformCur[4];
     float tz = transformCur[5];
@@ -1006,12 +1072,12 @@ struct FeatureAssociation {
 
   bool calculateTransformationCorner(int iterCount) {  // :928-1032
     int pointSelNum = (int)laserCloudOri.size();
-    float srx = sinf(transformCur[0]);
-    float crx = cosf(transformCur[0]);
-    float sry = sinf(transformCur[1]);
-    float cry = cosf(transformCur[1]);
-    float srz = sinf(transformCur[2]);
-    float crz = cosf(transformCur[2]);
+    float srx = lm_sin(transformCur[0]);
+    float crx = lm_cos(transformCur[0]);
+    float sry = lm_sin(transformCur[1]);
+    float cry = lm_cos(transformCur[1]);
+    float srz = lm_sin(transformCur[2]);
+    float crz = lm_cos(transformCur[2]);
     float tx = transformCur[3];
     float ty = transformCur[4];
     float tz = transformCur[5];
@@ -1082,19 +1148,24 @@ struct FeatureAssociation {
     }
   }
 
-  void integrateTransformation() {  // :1241-1270
+  void integrateTransformation() {
+    if (fp1) integrateTransformationT<double>(); else integrateTransformationT<float>();
+  }
+  template <class T>
+  void integrateTransformationT() {  // :1241-1270
+    typedef Lm<T> F;
     float rx, ry, rz, tx, ty, tz;
-    AccumulateRotation(transformSum[0], transformSum[1], transformSum[2], -transformCur[0], -transformCur[1],
-                       -transformCur[2], rx, ry, rz);
-    float x1 = cosf(rz) * (transformCur[3]) - sinf(rz) * (transformCur[4]);
-    float y1 = sinf(rz) * (transformCur[3]) + cosf(rz) * (transformCur[4]);
+    AccumulateRotation<T>(transformSum[0], transformSum[1], transformSum[2], -transformCur[0], -transformCur[1],
+                          -transformCur[2], rx, ry, rz);
+    float x1 = F::cs(rz) * (T)(transformCur[3]) - F::sn(rz) * (T)(transformCur[4]);
+    float y1 = F::sn(rz) * (T)(transformCur[3]) + F::cs(rz) * (T)(transformCur[4]);
     float z1 = transformCur[5];
     float x2 = x1;
-    float y2 = cosf(rx) * y1 - sinf(rx) * z1;
-    float z2 = sinf(rx) * y1 + cosf(rx) * z1;
-    tx = transformSum[3] - (cosf(ry) * x2 + sinf(ry) * z2);
+    float y2 = F::cs(rx) * (T)y1 - F::sn(rx) * (T)z1;
+    float z2 = F::sn(rx) * (T)y1 + F::cs(rx) * (T)z1;
+    tx = (T)transformSum[3] - (F::cs(ry) * (T)x2 + F::sn(ry) * (T)z2);
     ty = transformSum[4] - y2;
-    tz = transformSum[5] - (-sinf(ry) * x2 + cosf(ry) * z2);
+    tz = (T)transformSum[5] - (-F::sn(ry) * (T)x2 + F::cs(ry) * (T)z2);
     transformSum[0] = rx; transformSum[1] = ry; transformSum[2] = rz;
     transformSum[3] = tx; transformSum[4] = ty; transformSum[5] = tz;
   }

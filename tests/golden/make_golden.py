@@ -26,16 +26,21 @@ PROJ_HASH = ["segmented_cloud", "outlier_cloud", "scan_msg", "start_ring_index",
              "ground_mat", "range_mat"]
 FEAT_HASH = ["sharp_ind", "less_sharp_ind", "flat_ind", "sharp", "less_sharp", "flat", "less_flat"]
 
-# (name, sensor kind, synth overrides, sequence, number of scans)
+NOISE_FREE = {"range_noise": 0.0, "az_jitter_deg": 0.0, "roll_pitch_noise_deg": 0.0}
+# (name, sensor kind, synth overrides, sequence, number of scans, fp_mode)
 CASES = [
-    ("vlp16_seq0", "vlp16", {}, 0, 6),
-    ("vlp16_seq7", "vlp16", {}, 7, 3),
-    ("vlp16_noisefree_seq3", "vlp16", {"range_noise": 0.0, "az_jitter_deg": 0.0, "roll_pitch_noise_deg": 0.0}, 3, 3),
-    ("hdl64_seq0", "hdl64", {}, 0, 2),
+    ("vlp16_seq0", "vlp16", {}, 0, 6, 0),
+    ("vlp16_seq7", "vlp16", {}, 7, 3, 0),
+    ("vlp16_noisefree_seq3", "vlp16", NOISE_FREE, 3, 3, 0),
+    ("hdl64_seq0", "hdl64", {}, 0, 2, 0),
+    # fp_mode 1: the unqualified libm calls in double (the Indigo / Kinetic toolchains)
+    ("vlp16_seq0_fp1", "vlp16", {}, 0, 6, 1),
+    ("vlp16_noisefree_seq3_fp1", "vlp16", NOISE_FREE, 3, 3, 1),
+    ("hdl64_seq0_fp1", "hdl64", {}, 0, 2, 1),
 ]
 
 
-def params_for(kind):
+def params_for(kind, fp_mode=0):
     p = A.LegoParams()
     if kind == "vlp16":
         vals = (16, 1800, 7, -15.0, 15.0, 0.0, 0.1, 5, 3, 60.0, 0.1, 0.1, 5.0, 5, 0)
@@ -43,6 +48,7 @@ def params_for(kind):
         vals = (64, 2048, 55, -24.8, 2.0, 0.0, 0.1, 5, 3, 60.0, 0.1, 0.1, 5.0, 5, 0)
     for (name, _), v in zip(A.LegoParams._fields_, vals):
         setattr(p, name, v)
+    p.fp_mode = fp_mode
     return p
 
 
@@ -51,8 +57,8 @@ def h(a):
     return hashlib.sha256(a.tobytes()).hexdigest()[:24]
 
 
-def run_case(kind, over, seq, nscans):
-    params = params_for(kind)
+def run_case(kind, over, seq, nscans, fp_mode=0):
+    params = params_for(kind, fp_mode)
     cfg = A.synth_cfg(kind, **over)
     orc = O.Oracle(params)
     rows = []
@@ -76,9 +82,9 @@ def run_case(kind, over, seq, nscans):
 
 def main():
     out = {"generator": "oracle/lego_oracle.cpp via tests/golden/make_golden.py", "cases": {}}
-    for name, kind, over, seq, n in CASES:
-        rows, pts, pr, fa = run_case(kind, over, seq, n)
-        out["cases"][name] = {"kind": kind, "synth": over, "seq": seq, "scans": rows}
+    for name, kind, over, seq, n, fp_mode in CASES:
+        rows, pts, pr, fa = run_case(kind, over, seq, n, fp_mode)
+        out["cases"][name] = {"kind": kind, "synth": over, "seq": seq, "fp_mode": fp_mode, "scans": rows}
         print(name, [(r["M"], r["n_sharp"], r["n_flat"], hex(r["status"])) for r in rows])
     with open(os.path.join(HERE, "golden_oracle.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -39,8 +39,10 @@ def test_params_and_validation():
     assert (p.num_vertical_scans, p.num_horizontal_scans, p.ground_scan_index) == (16, 1800, 7)
     assert p.segment_theta == 60.0 and p.mapping_frequency_divider == 5
     assert L.lib().lego_params_validate(C.byref(p)) == A.LEGO_OK
-    p.fp_mode = 1
-    assert L.lib().lego_params_validate(C.byref(p)) == A.LEGO_ENOTSUP
+    p.fp_mode = 1  # double libm overloads (Indigo / Kinetic toolchains)
+    assert L.lib().lego_params_validate(C.byref(p)) == A.LEGO_OK
+    p.fp_mode = 2
+    assert L.lib().lego_params_validate(C.byref(p)) == A.LEGO_EINVAL
     q = L.params_hdl64()
     assert (q.num_vertical_scans, q.num_horizontal_scans, q.ground_scan_index) == (64, 2048, 55)
     q.num_horizontal_scans = 4096

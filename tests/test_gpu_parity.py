@@ -91,6 +91,48 @@ def test_device_libm_matches_glibc(gpu):
     assert Hs.bits_equal(q, xy[0] / xy[1])  # numpy float32 division is IEEE
 
 
+def test_device_double_libm_matches_glibc(gpu):
+    """fp_mode 1's double sin / cos / atan2 / asin (fdlibm on the device) against the host glibc double
+    functions the reference calls there: identical after the rounding to float the reference applies
+    (every sample), and identical doubles for all but a small fraction (fdlibm vs glibc's IBM library:
+    < 1 ulp each); double sqrt and division are IEEE (bit-identical)."""
+    rng = np.random.default_rng(2)
+    n = 1 << 20
+    small = (rng.uniform(-1, 1, n) * np.where(rng.random(n) < 0.5, 0.05, 3.5)).astype(np.float32).astype(np.float64)
+    unit = rng.uniform(-1, 1, n).astype(np.float32).astype(np.float64)
+    ptsa = rng.uniform(-80, 80, (2, n)).astype(np.float32).astype(np.float64)
+    wide = rng.integers(-2 ** 31, 2 ** 31, (2, n)).astype(np.float32).astype(np.float64)
+    pos = np.abs(rng.standard_normal(n) * 100)
+    libm = C.CDLL("libm.so.6")
+    for f in ("sin", "cos", "asin"):
+        getattr(libm, f).restype = C.c_double
+        getattr(libm, f).argtypes = [C.c_double]
+    libm.atan2.restype = C.c_double
+    libm.atan2.argtypes = [C.c_double, C.c_double]
+
+    def dev(x, y, which):
+        out = np.zeros_like(x)
+        fp = C.POINTER(C.c_double)
+        x, y = np.ascontiguousarray(x), np.ascontiguousarray(y)
+        assert L.lib().lego_test_libm_d(x.ctypes.data_as(fp), y.ctypes.data_as(fp), out.ctypes.data_as(fp), len(x),
+                                        which) == 0
+        return out
+
+    cases = [(small, small, 0, lambda x, y: libm.sin(x)), (small, small, 1, lambda x, y: libm.cos(x)),
+             (ptsa[0], ptsa[1], 2, lambda x, y: libm.atan2(x, y)), (wide[0], wide[1], 2, lambda x, y: libm.atan2(x, y)),
+             (unit, unit, 3, lambda x, y: libm.asin(x))]
+    for x, y, which, ref in cases:
+        got = dev(x, y, which)
+        idx = rng.choice(len(x), 40000, replace=False)
+        exp = np.array([ref(float(x[i]), float(y[i])) for i in idx])
+        g = got[idx]
+        assert Hs.bits_equal(g.astype(np.float32), exp.astype(np.float32)), which
+        assert np.mean(g != exp) < 0.25, which
+        assert np.all(np.abs(g - exp) <= 2 * np.spacing(np.abs(exp))), which  # within 2 ulp
+    assert Hs.bits_equal(dev(pos, pos, 4), np.sqrt(pos))
+    assert Hs.bits_equal(dev(ptsa[0], ptsa[1], 5), ptsa[0] / ptsa[1])
+
+
 def test_fast_ground_pair_decides_like_the_exact_path(gpu):
     """groundRemoval's pair test (imageProjection.cpp:276-285) as k_project decides it (polynomial
     atan with a margin) equals the glibc-faithful decision: random pairs, pairs within 1e-6 rad of the
@@ -109,12 +151,13 @@ def test_fast_ground_pair_decides_like_the_exact_path(gpu):
     rr[64:128] = np.nan
     fp = C.POINTER(C.c_float)
     out = {}
-    for which in (5, 6):
+    for which in (5, 6, 9, 10):  # fp_mode 0: fast + exact, exact; fp_mode 1: the same
         o = np.zeros(n, dtype=np.float32)
         assert L.lib().lego_test_libm(dz.ctypes.data_as(fp), rr.ctypes.data_as(fp), o.ctypes.data_as(fp), n,
                                       which) == 0
         out[which] = o
     assert np.array_equal(out[5], out[6])
+    assert np.array_equal(out[9], out[10])
     assert 0.2 < out[5].mean() < 0.9
 
 
@@ -227,9 +270,10 @@ def test_device_sort_matches_libstdcxx(gpu):
                     assert np.array_equal(gv, ev) and np.array_equal(gk, ek), ("adversary", n, c, mode)
 
 
+@pytest.mark.parametrize("fp_mode", [0, 1])
 @pytest.mark.parametrize("seq", [0, 7, 21])
-def test_vlp16_sequence_parity(gpu, seq):
-    params = L.params_vlp16()
+def test_vlp16_sequence_parity(gpu, seq, fp_mode):
+    params = L.params_vlp16(fp_mode=fp_mode)
     cfg = A.synth_cfg("vlp16")
     for row in run_pair(params, cfg, seq, 8):
         assert_scan_parity(*row)
@@ -265,24 +309,27 @@ def test_voxel_stable_order_meets_north_star_bar(gpu):
     fe.close()
 
 
-def test_vlp16_noise_free_ties(gpu):
+@pytest.mark.parametrize("fp_mode", [0, 1])
+def test_vlp16_noise_free_ties(gpu, fp_mode):
     """Noise-free sweeps make exact curvature / voxel-index ties common: the introsort emulation
     must give the reference's std::sort permutation."""
-    params = L.params_vlp16()
+    params = L.params_vlp16(fp_mode=fp_mode)
     cfg = A.synth_cfg("vlp16", range_noise=0.0, az_jitter_deg=0.0, roll_pitch_noise_deg=0.0)
     for row in run_pair(params, cfg, 3, 5):
         assert_scan_parity(*row)
 
 
-def test_hdl64_parity(gpu):
+@pytest.mark.parametrize("fp_mode", [0, 1])
+def test_hdl64_parity(gpu, fp_mode):
     """HDL-64E-like config: the wide layout (k_pw_* / k_sw_*: the V*H images do not fit LDS)."""
-    params = L.params_hdl64()
+    params = L.params_hdl64(fp_mode=fp_mode)
     cfg = A.synth_cfg("hdl64")
     for row in run_pair(params, cfg, 0, 3):
         assert_scan_parity(*row)
 
 
-@pytest.mark.parametrize("case", ["vlp16_seq0", "vlp16_noisefree_seq3", "hdl64_seq0"])
+@pytest.mark.parametrize("case", ["vlp16_seq0", "vlp16_noisefree_seq3", "hdl64_seq0", "vlp16_seq0_fp1",
+                                  "vlp16_noisefree_seq3_fp1", "hdl64_seq0_fp1"])
 def test_gpu_reproduces_golden(gpu, case):
     import hashlib
 
@@ -290,7 +337,8 @@ def test_gpu_reproduces_golden(gpu, case):
         return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:24]
 
     g = Hs.golden_case(case)
-    params = L.params_vlp16() if g["kind"] == "vlp16" else L.params_hdl64()
+    fpm = g.get("fp_mode", 0)
+    params = L.params_vlp16(fp_mode=fpm) if g["kind"] == "vlp16" else L.params_hdl64(fp_mode=fpm)
     cfg = A.synth_cfg(g["kind"], **g["synth"])
     fe = L.Frontend(params)
     for row in g["scans"]:
@@ -344,14 +392,15 @@ def test_injected_projection_rejects_malformed_cloud_info(gpu):
     assert not Hs.diff_report(Hs.FEAT_KEYS, fg, fr)
 
 
+@pytest.mark.parametrize("fp_mode", [0, 1])
 @pytest.mark.parametrize("groups,wide", [(1, -1), (3, -1), (1, 0), (3, 0)])
-def test_batch_streams_match_oracle(gpu, groups, wide):
+def test_batch_streams_match_oracle(gpu, groups, wide, fp_mode):
     """The batched engine (S sequences, one launch per stage, optionally as `groups` slices on their
     own HIP streams) equals S independent oracle runs, in both kernel layouts of the projection and
     segmentation (wide: many workgroups a scan, the default at this S; 0: one workgroup a scan with
     the images in LDS, the default at bench scale)."""
     import torch
-    params = L.params_vlp16()
+    params = L.params_vlp16(fp_mode=fp_mode)
     cfg = A.synth_cfg("vlp16")
     S, steps = 6, 5
     cap = params.num_vertical_scans * params.num_horizontal_scans

@@ -22,13 +22,15 @@ def _h(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:24]
 
 
-@pytest.mark.parametrize("case", ["vlp16_seq0", "vlp16_seq7", "vlp16_noisefree_seq3", "hdl64_seq0"])
+@pytest.mark.parametrize("case", ["vlp16_seq0", "vlp16_seq7", "vlp16_noisefree_seq3", "hdl64_seq0",
+                                  "vlp16_seq0_fp1", "vlp16_noisefree_seq3_fp1", "hdl64_seq0_fp1"])
 def test_oracle_reproduces_golden(case):
-    """The oracle restatement reproduces the committed golden vectors (regression pin)."""
+    """The oracle restatement reproduces the committed golden vectors (regression pin), in both libm
+    overload models (fp_mode 0 / 1)."""
     O = oracle_mod()
     import make_golden as MG
     g = Hs.golden_case(case)
-    params = MG.params_for(g["kind"])
+    params = MG.params_for(g["kind"], g.get("fp_mode", 0))
     cfg = A.synth_cfg(g["kind"], **g["synth"])
     orc = O.Oracle(params)
     for row in g["scans"]:
