@@ -14,9 +14,12 @@ all-gathered to rank 0 (RCCL), the only collective.  Rank 0 prints one JSON line
 
 The measured path runs PCL VoxelGrid with voxel_tie_order = 1 (each voxel's points summed in point
 order) unless --voxel-tie-order 0 is given; order 0 reproduces the GCC/libstdc++-built reference bit
-for bit (its introsort tie order); --alt-order also measures the other order on the same inputs and
-reports it as "other_voxel_tie_order".  Labels, feature indices and the 6-DoF transform meet the
-north_star bar in both orders (tests/test_gpu_parity.py).
+for bit (its introsort tie order).  At N = 1 the other order is measured too on the same inputs and
+reported as "other_voxel_tie_order" (--no-alt-order skips it).  Labels, feature indices and the 6-DoF
+transform meet the north_star bar in both orders (tests/test_gpu_parity.py).
+
+The roofline pair (k_project + k_fa_prep4) is also timed at --roofline-streams scans per launch (2048:
+a working set far above the 256 MiB Infinity Cache) and reported beside the S-stream figure.
 """
 import argparse
 import json
@@ -58,8 +61,14 @@ def parse():
                     help="lego_params.voxel_tie_order of the measured path: 1 = VoxelGrid sums each voxel in "
                          "point order (stable); 0 = libstdc++ std::sort order, bit-identical to the GCC-built "
                          "reference. At N=1 the other order is measured too and reported beside the value.")
-    ap.add_argument("--alt-order", action="store_true",
-                    help="also measure the other voxel_tie_order on the same inputs (reported beside the value)")
+    ap.add_argument("--no-alt-order", action="store_true",
+                    help="skip measuring the other voxel_tie_order on the same inputs (N = 1)")
+    ap.add_argument("--fp-mode", type=int, default=0, choices=[0, 1],
+                    help="lego_params.fp_mode: libm overload model of the reference build (0 = float overloads, "
+                         "GCC >= 6; 1 = double, the Indigo / Kinetic toolchains)")
+    ap.add_argument("--roofline-streams", type=int, default=2048,
+                    help="also time the roofline pair at this many scans per launch (0: skip)")
+    ap.add_argument("--dump-poses", default="", help="rank 0: write the gathered trajectories (.npy) here")
     return ap.parse_args()
 
 
@@ -159,6 +168,46 @@ def pmc_traffic(args, S, kernels):
     return int(sum(best[1][k]["hbm_bytes"] for k in kernels)), os.path.relpath(best[0], REPO)
 
 
+def roofline_at(args, L, A, mk_params, cfg, dev_index, stream):
+    """The roofline pair (k_project + k_fa_prep4) at args.roofline_streams scans per launch (SURVEY §8(d):
+    >= 2048 VLP-16 scans, ~2.7 GB, far above the 256 MiB Infinity Cache): a batch of that many sequences
+    runs two steps (so k_fa_prep4 has its inputs), then R back-to-back pairs are timed between hipEvents,
+    the projections alternating between the two steps' inputs.  Sequences 10^6 + s (not the timed
+    region's)."""
+    import torch
+    Sb = args.roofline_streams
+    params = mk_params(voxel_tie_order=args.voxel_tie_order, fp_mode=args.fp_mode)
+    V, H = params.num_vertical_scans, params.num_horizontal_scans
+    cap = V * H
+    seqs = np.repeat(np.arange(10 ** 6, 10 ** 6 + Sb, dtype=np.int32)[None, :], 2, 0).reshape(-1)
+    scans = np.repeat(np.arange(2, dtype=np.int32)[:, None], Sb, 1).reshape(-1)
+    pts, cnt = A.synth_batch(cfg, seqs, scans, nthreads=args.threads)
+    d_pts = torch.from_numpy(pts).to(torch.device("cuda", dev_index))
+    del pts
+    d_off = torch.from_numpy((np.arange(2 * Sb, dtype=np.int64) * cap).reshape(2, Sb)).to(d_pts.device)
+    d_cnt = torch.from_numpy(cnt.reshape(2, Sb).astype(np.int32)).to(d_pts.device)
+    b = L.Batch(params, Sb, cap, device=dev_index)
+    b.set_lag(args.lag)
+    b.set_wide(args.wide)
+    for k in range(2):
+        b.step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
+    b.flush()
+    torch.cuda.synchronize()
+    m_sum = float(b.counts()[:, 0].astype(np.float64).sum())
+    ms = b.time_hbm_stages(d_pts.data_ptr(), d_off[1].data_ptr(), d_cnt[1].data_ptr(), d_off[0].data_ptr(),
+                           d_cnt[0].data_ptr(), reps=args.roofline_reps, stream=stream.cuda_stream)
+    n_mean = float(cnt.reshape(2, Sb)[1].mean())
+    b_tot = Sb * (16.0 * n_mean + 20.0 * cap) + 22.0 * m_sum
+    b.close()
+    del d_pts
+    torch.cuda.empty_cache()
+    achieved = b_tot / (ms * 1e-3) / 1e9
+    traffic, src = pmc_traffic(args, Sb, ("k_project", "k_fa_prep4"))
+    return {"streams": Sb, "bytes_per_launch": int(b_tot), "launch_ms": round(ms, 4), "achieved": round(achieved, 1),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+            "note": "%d scans per launch: working set %.2f GB, above the 256 MiB Infinity Cache" % (Sb, b_tot / 1e9)}
+
+
 def main():
     args = parse()
     import torch
@@ -177,7 +226,8 @@ def main():
     dev = torch.device("cuda", local_dev)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
-    params = (L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64)(voxel_tie_order=args.voxel_tie_order)
+    mk_params = L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64
+    params = mk_params(voxel_tie_order=args.voxel_tie_order, fp_mode=args.fp_mode)
     cfg = A.synth_cfg(args.kind)
     V, H = params.num_vertical_scans, params.num_horizontal_scans
     cap = V * H
@@ -244,9 +294,9 @@ def main():
     total_scans = S * K * world
     value = total_scans / elapsed
     alt = None
-    if world == 1 and args.alt_order:  # the other VoxelGrid tie order, same inputs
+    if world == 1 and not args.no_alt_order:  # the other VoxelGrid tie order, same inputs
         alt_order = 1 - args.voxel_tie_order
-        params_alt = (L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64)(voxel_tie_order=alt_order)
+        params_alt = mk_params(voxel_tie_order=alt_order, fp_mode=args.fp_mode)
         batch_alt = L.Batch(params_alt, S, cap, device=local_dev)
         batch_alt.set_groups(args.groups)
         batch_alt.set_lag(args.lag)
@@ -284,6 +334,7 @@ def main():
     t_ms = pair_ms  # k_project + k_fa_prep4
     achieved = (b_proj + b_smooth) / (t_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args, S, ("k_project", "k_fa_prep4"))
+    big = roofline_at(args, L, A, mk_params, cfg, local_dev, stream) if world == 1 and args.roofline_streams > 0 else None
     roofline = {"kernel": "k_project+k_fa_prep4 (projection+smoothness)", "bound": "hbm",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -300,7 +351,8 @@ def main():
                 "traffic_source": traffic_src,
                 "note": ("%d scans per launch: working set below the 256 MiB Infinity Cache (cache-assisted)" % S
                          if b_proj + b_smooth < 256 * 2**20 else
-                         "%d scans per launch: working set above the 256 MiB Infinity Cache" % S)}
+                         "%d scans per launch: working set above the 256 MiB Infinity Cache" % S),
+                "at_roofline_streams": big}
 
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K, "warmup": W,
@@ -310,7 +362,7 @@ def main():
                                % ("C3" if args.kind == "vlp16" else "C4", args.kind.upper(), S),
                    "V": V, "H": H, "points_per_scan": round(n_mean, 1), "streams_per_gpu": S,
                    "parallelism": "sequence-sharded x%d" % world, "stream_groups": args.groups, "lag": args.lag,
-                   "voxel_tie_order": args.voxel_tie_order, "wide": int(batch.wide())},
+                   "voxel_tie_order": args.voxel_tie_order, "fp_mode": args.fp_mode, "wide": int(batch.wide())},
         "roofline": roofline,
         "stages_ms": {"project": round(stage[0], 4), "segment": round(stage[1], 4), "fa_prep": round(stage[2], 4),
                       "extract": round(stage[3], 4), "concat_publish": round(stage[4], 4),
@@ -321,13 +373,15 @@ def main():
         "input_gen_s": round(t_gen, 2),
     }
     if world == 1 and not args.no_cpu_baseline:  # N = 1 only; the reference's own VoxelGrid order (std::sort)
-        params_ref = (L.params_vlp16 if args.kind == "vlp16" else L.params_hdl64)(voxel_tie_order=0)
+        params_ref = mk_params(voxel_tie_order=0, fp_mode=args.fp_mode)
         out["cpu_baseline"] = cpu_baseline(params_ref, cfg, host_pts, host_cnt, args.cpu_seconds)
         out["speedup_vs_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
         if args.cpu_threads > 1:
             out["cpu_baseline_threads"] = cpu_baseline_threads(params_ref, cfg, host_pts, host_cnt, args.cpu_seconds,
                                                                args.cpu_threads)
     if rank == 0:
+        if args.dump_poses:
+            np.save(args.dump_poses, traj_all.cpu().numpy())
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -139,6 +139,12 @@ void lego_params_vlp16(lego_params* p);
 /* HDL-64E-like synthetic config: V=64 evenly spaced -24.8..+2.0 deg, H=2048, G=55. */
 void lego_params_hdl64(lego_params* p);
 int  lego_params_validate(const lego_params* p);
+/* lego_params from the reference's LeGO-LOAM/config/loam_config.yaml (the rosparam keys read by
+ * imageProjection.cpp:57-84 and featureAssociation.cpp:69-81; block-style YAML): keys the file does not
+ * set keep lego_params_vlp16's values; lego_loam/lego_amd/fp_mode and .../voxel_tie_order are this
+ * build's own.  LEGO_EINVAL for an unreadable file, a malformed line or value, or parameters that
+ * lego_params_validate rejects (*p is then unchanged).  Host only: needs no device. */
+int  lego_params_load_yaml(const char* path, lego_params* p);
 /* Number of visible HIP devices (0 when none). */
 int32_t lego_device_count(void);
 
@@ -240,6 +246,13 @@ int  lego_test_sort(uint32_t* keys, int32_t* vals, int32_t n, int32_t is_float);
  * of k_project (-2 = too close to a decision boundary, decided by the exact path) and by the exact
  * glibc-faithful path (imageProjection.cpp:186-207). */
 int  lego_test_project_cells(const lego_params* p, const float* xyzw, int32_t n, int32_t* fast, int32_t* exact);
+/* Overwrite the LM state the next lego_feature_association* call starts from: transformCur (the warm
+ * start), transformSum, isDegenerate, the Last clouds (TransformToEnd'ed, as AssociationOut returns them)
+ * and the kd-trees' staleness (fa.cpp:1356).  LEGO_EINVAL before the first association.  For per-pair LM
+ * parity with a reference's state injected. */
+int  lego_test_set_lm_state(lego_ctx* ctx, const float* transform_cur, const float* transform_sum,
+                            int32_t degenerate, const lego_point* corner_last, int32_t n_corner,
+                            const lego_point* surf_last, int32_t n_surf, int32_t tree_stale);
 /* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
  * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */
 int  lego_debug_prof(uint64_t* out256, int32_t reset);

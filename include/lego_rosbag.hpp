@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <initializer_list>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -82,9 +83,10 @@ inline uint32_t f32(const std::map<std::string, std::string>& f, const char* k) 
 
 // bz2 / lz4-frame inflation through the system libraries (no development headers needed)
 inline void inflate(const std::string& how, const uint8_t* src, size_t n, std::vector<uint8_t>& dst, size_t out_size) {
+  // a garbled size must not turn into a huge allocation (rosbag chunks are ~768 KB by default)
+  if (how == "none" ? n != out_size : out_size > ((size_t)1 << 30)) throw BagError("implausible chunk size");
   dst.resize(out_size);
   if (how == "none") {
-    if (n != out_size) throw BagError("uncompressed chunk size mismatch");
     std::memcpy(dst.data(), src, n);
     return;
   }
@@ -267,6 +269,8 @@ inline PointCloud2View decode_pointcloud2(const BagMessage& msg) {
   const uint32_t dl = rd32();
   need(dl);
   if (ox < 0 || oy < 0 || oz < 0) throw BagError("PointCloud2 without float32 x, y, z");
+  for (const int o : {ox, oy, oz})  // every field inside the point (found by the sanitizer build's fuzz corpus)
+    if ((uint64_t)(uint32_t)o + 4u > point_step) throw BagError("PointCloud2 field outside its point_step");
   const uint64_t npts = (uint64_t)height * width;
   if (npts * point_step > dl || npts > 0x7fffffffull) throw BagError("PointCloud2 data shorter than its points");
   v.data = p + i;

@@ -115,7 +115,10 @@ int  lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* io, void* h
  *     whose optimum is the pose just inserted (the first key frame at transformTobeMapped, later ones at
  *     transformAftMapped), so the key poses are those.
  * lego_mapper_step returns transformAftMapped after the cycle (publishTF's pose, :510-538) and info[4] as
- * lego_s2m_run's.  A mapper serves one call at a time. */
+ * lego_s2m_run's.  A mapper serves one call at a time.  max_map_points / max_key_points are initial
+ * capacities only (the reference has no limits): the raw surrounding map, the scan's clouds, the key-frame
+ * store and the LM's clouds grow on demand.  A failing call (LEGO_ENOMEM / LEGO_EDEVICE) leaves the mapper
+ * as it was before it. */
 typedef struct lego_mapper lego_mapper;
 int  lego_mapper_create(int32_t device, int32_t max_map_points, int64_t max_key_points, lego_mapper** out);
 void lego_mapper_destroy(lego_mapper* m);

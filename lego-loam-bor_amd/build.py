@@ -16,7 +16,7 @@ REPO = os.path.dirname(HERE)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("LEGO_OFFLOAD_ARCH", "gfx950")
 
-FRONTEND_SRC = ["lego_kernels.hip", "lego_frontend.hip", "lego_s2m.hip", "lego_mapper.hip"]
+FRONTEND_SRC = ["lego_kernels.hip", "lego_frontend.hip", "lego_s2m.hip", "lego_mapper.hip", "lego_config.cpp"]
 FRONTEND_DEPS = FRONTEND_SRC + ["lego_device.h", "lego_libm.h", "lego_introsort.h"]
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "--offload-arch=" + ARCH,
              # numerics contract: no FMA contraction, IEEE division/sqrt

@@ -1230,6 +1230,40 @@ int lego_feature_association(lego_ctx* c, lego_association_out* out) {
   return feature_association(c, out, false);
 }
 
+// Test hook: overwrite the LM state the next association starts from (per pair, the
+// reference's transformCur_in and Last clouds injected).  After the first association only.
+int lego_test_set_lm_state(lego_ctx* c, const float* cur6, const float* sum6, int32_t degenerate,
+                           const lego_point* corner_last, int32_t n_corner, const lego_point* surf_last,
+                           int32_t n_surf, int32_t tree_stale) {
+  if (!c || !cur6 || !sum6 || n_corner < 0 || n_surf < 0 || (n_corner && !corner_last) || (n_surf && !surf_last))
+    return LEGO_EINVAL;
+  lego_batch* b = c->b;
+  const LgParams& P = b->P;
+  const LgBufs& B = b->B;
+  if (n_corner > P.V * P.cap_lsharp || n_surf > P.VH) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  if (flush_pending(b) != LEGO_OK || hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  LgState S;
+  if (hipMemcpy(&S, B.state, sizeof(S), hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
+  if (!S.initialized) return LEGO_EINVAL;
+  for (int k = 0; k < 6; ++k) {
+    S.cur[k] = cur6[k];
+    S.sum[k] = sum6[k];
+  }
+  S.is_degenerate = degenerate ? 1 : 0;
+  S.n_corner_last = n_corner;
+  S.n_surf_last = n_surf;
+  S.tree_stale = tree_stale ? 1 : 0;
+  const size_t cls = (size_t)P.V * P.cap_lsharp;
+  if ((n_corner && hipMemcpy(B.corner_last + (size_t)S.last_buf * cls, corner_last, (size_t)n_corner * 16,
+                             hipMemcpyHostToDevice) != hipSuccess) ||
+      (n_surf && hipMemcpy(B.surf_last + (size_t)S.last_buf * P.VH, surf_last, (size_t)n_surf * 16,
+                           hipMemcpyHostToDevice) != hipSuccess) ||
+      hipMemcpy(B.state, &S, sizeof(S), hipMemcpyHostToDevice) != hipSuccess)
+    return LEGO_EDEVICE;
+  return LEGO_OK;
+}
+
 int lego_feature_association_from(lego_ctx* c, const lego_projection_out* in, lego_association_out* out) {
   if (!c || !in) return LEGO_EINVAL;
   lego_batch* b = c->b;

@@ -2429,6 +2429,9 @@ LG_DEVICE void voxel_sort_stable(unsigned* key, uint16_t* val, int n) {
 
 // kMode 0: voxel_tie_order 0 (libstdc++ introsort permutation); 1 / 2: stable order, rings of at most /
 // more than 1024 points; 3: either order, any ring (one kernel for the whole step).
+// The ring's points are read in batches of VX_U a lane with every load of a batch issued before any is
+// used (a loop of single loads pays one memory latency per point); L.vval is the identity on entry.
+#define VX_U 8
 template <int kMode>
 LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, int n, int base_pos, RingOut& o) {
   const float4* fa = v.fa + base_pos;  // L.vval holds positions relative to the ring start
@@ -2438,10 +2441,16 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
   const float leaf = 0.2f;
   const float inv = 1.0f / leaf;
   float mnx = FLT_MAX, mny = FLT_MAX, mnz = FLT_MAX, mxx = -FLT_MAX, mxy = -FLT_MAX, mxz = -FLT_MAX;
-  for (int t = lane; t < n; t += 64) {
-    const float4 p = fa[L.vval[t]];
-    mnx = (p.x < mnx) ? p.x : mnx; mny = (p.y < mny) ? p.y : mny; mnz = (p.z < mnz) ? p.z : mnz;
-    mxx = (p.x > mxx) ? p.x : mxx; mxy = (p.y > mxy) ? p.y : mxy; mxz = (p.z > mxz) ? p.z : mxz;
+  for (int t0 = lane; t0 < n; t0 += 64 * VX_U) {  // getMinMax3D (clamped repeats do not change a min / max)
+    float4 pk[VX_U];
+#pragma unroll
+    for (int u = 0; u < VX_U; ++u) pk[u] = fa[min(t0 + 64 * u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < VX_U; ++u) {
+      const float4 p = pk[u];
+      mnx = (p.x < mnx) ? p.x : mnx; mny = (p.y < mny) ? p.y : mny; mnz = (p.z < mnz) ? p.z : mnz;
+      mxx = (p.x > mxx) ? p.x : mxx; mxy = (p.y > mxy) ? p.y : mxy; mxz = (p.z > mxz) ? p.z : mxz;
+    }
   }
   mnx = wave_min(mnx); mny = wave_min(mny); mnz = wave_min(mnz);
   mxx = wave_max(mxx); mxy = wave_max(mxy); mxz = wave_max(mxz);
@@ -2458,12 +2467,19 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
   const int maxbx = (int)floorf(mxx * inv), maxby = (int)floorf(mxy * inv);
   const int divx = maxbx - minbx + 1, divy = maxby - minby + 1;
   const int mul1 = divx, mul2 = divx * divy;
-  for (int t = lane; t < n; t += 64) {
-    const float4 p = fa[L.vval[t]];
-    const int i0 = (int)(floorf(p.x * inv) - (float)minbx);
-    const int i1 = (int)(floorf(p.y * inv) - (float)minby);
-    const int i2 = (int)(floorf(p.z * inv) - (float)minbz);
-    L.u.vkey[t] = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+  for (int t0 = lane; t0 < n; t0 += 64 * VX_U) {
+    float4 pk[VX_U];
+#pragma unroll
+    for (int u = 0; u < VX_U; ++u) pk[u] = fa[min(t0 + 64 * u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < VX_U; ++u) {
+      const int t = t0 + 64 * u;
+      const float4 p = pk[u];
+      const int i0 = (int)(floorf(p.x * inv) - (float)minbx);
+      const int i1 = (int)(floorf(p.y * inv) - (float)minby);
+      const int i2 = (int)(floorf(p.z * inv) - (float)minbz);
+      if (t < n) L.u.vkey[t] = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+    }
   }
   __syncthreads();
   PROF_T(t_vs0);
@@ -2481,15 +2497,20 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
     const int t = base + lane;
     const bool start = t < n && (t == 0 || L.u.vkey[t] != L.u.vkey[t - 1]);
     const unsigned long long m = __ballot(start);
-    if (start) {
+    if (start) {  // CentroidPoint: float sums in sorted order; the run's loads VX_U at a time in flight
       const unsigned k = L.u.vkey[t];
+      int e = t + 1;
+      while (e < n && L.u.vkey[e] == k) ++e;
       float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-      int u = t;
-      for (; u < n && L.u.vkey[u] == k; ++u) {
-        const float4 p = fa[L.vval[u]];
-        sx += p.x; sy += p.y; sz += p.z; si += p.w;
+      for (int g = t; g < e; g += VX_U) {
+        float4 pk[VX_U];
+#pragma unroll
+        for (int u = 0; u < VX_U; ++u) pk[u] = fa[L.vval[min(g + u, e - 1)]];
+#pragma unroll
+        for (int u = 0; u < VX_U; ++u)
+          if (g + u < e) { sx += pk[u].x; sy += pk[u].y; sz += pk[u].z; si += pk[u].w; }
       }
-      const float cntf = (float)(u - t);
+      const float cntf = (float)(e - t);
       o.lflat[running + popc_below(m)] = make_float4(sx / cntf, sy / cntf, sz / cntf, si / cntf);
     }
     running += __popcll(m);

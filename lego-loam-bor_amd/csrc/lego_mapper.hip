@@ -132,19 +132,45 @@ bool dmalloc(T** p, size_t n) {
   return hipMalloc((void**)p, (n ? n : 1) * sizeof(T)) == hipSuccess;
 }
 
+// Grow a device array to hold `need` elements (at least doubling), keeping its first `keep` elements.
+// The mapper's calls are synchronous (null stream), so nothing still reads the old array.
+template <typename T>
+int grow(T** p, size_t need, size_t* cap, size_t keep) {
+  if (need <= *cap) return LEGO_OK;
+  const size_t nc = std::max(need, *cap * 2);
+  T* q = nullptr;
+  if (!dmalloc(&q, nc)) return LEGO_ENOMEM;
+  if (keep && *p && hipMemcpy(q, *p, keep * sizeof(T), hipMemcpyDeviceToDevice) != hipSuccess) {
+    hipFree(q);
+    return LEGO_EDEVICE;
+  }
+  if (*p) hipFree(*p);
+  *p = q;
+  *cap = nc;
+  return LEGO_OK;
+}
+
 }  // namespace
 
+// The reference's mapping thread has no size limits: the key-frame store, the raw surrounding map (the
+// key frames' parts concatenated before the VoxelGrid), the part lists and the scan-to-map LM's clouds
+// all grow on demand here; max_map_points / max_key_points are only the initial capacities.
 struct lego_mapper {
   int device = 0;
   int max_map = 0;
-  int64_t max_key = 0;
-  lego_s2m* s2m = nullptr;
+  lego_s2m* s2m = nullptr;       // scan-to-map LM (clouds up to lm_cap points)
+  int lm_cap = 0;
+  lego_s2m* vox = nullptr;       // VoxelGrid engine (clouds up to vox_cap points)
+  int vox_cap = 0;
   lego_point* d_keys = nullptr;  // key-frame store
+  size_t keys_cap = 0;
   int64_t key_used = 0;
   lego_point* d_raw = nullptr;   // [corner map raw | surf map raw | scan corner | scan surf | scan outlier]
   lego_point* d_vox = nullptr;   // their VoxelGrids, at the same offsets
-  lego_point* d_tot = nullptr;   // surf total: raw (2 * max_map) then its VoxelGrid
-  int parts_cap = 0;
+  size_t raw_cap = 0, vox_buf_cap = 0;
+  lego_point* d_tot = nullptr;   // surf total: raw, then its VoxelGrid right after it
+  size_t tot_cap = 0;
+  size_t parts_cap = 0, off_cap = 0, n_cap = 0, off2_cap = 0, pose_cap = 0;
   int64_t* d_off = nullptr;      // part / cloud offsets
   int32_t* d_n = nullptr;
   int64_t* d_off2 = nullptr;
@@ -173,8 +199,38 @@ extern "C" void lego_mapper_destroy(lego_mapper* m) {
                   (void*)m->d_s2m_off, (void*)m->d_s2m_n, (void*)m->d_t, (void*)m->d_dg, (void*)m->d_info})
     if (p) hipFree(p);
   if (m->s2m) lego_s2m_destroy(m->s2m);
+  if (m->vox) lego_s2m_destroy(m->vox);
   delete m;
 }
+
+namespace {
+// an s2m engine (LM or VoxelGrid) for clouds of at least `need` points: recreated larger when needed
+int ensure_engine(int device, lego_s2m** e, int* cap, int64_t need) {
+  if (need <= *cap && *e) return LEGO_OK;
+  if (need > LEGO_MAX_POINTS) return LEGO_EINVAL;
+  const int64_t nc = std::min<int64_t>(LEGO_MAX_POINTS, std::max<int64_t>(need, 2 * (int64_t)*cap));
+  if (*e) {
+    hipDeviceSynchronize();
+    lego_s2m_destroy(*e);
+    *e = nullptr;
+    *cap = 0;
+  }
+  const int rc = lego_s2m_create(device, 1, (int32_t)nc, e);
+  if (rc != LEGO_OK) return rc;
+  *cap = (int)nc;
+  return LEGO_OK;
+}
+int ensure_parts(lego_mapper* m, size_t np) {  // part lists of np parts (and >= 8 VoxelGrid clouds)
+  np = std::max<size_t>(np, 8);
+  if (np <= m->parts_cap) return LEGO_OK;
+  int rc;
+  if ((rc = grow(&m->d_off, np, &m->off_cap, 0)) || (rc = grow(&m->d_n, np, &m->n_cap, 0)) ||
+      (rc = grow(&m->d_off2, np, &m->off2_cap, 0)) || (rc = grow(&m->d_pose, 6 * np, &m->pose_cap, 0)))
+    return rc;
+  m->parts_cap = np;
+  return LEGO_OK;
+}
+}  // namespace
 
 extern "C" int lego_mapper_create(int32_t device, int32_t max_map_points, int64_t max_key_points, lego_mapper** out) {
   if (!out) return LEGO_EINVAL;
@@ -184,19 +240,22 @@ extern "C" int lego_mapper_create(int32_t device, int32_t max_map_points, int64_
   if (!m) return LEGO_ENOMEM;
   m->device = device;
   m->max_map = max_map_points;
-  m->max_key = max_key_points;
-  int rc = lego_s2m_create(device, 1, max_map_points, &m->s2m);
-  if (rc != LEGO_OK) {
+  if (hipSetDevice(device) != hipSuccess) {
     delete m;
+    return LEGO_EDEVICE;
+  }
+  int rc = ensure_engine(device, &m->s2m, &m->lm_cap, max_map_points);
+  if (rc == LEGO_OK) rc = ensure_engine(device, &m->vox, &m->vox_cap, 2 * (int64_t)max_map_points);
+  if (rc != LEGO_OK) {
+    lego_mapper_destroy(m);
     return rc;
   }
   const size_t R = (size_t)5 * max_map_points;
-  m->parts_cap = 4096;
-  if (!dmalloc(&m->d_keys, (size_t)max_key_points) || !dmalloc(&m->d_raw, R) || !dmalloc(&m->d_vox, R) ||
-      !dmalloc(&m->d_tot, (size_t)4 * max_map_points) || !dmalloc(&m->d_off, m->parts_cap) ||
-      !dmalloc(&m->d_n, m->parts_cap) || !dmalloc(&m->d_off2, m->parts_cap) || !dmalloc(&m->d_pose, 6 * m->parts_cap) ||
-      !dmalloc(&m->d_leaf, 8) || !dmalloc(&m->d_out_n, 8) || !dmalloc(&m->d_status, 8) || !dmalloc(&m->d_s2m_off, 4) ||
-      !dmalloc(&m->d_s2m_n, 4) || !dmalloc(&m->d_t, 6) || !dmalloc(&m->d_dg, 1) || !dmalloc(&m->d_info, 4)) {
+  if (grow(&m->d_keys, (size_t)max_key_points, &m->keys_cap, 0) || grow(&m->d_raw, R, &m->raw_cap, 0) ||
+      grow(&m->d_vox, R, &m->vox_buf_cap, 0) || grow(&m->d_tot, (size_t)4 * max_map_points, &m->tot_cap, 0) ||
+      ensure_parts(m, 4096) || !dmalloc(&m->d_leaf, 8) || !dmalloc(&m->d_out_n, 8) || !dmalloc(&m->d_status, 8) ||
+      !dmalloc(&m->d_s2m_off, 4) || !dmalloc(&m->d_s2m_n, 4) || !dmalloc(&m->d_t, 6) || !dmalloc(&m->d_dg, 1) ||
+      !dmalloc(&m->d_info, 4)) {
     lego_mapper_destroy(m);
     return LEGO_ENOMEM;
   }
@@ -267,11 +326,13 @@ extern "C" int lego_mapper_step(lego_mapper* m, const lego_point* corner_last, i
   if (!m || !transform_sum || !transform_aft_mapped || !info || n_corner < 0 || n_surf < 0 || n_outlier < 0 ||
       (n_corner && !corner_last) || (n_surf && !surf_last) || (n_outlier && !outlier_last))
     return LEGO_EINVAL;
-  if (n_corner > m->max_map || n_surf > m->max_map || n_outlier > m->max_map) return LEGO_EINVAL;
   MCHECK(hipSetDevice(m->device));
+  // Nothing of the mapper's state is committed before every capacity is in place: a failure leaves the
+  // mapper as it was before the call (the caller may retry the same scan).
+  float t_tobe[6];
+  std::vector<int> existing = m->existing;
   // OdometryToTransform (:1540) + transformAssociateToMap (:1542)
-  memcpy(m->t_sum, transform_sum, sizeof(m->t_sum));
-  associate_to_map(m->t_sum, m->t_bef, m->t_aft, m->t_tobe);
+  associate_to_map(transform_sum, m->t_bef, m->t_aft, t_tobe);
   // extractSurroundingKeyFrames, loop closure off (:915-995)
   if (!m->kf.empty()) {
     const float* c = m->t_aft + 3;  // currentRobotPosPoint, set by the last saveKeyFramesAndFactor
@@ -293,34 +354,41 @@ extern "C" int lego_mapper_step(lego_mapper* m, const lego_point* corner_last, i
     std::vector<int> ids;
     for (const auto& q : ds) ids.push_back((int)q.intensity);
     std::vector<int> keep;
-    for (int id : m->existing)
+    for (int id : existing)
       if (std::find(ids.begin(), ids.end(), id) != ids.end()) keep.push_back(id);
-    m->existing = keep;
+    existing = keep;
     for (int id : ids)
-      if (std::find(m->existing.begin(), m->existing.end(), id) == m->existing.end()) m->existing.push_back(id);
+      if (std::find(existing.begin(), existing.end(), id) == existing.end()) existing.push_back(id);
   }
   // the map's parts: corner clouds of the existing key frames, then their surf and outlier clouds, frame
   // by frame (:982-986), transformed by their key poses into [corner raw | surf raw]
-  const int np = 3 * (int)m->existing.size();
-  if (np > m->parts_cap) return LEGO_EINVAL;
+  const int np = 3 * (int)existing.size();
+  int rc = ensure_parts(m, (size_t)np);
+  if (rc) return rc;
   std::vector<int64_t> in_off, out_off;
   std::vector<int32_t> in_n;
   std::vector<float> pose;
   int64_t ncm = 0, nsm = 0;
-  for (int id : m->existing) {
+  for (int id : existing) {
     const KeyFrame& k = m->kf[id];
     in_off.push_back(k.off[0]); in_n.push_back(k.n[0]); out_off.push_back(ncm); ncm += k.n[0];
     pose.insert(pose.end(), k.pose, k.pose + 6);
   }
-  for (int id : m->existing) {
+  for (int id : existing) {
     const KeyFrame& k = m->kf[id];
     for (int j = 1; j < 3; ++j) {
       in_off.push_back(k.off[j]); in_n.push_back(k.n[j]); out_off.push_back(ncm + nsm); nsm += k.n[j];
       pose.insert(pose.end(), k.pose, k.pose + 6);
     }
   }
-  if (ncm > m->max_map || nsm > m->max_map) return LEGO_EINVAL;
+  // capacities for this cycle's clouds: the raw map, the scan's clouds, their VoxelGrids
   const int64_t base_sc = ncm + nsm;
+  const int64_t n_raw = base_sc + n_corner + n_surf + n_outlier;
+  const int64_t big = std::max<int64_t>(std::max<int64_t>(ncm, nsm), (int64_t)n_corner + n_surf + n_outlier);
+  if ((rc = grow(&m->d_raw, (size_t)n_raw, &m->raw_cap, 0)) || (rc = grow(&m->d_vox, (size_t)n_raw, &m->vox_buf_cap, 0)) ||
+      (rc = grow(&m->d_tot, (size_t)2 * (n_surf + n_outlier), &m->tot_cap, 0)) ||
+      (rc = ensure_engine(m->device, &m->vox, &m->vox_cap, big)))
+    return rc;
   // the scan's clouds after the map's
   if (n_corner) MCHECK(hipMemcpy(m->d_raw + base_sc, corner_last, (size_t)n_corner * sizeof(lego_point), hipMemcpyHostToDevice));
   if (n_surf) MCHECK(hipMemcpy(m->d_raw + base_sc + n_corner, surf_last, (size_t)n_surf * sizeof(lego_point), hipMemcpyHostToDevice));
@@ -344,7 +412,7 @@ extern "C" int lego_mapper_step(lego_mapper* m, const lego_point* corner_last, i
   MCHECK(hipMemcpy(m->d_n, vn, sizeof(vn), hipMemcpyHostToDevice));
   MCHECK(hipMemcpy(m->d_leaf, leaf, sizeof(leaf), hipMemcpyHostToDevice));
   lego_map_voxel_io vio{m->d_raw, m->d_off, m->d_n, m->d_leaf, m->d_vox, m->d_off, m->d_out_n, m->d_status};
-  int rc = lego_map_voxel(m->s2m, 5, &vio, nullptr);
+  rc = lego_map_voxel(m->vox, 5, &vio, nullptr);
   if (rc) return rc;
   int32_t on[5];
   MCHECK(hipMemcpy(on, m->d_out_n, sizeof(on), hipMemcpyDeviceToHost));
@@ -355,23 +423,30 @@ extern "C" int lego_mapper_step(lego_mapper* m, const lego_point* corner_last, i
   if (on[3]) MCHECK(hipMemcpy(m->d_tot, m->d_vox + voff[3], (size_t)on[3] * sizeof(lego_point), hipMemcpyDeviceToDevice));
   if (on[4])
     MCHECK(hipMemcpy(m->d_tot + on[3], m->d_vox + voff[4], (size_t)on[4] * sizeof(lego_point), hipMemcpyDeviceToDevice));
-  const int64_t toff[2] = {0, 2 * (int64_t)m->max_map};
+  const int64_t toff[2] = {0, (int64_t)ntot};  // the VoxelGrid's output right after its input
   MCHECK(hipMemcpy(m->d_off2, toff, sizeof(toff), hipMemcpyHostToDevice));
   MCHECK(hipMemcpy(m->d_n + 5, &ntot, sizeof(ntot), hipMemcpyHostToDevice));
   lego_map_voxel_io vio2{m->d_tot, m->d_off2, m->d_n + 5, m->d_leaf + 1, m->d_tot, m->d_off2 + 1, m->d_out_n + 5,
                          m->d_status + 5};
-  rc = lego_map_voxel(m->s2m, 1, &vio2, nullptr);
+  rc = lego_map_voxel(m->vox, 1, &vio2, nullptr);
   if (rc) return rc;
   // scan2MapOptimization (:1548)
-  const int64_t s_off[4] = {voff[2], 2 * (int64_t)m->max_map, voff[0], voff[1]};
+  const int64_t s_off[4] = {voff[2], (int64_t)ntot, voff[0], voff[1]};
   MCHECK(hipMemcpy(m->d_s2m_off, s_off, sizeof(s_off), hipMemcpyHostToDevice));
   const int32_t s_n[3] = {on[2], on[0], on[1]};  // corner DS; surf total from the second VoxelGrid
   int32_t ntot_ds = -1;
   MCHECK(hipMemcpy(&ntot_ds, m->d_out_n + 5, sizeof(int32_t), hipMemcpyDeviceToHost));
   if (ntot_ds < 0) return LEGO_EINVAL;
   const int32_t s_cnt[4] = {s_n[0], ntot_ds, s_n[1], s_n[2]};
+  // the LM engine's clouds (its gate: each map <= its capacity, the scan's corner + surf <= it)
+  if ((rc = ensure_engine(m->device, &m->s2m, &m->lm_cap,
+                          std::max<int64_t>(std::max(s_n[1], s_n[2]), (int64_t)s_n[0] + ntot_ds))))
+    return rc;
+  // the key frame this cycle may store (saveKeyFramesAndFactor), before any state changes
+  if ((rc = grow(&m->d_keys, (size_t)(m->key_used + on[2] + on[3] + on[4]), &m->keys_cap, (size_t)m->key_used)))
+    return rc;
   MCHECK(hipMemcpy(m->d_s2m_n, s_cnt, sizeof(s_cnt), hipMemcpyHostToDevice));
-  MCHECK(hipMemcpy(m->d_t, m->t_tobe, sizeof(m->t_tobe), hipMemcpyHostToDevice));
+  MCHECK(hipMemcpy(m->d_t, t_tobe, sizeof(t_tobe), hipMemcpyHostToDevice));
   MCHECK(hipMemcpy(m->d_dg, &m->degenerate, sizeof(int32_t), hipMemcpyHostToDevice));
   lego_s2m_io sio;
   sio.corner = m->d_vox; sio.corner_off = m->d_s2m_off; sio.corner_n = m->d_s2m_n;
@@ -381,10 +456,17 @@ extern "C" int lego_mapper_step(lego_mapper* m, const lego_point* corner_last, i
   sio.transform = m->d_t; sio.degenerate = m->d_dg; sio.info = m->d_info;
   rc = lego_s2m_run(m->s2m, 1, &sio, nullptr);
   if (rc) return rc;
-  MCHECK(hipMemcpy(m->t_tobe, m->d_t, sizeof(m->t_tobe), hipMemcpyDeviceToHost));
-  MCHECK(hipMemcpy(&m->degenerate, m->d_dg, sizeof(int32_t), hipMemcpyDeviceToHost));
-  MCHECK(hipMemcpy(info, m->d_info, 4 * sizeof(int32_t), hipMemcpyDeviceToHost));
-  if (info[0] < 0) return LEGO_EINVAL;  // a cloud over max_map_points (lego_s2m_run's gate)
+  int32_t degenerate = 0, inf[4];
+  MCHECK(hipMemcpy(t_tobe, m->d_t, sizeof(t_tobe), hipMemcpyDeviceToHost));
+  MCHECK(hipMemcpy(&degenerate, m->d_dg, sizeof(int32_t), hipMemcpyDeviceToHost));
+  MCHECK(hipMemcpy(inf, m->d_info, 4 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (inf[0] < 0) return LEGO_EDEVICE;  // cannot happen: the LM engine was sized for these clouds
+  // commit: every fallible step is behind us
+  memcpy(info, inf, sizeof(inf));
+  memcpy(m->t_sum, transform_sum, sizeof(m->t_sum));
+  memcpy(m->t_tobe, t_tobe, sizeof(t_tobe));
+  m->degenerate = degenerate;
+  m->existing.swap(existing);
   if (info[0] == 1) {  // transformUpdate (:389-395)
     memcpy(m->t_bef, m->t_sum, sizeof(m->t_sum));
     memcpy(m->t_aft, m->t_tobe, sizeof(m->t_tobe));
@@ -397,8 +479,7 @@ extern "C" int lego_mapper_step(lego_mapper* m, const lego_point* corner_last, i
     memcpy(m->prev_pos, cur, sizeof(m->prev_pos));
     KeyFrame k;
     memcpy(k.pose, m->kf.empty() ? m->t_tobe : m->t_aft, sizeof(k.pose));
-    const int32_t kn[3] = {on[2], on[3], on[4]};
-    if (m->key_used + kn[0] + kn[1] + kn[2] > m->max_key) return LEGO_ENOMEM;
+    const int32_t kn[3] = {on[2], on[3], on[4]};  // room reserved above
     for (int j = 0; j < 3; ++j) {
       k.off[j] = m->key_used;
       k.n[j] = kn[j];

@@ -1156,8 +1156,8 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vxf_keys(lego_map_voxel_io io, 
   const int i = t * S2M_THREADS + tid;
   if (i >= ns) return;
   const size_t slot = (size_t)base + i;
-  if (bad) {  // sorts after every cloud's entries; never read
-    k64[slot] = (unsigned long long)n_clouds << 32;
+  if (bad) {  // sorts inside cloud c's own range (every later cloud keeps its compact offset); never read
+    k64[slot] = (unsigned long long)c << 32;
     vals[slot] = 0u;
     return;
   }

@@ -58,6 +58,8 @@ def lib():
         L.lego_params_vlp16.argtypes = [P(LegoParams)]
         L.lego_params_hdl64.argtypes = [P(LegoParams)]
         L.lego_params_validate.argtypes = [P(LegoParams)]
+        L.lego_params_load_yaml.argtypes = [C.c_char_p, P(LegoParams)]
+        L.lego_test_libm_d.argtypes = [P(C.c_double), P(C.c_double), P(C.c_double), C.c_int32, C.c_int32]
         L.lego_device_count.restype = C.c_int32
         L.lego_ctx_create.argtypes = [P(LegoParams), C.c_int32, P(C.c_void_p)]
         L.lego_ctx_destroy.argtypes = [C.c_void_p]
@@ -65,6 +67,8 @@ def lib():
                                          C.c_int32, P(LegoProjectionOut)]
         L.lego_feature_association.argtypes = [C.c_void_p, P(LegoAssociationOut)]
         L.lego_feature_association_from.argtypes = [C.c_void_p, P(LegoProjectionOut), P(LegoAssociationOut)]
+        L.lego_test_set_lm_state.argtypes = [C.c_void_p, P(C.c_float), P(C.c_float), C.c_int32, C.c_void_p, C.c_int32,
+                                             C.c_void_p, C.c_int32, C.c_int32]
         L.lego_batch_create.argtypes = [P(LegoParams), C.c_int32, C.c_int32, C.c_int32, P(C.c_void_p)]
         L.lego_batch_destroy.argtypes = [C.c_void_p]
         L.lego_batch_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -112,6 +116,16 @@ def _check(rc, what):
 def params_vlp16(**over):
     p = LegoParams()
     lib().lego_params_vlp16(C.byref(p))
+    for k, v in over.items():
+        setattr(p, k, v)
+    return p
+
+
+def params_from_yaml(path, **over):
+    """lego_params from the reference's loam_config.yaml (lego_params_load_yaml)."""
+    p = LegoParams()
+    lib().lego_params_vlp16(C.byref(p))
+    _check(lib().lego_params_load_yaml(os.fsencode(path), C.byref(p)), "lego_params_load_yaml(%s)" % path)
     for k, v in over.items():
         setattr(p, k, v)
     return p
@@ -169,6 +183,15 @@ class Frontend:
             _check(lib().lego_feature_association_from(self.h, C.byref(pin), C.byref(out)),
                    "lego_feature_association_from")
         return association_to_dict(out)
+
+    def set_lm_state(self, transform_cur, transform_sum, degenerate, corner_last, surf_last, tree_stale):
+        """Test hook (lego_test_set_lm_state): the LM state the next association starts from."""
+        f = lambda a, k: np.ascontiguousarray(np.asarray(a, np.float32).reshape(-1, k))  # noqa: E731
+        cur, sm, cl, sl = f(transform_cur, 6), f(transform_sum, 6), f(corner_last, 4), f(surf_last, 4)
+        fp = C.POINTER(C.c_float)
+        _check(lib().lego_test_set_lm_state(self.h, cur.ctypes.data_as(fp), sm.ctypes.data_as(fp), int(degenerate),
+                                            cl.ctypes.data, len(cl), sl.ctypes.data, len(sl), int(tree_stale)),
+               "lego_test_set_lm_state")
 
 
 class Batch:

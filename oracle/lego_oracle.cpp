@@ -1346,6 +1346,14 @@ int oracle_smoothness(oracle_ctx* c, int k, float* value, int64_t* ind) {
   return LEGO_OK;
 }
 
+// Test hook: the LM members that are not in the AssociationOut (featureAssociation.h:115, the kd-tree
+// rebuild flag of :1356): isDegenerate and "trees stale" after the last call.
+int oracle_lm_flags(oracle_ctx* c, int32_t* degenerate, int32_t* tree_stale) {
+  *degenerate = c->fa.isDegenerate ? 1 : 0;
+  *tree_stale = c->fa.tree_stale ? 1 : 0;
+  return LEGO_OK;
+}
+
 // Test hook: libstdc++ std::sort of (key, val) pairs by key only (the reference's sort semantics).
 int oracle_std_sort(uint32_t* keys, int32_t* vals, int n, int is_float) {
   if (is_float) {
@@ -1371,9 +1379,9 @@ float oracle_asinf(float x) { return asinf(x); }
 // bits (LEGO_ST_VOXEL_OVERFLOW) and the output size in *n_out.
 int oracle_voxel_grid(const float* in, int n, float leaf, int stable, float* out, int* n_out) {
   std::vector<Pt> v((size_t)n), o;
-  std::memcpy(v.data(), in, (size_t)n * sizeof(Pt));
+  if (n > 0) std::memcpy(v.data(), in, (size_t)n * sizeof(Pt));
   const int st = voxel_grid(v, leaf, o, stable != 0);
-  std::memcpy(out, o.data(), o.size() * sizeof(Pt));
+  if (!o.empty()) std::memcpy(out, o.data(), o.size() * sizeof(Pt));
   *n_out = (int)o.size();
   return st;
 }

@@ -38,6 +38,7 @@ def lib():
         L.oracle_feature_association.argtypes = [C.c_void_p, P(A.LegoAssociationOut)]
         L.oracle_feature_association_from.argtypes = [C.c_void_p, P(A.LegoProjectionOut), P(A.LegoAssociationOut)]
         L.oracle_smoothness.argtypes = [C.c_void_p, C.c_int, P(C.c_float), P(C.c_int64)]
+        L.oracle_lm_flags.argtypes = [C.c_void_p, P(C.c_int32), P(C.c_int32)]
         L.oracle_std_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int, C.c_int]
         L.oracle_atan2f.argtypes = [C.c_float, C.c_float]
         L.oracle_atan2f.restype = C.c_float
@@ -83,6 +84,12 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("oracle_feature_association rc=%d" % rc)
         return A.association_to_dict(out)
+
+    def lm_flags(self):
+        """(isDegenerate, kd-trees stale) after the last feature_association."""
+        d, t = C.c_int32(), C.c_int32()
+        lib().oracle_lm_flags(self.h, C.byref(d), C.byref(t))
+        return d.value, t.value
 
     def smoothness(self, k):
         v = C.c_float()

@@ -93,3 +93,59 @@ def test_synth_is_deterministic():
     pts, cnt = A.synth_batch(cfg, [3, 4], [5, 5], nthreads=2)
     assert cnt[0] == a.shape[0] and np.array_equal(pts[0, :cnt[0]], a)
     assert not np.array_equal(pts[1, :cnt[1]][:100], a[:100])
+
+
+YAML_VLP16 = """\
+lego_loam:
+    # a VLP-16, as the reference's config/loam_config.yaml
+    laser:
+        num_vertical_scans: 16          # rings
+        num_horizontal_scans: 1800
+        ground_scan_index: 7
+        vertical_angle_bottom: -15      # degrees
+        vertical_angle_top: 15
+        sensor_mount_angle: 0
+        scan_period: 0.1
+    imageProjection:
+        segment_valid_point_num: 5
+        segment_valid_line_num: 3
+        segment_theta: 60.0
+    featureAssociation:
+        edge_threshold: 0.1
+        surf_threshold: 0.1
+        nearest_feature_search_distance: 5
+    mapping:
+        enable_loop_closure: false
+        mapping_frequency_divider: 5
+        surrounding_keyframe_search_radius: 50.0
+"""
+
+
+def test_params_from_yaml(tmp_path):
+    """lego_params_load_yaml reads the reference's loam_config.yaml layout: the VLP-16 file gives
+    lego_params_vlp16 exactly; an HDL-64E-like file and this build's own keys override; malformed
+    files and values are rejected without touching the output."""
+    f = tmp_path / "loam_config.yaml"
+    f.write_text(YAML_VLP16)
+    p, q = L.params_from_yaml(str(f)), L.params_vlp16()
+    assert bytes(p) == bytes(q)
+    f.write_text(YAML_VLP16.replace("num_vertical_scans: 16", "num_vertical_scans: 64")
+                 .replace("num_horizontal_scans: 1800", "num_horizontal_scans: 2048")
+                 .replace("ground_scan_index: 7", "ground_scan_index: 55")
+                 .replace("vertical_angle_bottom: -15", "vertical_angle_bottom: -24.8")
+                 .replace("vertical_angle_top: 15", "vertical_angle_top: 2.0")
+                 + "    lego_amd:\n        fp_mode: 1\n        voxel_tie_order: 1\n")
+    p = L.params_from_yaml(str(f))
+    h = L.params_hdl64(fp_mode=1, voxel_tie_order=1)
+    assert bytes(p) == bytes(h)
+    for bad in (YAML_VLP16.replace("scan_period: 0.1", "scan_period: fast"),        # malformed value
+                YAML_VLP16.replace("ground_scan_index: 7", "ground_scan_index: 99"),  # fails validation
+                YAML_VLP16 + "  - a sequence item\n"):                               # not the file's YAML
+        f.write_text(bad)
+        out = L.params_vlp16(segment_theta=1.0)
+        rc = L.lib().lego_params_load_yaml(os.fsencode(str(f)), C.byref(out))
+        assert rc == A.LEGO_EINVAL and out.segment_theta == 1.0
+    assert L.lib().lego_params_load_yaml(b"/nonexistent/loam_config.yaml", C.byref(out)) == A.LEGO_EINVAL
+    ref = "/root/reference/LeGO-LOAM/config/loam_config.yaml"
+    if os.path.exists(ref):  # the reference's own file (build container only)
+        assert bytes(L.params_from_yaml(ref)) == bytes(L.params_vlp16())

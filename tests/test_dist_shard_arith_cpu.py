@@ -1,6 +1,7 @@
-"""World-size-2 gloo test of the multi-GPU layout: sequences are sharded across ranks
-with no collective on the data path; the only exchange is the final all-gather of per-sequence
-trajectories to rank 0.  Run on CPU with the oracle standing in for each rank's device."""
+"""Shard / gather ARITHMETIC only (world-size-2 gloo, CPU): sequences are sharded across ranks with no
+collective on the data path; the only exchange is the final all-gather of per-sequence trajectories to
+rank 0.  The oracle stands in for each rank's device here; tests/test_gpu_dist.py runs the product path
+(bench.py under torch.distributed.run, lego_amd.Batch on the HIP library)."""
 import os
 import socket
 
@@ -55,7 +56,7 @@ def _worker(rank, world, port, nseq, nscans, q):
     dist.destroy_process_group()
 
 
-def test_sequence_sharding_and_trajectory_gather():
+def test_shard_and_gather_arithmetic_with_oracle_ranks():
     world, nseq, nscans = 2, 4, 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

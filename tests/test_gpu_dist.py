@@ -1,0 +1,54 @@
+"""The multi-GPU path with the product: bench.py launched by torch.distributed.run with two
+ranks, each running its own 8 sequences through lego_amd.Batch on the HIP library, the trajectories
+all-gathered to rank 0 and the step time max-reduced over ranks.  On a one-GPU box both ranks share
+cuda:0 and the collectives run over gloo (RCCL over xGMI is the driver's 8-GPU run).  Rank 0's gathered
+poses must equal one process running the same 16 sequences.  (tests/test_dist_cpu.py checks only the
+shard / gather arithmetic, on the oracle.)"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMMON = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-alt-order", "--roofline-streams", "0",
+          "--roofline-reps", "2", "--threads", "4"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_line(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(lines) == 1, stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_torchrun_two_ranks_match_single_process(gpu, tmp_path):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
+    p2, p1 = str(tmp_path / "poses2.npy"), str(tmp_path / "poses1.npy")
+    cmd2 = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2",
+            "--dist-backend", "gloo", "--streams", "8", "--dump-poses", p2] + COMMON
+    r2 = subprocess.run(cmd2, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, universal_newlines=True, env=env,
+                        timeout=300, cwd=REPO)
+    assert r2.returncode == 0, r2.stdout[-3000:]
+    d2 = _json_line(r2.stdout)
+    assert d2["n_gpus"] == 2 and d2["trajectories_gathered"] == 16 and d2["scaling"] == "weak"
+    assert d2["value"] > 0 and d2["config"]["streams_per_gpu"] == 8
+    cmd1 = [sys.executable, os.path.join(REPO, "bench.py"), "--streams", "16", "--dump-poses", p1] + COMMON
+    r1 = subprocess.run(cmd1, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, universal_newlines=True, env=env,
+                        timeout=300, cwd=REPO)
+    assert r1.returncode == 0, r1.stdout[-3000:]
+    d1 = _json_line(r1.stdout)
+    assert d1["n_gpus"] == 1 and d1["trajectories_gathered"] == 16
+    a2, a1 = np.load(p2), np.load(p1)
+    assert a2.shape == a1.shape == (16, 12)
+    assert np.array_equal(a2.view(np.int32), a1.view(np.int32)), np.abs(a2 - a1).max()

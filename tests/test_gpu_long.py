@@ -1,0 +1,113 @@
+"""C5-length sequences (BASELINE config C5's 250-scan sequences): LM parity per pair with
+the reference's state injected, and the free-running trajectory drift reported.
+
+* Per pair: the oracle (the reference restated) runs each sequence free; before every association the
+  GPU context gets the oracle's state going into that pair (transformCur_in, transformSum, isDegenerate,
+  the TransformToEnd'ed Last clouds, the kd-tree staleness; lego_test_set_lm_state) and the oracle's
+  ProjectionOut (the Channel hop, lego_feature_association_from).  Asserted every pair: features bit-exact
+  and transformCur_out within 1e-4 (north_star), featureAssociation.cpp:1213-1235, 1419-1421.
+* Sequence level: transformSum drift of the free-running GPU batch (no injection) against the oracle's
+  free run, for both VoxelGrid tie orders: reported (written to $LEGO_REPORT_DIR or the test's tmp dir),
+  not asserted, because one threshold flip propagates through the warm start.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import helpers as Hs
+import lego_amd as L
+from lego_amd import _abi as A
+
+pytestmark = pytest.mark.gpu
+
+S_SEQ, K_SCANS = 8, 250
+
+
+def _oracle_run(params, cfg, seq):
+    import oracle as O
+    orc = O.Oracle(params)
+    out = []
+    for k in range(K_SCANS):
+        pr = orc.cloud_handler(A.synth_scan(cfg, seq, k))
+        fr = orc.feature_association()
+        out.append((pr, fr, orc.lm_flags()))
+    return out
+
+
+@pytest.fixture(scope="module")
+def runs():
+    cache = {}
+
+    def get(fp_mode):
+        if fp_mode not in cache:
+            params = L.params_vlp16(fp_mode=fp_mode)
+            cfg = A.synth_cfg("vlp16")
+            cache[fp_mode] = [_oracle_run(params, cfg, 700 + s) for s in range(S_SEQ)]
+        return cache[fp_mode]
+    return get
+
+
+@pytest.mark.parametrize("fp_mode", [0, 1])
+def test_long_sequence_lm_parity_injected(gpu, runs, fp_mode):
+    params = L.params_vlp16(fp_mode=fp_mode)
+    worst, pairs, iters_differ = 0.0, 0, 0
+    for s, run in enumerate(runs(fp_mode)):
+        fe = L.Frontend(params)
+        prev = None
+        for k, (pr, fr, _) in enumerate(run):
+            if prev is not None:
+                p_fr, (dg, stale) = prev[1], prev[2]
+                fe.set_lm_state(p_fr["transform_cur"], p_fr["transform_sum"], dg, p_fr["corner_last"],
+                                p_fr["surf_last"], stale)
+            fg = fe.feature_association(pr)
+            bad = Hs.diff_report(Hs.FEAT_KEYS, fg, fr)
+            assert not bad, (s, k, bad)
+            d = float(np.abs(np.asarray(fg["transform_cur"], np.float64) - fr["transform_cur"]).max())
+            assert d <= Hs.TF_TOL, (s, k, fg["transform_cur"], fr["transform_cur"])
+            worst = max(worst, d)
+            pairs += int(k > 0)
+            iters_differ += int((fg["lm_iter_surf"], fg["lm_iter_corner"]) != (fr["lm_iter_surf"], fr["lm_iter_corner"]))
+            prev = (pr, fr, run[k][2])
+        fe.close()
+    print("fp_mode %d: %d pairs, max |d transformCur_out| %.3g, LM iteration counts differ in %d" % (
+        fp_mode, pairs, worst, iters_differ))
+    assert pairs == S_SEQ * (K_SCANS - 1)
+
+
+def test_long_sequence_free_running_drift(gpu, runs, tmp_path):
+    """Free-running GPU batch (8 sequences, 250 scans, lag-1 pipeline) vs the oracle's free run: max
+    |transformSum| difference per sequence, both VoxelGrid tie orders (order 0 = the reference's).
+    Reported; asserted only loosely (a diverged trajectory, not a threshold flip, would fail)."""
+    import torch
+    run = runs(0)
+    cfg = A.synth_cfg("vlp16")
+    cap = 16 * 1800
+    seqs = np.repeat(np.arange(S_SEQ)[None, :] + 700, K_SCANS, 0).reshape(-1)
+    scans = np.repeat(np.arange(K_SCANS)[:, None], S_SEQ, 1).reshape(-1)
+    pts, cnt = A.synth_batch(cfg, seqs, scans)
+    d_pts = torch.from_numpy(pts).cuda()
+    offs = torch.from_numpy((np.arange(S_SEQ * K_SCANS, dtype=np.int64) * cap).reshape(K_SCANS, S_SEQ)).cuda()
+    cnts = torch.from_numpy(cnt.reshape(K_SCANS, S_SEQ).astype(np.int32)).cuda()
+    ref_sum = np.array([[fr["transform_sum"] for (_, fr, _) in r] for r in run])  # [S, K, 6]
+    report = {"sequences": S_SEQ, "scans": K_SCANS, "fp_mode": 0, "orders": {}}
+    for order in (0, 1):
+        b = L.Batch(L.params_vlp16(voxel_tie_order=order), S_SEQ, cap)
+        b.set_lag(0)
+        drift = np.zeros((S_SEQ, K_SCANS))
+        for k in range(K_SCANS):
+            b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), torch.cuda.current_stream().cuda_stream)
+            poses, _ = b.poses()
+            drift[:, k] = np.abs(poses[:, 6:].astype(np.float64) - ref_sum[:, k]).max(1)
+        b.close()
+        first = [int(np.argmax(drift[s] > Hs.TF_TOL)) if (drift[s] > Hs.TF_TOL).any() else None for s in range(S_SEQ)]
+        report["orders"][str(order)] = {"max_drift_per_sequence": [float(x) for x in drift.max(1)],
+                                        "drift_at_scan_249": [float(x) for x in drift[:, -1]],
+                                        "first_scan_over_1e-4": first}
+        assert drift.max() < 0.5, (order, drift.max(1))  # same trajectory, not a divergence
+    out = os.environ.get("LEGO_REPORT_DIR", str(tmp_path))
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "long_sequence_drift.json"), "w") as f:
+        json.dump(report, f, indent=1)
+    print(json.dumps(report))

@@ -104,6 +104,25 @@ def test_voxel_limits(s2m):
     assert got[1][1] == -1
 
 
+def test_voxel_overflow_then_normal_clouds(s2m, sequences):
+    """An overflowing cloud (PCL's int32 leaf-index warning path: copied unfiltered) FOLLOWED by normal
+    clouds, through the few-clouds layout (one device-wide sort of cloud|leaf keys): the later clouds'
+    sorted ranges must not shift, so each equals the oracle (the overflowed slots once
+    sorted past every cloud)."""
+    fr = sequences[2]
+    rng = np.random.default_rng(21)
+    wide = rng.uniform(-1000, 1000, (3000, 4)).astype(np.float32)
+    clouds = [wide, fr[3]["corner_last"], fr[3]["surf_last"], np.repeat(rng.uniform(-1, 1, (40, 4)).astype(np.float32),
+                                                                         5, axis=0), wide[:500]]
+    leaves = [1e-3, 0.2, 0.4, 0.4, 1e-3]
+    got = _gpu_voxel(s2m, clouds, leaves)
+    for c, leaf, (o, on, st) in zip(clouds, leaves, got):
+        ref, rst = O.voxel_grid(c, leaf, stable=True)
+        assert st == rst and on == len(ref), (leaf, len(c), on, len(ref), st, rst)
+        assert np.array_equal(o.view(np.int32), ref.view(np.int32)), (leaf, len(c))
+    assert got[0][2] == 0x100 and got[4][2] == 0x100
+
+
 def test_transform_matches_oracle(s2m, sequences):
     import torch
     import lego_amd as LA

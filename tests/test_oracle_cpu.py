@@ -225,3 +225,12 @@ def test_libm_restatement_matches_glibc(tmp_path):
     rc, out = _compile_and_run(os.path.join(REPO, "tests", "native", "libm_check.cpp"), str(tmp_path / "lc"),
                                ["3000000"])
     assert rc == 0, out
+
+
+def test_double_libm_restatement_vs_glibc(tmp_path):
+    """fp_mode 1: the device's double sin / cos / atan2 / asin (fdlibm) against the host glibc double
+    functions: after the reference's rounding to float, identical on every sample (the double results
+    themselves may differ in the last bit: reported, not asserted)."""
+    rc, out = _compile_and_run(os.path.join(REPO, "tests", "native", "libm_d_check.cpp"), str(tmp_path / "ld"),
+                               ["3000000"])
+    assert rc == 0, out
