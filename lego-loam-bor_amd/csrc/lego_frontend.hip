@@ -52,10 +52,9 @@ LgParams derive(const lego_params& p) {
   P.mount = mount;
   P.fp1 = p.fp_mode == 1;
   P.theta_thr = P.fp1 ? (float)tan((double)theta) : tanf(theta);
-  P.sinXd = sin((double)P.ang_res_x);
-  P.cosXd = cos((double)P.ang_res_x);
-  P.sinYd = sin((double)P.ang_res_y);
-  P.cosYd = cos((double)P.ang_res_y);
+  // the reference's sin(alpha) / cos(alpha) pair, merged into one sincos by GCC (see oracle Lm<double>)
+  sincos((double)P.ang_res_x, &P.sinXd, &P.cosXd);
+  sincos((double)P.ang_res_y, &P.sinYd, &P.cosYd);
   P.sinX = sinf(P.ang_res_x);
   P.cosX = cosf(P.ang_res_x);
   P.sinY = sinf(P.ang_res_y);

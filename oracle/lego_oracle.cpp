@@ -17,12 +17,16 @@
 //     reference itself, except for two pinned boundaries:
 //       - libm: unqualified float sin/cos/atan2/asin resolve to glibc's float functions
 //         (fp_mode 0).  The oracle calls glibc directly.
-//       - kd-tree 1-NN: oracle/_ref builds the reference's vendored nanoflann 1.3.0 and checks
-//         this file's brute-force 1-NN (lowest index among exact ties) against it.
+//       - kd-tree 1-NN: nanoflann 1.3.0's tree and search restated (nanoflann_restated.h), exact
+//         distance ties resolved as nanoflann resolves them (first visited); oracle/_ref builds the
+//         reference's vendored nanoflann and checks the restatement against it.
 //   * Restated third-party boundaries (unpinned): PCL VoxelGrid::applyFilter (PCL 1.7/1.8 algorithm,
 //     restated below), Eigen AtA/QR/eigen (modelled: float products summed in double, column-pivoting
 //     Householder QR in float, symmetric eigenvalues in double).
 //   * Reference UB is given defined behaviour and flagged (LEGO_ST_* bits in include/lego_frontend.h).
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE  // sincos
+#endif
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -35,6 +39,7 @@
 #include <vector>
 
 #include "../include/lego_frontend.h"
+#include "nanoflann_restated.h"
 
 namespace {
 
@@ -51,20 +56,31 @@ typedef lego_point Pt;
 //              where the reference stores it to float.
 // T is the type the reference's expression is evaluated in.  Explicitly std::-qualified calls
 // (imageProjection.cpp:190,198,237,240) are float in both models.
+//
+// sin and cos of the same argument: every unqualified sin(x) of the path has a cos(x) of the same x in
+// the same function (TransformToStart/End, AccumulateRotation, calculateTransformation*,
+// integrateTransformation, labelComponents), and GCC at -O1 and above merges such pairs into one
+// sincos(x) call (its cse_sincos pass; the reference builds with -O3, CMakeLists.txt:4).  glibc 2.35's
+// double sincos is not bit-identical to its sin / cos (6e-5 of float arguments in [-4, 4] differ in
+// the last bit; sincosf equals sinf / cosf), so the oracle calls sincos explicitly for sn / cs, as the
+// reference binary does, and plain cos for the one unpaired call, cos(ox) in AccumulateRotation
+// (:489, cs1).  Without this the oracle's own results depended on how GCC inlined it.
 template <class T>
 struct Lm;
 template <>
 struct Lm<float> {
   static float sn(float x) { return sinf(x); }
   static float cs(float x) { return cosf(x); }
+  static float cs1(float x) { return cosf(x); }
   static float at2(float y, float x) { return atan2f(y, x); }
   static float as(float x) { return asinf(x); }
   static float sq(float x) { return sqrtf(x); }
 };
 template <>
 struct Lm<double> {
-  static double sn(double x) { return sin(x); }
-  static double cs(double x) { return cos(x); }
+  static double sn(double x) { double s, c; sincos(x, &s, &c); return s; }
+  static double cs(double x) { double s, c; sincos(x, &s, &c); return c; }
+  static double cs1(double x) { return cos(x); }
   static double at2(double y, double x) { return atan2(y, x); }
   static double as(double x) { return asin(x); }
   static double sq(double x) { return sqrt(x); }
@@ -132,8 +148,8 @@ struct ImageProjection {
     theta_thr = fp1 ? (float)tan((double)segment_theta) : tanf(segment_theta);  // :414
     sinX = sinf(ang_res_x); cosX = cosf(ang_res_x);                           // :463 alpha=_ang_resolution_X
     sinY = sinf(ang_res_y); cosY = cosf(ang_res_y);                           // :463 alpha=_ang_resolution_Y
-    sinXd = sin((double)ang_res_x); cosXd = cos((double)ang_res_x);           // fp_mode 1: double sin/cos
-    sinYd = sin((double)ang_res_y); cosYd = cos((double)ang_res_y);
+    sincos((double)ang_res_x, &sinXd, &cosXd);  // fp_mode 1: sin / cos(alpha) in double (one sincos, see Lm)
+    sincos((double)ang_res_y, &sinYd, &cosYd);
     full_cloud.resize((size_t)V * H);
   }
 
@@ -808,30 +824,28 @@ struct FeatureAssociation {
     float crycrx = F::cs(lx) * F::cs(ly) * F::cs(cx) * F::cs(cy) -
                    F::cs(lx) * F::sn(ly) * (F::cs(cz) * F::sn(cy) - F::cs(cy) * F::sn(cx) * F::sn(cz)) -
                    F::sn(lx) * (F::sn(cy) * F::sn(cz) + F::cs(cy) * F::cs(cz) * F::sn(cx));
-    oy = F::at2((T)srycrx / F::cs(ox), (T)crycrx / F::cs(ox));
+    oy = F::at2((T)srycrx / F::cs1(ox), (T)crycrx / F::cs1(ox));
     float srzcrx = F::sn(cx) * (F::cs(lz) * F::sn(ly) - F::cs(ly) * F::sn(lx) * F::sn(lz)) +
                    F::cs(cx) * F::sn(cz) * (F::cs(ly) * F::cs(lz) + F::sn(lx) * F::sn(ly) * F::sn(lz)) +
                    F::cs(lx) * F::cs(cx) * F::cs(cz) * F::sn(lz);
     float crzcrx = F::cs(lx) * F::cs(lz) * F::cs(cx) * F::cs(cz) -
                    F::cs(cx) * F::sn(cz) * (F::cs(ly) * F::sn(lz) - F::cs(lz) * F::sn(lx) * F::sn(ly)) -
                    F::sn(cx) * (F::sn(ly) * F::sn(lz) + F::cs(ly) * F::cs(lz) * F::sn(lx));
-    oz = F::at2((T)srzcrx / F::cs(ox), (T)crzcrx / F::cs(ox));
+    oz = F::at2((T)srzcrx / F::cs1(ox), (T)crzcrx / F::cs1(ox));
   }
 
-  // nanoflann KdTreeFLANN::nearestKSearch(k=1) (nanoflann_pcl.h:141-152): exact L2^2 1-NN,
-  // distance summed dx^2+dy^2+dz^2 in float (nanoflann.hpp:432-440).  Restated as brute force,
-  // lowest index among exact ties (pinned against nanoflann by oracle/_ref).
-  int nearest(const std::vector<Pt>& cloud, int n, const Pt& q, float* d_out) {
-    int best = -1;
+  // kdtreeCornerLast / kdtreeSurfLast->nearestKSearch(pointSel, 1, ...) (fa.cpp:512, 650;
+  // nanoflann_pcl.h:141-152): nanoflann's kd-tree over the Last cloud (nanoflann_restated.h), built
+  // when the LM starts (a pure function of the cloud: the reference builds it in publishCloudsLast /
+  // checkSystemInitialization).  Exact distance ties go to the first point the search visits, as in
+  // nanoflann; LEGO_ST_NN_TIE reports that one happened (and mattered: the point was accepted).
+  nfr::KdTree<Pt> tree_corner, tree_surf;
+  int nearest(const nfr::KdTree<Pt>& tree, const Pt& q, float* d_out) {
+    const float qv[3] = {q.x, q.y, q.z};
+    int best = -1, ties = 0;
     float bd = std::numeric_limits<float>::max();
-    int ties = 0;
-    for (int j = 0; j < n; ++j) {
-      float dx = q.x - cloud[j].x, dy = q.y - cloud[j].y, dz = q.z - cloud[j].z;
-      float d = dx * dx + dy * dy + dz * dz;
-      if (d < bd) { bd = d; best = j; ties = 0; }
-      else if (d == bd) ++ties;
-    }
-    if (ties && bd < nn_dist_sqr) status |= LEGO_ST_NN_TIE;  // tie-break only matters when accepted
+    if (tree.knn(qv, 1, &best, &bd, &ties) == 0) best = -1;
+    if (ties && bd < nn_dist_sqr) status |= LEGO_ST_NN_TIE;
     *d_out = bd;
     return best;
   }
@@ -843,7 +857,7 @@ struct FeatureAssociation {
       TransformToStart(&sharp[i], &pointSel);
       if (iterCount % 5 == 0) {
         float sqd;
-        int nn = nearest(corner_last, laserCloudCornerLastNum, pointSel, &sqd);
+        int nn = nearest(tree_corner, pointSel, &sqd);
         int closestPointInd = -1, minPointInd2 = -1;
         if (sqd < nn_dist_sqr) {
           closestPointInd = nn;
@@ -910,7 +924,7 @@ struct FeatureAssociation {
       TransformToStart(&flat[i], &pointSel);
       if (iterCount % 5 == 0) {
         float sqd;
-        int nn = nearest(surf_last, laserCloudSurfLastNum, pointSel, &sqd);
+        int nn = nearest(tree_surf, pointSel, &sqd);
         int closestPointInd = -1, minPointInd2 = -1, minPointInd3 = -1;
         if (sqd < nn_dist_sqr) {
           closestPointInd = nn;
@@ -976,8 +990,8 @@ struct FeatureAssociation {
   }
 
   // float srx = sin(transformCur[0]) (:797-802, :939-944) in either libm model
-  float lm_sin(float x) const { return fp1 ? (float)sin((double)x) : sinf(x); }
-  float lm_cos(float x) const { return fp1 ? (float)cos((double)x) : cosf(x); }
+  float lm_sin(float x) const { return fp1 ? (float)Lm<double>::sn(x) : sinf(x); }
+  float lm_cos(float x) const { return fp1 ? (float)Lm<double>::cs(x) : cosf(x); }
 
   // AtA / AtB (Eigen GEMM, modelled) + solve + degeneracy; returns x[3]
   void solve_normal(const std::vector<float>& A, const std::vector<float>& B, int iterCount, float x[3]) {
@@ -1130,6 +1144,8 @@ struct FeatureAssociation {
       return;
     }
     if (tree_stale) status |= LEGO_ST_STALE_TREE;  // defined behaviour: search the Last cloud anyway
+    tree_corner.build(corner_last.data(), laserCloudCornerLastNum);
+    tree_surf.build(surf_last.data(), laserCloudSurfLastNum);
     for (int iterCount1 = 0; iterCount1 < 25; iterCount1++) {
       laserCloudOri.clear();
       coeffSel.clear();
@@ -1366,6 +1382,18 @@ int oracle_std_sort(uint32_t* keys, int32_t* vals, int n, int is_float) {
     for (int i = 0; i < n; ++i) { v[i].idx = keys[i]; v[i].cloud_point_index = (unsigned)vals[i]; }
     std::sort(v.begin(), v.end(), std::less<cloud_point_index_idx>());
     for (int i = 0; i < n; ++i) { keys[i] = v[i].idx; vals[i] = (int32_t)v[i].cloud_point_index; }
+  }
+  return 0;
+}
+
+// Test hook: nanoflann k-NN (the restated tree) of m queries against a cloud of n points (x, y, z, w
+// float32 each): idx / dist [m][k], nearest first; returns 0.
+int oracle_knn_tree(const float* cloud, int n, const float* q, int m, int k, int32_t* idx, float* dist) {
+  nfr::KdTree<Pt> t;
+  t.build((const Pt*)cloud, n);
+  for (int i = 0; i < m; ++i) {
+    for (int j = 0; j < k; ++j) { idx[(size_t)i * k + j] = -1; dist[(size_t)i * k + j] = 0.f; }
+    t.knn(q + (size_t)4 * i, k, idx + (size_t)i * k, dist + (size_t)i * k);
   }
   return 0;
 }

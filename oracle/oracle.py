@@ -158,6 +158,17 @@ def knn5(cloud, queries):
     return ind, d, fl
 
 
+def knn_tree(cloud, queries, k=1):
+    """nanoflann k-NN restated (oracle/nanoflann_restated.h): (indices [m, k], squared distances [m, k])."""
+    import numpy as np
+    c, q = _f32(cloud), _f32(queries)
+    idx = np.zeros((len(q), k), np.int32)
+    d = np.zeros((len(q), k), np.float32)
+    lib().oracle_knn_tree(c.ctypes.data_as(P(C.c_float)), len(c), q.ctypes.data_as(P(C.c_float)), len(q), int(k),
+                          idx.ctypes.data_as(P(C.c_int32)), d.ctypes.data_as(P(C.c_float)))
+    return idx, d
+
+
 def voxel_grid(points, leaf, stable=True):
     """pcl::VoxelGrid::filter restated (oracle/lego_oracle.cpp): (output (M, 4) float32, status bits)."""
     import numpy as np

@@ -6,6 +6,9 @@
 // figure: must be 0 on the sample).
 //
 // usage: libm_d_check [samples]   exit status 1 if any float-rounded mismatch
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE  // sincos
+#endif
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -42,8 +45,10 @@ int main(int argc, char** argv) {
   for (long i = 0; i < n; ++i) {
     // LM / TransformToStart angles: s * transformCur (small) and transformSum (any heading)
     const float x = (float)((u01() * 2 - 1) * (i & 1 ? 0.05 : 3.5));
-    s.add(sin((double)x), lg::sin_d(x));
-    c.add(cos((double)x), lg::cos_d(x));
+    double gs, gc;  // the reference's sin / cos pairs are one glibc sincos call (GCC's cse_sincos)
+    sincos((double)x, &gs, &gc);
+    s.add(gs, lg::sin_d(x));
+    c.add(gc, lg::cos_d(x));
     // adjustDistortion: -atan2(point.x, point.z) of lidar points (featureAssociation.cpp:172)
     const float py = (float)((u01() * 2 - 1) * 80), px = (float)((u01() * 2 - 1) * 80);
     ori.add(-atan2((double)py, (double)px), -lg::atan2_d(py, px));

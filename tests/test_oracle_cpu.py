@@ -163,9 +163,40 @@ def test_oracle_last_writer_wins():
     assert Hs.bits_equal(r_both, r_dup)
 
 
+def _nanoflann_ref(exe, xyz, q, k):
+    blob = struct.pack("<i", len(xyz)) + xyz.tobytes() + struct.pack("<i", len(q)) + q.tobytes()
+    out = subprocess.run([exe, str(k)], input=blob, stdout=subprocess.PIPE, check=True).stdout
+    res = np.frombuffer(out, dtype=np.dtype([("i", "<i4"), ("d", "<f4")])).reshape(len(q), k)
+    return res["i"], res["d"]
+
+
+def _tie_clouds(rng, fa):
+    """(name, cloud xyz, queries) cases where exact distance ties are common: duplicated points, an
+    integer lattice queried at cell centres (8 equidistant corners) and edge midpoints, a lattice with
+    half-integer steps, mirrored pairs around the queries; plus the real Last clouds."""
+    g = np.stack(np.meshgrid(np.arange(12), np.arange(9), np.arange(5), indexing="ij"), -1).reshape(-1, 3)
+    lat = g.astype(np.float32) * np.float32(0.5)
+    centres = (rng.integers(0, 8, (300, 3)) + 0.5).astype(np.float32) * np.float32(0.5)
+    edges = lat[rng.integers(0, len(lat), 300)] + np.float32(0.25) * np.eye(3, dtype=np.float32)[rng.integers(0, 3, 300)]
+    surf = np.ascontiguousarray(fa["surf_last"][:, :3], np.float32)
+    dup = np.concatenate([surf[::3], surf[::3], surf[1::7]])[rng.permutation(len(surf[::3]) * 2 + len(surf[1::7]))]
+    qmir = rng.normal(0, 5, (200, 3)).astype(np.float32)
+    off = rng.integers(-8, 9, (200, 3)).astype(np.float32) * np.float32(0.125)
+    mirror = np.concatenate([qmir + off, qmir - off, rng.normal(0, 5, (500, 3)).astype(np.float32)])
+    return [("lattice", lat, np.concatenate([centres, edges])),
+            ("lattice_shuffled", lat[rng.permutation(len(lat))], centres),
+            ("duplicates", dup, dup[rng.integers(0, len(dup), 300)] + rng.normal(0, 0.2, (300, 3)).astype(np.float32)),
+            ("mirrored", mirror, qmir),
+            ("surf_last", surf, np.concatenate([fa["flat"][:, :3], surf[rng.integers(0, len(surf), 200)] +
+                                                 rng.normal(0, 0.3, (200, 3))]).astype(np.float32)),
+            ("corner_last", np.ascontiguousarray(fa["corner_last"][:, :3], np.float32), fa["sharp"][:, :3].astype(np.float32))]
+
+
 def test_nanoflann_pin():
-    """The oracle's brute-force 1-NN equals the reference's vendored nanoflann 1.3.0 (built from
-    /root/reference into oracle/_ref; skipped where the reference is not mounted, e.g. the GPU box)."""
+    """The oracle's restated nanoflann kd-tree (build + search, oracle/nanoflann_restated.h) equals the
+    reference's vendored nanoflann 1.3.0 (built from /root/reference into oracle/_ref; skipped where
+    the reference is not mounted, e.g. the GPU box): identical indices (exact-tie order included) and
+    distances for k = 1 (FeatureAssociation) and k = 5 (MapOptimization), on tie-heavy clouds."""
     if not os.path.exists("/root/reference/LeGO-LOAM/include/lego_loam/nanoflann.hpp"):
         pytest.skip("reference sources not mounted here")
     subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "ref"])
@@ -179,17 +210,20 @@ def test_nanoflann_pin():
     orc.cloud_handler(A.synth_scan(cfg, 0, 1))
     fa = orc.feature_association()
     rng = np.random.default_rng(0)
-    for cloud, queries in ((fa["surf_last"], fa["flat"]), (fa["corner_last"], fa["sharp"])):
-        xyz = np.ascontiguousarray(cloud[:, :3], np.float32)
-        q = np.concatenate([queries[:, :3], xyz[rng.integers(0, len(xyz), 200)] + rng.normal(0, 0.3, (200, 3))]).astype(np.float32)
-        blob = struct.pack("<i", len(xyz)) + xyz.tobytes() + struct.pack("<i", len(q)) + q.tobytes()
-        out = subprocess.run([exe], input=blob, stdout=subprocess.PIPE, check=True).stdout
-        res = np.frombuffer(out, dtype=np.dtype([("i", "<i4"), ("d", "<f4")]))
-        # brute force exactly as the oracle: float ((dx*dx + dy*dy) + dz*dz), lowest index among ties
-        d = ((q[:, None, 0] - xyz[None, :, 0]) ** 2 + (q[:, None, 1] - xyz[None, :, 1]) ** 2) + (q[:, None, 2] - xyz[None, :, 2]) ** 2
-        bi = np.argmin(d, axis=1)
-        np.testing.assert_array_equal(res["i"], bi)
-        assert Hs.bits_equal(res["d"], d[np.arange(len(q)), bi])
+    ties_seen = 0
+    for name, xyz, q in _tie_clouds(rng, fa):
+        xyz, q = np.ascontiguousarray(xyz, np.float32), np.ascontiguousarray(q, np.float32)
+        for k in (1, 5):
+            ri, rd = _nanoflann_ref(exe, xyz, q, k)
+            oi, od = O.knn_tree(np.concatenate([xyz, np.zeros((len(xyz), 1), np.float32)], 1),
+                                np.concatenate([q, np.zeros((len(q), 1), np.float32)], 1), k)
+            np.testing.assert_array_equal(oi, ri, err_msg="%s k=%d" % (name, k))
+            assert Hs.bits_equal(od, rd), (name, k)
+            if k == 1:  # exact ties among the nearest: brute force finds more than one point at the minimum
+                d = ((q[:, None, 0] - xyz[None, :, 0]) ** 2 + (q[:, None, 1] - xyz[None, :, 1]) ** 2) + \
+                    (q[:, None, 2] - xyz[None, :, 2]) ** 2
+                ties_seen += int(((d == d.min(1, keepdims=True)).sum(1) > 1).sum())
+    assert ties_seen > 300  # the tie-heavy cases really exercise nanoflann's visit order
 
 
 def _compile_and_run(src, exe, args=()):
