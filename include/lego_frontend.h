@@ -44,7 +44,7 @@ extern "C" {
 #define LEGO_ST_DEGENERATE      0x004  /* eigenvalue degeneracy hit in a solve (fa.cpp:869-898)      */
 #define LEGO_ST_STALE_TREE      0x008  /* ref UB: kd-tree not rebuilt but LM ran (fa.cpp:1214,1356)   */
 #define LEGO_ST_FWD_OOB         0x010  /* ref UB: forward scan bound > |Last| (fa.cpp:522,661)        */
-#define LEGO_ST_NN_TIE          0x020  /* exact 1-NN distance tie (nanoflann first-visited unpinned)  */
+#define LEGO_ST_NN_TIE          0x020  /* exact 1-NN distance tie, resolved as nanoflann (first visited) */
 #define LEGO_ST_STALE_IND_OOB   0x040  /* ref UB: stale smoothness entry indexes past the cloud       */
 #define LEGO_ST_EMITTED         0x080  /* AssociationOut sent to mapping this cycle (fa.cpp:1432)     */
 #define LEGO_ST_VOXEL_OVERFLOW  0x100  /* PCL VoxelGrid index overflow: cloud copied unfiltered       */
@@ -253,6 +253,10 @@ int  lego_test_project_cells(const lego_params* p, const float* xyzw, int32_t n,
 int  lego_test_set_lm_state(lego_ctx* ctx, const float* transform_cur, const float* transform_sum,
                             int32_t degenerate, const lego_point* corner_last, int32_t n_corner,
                             const lego_point* surf_last, int32_t n_surf, int32_t tree_stale);
+/* nanoflann's 1-NN as the LM resolves exact distance ties on the device (the tree built as nanoflann
+ * 1.3.0 builds it, its searchLevel): m queries against a cloud of n points (x, y, z, w float32 each);
+ * out idx (-2: search stack overflow) and squared distance. */
+int  lego_test_kd_knn1(const float* cloud, int32_t n, const float* queries, int32_t m, int32_t* idx, float* dist);
 /* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
  * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */
 int  lego_debug_prof(uint64_t* out256, int32_t reset);

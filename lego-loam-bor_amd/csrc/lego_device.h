@@ -84,6 +84,15 @@ enum {
   CNT_STATUS = 7, CNT_N = 8
 };
 
+// nanoflann kd-tree node (exact-tie resolution of the LM's 1-NN): children (-1: leaf), vind range,
+// split dimension and the children's facing bounds (nanoflann.hpp node_type.sub / .lr)
+struct KdNode {
+  int c1, c2, left, right;
+  int divfeat;
+  float divlow, divhigh;
+  int pad;
+};
+
 struct LgBufs {  // device buffers, all indexed [stream][...]
   // ImageProjection
   float* range;          // [S][VH]
@@ -140,6 +149,11 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   float4* surf_last;     // [S][2][VH]
   float4* grid_pts;      // [S][VH]  LM scratch: Last cloud bucketed by grid cell (xyz, index bits)
   LgState* state;        // [S]      written by k_lm / k_publish only (k_lm stores it whole)
+  // nanoflann tree of a Last cloud, built by k_lm only when a 1-NN has an exact distance tie
+  KdNode* kd_node;       // [S][2*VH]
+  int32_t* kd_vind;      // [S][VH]
+  int32_t* kd_tmp;       // [S][2*VH]  stop positions of planeSplit's passes
+  float* kd_frames;      // [S][10*VH] build stack, then the searches' stacks
   int32_t* fe_state;     // [S][2]   written by the front end only: [0] 0 or LEGO_EEMPTY for the last
                          // projection; [1] scans whose features k_concat has assembled, > 0 at a scan's
                          // front end iff its FeatureAssociation pass is not the initialising one

@@ -350,6 +350,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   A(f_lflat, S * VH);
   A(corner_last, S * 2 * V * P.cap_lsharp); A(surf_last, S * 2 * VH); A(grid_pts, S * VH);
   A(state, S); A(fe_state, S * 2);
+  A(kd_node, S * 2 * VH); A(kd_vind, S * VH); A(kd_tmp, S * 2 * VH); A(kd_frames, S * 10 * VH);
 #undef A
   if (rc != LEGO_OK) {
     delete b;

@@ -3284,6 +3284,10 @@ struct LmLdsT {  // kMaxQ: feature queries of one loop (V * max(cap_sharp, cap_f
   int last_le[LM_RMAX + 4];   // last index with ring <= r (index r + 1), -1 if none
   int nfall;                  // queries whose ring breaks need the sequential scan
   int fall[kMaxQ];
+  int ntie;                   // queries of this search with an exact 1-NN distance tie
+  int tieq[kMaxQ];
+  int kd_built;               // nanoflann's tree of this loop's Last cloud is in B.kd_*
+  float kd_box[6];            // its root bbox
   float fred[6][16];
   int iscan[16];
   float cur[6];
@@ -3903,6 +3907,276 @@ LG_DEVICE int lds_nn(const float4* last, int nl, float4 q, float r2, bool& tie, 
   return (bd < r2) ? bi : -1;
 }
 
+// ============================================================================================
+// nanoflann's kd-tree, for the rare 1-NN with an exact distance tie
+// ============================================================================================
+// The grid search returns the exact nearest distance and flags a query when several points share it.
+// Which of them kdtree->nearestKSearch returns is nanoflann's first visited (strict < in searchLevel
+// and KNNResultSet::addPoint), a function of its tree.  So when a search has tied queries, wave 0
+// builds the tree of the Last cloud exactly as nanoflann 1.3.0 does (buildIndex / divideTree /
+// middleSplit_ / planeSplit, nanoflann.hpp:857-1003, 1190-1202, 1316-1337; leaf_max_size 10;
+// oracle/nanoflann_restated.h is the host statement) and re-runs nanoflann's searchLevel (:1346-1409)
+// for those queries.  planeSplit's two Hoare passes are rank pairings: the k-th left stop (from the
+// left) swaps with the k-th right stop (from the right) while it lies left of it, so each pass is two
+// stop lists and one parallel swap.  Scratch per stream: B.kd_* (built once per LM loop, on demand).
+#define KD_LEAF 10
+struct KdView {
+  const float4* pts;  // the Last cloud, in its own order
+  KdNode* node;
+  int* vind;
+  int* tmp;           // [2 * VH]: left stops, right stops
+  float* frames;      // [10 * VH]
+  int vh;
+};
+
+LG_DEVICE float kd_get(const float4* pts, int i, int d) {
+  const float4 p = pts[i];
+  return d == 0 ? p.x : (d == 1 ? p.y : p.z);
+}
+LG_DEVICE void kd_sync() {  // this wave's global stores before its other lanes' loads of them
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+}
+
+// computeMinMax (:836-848) of all three dimensions over ind[0, count) (order-independent)
+LG_DEVICE void kd_minmax(const float4* pts, const int* ind, int count, float* mn, float* mx) {
+  float a0 = FLT_MAX, a1 = FLT_MAX, a2 = FLT_MAX, b0 = -FLT_MAX, b1 = -FLT_MAX, b2 = -FLT_MAX;
+  for (int t0 = lane_id(); t0 < count; t0 += 64 * 4) {
+    float4 p4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p4[u] = pts[ind[min(t0 + 64 * u, count - 1)]];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a0 = fminf(a0, p4[u].x); a1 = fminf(a1, p4[u].y); a2 = fminf(a2, p4[u].z);
+      b0 = fmaxf(b0, p4[u].x); b1 = fmaxf(b1, p4[u].y); b2 = fmaxf(b2, p4[u].z);
+    }
+  }
+  mn[0] = wave_min(a0); mn[1] = wave_min(a1); mn[2] = wave_min(a2);
+  mx[0] = wave_max(b0); mx[1] = wave_max(b1); mx[2] = wave_max(b2);
+}
+
+// One planeSplit pass over ind[b, count) (:967-1003): mode 0 moves the keys < cv to the front (left
+// stops: !(key < cv), right stops: key < cv), mode 1 the keys <= cv.  Returns b + the number of
+// moved-to-front keys (lim1 / lim2).
+LG_DEVICE int kd_pass(const float4* pts, int* ind, int b, int count, int d, float cv, int mode, int* tL, int* tR) {
+  const int lane = lane_id();
+  int nL = 0, nR = 0;
+  // each position is a left stop (!front) or a right stop (front); four chunks' keys in flight at a time
+  for (int t0 = b; t0 < count; t0 += 256) {  // left stops ascending
+    float k4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k4[u] = kd_get(pts, ind[min(t0 + 64 * u + lane, count - 1)], d);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = t0 + 64 * u + lane;
+      const bool front = mode == 0 ? k4[u] < cv : k4[u] <= cv;
+      const bool ls = i < count && !front;
+      const unsigned long long m = __ballot(ls);
+      if (ls) tL[nL + popc_below(m)] = i;
+      nL += __popcll(m);
+    }
+  }
+  for (int t0 = count - 1; t0 >= b; t0 -= 256) {  // right stops descending
+    float k4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k4[u] = kd_get(pts, ind[max(t0 - 64 * u - lane, b)], d);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = t0 - 64 * u - lane;
+      const bool front = mode == 0 ? k4[u] < cv : k4[u] <= cv;
+      const bool rs = i >= b && front;
+      const unsigned long long m = __ballot(rs);
+      if (rs) tR[nR + popc_below(m)] = i;
+      nR += __popcll(m);
+    }
+  }
+  kd_sync();
+  const int K = min(nL, nR);
+  for (int k0 = 0; k0 < K; k0 += 64) {  // the valid pairs (L_k < R_k) are a prefix; swaps are disjoint
+    const int k = k0 + lane;
+    if (k < K) {
+      const int l = tL[k], r = tR[k];
+      if (l < r) {
+        const int x = ind[l];
+        ind[l] = ind[r];
+        ind[r] = x;
+      }
+    }
+  }
+  kd_sync();
+  return b + nR;
+}
+
+// buildIndex by one wave (DFS over an explicit stack of {node, left, right, bbox} frames); returns the
+// node count (root 0) and the root bbox in box[0..5] (lo xyz, hi xyz).
+LG_DEVICE int kd_build(const KdView& K, int n, float* box) {
+  const int lane = lane_id();
+  for (int i = lane; i < n; i += 64) K.vind[i] = i;
+  kd_sync();
+  if (n <= 0) return 0;
+  float lo[3], hi[3];
+  kd_minmax(K.pts, K.vind, n, lo, hi);  // computeBoundingBox (:1316-1337)
+  if (lane < 3) { box[lane] = lo[lane]; box[3 + lane] = hi[lane]; }
+  float* fr = K.frames;  // frame: node, left, right, lo[3], hi[3] (9 words, ints as bits)
+  auto push = [&](int sp, int nd, int l, int r, const float* a, const float* z) {  // lanes 0..8, a field each
+    const float w = lane == 0 ? __int_as_float(nd) : lane == 1 ? __int_as_float(l) : lane == 2 ? __int_as_float(r)
+                  : lane == 3 ? a[0] : lane == 4 ? a[1] : lane == 5 ? a[2] : lane == 6 ? z[0] : lane == 7 ? z[1] : z[2];
+    if (lane < 9) fr[9 * sp + lane] = w;
+  };
+  push(0, 0, 0, n, lo, hi);
+  kd_sync();
+  int sp = 1, nodes = 1;
+  const float EPS = 0.00001f;
+  while (sp > 0) {
+    --sp;
+    const int nd = __float_as_int(fr[9 * sp]), left = __float_as_int(fr[9 * sp + 1]), right = __float_as_int(fr[9 * sp + 2]);
+    float blo[3] = {fr[9 * sp + 3], fr[9 * sp + 4], fr[9 * sp + 5]}, bhi[3] = {fr[9 * sp + 6], fr[9 * sp + 7], fr[9 * sp + 8]};
+    KdNode node;
+    node.left = left;
+    node.right = right;
+    node.c1 = node.c2 = -1;
+    node.divfeat = 0;
+    node.divlow = node.divhigh = 0.f;
+    node.pad = 0;
+    const int count = right - left;
+    if (count > KD_LEAF) {
+      int* ind = K.vind + left;
+      float mn[3], mx[3];
+      kd_minmax(K.pts, ind, count, mn, mx);
+      // middleSplit_ (:909-958)
+      float max_span = bhi[0] - blo[0];
+      for (int d = 1; d < 3; ++d) {
+        const float span = bhi[d] - blo[d];
+        if (span > max_span) max_span = span;
+      }
+      float max_spread = -1;
+      int cf = 0;
+      for (int d = 0; d < 3; ++d) {
+        const float span = bhi[d] - blo[d];
+        if (span > (1 - EPS) * max_span) {
+          const float spread = mx[d] - mn[d];
+          if (spread > max_spread) { cf = d; max_spread = spread; }
+        }
+      }
+      const float split_val = (blo[cf] + bhi[cf]) / 2;
+      const float cv = split_val < mn[cf] ? mn[cf] : (split_val > mx[cf] ? mx[cf] : split_val);
+      const int lim1 = kd_pass(K.pts, ind, 0, count, cf, cv, 0, K.tmp, K.tmp + K.vh);
+      const int lim2 = kd_pass(K.pts, ind, lim1, count, cf, cv, 1, K.tmp, K.tmp + K.vh);
+      const int idx = lim1 > count / 2 ? lim1 : (lim2 < count / 2 ? lim2 : count / 2);
+      // the children's tight bounds along cf (divideTree's left_bbox.high / right_bbox.low, :898-899)
+      float dl = -FLT_MAX, dh = FLT_MAX;
+      for (int t = lane; t < count; t += 64) {
+        const float k = kd_get(K.pts, ind[t], cf);
+        if (t < idx) dl = fmaxf(dl, k);
+        else dh = fminf(dh, k);
+      }
+      node.divfeat = cf;
+      node.divlow = wave_max(dl);
+      node.divhigh = wave_min(dh);
+      node.c1 = nodes;
+      node.c2 = nodes + 1;
+      nodes += 2;
+      float lhi[3] = {bhi[0], bhi[1], bhi[2]}, rlo[3] = {blo[0], blo[1], blo[2]};
+      lhi[cf] = cv;
+      rlo[cf] = cv;
+      push(sp, node.c2, left + idx, right, rlo, bhi);     // child2 below child1: child1 is built first
+      push(sp + 1, node.c1, left, left + idx, blo, lhi);
+      sp += 2;
+    }
+    if (lane == 0) K.node[nd] = node;
+    kd_sync();
+  }
+  return nodes;
+}
+
+// nanoflann's searchLevel for k = 1 (one lane; explicit stack of {node, mindistsq, dists[3]} frames,
+// the other child pushed when descending and tested against the then-current worst distance when
+// popped, as the recursion tests it after the best child's subtree).  *d = the distance found.
+LG_DEVICE int kd_nn1(const KdView& K, const float* box, float4 q, float* stk, int cap, float& dout, bool& ovf) {
+  const float qv[3] = {q.x, q.y, q.z};
+  float worst = FLT_MAX;
+  int best = -1;
+  float dists[3] = {0.f, 0.f, 0.f};
+  float distsq = 0.f;  // computeInitialDistances (:1005-1022)
+  for (int d = 0; d < 3; ++d) {
+    if (qv[d] < box[d]) { dists[d] = (qv[d] - box[d]) * (qv[d] - box[d]); distsq += dists[d]; }
+    if (qv[d] > box[3 + d]) { dists[d] = (qv[d] - box[3 + d]) * (qv[d] - box[3 + d]); distsq += dists[d]; }
+  }
+  int sp = 0;
+  int nd = 0;
+  bool popped = false;
+  float mind = distsq;
+  while (true) {
+    if (popped) {
+      if (sp == 0) break;
+      --sp;
+      nd = __float_as_int(stk[5 * sp]);
+      mind = stk[5 * sp + 1];
+      dists[0] = stk[5 * sp + 2]; dists[1] = stk[5 * sp + 3]; dists[2] = stk[5 * sp + 4];
+      if (!(mind * 1.0f <= worst)) continue;  // epsError = 1 + eps, eps 0
+    }
+    popped = true;
+    KdNode n = K.node[nd];
+    while (n.c1 >= 0) {
+      const int idx = n.divfeat;
+      const float val = qv[idx];
+      const float diff1 = val - n.divlow, diff2 = val - n.divhigh;
+      int bestc, other;
+      float cut;
+      if ((diff1 + diff2) < 0) { bestc = n.c1; other = n.c2; cut = (val - n.divhigh) * (val - n.divhigh); }
+      else { bestc = n.c2; other = n.c1; cut = (val - n.divlow) * (val - n.divlow); }
+      if (sp < cap) {
+        stk[5 * sp] = __int_as_float(other);
+        stk[5 * sp + 1] = mind + cut - dists[idx];
+        for (int d = 0; d < 3; ++d) stk[5 * sp + 2 + d] = d == idx ? cut : dists[d];
+        ++sp;
+      } else {
+        ovf = true;
+      }
+      n = K.node[bestc];
+    }
+    const float worst_entry = worst;  // searchLevel's leaf: worstDist() once, then addPoint
+    for (int i = n.left; i < n.right; ++i) {
+      const int index = K.vind[i];
+      const float4 p = K.pts[index];
+      float dist = 0.f;  // L2_Simple_Adaptor::evalMetric (:432-440)
+      float df = qv[0] - p.x;
+      dist += df * df;
+      df = qv[1] - p.y;
+      dist += df * df;
+      df = qv[2] - p.z;
+      dist += df * df;
+      if (dist < worst_entry && dist < worst) {  // KNNResultSet(1)::addPoint: replace iff strictly closer
+        worst = dist;
+        best = index;
+      }
+    }
+  }
+  dout = worst;
+  return best;
+}
+
+// Re-resolve the tied queries L.tieq[0, L.ntie) with nanoflann's tree (built on first use in this LM
+// loop).  Wave 0 only; the caller synchronises the workgroup around it.
+template <class Lds>
+LG_DEVICE void kd_resolve_ties(Lds& L, const KdView& K, int nl, int& st) {
+  if (!L.kd_built) {
+    kd_build(K, nl, L.kd_box);
+    if (lane_id() == 0) L.kd_built = 1;
+  }
+  const int cap = (10 * K.vh) / (5 * 64);  // search frames per lane
+  for (int k0 = 0; k0 < L.ntie; k0 += 64) {
+    const int k = k0 + lane_id();
+    if (k < L.ntie) {
+      const int q = L.tieq[k];
+      float d;
+      bool ovf = false;
+      const int c = kd_nn1(K, L.kd_box, L.sel[q], K.frames + (size_t)lane_id() * cap * 5, cap, d, ovf);
+      if (!ovf) L.ind1[q] = c;  // (a stack overflow keeps the grid's lowest index)
+    }
+  }
+}
+
 // one LM loop (surf or corner), <= 25 iterations.  The correspondence search (iterations 0, 5, 10,
 // 15, 20) uses the whole workgroup; the other iterations only re-weight the same correspondences
 // with the updated transform, so wave 0 runs each block of up to 5 iterations on its own
@@ -3910,7 +4184,7 @@ LG_DEVICE int lds_nn(const float4* last, int nl, float4 q, float r2, bool& tie, 
 // in registers) and the workgroup meets once per block instead of three times per iteration.
 template <bool kF1, class Lds>
 LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __restrict__ feat, int nq,
-                       const float4* __restrict__ last_g, int nl, bool surf, float4* gp, int& iters) {
+                       const float4* __restrict__ last_g, int nl, bool surf, float4* gp, int& iters, KdView Kv) {
   const int tid = threadIdx.x;
   const int nw = (int)(blockDim.x >> 6);
   const bool small = nl <= LM_LAST_LDS;
@@ -3928,7 +4202,8 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
   const float4* last = small ? (const float4*)L.u.lastc : last_g;
   ring_index(L, last, nl);
   PROF_ADD(surf ? 16 : 48, t_bg0);
-  if (tid == 0) L.iters = 0;
+  if (tid == 0) { L.iters = 0; L.kd_built = 0; }
+  Kv.pts = last;
   for (int iter = 0; iter < 25; iter += 5) {
     {  // search (all waves)
       float cur[6];
@@ -3943,7 +4218,7 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
       // as many lanes per query as the block allows (8, 4, 2 or 1); with 512 threads (VLP-16) the
       // surf ~170 and corner ~115 queries get 2 and 4 lanes, with 768 threads both get 4
       const int tpq = nq * 8 <= (int)blockDim.x ? 8 : nq * 4 <= (int)blockDim.x ? 4 : nq * 2 <= (int)blockDim.x ? 2 : 1;
-      if (tid == 0) L.nfall = 0;
+      if (tid == 0) { L.nfall = 0; L.ntie = 0; }
       for (int base = 0; base < nq * tpq; base += (int)blockDim.x) {
         const int t = base + tid, q = t / tpq, sub = t % tpq;
         const bool act = q < nq;
@@ -3953,10 +4228,17 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
         c = grid_nn(L, gcell, gp, qs, P.nn_dist_sqr, tie, sub, tpq, act);
         if (act && sub == 0) {
           L.ind1[q] = c;
-          if (tie) st |= LEGO_ST_NN_TIE;
+          if (tie) {
+            st |= LEGO_ST_NN_TIE;
+            L.tieq[atomicAdd(&L.ntie, 1)] = q;
+          }
         }
       }
       __syncthreads();
+      if (L.ntie > 0) {  // exact ties: nanoflann's choice (its first visited point), from its tree
+        if (wave_id() == 0) kd_resolve_ties(L, Kv, nl, st);
+        __syncthreads();
+      }
       PROF_ADD(surf ? 37 : 46, t_nn0);
       PROF_T(t_rs0);
       // ring-limited 2nd / 3rd points (fa.cpp:514-564, 652-713).  Larger clouds: one wave per query
@@ -4209,11 +4491,18 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
   } else {
     if (tid == 0 && S.tree_stale) L.status |= LEGO_ST_STALE_TREE;
     float4* gp = B.grid_pts + (size_t)s * VH;
+    KdView kv;
+    kv.pts = nullptr;
+    kv.node = B.kd_node + (size_t)s * 2 * VH;
+    kv.vind = B.kd_vind + (size_t)s * VH;
+    kv.tmp = B.kd_tmp + (size_t)s * 2 * VH;
+    kv.frames = B.kd_frames + (size_t)s * 10 * VH;
+    kv.vh = VH;
     PROF_T(t_ls0);
-    lm_loop<kF1>(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, gp, it_s);
+    lm_loop<kF1>(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, gp, it_s, kv);
     PROF_ADD(17, t_ls0);
     PROF_T(t_lc0);
-    lm_loop<kF1>(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, gp, it_c);
+    lm_loop<kF1>(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, gp, it_c, kv);
     PROF_ADD(18, t_lc0);
   }
   __syncthreads();
@@ -4484,6 +4773,55 @@ extern "C" int lego_test_libm(const float* h_a, const float* h_b, float* h_out, 
       rc = LEGO_EDEVICE;
   }
   hipFree(a); hipFree(b); hipFree(o);
+  return rc;
+}
+
+__global__ __launch_bounds__(64) void k_kd_test(KdView K, int n, const float4* q, int m, int* idx, float* dist) {
+  __shared__ float box[6];
+  kd_build(K, n, box);
+  const int cap = (10 * K.vh) / (5 * 64);
+  for (int k0 = 0; k0 < m; k0 += 64) {
+    const int k = k0 + lane_id();
+    if (k < m) {
+      float d = 0.f;
+      bool ovf = false;
+      const int c = n > 0 ? kd_nn1(K, box, q[k], K.frames + (size_t)lane_id() * cap * 5, cap, d, ovf) : -1;
+      idx[k] = ovf ? -2 : c;
+      dist[k] = n > 0 ? d : FLT_MAX;
+    }
+  }
+}
+
+// nanoflann's 1-NN on the device (the LM's exact-tie path: kd_build + kd_nn1) for m queries against a
+// cloud of n points (x, y, z, w float32 each); idx -2 = search stack overflow.
+extern "C" int lego_test_kd_knn1(const float* h_cloud, int32_t n, const float* h_q, int32_t m, int32_t* h_idx,
+                                 float* h_dist) {
+  if (n < 0 || m < 0 || (n && !h_cloud) || (m && (!h_q || !h_idx || !h_dist)) || n > (1 << 22)) return LEGO_EINVAL;
+  const int vh = std::max(n, 64);
+  float4 *c = nullptr, *q = nullptr;
+  KdView K = {};
+  int *idx = nullptr;
+  float* dist = nullptr;
+  int rc = LEGO_OK;
+  if (hipMalloc((void**)&c, (size_t)vh * 16) != hipSuccess || hipMalloc((void**)&q, (size_t)std::max(m, 1) * 16) != hipSuccess ||
+      hipMalloc((void**)&K.node, (size_t)2 * vh * sizeof(KdNode)) != hipSuccess ||
+      hipMalloc((void**)&K.vind, (size_t)vh * 4) != hipSuccess || hipMalloc((void**)&K.tmp, (size_t)2 * vh * 4) != hipSuccess ||
+      hipMalloc((void**)&K.frames, (size_t)10 * vh * 4) != hipSuccess ||
+      hipMalloc((void**)&idx, (size_t)std::max(m, 1) * 4) != hipSuccess || hipMalloc((void**)&dist, (size_t)std::max(m, 1) * 4) != hipSuccess)
+    rc = LEGO_ENOMEM;
+  K.pts = c;
+  K.vh = vh;
+  if (rc == LEGO_OK && ((n && hipMemcpy(c, h_cloud, (size_t)n * 16, hipMemcpyHostToDevice) != hipSuccess) ||
+                        (m && hipMemcpy(q, h_q, (size_t)m * 16, hipMemcpyHostToDevice) != hipSuccess)))
+    rc = LEGO_EDEVICE;
+  if (rc == LEGO_OK) {
+    hipLaunchKernelGGL(k_kd_test, dim3(1), dim3(64), 0, 0, K, n, q, m, idx, dist);
+    if (hipGetLastError() != hipSuccess || (m && (hipMemcpy(h_idx, idx, (size_t)m * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+                                                  hipMemcpy(h_dist, dist, (size_t)m * 4, hipMemcpyDeviceToHost) != hipSuccess)))
+      rc = LEGO_EDEVICE;
+  }
+  for (void* p : {(void*)c, (void*)q, (void*)K.node, (void*)K.vind, (void*)K.tmp, (void*)K.frames, (void*)idx, (void*)dist})
+    if (p) hipFree(p);
   return rc;
 }
 

@@ -25,7 +25,7 @@ ST_EMITTED = 0x080
 ST_VOXEL_OVERFLOW = 0x100
 ST_DEGEN_UB = 0x200
 # bits that mark reference undefined behaviour given defined behaviour here
-ST_UB_MASK = ST_STALE_TREE | ST_FWD_OOB | ST_NN_TIE | ST_STALE_IND_OOB | ST_DEGEN_UB
+ST_UB_MASK = ST_STALE_TREE | ST_FWD_OOB | ST_STALE_IND_OOB | ST_DEGEN_UB  # (NN_TIE: resolved as nanoflann does)
 
 
 class LegoParams(C.Structure):

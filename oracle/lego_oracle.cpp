@@ -1362,6 +1362,22 @@ int oracle_smoothness(oracle_ctx* c, int k, float* value, int64_t* ind) {
   return LEGO_OK;
 }
 
+// Test hook: overwrite the LM state the next association starts from (lego_test_set_lm_state's
+// counterpart): transformCur / transformSum, isDegenerate, the Last clouds and the trees' staleness.
+int oracle_set_lm_state(oracle_ctx* c, const float* cur, const float* sum, int32_t degenerate, const float* corner,
+                        int32_t n_corner, const float* surf, int32_t n_surf, int32_t tree_stale) {
+  FeatureAssociation& f = c->fa;
+  if (!f.systemInitedLM) return LEGO_EINVAL;
+  for (int k = 0; k < 6; ++k) { f.transformCur[k] = cur[k]; f.transformSum[k] = sum[k]; }
+  f.isDegenerate = degenerate != 0;
+  f.corner_last.assign((const Pt*)corner, (const Pt*)corner + n_corner);
+  f.surf_last.assign((const Pt*)surf, (const Pt*)surf + n_surf);
+  f.laserCloudCornerLastNum = n_corner;
+  f.laserCloudSurfLastNum = n_surf;
+  f.tree_stale = tree_stale != 0;
+  return LEGO_OK;
+}
+
 // Test hook: the LM members that are not in the AssociationOut (featureAssociation.h:115, the kd-tree
 // rebuild flag of :1356): isDegenerate and "trees stale" after the last call.
 int oracle_lm_flags(oracle_ctx* c, int32_t* degenerate, int32_t* tree_stale) {

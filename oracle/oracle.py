@@ -39,6 +39,8 @@ def lib():
         L.oracle_feature_association_from.argtypes = [C.c_void_p, P(A.LegoProjectionOut), P(A.LegoAssociationOut)]
         L.oracle_smoothness.argtypes = [C.c_void_p, C.c_int, P(C.c_float), P(C.c_int64)]
         L.oracle_lm_flags.argtypes = [C.c_void_p, P(C.c_int32), P(C.c_int32)]
+        L.oracle_set_lm_state.argtypes = [C.c_void_p, P(C.c_float), P(C.c_float), C.c_int32, P(C.c_float), C.c_int32,
+                                          P(C.c_float), C.c_int32, C.c_int32]
         L.oracle_std_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int, C.c_int]
         L.oracle_atan2f.argtypes = [C.c_float, C.c_float]
         L.oracle_atan2f.restype = C.c_float
@@ -84,6 +86,18 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("oracle_feature_association rc=%d" % rc)
         return A.association_to_dict(out)
+
+    def feature_association_with_state(self, proj, cur, tsum, degenerate, corner_last, surf_last, tree_stale):
+        """feature_association(proj) starting from the given LM state (oracle_set_lm_state)."""
+        import numpy as np
+        f = lambda a, k: np.ascontiguousarray(np.asarray(a, np.float32).reshape(-1, k))  # noqa: E731
+        c6, s6, cl, sl = f(cur, 6), f(tsum, 6), f(corner_last, 4), f(surf_last, 4)
+        fp = lambda a: a.ctypes.data_as(P(C.c_float))  # noqa: E731
+        rc = lib().oracle_set_lm_state(self.h, fp(c6), fp(s6), int(degenerate), fp(cl), len(cl), fp(sl), len(sl),
+                                       int(tree_stale))
+        if rc != 0:
+            raise RuntimeError("oracle_set_lm_state rc=%d" % rc)
+        return self.feature_association(proj)
 
     def lm_flags(self):
         """(isDegenerate, kd-trees stale) after the last feature_association."""

@@ -11,9 +11,10 @@
 //
 // PARITY STATUS:
 //   * kNN-5 (nanoflann nearestKSearch(k = 5), :1033, :1141): the 5 nearest by (distance, index) from an
-//     exact search of the 1 m ball (only the 5th distance < 1.0 is ever used, :1036, :1144).
-//     oracle/_ref/nanoflann_pin (the reference's vendored nanoflann 1.3.0) pins it: same 5 points in
-//     the same order whenever the 6 nearest distances are distinct.
+//     exact search of the 1 m ball (only the 5th distance < 1.0 is ever used, :1036, :1144); when any
+//     of the 6 nearest distances are equal, nanoflann's own answer from its restated tree
+//     (nanoflann_restated.h, built on the first such query of a map).  oracle/_ref/nanoflann_pin (the
+//     reference's vendored nanoflann 1.3.0) pins both: test_knn5_pin_nanoflann, test_nanoflann_pin.
 //   * Eigen (absent here, unpinned; ROS Melodic's Eigen 3.3.4 restated):
 //       SelfAdjointEigenSolver<Matrix3f> (:1077): scaling, the 3x3 Householder tridiagonalisation,
 //         implicit symmetric QR with Wilkinson shifts, ascending sort with column swaps.  The
@@ -35,6 +36,7 @@
 #include <vector>
 
 #include "../include/lego_s2m.h"
+#include "nanoflann_restated.h"
 
 namespace s2m {
 
@@ -300,6 +302,8 @@ struct Grid {
   std::unordered_map<long long, std::vector<int>> cells;
   const Pt* pts = nullptr;
   int n = 0;
+  mutable nfr::KdTree<Pt> tree;  // nanoflann's tree of the map, for tied queries (built on first use)
+  mutable bool tree_built = false;
   static long long key(long long x, long long y, long long z) { return (x * 73856093LL) ^ (y * 19349663LL) ^ (z * 83492791LL); }
   void build(const Pt* p, int np) {
     pts = p;
@@ -310,6 +314,7 @@ struct Grid {
       mn[0] = std::min(mn[0], p[j].x); mn[1] = std::min(mn[1], p[j].y); mn[2] = std::min(mn[2], p[j].z);
     }
     for (int j = 0; j < np; ++j) cells[key(cell(p[j].x, 0), cell(p[j].y, 1), cell(p[j].z, 2))].push_back(j);
+    tree_built = false;
   }
   long long cell(float v, int a) const { return (long long)std::floor((double)(v - mn[a]) / cs); }
   // the 5 nearest as (d, index) pairs, true if the 5th is closer than 1.0 (d^2); tie flags the 6th
@@ -335,6 +340,15 @@ struct Grid {
     for (int k = 0; k < 5; ++k) { out[k] = cand[k].second; dist[k] = cand[k].first; }
     for (int k = 0; k + 1 < (int)cand.size() && k < 5; ++k)
       if (cand[k].first == cand[k + 1].first) tie = true;
+    if (tie) {  // equal distances among the 6 nearest: nanoflann's order (first visited wins)
+      if (!tree_built) {
+        tree.build(pts, n);
+        tree_built = true;
+      }
+      const float qv[3] = {q.x, q.y, q.z};
+      tree.knn(qv, 5, out, dist);
+      return dist[4] < 1.0f;
+    }
     return true;
   }
 };
