@@ -253,10 +253,12 @@ int  lego_test_project_cells(const lego_params* p, const float* xyzw, int32_t n,
 int  lego_test_set_lm_state(lego_ctx* ctx, const float* transform_cur, const float* transform_sum,
                             int32_t degenerate, const lego_point* corner_last, int32_t n_corner,
                             const lego_point* surf_last, int32_t n_surf, int32_t tree_stale);
-/* nanoflann's 1-NN as the LM resolves exact distance ties on the device (the tree built as nanoflann
- * 1.3.0 builds it, its searchLevel): m queries against a cloud of n points (x, y, z, w float32 each);
- * out idx (-2: search stack overflow) and squared distance. */
-int  lego_test_kd_knn1(const float* cloud, int32_t n, const float* queries, int32_t m, int32_t* idx, float* dist);
+/* nanoflann's kNN as the device resolves exact distance ties (the tree built as nanoflann 1.3.0 builds
+ * it, its searchLevel with a KNNResultSet(k)): k = 1 the LM's 1-NN, k = 5 scan-to-map's kNN-5; m queries
+ * against a cloud of n points (x, y, z, w float32 each); out idx[m][k] nearest first (-1 past the count
+ * found, -2: search stack overflow) and squared distances. */
+int  lego_test_kd_knn(const float* cloud, int32_t n, const float* queries, int32_t m, int32_t k, int32_t* idx,
+                      float* dist);
 /* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
  * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */
 int  lego_debug_prof(uint64_t* out256, int32_t reset);

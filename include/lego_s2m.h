@@ -38,7 +38,7 @@ extern "C" {
 /* info[4] of a problem: [0] 1 if the optimisation ran (:1316: corner map > 10 and surf map > 100
  * points), [1] LM iterations run (<= 10), [2] correspondences of the last iteration
  * (laserCloudOri size), [3] status bits below. */
-#define LEGO_S2M_ST_KNN_TIE     0x01  /* equal distances among a query's 6 nearest (kd-tree visit order unpinned) */
+#define LEGO_S2M_ST_KNN_TIE     0x01  /* equal distances among a query's 6 nearest: resolved by nanoflann's tree, as the reference */
 #define LEGO_S2M_ST_DEGENERATE  0x02  /* iteration 0: largest eigenvalue of AtA < 100 (:1267-1285)        */
 #define LEGO_S2M_ST_FEW         0x04  /* an iteration had < 50 correspondences (:1208: no update)           */
 #define LEGO_S2M_ST_CONVERGED   0x08  /* LMOptimization returned true (:1308) before the 10th iteration     */

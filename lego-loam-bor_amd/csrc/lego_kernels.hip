@@ -24,6 +24,7 @@
 
 #include "../../include/lego_frontend.h"
 #include "lego_device.h"
+#include "lego_kdtree.h"
 #include "lego_introsort.h"
 
 using namespace lg;
@@ -833,28 +834,67 @@ LG_DEVICE void distort_segmented(const LgParams& P, const LgBufs& B, int s, int 
   }
 }
 
-// ---- k_segment (LDS path: V <= 16, V*H < 32768) ---------------------------------------------
-// One LDS word per cell carries the whole labelling state:
-//   cell index (>= 0)        eligible cell: union-find parent, after path compression its root
+// ---- k_segment (LDS path: V <= 16, V*H <= SEG_VH_MAX) ----------------------------------------
+// One 16-bit LDS word per cell carries the whole labelling state (57.6 KB for VLP-16, so the kernel
+// co-resides with k_lm's 66 KB on a CU):
+//   cell index (< 0x7ffe)    eligible cell: union-find parent, after path compression its root
 //   SEG_GND / SEG_EMPTY      ground cell / no return (label -1, :293-300)
-//   SEG_FLAG | payload       a root: first {count:15 << 16 | row mask of non-seed members:16},
-//                            then its label (k + 1 in seed raster order, or 999999)
-// so no per-cell state leaves LDS before the final label / compaction pass.  Global reads are
-// batched (kSegU cells per lane per round, all loads issued before use).
-#define SEG_GND 0x7ffffffe
-#define SEG_EMPTY 0x7fffffff
-#define SEG_FLAG 0x80000000u
+//   SEG_FLAG | payload       a root: its member count (seed included); then, for 5 <= count < 30, the
+//                            pending flag and the rows its non-seed members occupy relative to the
+//                            seed's (bit d: d rows below, d = 0..SEG_DMAX, the last bit for any
+//                            deeper); finally its label (k + 1 in seed raster order, or SEG_LBAD for
+//                            999999)
+// A component's rows form an interval that starts at its seed's row (edges join cells of one row or
+// of adjacent rows, and the seed is its first cell in raster order), so lineCountFlag's count of
+// distinct non-seed rows (:466-470) is bit 0 plus the deepest d present: exact while
+// segment_valid_line_num <= SEG_DMAX (lg_lds_segment).  LDS atomics are 32-bit: a half-word's CAS / add / or operates on its word
+// (the other half is never changed; counts stay below 0x8000, so an add never carries across).
+// Global reads are batched (SEG_U cells per lane per round, all loads issued before use).
+#define SEG_GND 0x7ffe
+#define SEG_EMPTY 0x7fff
+#define SEG_FLAG 0x8000
+#define SEG_PEND 0x2000
+#define SEG_FEAS 0x4000
+#define SEG_LBAD 0x7fff   // label payload of an infeasible root (999999)
+#define SEG_DMAX 12       // row bits 0..12 of a pending root (below SEG_PEND)
+#define SEG_VH_MAX 32765  // cell indices stay below SEG_GND
 #define SEG_U 8
 #define SEG_ROUNDS 4  // 4 * 1024 * SEG_U = 32768 >= V*H on this path
 
 LG_DEVICE bool seg_eligible(int8_t g, float r) { return g != 1 && r != FLT_MAX; }  // _label_mat == 0
+
+// half-word LDS atomics through the containing 32-bit word
+LG_DEVICE unsigned* h16_word(uint16_t* p, int i) { return (unsigned*)p + (i >> 1); }
+LG_DEVICE int h16_shift(int i) { return (i & 1) << 4; }
+LG_DEVICE int cas16(uint16_t* p, int i, int expected, int desired) {  // returns the value found
+  unsigned* w = h16_word(p, i);
+  const int sh = h16_shift(i);
+  unsigned old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (true) {
+    const int cur = (int)((old >> sh) & 0xffffu);
+    if (cur != expected) return cur;
+    const unsigned nw = (old & ~(0xffffu << sh)) | ((unsigned)desired << sh);
+    const unsigned got = atomicCAS(w, old, nw);
+    if (got == old) return expected;
+    old = got;
+  }
+}
+LG_DEVICE void uf_unite_rep16(uint16_t* parent, int a, int b) {  // uf_unite_rep on half-words
+  int ra = uf_rep(parent, a), rb = uf_rep(parent, b);
+  while (ra != rb) {
+    if (ra > rb) { const int t = ra; ra = rb; rb = t; }
+    const int old = cas16(parent, rb, rb, ra);  // hook root rb under ra
+    if (old == rb) break;
+    rb = uf_rep(parent, old);
+  }
+}
 
 __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, H = P.H, VH = P.VH, G = P.G;
   int* scratch = smem;  // 64 ints
-  int* parent = smem + 64;
+  uint16_t* parent = (uint16_t*)(smem + 64);
   const float* __restrict__ range = B.range + (size_t)s * VH;
   const int8_t* __restrict__ ground = B.ground + (size_t)s * VH;
   const float4* __restrict__ cloud = B.cloud + (size_t)s * VH;
@@ -896,7 +936,7 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
       if (eu) p0 = c - H;
       if (ew) { if (p0 == c) p0 = i * H; else rest |= 2u; }
       if (el) { if (p0 == c) p0 = c - 1; else rest |= 4u; }
-      parent[c] = e0 ? p0 : (g0[u] == 1 ? SEG_GND : SEG_EMPTY);
+      parent[c] = (uint16_t)(e0 ? p0 : (g0[u] == 1 ? SEG_GND : SEG_EMPTY));
       ebits[rd] |= rest << (3 * u);
     }
   }
@@ -915,7 +955,7 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
       const int i = c / H;
       const int k = b % 3;
       const int o = k == 0 ? c - H : (k == 1 ? i * H : c - 1);
-      uf_unite_rep(parent, c, o);
+      uf_unite_rep16(parent, c, o);
     }
   }
   __syncthreads();
@@ -925,20 +965,34 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   PROF_T(t_s2);
   for (int c = tid; c < VH; c += nt) {
     const int p = parent[c];
-    if (p < SEG_GND && p != c) parent[c] = uf_find(parent, p);
+    if (p < SEG_GND && p != c) parent[c] = (uint16_t)uf_find(parent, p);
   }
   __syncthreads();
   PROF_ADD(27, t_s2);
   // ---- pass 4: per-root size (seed included) and rows of the non-seed members (:466-470) ---------
   PROF_T(t_s3);
   for (int c = tid; c < VH; c += nt)
-    if (parent[c] == c) parent[c] = (int)(SEG_FLAG | (1u << 16));
+    if (parent[c] == c) parent[c] = (uint16_t)(SEG_FLAG | 1);
   __syncthreads();
   for (int c = tid; c < VH; c += nt) {
     const int r = parent[c];
-    if (r >= 0 && r < SEG_GND) {
-      atomicAdd((unsigned*)&parent[r], 1u << 16);
-      atomicOr((unsigned*)&parent[r], 1u << (c / H));
+    if (r < SEG_GND) atomicAdd(h16_word(parent, r), 1u << h16_shift(r));
+  }
+  __syncthreads();
+  // count >= 30: feasible; < seg_valid_pt: not; otherwise the rows decide (pending)
+  for (int c = tid; c < VH; c += nt) {
+    const int a = parent[c];
+    if (a & SEG_FLAG) {
+      const int cnt = a & 0x7fff;
+      parent[c] = (uint16_t)(SEG_FLAG | (cnt >= 30 ? SEG_FEAS : (cnt >= P.seg_valid_pt ? SEG_PEND : 0)));
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < VH; c += nt) {
+    const int r = parent[c];
+    if (r < SEG_GND && (parent[r] & SEG_PEND)) {
+      const int d = c / H - r / H;  // >= 0: the seed is the component's first cell in raster order
+      atomicOr(h16_word(parent, r), (1u << min(d, SEG_DMAX)) << h16_shift(r));
     }
   }
   __syncthreads();
@@ -946,16 +1000,16 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   wave_raster_compact(
       VH, scratch,
       [&](int c, bool& feas, bool& isroot) {
-        const unsigned a = (unsigned)parent[c];
-        isroot = (a & SEG_FLAG) != 0u;
+        const int a = parent[c];
+        isroot = (a & SEG_FLAG) != 0;
         if (isroot) {
-          const int cnt = (int)((a >> 16) & 0x7fffu);
-          const int lines = __popc(a & 0xffffu);
-          feas = cnt >= 30 || (cnt >= P.seg_valid_pt && lines >= P.seg_valid_line);
+          // distinct non-seed rows: the seed's row (bit 0) + the rows below it up to the deepest
+          const int lines = (a & 1) + (31 - __clz((a & ((2 << SEG_DMAX) - 2)) | 1));
+          feas = (a & SEG_FEAS) || ((a & SEG_PEND) && lines >= P.seg_valid_line);
         }
       },
       [&](int c, bool feas, bool isroot, int k, int) {
-        if (isroot) parent[c] = (int)(SEG_FLAG | (feas ? (unsigned)(k + 1) : 999999u));
+        if (isroot) parent[c] = (uint16_t)(SEG_FLAG | (feas ? k + 1 : SEG_LBAD));
       });
   PROF_ADD(28, t_s3);
   // ---- pass 5: label image + cloudSegmentation's raster-order compaction (:358-396) -------------
@@ -974,9 +1028,12 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   auto cell_label = [&](int c, int& lab, bool& gnd) {
     const int v = parent[c];
     gnd = v == SEG_GND;
-    if (v == SEG_GND || v == SEG_EMPTY) lab = -1;
-    else if (v < 0) lab = v & 0x7fffffff;
-    else lab = parent[v] & 0x7fffffff;
+    if (v == SEG_GND || v == SEG_EMPTY) {
+      lab = -1;
+    } else {
+      const int l = ((v & SEG_FLAG) ? v : (int)parent[v]) & 0x7fff;
+      lab = l == SEG_LBAD ? 999999 : l;
+    }
   };
   auto classify = [&](int c, int lab, bool gnd, bool& pseg, bool& pout) {
     const int i = c / H, j = c - i * H;
@@ -3908,260 +3965,17 @@ LG_DEVICE int lds_nn(const float4* last, int nl, float4 q, float r2, bool& tie, 
 }
 
 // ============================================================================================
-// nanoflann's kd-tree, for the rare 1-NN with an exact distance tie
+// nanoflann's kd-tree, for the rare 1-NN with an exact distance tie (lego_kdtree.h)
 // ============================================================================================
-// The grid search returns the exact nearest distance and flags a query when several points share it.
-// Which of them kdtree->nearestKSearch returns is nanoflann's first visited (strict < in searchLevel
-// and KNNResultSet::addPoint), a function of its tree.  So when a search has tied queries, wave 0
-// builds the tree of the Last cloud exactly as nanoflann 1.3.0 does (buildIndex / divideTree /
-// middleSplit_ / planeSplit, nanoflann.hpp:857-1003, 1190-1202, 1316-1337; leaf_max_size 10;
-// oracle/nanoflann_restated.h is the host statement) and re-runs nanoflann's searchLevel (:1346-1409)
-// for those queries.  planeSplit's two Hoare passes are rank pairings: the k-th left stop (from the
-// left) swaps with the k-th right stop (from the right) while it lies left of it, so each pass is two
-// stop lists and one parallel swap.  Scratch per stream: B.kd_* (built once per LM loop, on demand).
-#define KD_LEAF 10
-struct KdView {
-  const float4* pts;  // the Last cloud, in its own order
-  KdNode* node;
-  int* vind;
-  int* tmp;           // [2 * VH]: left stops, right stops
-  float* frames;      // [10 * VH]
-  int vh;
-};
-
-LG_DEVICE float kd_get(const float4* pts, int i, int d) {
-  const float4 p = pts[i];
-  return d == 0 ? p.x : (d == 1 ? p.y : p.z);
-}
-LG_DEVICE void kd_sync() {  // this wave's global stores before its other lanes' loads of them
-  __threadfence_block();
-  __builtin_amdgcn_wave_barrier();
-}
-
-// computeMinMax (:836-848) of all three dimensions over ind[0, count) (order-independent)
-LG_DEVICE void kd_minmax(const float4* pts, const int* ind, int count, float* mn, float* mx) {
-  float a0 = FLT_MAX, a1 = FLT_MAX, a2 = FLT_MAX, b0 = -FLT_MAX, b1 = -FLT_MAX, b2 = -FLT_MAX;
-  for (int t0 = lane_id(); t0 < count; t0 += 64 * 4) {
-    float4 p4[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) p4[u] = pts[ind[min(t0 + 64 * u, count - 1)]];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a0 = fminf(a0, p4[u].x); a1 = fminf(a1, p4[u].y); a2 = fminf(a2, p4[u].z);
-      b0 = fmaxf(b0, p4[u].x); b1 = fmaxf(b1, p4[u].y); b2 = fmaxf(b2, p4[u].z);
-    }
-  }
-  mn[0] = wave_min(a0); mn[1] = wave_min(a1); mn[2] = wave_min(a2);
-  mx[0] = wave_max(b0); mx[1] = wave_max(b1); mx[2] = wave_max(b2);
-}
-
-// One planeSplit pass over ind[b, count) (:967-1003): mode 0 moves the keys < cv to the front (left
-// stops: !(key < cv), right stops: key < cv), mode 1 the keys <= cv.  Returns b + the number of
-// moved-to-front keys (lim1 / lim2).
-LG_DEVICE int kd_pass(const float4* pts, int* ind, int b, int count, int d, float cv, int mode, int* tL, int* tR) {
-  const int lane = lane_id();
-  int nL = 0, nR = 0;
-  // each position is a left stop (!front) or a right stop (front); four chunks' keys in flight at a time
-  for (int t0 = b; t0 < count; t0 += 256) {  // left stops ascending
-    float k4[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) k4[u] = kd_get(pts, ind[min(t0 + 64 * u + lane, count - 1)], d);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = t0 + 64 * u + lane;
-      const bool front = mode == 0 ? k4[u] < cv : k4[u] <= cv;
-      const bool ls = i < count && !front;
-      const unsigned long long m = __ballot(ls);
-      if (ls) tL[nL + popc_below(m)] = i;
-      nL += __popcll(m);
-    }
-  }
-  for (int t0 = count - 1; t0 >= b; t0 -= 256) {  // right stops descending
-    float k4[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) k4[u] = kd_get(pts, ind[max(t0 - 64 * u - lane, b)], d);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = t0 - 64 * u - lane;
-      const bool front = mode == 0 ? k4[u] < cv : k4[u] <= cv;
-      const bool rs = i >= b && front;
-      const unsigned long long m = __ballot(rs);
-      if (rs) tR[nR + popc_below(m)] = i;
-      nR += __popcll(m);
-    }
-  }
-  kd_sync();
-  const int K = min(nL, nR);
-  for (int k0 = 0; k0 < K; k0 += 64) {  // the valid pairs (L_k < R_k) are a prefix; swaps are disjoint
-    const int k = k0 + lane;
-    if (k < K) {
-      const int l = tL[k], r = tR[k];
-      if (l < r) {
-        const int x = ind[l];
-        ind[l] = ind[r];
-        ind[r] = x;
-      }
-    }
-  }
-  kd_sync();
-  return b + nR;
-}
-
-// buildIndex by one wave (DFS over an explicit stack of {node, left, right, bbox} frames); returns the
-// node count (root 0) and the root bbox in box[0..5] (lo xyz, hi xyz).
-LG_DEVICE int kd_build(const KdView& K, int n, float* box) {
-  const int lane = lane_id();
-  for (int i = lane; i < n; i += 64) K.vind[i] = i;
-  kd_sync();
-  if (n <= 0) return 0;
-  float lo[3], hi[3];
-  kd_minmax(K.pts, K.vind, n, lo, hi);  // computeBoundingBox (:1316-1337)
-  if (lane < 3) { box[lane] = lo[lane]; box[3 + lane] = hi[lane]; }
-  float* fr = K.frames;  // frame: node, left, right, lo[3], hi[3] (9 words, ints as bits)
-  auto push = [&](int sp, int nd, int l, int r, const float* a, const float* z) {  // lanes 0..8, a field each
-    const float w = lane == 0 ? __int_as_float(nd) : lane == 1 ? __int_as_float(l) : lane == 2 ? __int_as_float(r)
-                  : lane == 3 ? a[0] : lane == 4 ? a[1] : lane == 5 ? a[2] : lane == 6 ? z[0] : lane == 7 ? z[1] : z[2];
-    if (lane < 9) fr[9 * sp + lane] = w;
-  };
-  push(0, 0, 0, n, lo, hi);
-  kd_sync();
-  int sp = 1, nodes = 1;
-  const float EPS = 0.00001f;
-  while (sp > 0) {
-    --sp;
-    const int nd = __float_as_int(fr[9 * sp]), left = __float_as_int(fr[9 * sp + 1]), right = __float_as_int(fr[9 * sp + 2]);
-    float blo[3] = {fr[9 * sp + 3], fr[9 * sp + 4], fr[9 * sp + 5]}, bhi[3] = {fr[9 * sp + 6], fr[9 * sp + 7], fr[9 * sp + 8]};
-    KdNode node;
-    node.left = left;
-    node.right = right;
-    node.c1 = node.c2 = -1;
-    node.divfeat = 0;
-    node.divlow = node.divhigh = 0.f;
-    node.pad = 0;
-    const int count = right - left;
-    if (count > KD_LEAF) {
-      int* ind = K.vind + left;
-      float mn[3], mx[3];
-      kd_minmax(K.pts, ind, count, mn, mx);
-      // middleSplit_ (:909-958)
-      float max_span = bhi[0] - blo[0];
-      for (int d = 1; d < 3; ++d) {
-        const float span = bhi[d] - blo[d];
-        if (span > max_span) max_span = span;
-      }
-      float max_spread = -1;
-      int cf = 0;
-      for (int d = 0; d < 3; ++d) {
-        const float span = bhi[d] - blo[d];
-        if (span > (1 - EPS) * max_span) {
-          const float spread = mx[d] - mn[d];
-          if (spread > max_spread) { cf = d; max_spread = spread; }
-        }
-      }
-      const float split_val = (blo[cf] + bhi[cf]) / 2;
-      const float cv = split_val < mn[cf] ? mn[cf] : (split_val > mx[cf] ? mx[cf] : split_val);
-      const int lim1 = kd_pass(K.pts, ind, 0, count, cf, cv, 0, K.tmp, K.tmp + K.vh);
-      const int lim2 = kd_pass(K.pts, ind, lim1, count, cf, cv, 1, K.tmp, K.tmp + K.vh);
-      const int idx = lim1 > count / 2 ? lim1 : (lim2 < count / 2 ? lim2 : count / 2);
-      // the children's tight bounds along cf (divideTree's left_bbox.high / right_bbox.low, :898-899)
-      float dl = -FLT_MAX, dh = FLT_MAX;
-      for (int t = lane; t < count; t += 64) {
-        const float k = kd_get(K.pts, ind[t], cf);
-        if (t < idx) dl = fmaxf(dl, k);
-        else dh = fminf(dh, k);
-      }
-      node.divfeat = cf;
-      node.divlow = wave_max(dl);
-      node.divhigh = wave_min(dh);
-      node.c1 = nodes;
-      node.c2 = nodes + 1;
-      nodes += 2;
-      float lhi[3] = {bhi[0], bhi[1], bhi[2]}, rlo[3] = {blo[0], blo[1], blo[2]};
-      lhi[cf] = cv;
-      rlo[cf] = cv;
-      push(sp, node.c2, left + idx, right, rlo, bhi);     // child2 below child1: child1 is built first
-      push(sp + 1, node.c1, left, left + idx, blo, lhi);
-      sp += 2;
-    }
-    if (lane == 0) K.node[nd] = node;
-    kd_sync();
-  }
-  return nodes;
-}
-
-// nanoflann's searchLevel for k = 1 (one lane; explicit stack of {node, mindistsq, dists[3]} frames,
-// the other child pushed when descending and tested against the then-current worst distance when
-// popped, as the recursion tests it after the best child's subtree).  *d = the distance found.
-LG_DEVICE int kd_nn1(const KdView& K, const float* box, float4 q, float* stk, int cap, float& dout, bool& ovf) {
-  const float qv[3] = {q.x, q.y, q.z};
-  float worst = FLT_MAX;
-  int best = -1;
-  float dists[3] = {0.f, 0.f, 0.f};
-  float distsq = 0.f;  // computeInitialDistances (:1005-1022)
-  for (int d = 0; d < 3; ++d) {
-    if (qv[d] < box[d]) { dists[d] = (qv[d] - box[d]) * (qv[d] - box[d]); distsq += dists[d]; }
-    if (qv[d] > box[3 + d]) { dists[d] = (qv[d] - box[3 + d]) * (qv[d] - box[3 + d]); distsq += dists[d]; }
-  }
-  int sp = 0;
-  int nd = 0;
-  bool popped = false;
-  float mind = distsq;
-  while (true) {
-    if (popped) {
-      if (sp == 0) break;
-      --sp;
-      nd = __float_as_int(stk[5 * sp]);
-      mind = stk[5 * sp + 1];
-      dists[0] = stk[5 * sp + 2]; dists[1] = stk[5 * sp + 3]; dists[2] = stk[5 * sp + 4];
-      if (!(mind * 1.0f <= worst)) continue;  // epsError = 1 + eps, eps 0
-    }
-    popped = true;
-    KdNode n = K.node[nd];
-    while (n.c1 >= 0) {
-      const int idx = n.divfeat;
-      const float val = qv[idx];
-      const float diff1 = val - n.divlow, diff2 = val - n.divhigh;
-      int bestc, other;
-      float cut;
-      if ((diff1 + diff2) < 0) { bestc = n.c1; other = n.c2; cut = (val - n.divhigh) * (val - n.divhigh); }
-      else { bestc = n.c2; other = n.c1; cut = (val - n.divlow) * (val - n.divlow); }
-      if (sp < cap) {
-        stk[5 * sp] = __int_as_float(other);
-        stk[5 * sp + 1] = mind + cut - dists[idx];
-        for (int d = 0; d < 3; ++d) stk[5 * sp + 2 + d] = d == idx ? cut : dists[d];
-        ++sp;
-      } else {
-        ovf = true;
-      }
-      n = K.node[bestc];
-    }
-    const float worst_entry = worst;  // searchLevel's leaf: worstDist() once, then addPoint
-    for (int i = n.left; i < n.right; ++i) {
-      const int index = K.vind[i];
-      const float4 p = K.pts[index];
-      float dist = 0.f;  // L2_Simple_Adaptor::evalMetric (:432-440)
-      float df = qv[0] - p.x;
-      dist += df * df;
-      df = qv[1] - p.y;
-      dist += df * df;
-      df = qv[2] - p.z;
-      dist += df * df;
-      if (dist < worst_entry && dist < worst) {  // KNNResultSet(1)::addPoint: replace iff strictly closer
-        worst = dist;
-        best = index;
-      }
-    }
-  }
-  dout = worst;
-  return best;
-}
+// Scratch per stream: B.kd_* (built once per LM loop, on demand).
+using namespace lgkd;
 
 // Re-resolve the tied queries L.tieq[0, L.ntie) with nanoflann's tree (built on first use in this LM
 // loop).  Wave 0 only; the caller synchronises the workgroup around it.
 template <class Lds>
 LG_DEVICE void kd_resolve_ties(Lds& L, const KdView& K, int nl, int& st) {
   if (!L.kd_built) {
-    kd_build(K, nl, L.kd_box);
+    if (kd_build(K, nl, L.kd_box) < 0) return;  // (a build-stack overflow keeps the grid's lowest indices)
     if (lane_id() == 0) L.kd_built = 1;
   }
   const int cap = (10 * K.vh) / (5 * 64);  // search frames per lane
@@ -4170,8 +3984,9 @@ LG_DEVICE void kd_resolve_ties(Lds& L, const KdView& K, int nl, int& st) {
     if (k < L.ntie) {
       const int q = L.tieq[k];
       float d;
+      int c;
       bool ovf = false;
-      const int c = kd_nn1(K, L.kd_box, L.sel[q], K.frames + (size_t)lane_id() * cap * 5, cap, d, ovf);
+      kd_knn<1>(K, L.kd_box, L.sel[q], K.frames + (size_t)lane_id() * cap * 5, cap, &c, &d, ovf);
       if (!ovf) L.ind1[q] = c;  // (a stack overflow keeps the grid's lowest index)
     }
   }
@@ -4586,7 +4401,9 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
   } while (0)
 
 bool lg_lds_projection(const LgParams& P) { return (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4 <= 160 * 1024; }
-bool lg_lds_segment(const LgParams& P) { return P.V <= 16 && P.VH < 32768; }  // k_segment_lds packing
+bool lg_lds_segment(const LgParams& P) {  // k_segment_lds packing
+  return P.V <= 16 && P.VH <= SEG_VH_MAX && P.seg_valid_line <= SEG_DMAX;
+}
 
 int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
                       const int32_t* cnts, hipStream_t st) {
@@ -4625,7 +4442,7 @@ int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_sw_finish, dim3(S), dim3(1024), 0, st, P, B, (int)g.x);
   } else {
-    size_t sm = (size_t)(P.VH + 64) * 4;
+    size_t sm = (size_t)64 * 4 + (((size_t)P.VH * 2 + 3) & ~(size_t)3);
     hipLaunchKernelGGL(k_segment_lds, dim3(S), dim3(1024), sm, st, P, B);
   }
   LG_CHECK_LAUNCH();
@@ -4776,28 +4593,34 @@ extern "C" int lego_test_libm(const float* h_a, const float* h_b, float* h_out, 
   return rc;
 }
 
+template <int KN>
 __global__ __launch_bounds__(64) void k_kd_test(KdView K, int n, const float4* q, int m, int* idx, float* dist) {
   __shared__ float box[6];
-  kd_build(K, n, box);
+  const bool built = kd_build(K, n, box) >= 0;
   const int cap = (10 * K.vh) / (5 * 64);
   for (int k0 = 0; k0 < m; k0 += 64) {
     const int k = k0 + lane_id();
     if (k < m) {
-      float d = 0.f;
-      bool ovf = false;
-      const int c = n > 0 ? kd_nn1(K, box, q[k], K.frames + (size_t)lane_id() * cap * 5, cap, d, ovf) : -1;
-      idx[k] = ovf ? -2 : c;
-      dist[k] = n > 0 ? d : FLT_MAX;
+      int ix[KN];
+      float d[KN];
+      bool ovf = !built;
+      if (n > 0 && built) kd_knn<KN>(K, box, q[k], K.frames + (size_t)lane_id() * cap * 5, cap, ix, d, ovf);
+      for (int j = 0; j < KN; ++j) {
+        idx[(size_t)k * KN + j] = ovf ? -2 : (n > 0 ? ix[j] : -1);
+        dist[(size_t)k * KN + j] = n > 0 && !ovf ? d[j] : FLT_MAX;
+      }
     }
   }
 }
 
-// nanoflann's 1-NN on the device (the LM's exact-tie path: kd_build + kd_nn1) for m queries against a
-// cloud of n points (x, y, z, w float32 each); idx -2 = search stack overflow.
-extern "C" int lego_test_kd_knn1(const float* h_cloud, int32_t n, const float* h_q, int32_t m, int32_t* h_idx,
-                                 float* h_dist) {
-  if (n < 0 || m < 0 || (n && !h_cloud) || (m && (!h_q || !h_idx || !h_dist)) || n > (1 << 22)) return LEGO_EINVAL;
-  const int vh = std::max(n, 64);
+// nanoflann's kNN (k = 1: the LM's exact-tie path; k = 5: MapOptimization's) on the device (kd_build +
+// kd_knn) for m queries against a cloud of n points (x, y, z, w float32 each); idx[m][k] nearest first,
+// -1 past the count found, -2 = stack overflow.
+extern "C" int lego_test_kd_knn(const float* h_cloud, int32_t n, const float* h_q, int32_t m, int32_t k,
+                                int32_t* h_idx, float* h_dist) {
+  if (n < 0 || m < 0 || (k != 1 && k != 5) || (n && !h_cloud) || (m && (!h_q || !h_idx || !h_dist)) || n > (1 << 22))
+    return LEGO_EINVAL;
+  const int vh = std::max(n, 1024);
   float4 *c = nullptr, *q = nullptr;
   KdView K = {};
   int *idx = nullptr;
@@ -4807,7 +4630,8 @@ extern "C" int lego_test_kd_knn1(const float* h_cloud, int32_t n, const float* h
       hipMalloc((void**)&K.node, (size_t)2 * vh * sizeof(KdNode)) != hipSuccess ||
       hipMalloc((void**)&K.vind, (size_t)vh * 4) != hipSuccess || hipMalloc((void**)&K.tmp, (size_t)2 * vh * 4) != hipSuccess ||
       hipMalloc((void**)&K.frames, (size_t)10 * vh * 4) != hipSuccess ||
-      hipMalloc((void**)&idx, (size_t)std::max(m, 1) * 4) != hipSuccess || hipMalloc((void**)&dist, (size_t)std::max(m, 1) * 4) != hipSuccess)
+      hipMalloc((void**)&idx, (size_t)std::max(m, 1) * 4 * k) != hipSuccess ||
+      hipMalloc((void**)&dist, (size_t)std::max(m, 1) * 4 * k) != hipSuccess)
     rc = LEGO_ENOMEM;
   K.pts = c;
   K.vh = vh;
@@ -4815,9 +4639,10 @@ extern "C" int lego_test_kd_knn1(const float* h_cloud, int32_t n, const float* h
                         (m && hipMemcpy(q, h_q, (size_t)m * 16, hipMemcpyHostToDevice) != hipSuccess)))
     rc = LEGO_EDEVICE;
   if (rc == LEGO_OK) {
-    hipLaunchKernelGGL(k_kd_test, dim3(1), dim3(64), 0, 0, K, n, q, m, idx, dist);
-    if (hipGetLastError() != hipSuccess || (m && (hipMemcpy(h_idx, idx, (size_t)m * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-                                                  hipMemcpy(h_dist, dist, (size_t)m * 4, hipMemcpyDeviceToHost) != hipSuccess)))
+    if (k == 1) hipLaunchKernelGGL(k_kd_test<1>, dim3(1), dim3(64), 0, 0, K, n, q, m, idx, dist);
+    else hipLaunchKernelGGL(k_kd_test<5>, dim3(1), dim3(64), 0, 0, K, n, q, m, idx, dist);
+    if (hipGetLastError() != hipSuccess || (m && (hipMemcpy(h_idx, idx, (size_t)m * 4 * k, hipMemcpyDeviceToHost) != hipSuccess ||
+                                                  hipMemcpy(h_dist, dist, (size_t)m * 4 * k, hipMemcpyDeviceToHost) != hipSuccess)))
       rc = LEGO_EDEVICE;
   }
   for (void* p : {(void*)c, (void*)q, (void*)K.node, (void*)K.vind, (void*)K.tmp, (void*)K.frames, (void*)idx, (void*)dist})

@@ -30,6 +30,7 @@
 
 #include "../../include/lego_s2m.h"
 #include "lego_device.h"
+#include "lego_kdtree.h"
 
 using namespace lg;
 
@@ -39,6 +40,7 @@ constexpr int S2M_THREADS = 1024;
 constexpr int S2M_NB_MAX = 65536;  // hash buckets per map cloud (power of two)
 constexpr float S2M_CELL = 1.01f;  // cell edge: >= the 1 m kNN gate plus rounding
 constexpr int S2M_DIM = 1024;
+constexpr int S2M_KD_STACK = 64 * 5 * 48;  // floats: 48 search frames a lane beyond 10 per map point
 constexpr int S2M_LATENCY_MAX = 16;  // lego_s2m_run: up to this many problems take the latency layout
 constexpr size_t S2M_WIDE_MAX = (size_t)8 << 20;  // few-clouds VoxelGrid layout: n * max_map_points <= this      // cells per axis a packed cell can hold (10 bits)
 
@@ -50,6 +52,13 @@ struct S2mScratch {  // per problem, per map cloud
   float4* pts;       // [max_map_points] x, y, z, packed cell
   int* idx;          // [max_map_points] index in the caller's cloud
   float4* rows;      // [max_map_points][2] (corner scratch only) the queries' LM rows of an iteration
+  // nanoflann's tree of the map cloud, built only when a kNN-5 has an exact distance tie (lego_kdtree.h)
+  KdNode* kd_node;   // [2 * max_map_points]
+  int* kd_vind;      // [max_map_points]
+  // shared by the problem's two clouds (the same pointers in both entries)
+  int* kd_tmp;       // [2 * max_map_points] planeSplit's stop lists
+  float* kd_frames;  // [10 * max_map_points + S2M_KD_STACK] the builds' stack, then the searches' stacks
+  int* tieq;         // [max_map_points] an iteration's tied queries
 };
 
 // ---- restated Eigen pieces (oracle/s2m_oracle.cpp) ------------------------------------------------
@@ -593,8 +602,14 @@ struct QueryRow {
   float4 r0, r1;
   int st;
 };
+constexpr int S2M_ST_DEFER = 0x100;  // internal: a tied query whose row the tree search computes
+
+LG_DEVICE QueryRow row_from_nb(bool is_corner, float4 ori, float4 sel, Trig T, const float4* nb, QueryRow out);
+
+// defer: a query with tied distances returns S2M_ST_DEFER and no row (resolved by s2m_resolve_ties);
+// otherwise the grid's (distance, index) order decides the tie
 __device__ __attribute__((noinline)) QueryRow query_row(bool is_corner, float4 ori, Trig T, S2mScratch G,
-                                                        GridInfo gi) {
+                                                        GridInfo gi, bool defer = true) {
   QueryRow out;
   out.r0 = make_float4(0.f, 0.f, 0.f, 0.f);
   out.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -604,10 +619,21 @@ __device__ __attribute__((noinline)) QueryRow query_row(bool is_corner, float4 o
   bool tie = false;
   if (!knn5(G, gi, sel, sl, tie)) return out;
 
-  if (tie) out.st |= LEGO_S2M_ST_KNN_TIE;
+  if (tie) {
+    out.st |= LEGO_S2M_ST_KNN_TIE;
+    if (defer) {
+      out.st |= S2M_ST_DEFER;
+      return out;
+    }
+  }
   float4 nb[5];
 #pragma unroll
   for (int j = 0; j < 5; ++j) nb[j] = G.pts[sl[j]];
+  return row_from_nb(is_corner, ori, sel, T, nb, out);
+}
+
+// the query's fit and LM row from its 5 neighbours (x, y, z used)
+LG_DEVICE QueryRow row_from_nb(bool is_corner, float4 ori, float4 sel, Trig T, const float4* nb, QueryRow out) {
   float4 c;
   if (!(is_corner ? corner_coeff(nb, sel, c) : surf_coeff(nb, sel, c))) return out;
   const float srx = T.sRoll, crx = T.cRoll, sry = T.sPitch, cry = T.cPitch, srz = T.sYaw, crz = T.cYaw;
@@ -624,6 +650,72 @@ __device__ __attribute__((noinline)) QueryRow query_row(bool is_corner, float4 o
   return out;
 }
 
+
+// Re-resolve an iteration's tied queries Gc.tieq[0, ntie) (S2M_ST_DEFER) with nanoflann's tree of their map
+// cloud (kdtreeCornerFromMap / kdtreeSurfFromMap, :1317-1318; built on first use for the problem, built[c]
+// 1, or -1 after a build-stack overflow), its searchLevel with a KNNResultSet(5) and the reference's
+// pointSearchSqDis[4] < 1.0 gate (:1036, :1144).  A search-stack overflow keeps the grid's order.  Wave 0
+// only; box: [2][6].
+__device__ __attribute__((noinline)) void s2m_resolve_ties(const S2mScratch& Gc, const S2mScratch& Gs, GridInfo gc, GridInfo gs,
+                                const float4* cmap, int ncm, const float4* smap, int nsm, const float4* corner,
+                                const float4* surf, int nc, int ntie, const Trig& T, int* built, float* box,
+                                int max_map) {
+  const int lane = lane_id();
+  bool need0 = false, need1 = false;
+  for (int k = lane; k < ntie; k += 64) {
+    if (Gc.tieq[k] < nc) need0 = true;
+    else need1 = true;
+  }
+  const bool need[2] = {__ballot(need0) != 0ull, __ballot(need1) != 0ull};
+  int bs[2];
+  for (int c = 0; c < 2; ++c) {
+    bs[c] = built[c];
+    if (need[c] && bs[c] == 0) {
+      const S2mScratch& G = c == 0 ? Gc : Gs;
+      const lgkd::KdView K = {c == 0 ? cmap : smap, G.kd_node, G.kd_vind, Gc.kd_tmp, Gc.kd_frames, max_map};
+      bs[c] = lgkd::kd_build(K, c == 0 ? ncm : nsm, box + 6 * c) < 0 ? -1 : 1;
+      if (lane == 0) built[c] = bs[c];
+      lgkd::kd_sync();
+    }
+  }
+  const int cap = (10 * max_map + S2M_KD_STACK) / (5 * 64);  // search frames per lane (>= 48)
+  for (int k0 = 0; k0 < ntie; k0 += 64) {
+    const int k = k0 + lane;
+    if (k >= ntie) continue;
+    const int q = Gc.tieq[k];
+    const bool is_corner = q < nc;
+    const int c = is_corner ? 0 : 1;
+    const float4 ori = is_corner ? corner[q] : surf[q - nc];
+    QueryRow r;
+    bool done = false;
+    if (bs[c] == 1) {
+      const S2mScratch& G = is_corner ? Gc : Gs;
+      const float4* map = is_corner ? cmap : smap;
+      const lgkd::KdView K = {map, G.kd_node, G.kd_vind, Gc.kd_tmp, Gc.kd_frames, max_map};
+      const float4 sel = associate(T, ori);
+      int idx[5];
+      float dst[5];
+      bool ovf = false;
+      const int cnt = lgkd::kd_knn<5>(K, box + 6 * c, sel, Gc.kd_frames + (size_t)lane * cap * 5, cap, idx, dst, ovf);
+      if (!ovf) {
+        r.r0 = make_float4(0.f, 0.f, 0.f, 0.f);
+        r.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        r.st = 0;
+        if (cnt == 5 && dst[4] < 1.0f) {
+          float4 nb[5];
+#pragma unroll
+          for (int j = 0; j < 5; ++j) nb[j] = map[idx[j]];
+          r = row_from_nb(is_corner, ori, sel, T, nb, r);
+        }
+        done = true;
+      }
+    }
+    if (!done) r = query_row(is_corner, ori, T, is_corner ? Gc : Gs, is_corner ? gc : gs, false);
+    Gc.rows[2 * q] = r.r0;
+    Gc.rows[2 * q + 1] = r.r1;
+  }
+}
+
 constexpr int S2M_LG_SURF = 14, S2M_LG_CORNER = 13;  // bucket tables held in LDS: 64 KB + 32 KB
 
 struct S2mLds {
@@ -636,6 +728,8 @@ struct S2mLds {
   float t[6];
   Trig T;
   int flag, status, iters, nsel, degenerate;
+  int ntie, kd_built[2];
+  float kd_box[2][6];
 };
 
 // The normal equations (AtA upper triangle, AtB, count) over the rows of nq queries in two passes of 14
@@ -755,6 +849,7 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch*
     L.iters = 0;
     L.nsel = 0;
     L.flag = 0;
+    L.kd_built[0] = L.kd_built[1] = 0;
   }
   __syncthreads();
   if (!L.gc.ok || !L.gs.ok) {  // a map wider than 1024 cells (1 km) on an axis
@@ -766,6 +861,7 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch*
     if (tid == 0) {  // updatePointAssociateToMapSinCos (:397-410); LMOptimization's trig is the same
       const float* t = L.t;
       L.T = Trig{cosf_g(t[0]), sinf_g(t[0]), cosf_g(t[1]), sinf_g(t[1]), cosf_g(t[2]), sinf_g(t[2]), t[3], t[4], t[5]};
+      L.ntie = 0;
     }
     __syncthreads();
     const Trig T = L.T;
@@ -774,11 +870,18 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch*
       const bool is_corner = q < nc;
       const float4 ori = is_corner ? corner[q] : surf[q - nc];
       const QueryRow r = query_row(is_corner, ori, T, is_corner ? Gc : Gs, is_corner ? gc : gs);
+      if (r.st & S2M_ST_DEFER) Gc.tieq[atomicAdd(&L.ntie, 1)] = q;
       Gc.rows[2 * q] = r.r0;
       Gc.rows[2 * q + 1] = r.r1;
-      if (r.st) atomicOr(&L.status, r.st);
+      if (r.st) atomicOr(&L.status, r.st & ~S2M_ST_DEFER);
     }
     __syncthreads();
+    if (L.ntie > 0) {  // (uniform)
+      if (wave_id() == 0)
+        s2m_resolve_ties(Gc, Gs, gc, gs, cmap, ncm, smap, nsm, corner, surf, nc, L.ntie, T, L.kd_built, &L.kd_box[0][0],
+                         max_map);
+      __syncthreads();
+    }
     normal_equations(L, Gc.rows, nc + ns);
     __syncthreads();
     if (tid == 0) lm_solve(L, iterCount);
@@ -806,6 +909,8 @@ struct S2mState {
   float t[6];
   int degenerate, status, iters, nsel, done;
   GridInfo gc, gs;
+  int ntie, kd_built[2];  // tied queries of the iteration (k_s2m_rows -> k_s2m_solve); the trees' states
+  float kd_box[2][6];
 };
 
 LG_DEVICE bool s2m_gates(const lego_s2m_io& io, int p, int max_map, int* info) {  // k_s2m's entry checks
@@ -851,6 +956,8 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m_grid(lego_s2m_io io, S2mScr
       st[p].iters = 0;
       st[p].nsel = 0;
       st[p].done = 0;
+      st[p].ntie = 0;
+      st[p].kd_built[0] = st[p].kd_built[1] = 0;
     } else {
       st[p].gs = gi;
     }
@@ -883,9 +990,10 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m_rows(lego_s2m_io io, S2mScr
     const bool is_corner = q < nc;
     const float4 ori = is_corner ? corner[q] : surf[q - nc];
     const QueryRow r = query_row(is_corner, ori, T, is_corner ? Gc : Gs, is_corner ? gc : gs);
+    if (r.st & S2M_ST_DEFER) Gc.tieq[atomicAdd(&st[p].ntie, 1)] = q;
     Gc.rows[2 * q] = r.r0;
     Gc.rows[2 * q + 1] = r.r1;
-    if (r.st) atomicOr(&L.status, r.st);
+    if (r.st) atomicOr(&L.status, r.st & ~S2M_ST_DEFER);
   }
   __syncthreads();
   if (tid == 0 && L.status) atomicOr(&st[p].status, L.status);
@@ -893,7 +1001,7 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m_rows(lego_s2m_io io, S2mScr
 
 // grid (n): one iteration's normal equations and solve; the outputs are written after every iteration
 __global__ __launch_bounds__(S2M_THREADS) void k_s2m_solve(lego_s2m_io io, S2mScratch* scratch, S2mState* st,
-                                                           int iterCount, int max_iters) {
+                                                           int iterCount, int max_iters, int max_map) {
   __shared__ S2mLds L;
   const int p = blockIdx.x, tid = threadIdx.x;
   S2mState* S = st + p;
@@ -903,6 +1011,20 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m_solve(lego_s2m_io io, S2mSc
     __syncthreads();
     if (tid == 0) { info[0] = -1; info[1] = 0; info[2] = 0; info[3] = LEGO_S2M_ST_SKIPPED; S->done = 1; }
     return;
+  }
+  const int ntie = S->ntie;
+  if (ntie > 0) {  // the iteration's tied queries (k_s2m_rows deferred them)
+    if (wave_id() == 0) {
+      const float* t = S->t;
+      const Trig T = {cosf_g(t[0]), sinf_g(t[0]), cosf_g(t[1]), sinf_g(t[1]), cosf_g(t[2]), sinf_g(t[2]), t[3], t[4], t[5]};
+      S2mScratch Gc = scratch[2 * p], Gs = scratch[2 * p + 1];
+      s2m_resolve_ties(Gc, Gs, S->gc, S->gs, (const float4*)io.corner_map + io.corner_map_off[p], io.corner_map_n[p],
+                       (const float4*)io.surf_map + io.surf_map_off[p], io.surf_map_n[p],
+                       (const float4*)io.corner + io.corner_off[p], (const float4*)io.surf + io.surf_off[p],
+                       io.corner_n[p], ntie, T, S->kd_built, &S->kd_box[0][0], max_map);
+    }
+    __syncthreads();
+    if (tid == 0) S->ntie = 0;
   }
   normal_equations(L, scratch[2 * p].rows, io.corner_n[p] + io.surf_n[p]);
   __syncthreads();
@@ -1242,6 +1364,7 @@ struct lego_s2m {
   S2mState* d_state = nullptr;
   S2mScratch* d_scratch = nullptr;
   void* d_mem = nullptr;
+  void* d_kd = nullptr;  // the problems' nanoflann trees (S2mScratch.kd_*)
   // host-call staging
   lego_point* d_clouds = nullptr;
   size_t cloud_cap = 0;
@@ -1278,7 +1401,14 @@ extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max
   const size_t tab = (size_t)(S2M_NB_MAX + 1) * 4, pts = (size_t)max_map_points * 16, idx = (size_t)max_map_points * 4;
   const size_t rows = (size_t)max_map_points * 32;
   const size_t per = ((tab + 255) & ~(size_t)255) + pts + ((idx + 255) & ~(size_t)255) + rows;
+  // per problem: each cloud's tree nodes and index permutation, then the shared stop lists, stacks and
+  // tied-query list (every size a multiple of 256 bytes)
+  const size_t mp = ((size_t)max_map_points + 63) & ~(size_t)63;
+  const size_t kd_node = 2 * mp * sizeof(KdNode), kd_vind = mp * 4, kd_tmp = 2 * mp * 4, kd_frames = (10 * mp + S2M_KD_STACK) * 4,
+               tieq = mp * 4;
+  const size_t kd_per = 2 * (kd_node + kd_vind) + kd_tmp + kd_frames + tieq;
   if (hipMalloc(&m->d_mem, per * 2 * max_problems) != hipSuccess ||
+      hipMalloc(&m->d_kd, kd_per * max_problems) != hipSuccess ||
       hipMalloc((void**)&m->d_scratch, sizeof(S2mScratch) * 2 * max_problems) != hipSuccess ||
       hipMalloc((void**)&m->d_meta, 256) != hipSuccess ||
       hipMalloc((void**)&m->d_state, sizeof(S2mState) * max_problems) != hipSuccess) {
@@ -1294,6 +1424,12 @@ extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max
     h[k].pts = (float4*)(b + ((tab + 255) & ~(size_t)255));
     h[k].idx = (int*)(b + ((tab + 255) & ~(size_t)255) + pts);
     h[k].rows = (float4*)(b + ((tab + 255) & ~(size_t)255) + pts + ((idx + 255) & ~(size_t)255));
+    char* kb = (char*)m->d_kd + kd_per * (k / 2);
+    h[k].kd_node = (KdNode*)(kb + (k % 2) * (kd_node + kd_vind));
+    h[k].kd_vind = (int*)(kb + (k % 2) * (kd_node + kd_vind) + kd_node);
+    h[k].kd_tmp = (int*)(kb + 2 * (kd_node + kd_vind));
+    h[k].kd_frames = (float*)(kb + 2 * (kd_node + kd_vind) + kd_tmp);
+    h[k].tieq = (int*)(kb + 2 * (kd_node + kd_vind) + kd_tmp + kd_frames);
   }
   const bool ok = hipMemcpy(m->d_scratch, h, sizeof(S2mScratch) * 2 * max_problems, hipMemcpyHostToDevice) == hipSuccess;
   delete[] h;
@@ -1307,6 +1443,7 @@ extern "C" void lego_s2m_destroy(lego_s2m* m) {
   hipSetDevice(m->device);
   hipDeviceSynchronize();
   if (m->d_mem) hipFree(m->d_mem);
+  if (m->d_kd) hipFree(m->d_kd);
   if (m->d_scratch) hipFree(m->d_scratch);
   if (m->d_clouds) hipFree(m->d_clouds);
   if (m->d_meta) hipFree(m->d_meta);
@@ -1336,7 +1473,8 @@ extern "C" int lego_s2m_run(lego_s2m* m, int32_t n, const lego_s2m_io* io, void*
   hipLaunchKernelGGL(k_s2m_grid, dim3(2, n), dim3(S2M_THREADS), 0, st, *io, m->d_scratch, m->d_state, m->max_map);
   for (int it = 0; it < m->max_iters; ++it) {
     hipLaunchKernelGGL(k_s2m_rows, dim3(g, n), dim3(S2M_THREADS), 0, st, *io, m->d_scratch, m->d_state);
-    hipLaunchKernelGGL(k_s2m_solve, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_scratch, m->d_state, it, m->max_iters);
+    hipLaunchKernelGGL(k_s2m_solve, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_scratch, m->d_state, it, m->max_iters,
+                       m->max_map);
   }
   return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }

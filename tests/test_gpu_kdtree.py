@@ -18,13 +18,13 @@ from lego_amd import _abi as A
 pytestmark = pytest.mark.gpu
 
 
-def _dev_knn1(cloud4, q4):
+def _dev_knn(cloud4, q4, k):
     cloud4, q4 = np.ascontiguousarray(cloud4, np.float32), np.ascontiguousarray(q4, np.float32)
-    idx = np.zeros(len(q4), np.int32)
-    d = np.zeros(len(q4), np.float32)
+    idx = np.zeros((len(q4), k), np.int32)
+    d = np.zeros((len(q4), k), np.float32)
     fp, ip = C.POINTER(C.c_float), C.POINTER(C.c_int32)
-    rc = L.lib().lego_test_kd_knn1(cloud4.ctypes.data_as(fp), len(cloud4), q4.ctypes.data_as(fp), len(q4),
-                                   idx.ctypes.data_as(ip), d.ctypes.data_as(fp))
+    rc = L.lib().lego_test_kd_knn(cloud4.ctypes.data_as(fp), len(cloud4), q4.ctypes.data_as(fp), len(q4), k,
+                                  idx.ctypes.data_as(ip), d.ctypes.data_as(fp))
     assert rc == 0
     return idx, d
 
@@ -40,7 +40,8 @@ def _frames(params, seq, n):
     return out
 
 
-def test_device_tree_matches_nanoflann_restatement(gpu):
+@pytest.mark.parametrize("k", [1, 5])
+def test_device_tree_matches_nanoflann_restatement(gpu, k):
     import oracle as O
     import test_oracle_cpu as T
     fr = _frames(L.params_vlp16(), 0, 2)[1][1]
@@ -49,10 +50,10 @@ def test_device_tree_matches_nanoflann_restatement(gpu):
     ties = 0
     for name, xyz, q in T._tie_clouds(rng, fr):
         c4, q4 = pad(np.asarray(xyz, np.float32)), pad(np.asarray(q, np.float32))
-        gi, gd = _dev_knn1(c4, q4)
-        oi, od = O.knn_tree(c4, q4, 1)
-        np.testing.assert_array_equal(gi, oi[:, 0], err_msg=name)
-        assert Hs.bits_equal(gd, od[:, 0]), name
+        gi, gd = _dev_knn(c4, q4, k)
+        oi, od = O.knn_tree(c4, q4, k)
+        np.testing.assert_array_equal(gi, oi, err_msg=name)
+        assert Hs.bits_equal(gd, od), name
         d = ((q4[:, None, :3] - c4[None, :, :3]) ** 2).sum(-1)
         ties += int(((d == d.min(1, keepdims=True)).sum(1) > 1).sum())
     assert ties > 300
