@@ -57,16 +57,12 @@ LG_DEVICE void kd_sync() {  // this wave's global stores before its other lanes'
 
 // computeMinMax (:836-848) of all three dimensions over ind[0, count) (order-independent)
 LG_DEVICE void kd_minmax(const float4* pts, const int* ind, int count, float* mn, float* mx) {
+  // (one load in flight a lane: a rare path, kept lean in registers for the kernels that call it)
   float a0 = FLT_MAX, a1 = FLT_MAX, a2 = FLT_MAX, b0 = -FLT_MAX, b1 = -FLT_MAX, b2 = -FLT_MAX;
-  for (int t0 = kd_lane(); t0 < count; t0 += 64 * 4) {
-    float4 p4[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) p4[u] = pts[ind[min(t0 + 64 * u, count - 1)]];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a0 = fminf(a0, p4[u].x); a1 = fminf(a1, p4[u].y); a2 = fminf(a2, p4[u].z);
-      b0 = fmaxf(b0, p4[u].x); b1 = fmaxf(b1, p4[u].y); b2 = fmaxf(b2, p4[u].z);
-    }
+  for (int t = kd_lane(); t < count; t += 64) {
+    const float4 p = pts[ind[t]];
+    a0 = fminf(a0, p.x); a1 = fminf(a1, p.y); a2 = fminf(a2, p.z);
+    b0 = fmaxf(b0, p.x); b1 = fmaxf(b1, p.y); b2 = fmaxf(b2, p.z);
   }
   mn[0] = kd_wmin(a0); mn[1] = kd_wmin(a1); mn[2] = kd_wmin(a2);
   mx[0] = kd_wmax(b0); mx[1] = kd_wmax(b1); mx[2] = kd_wmax(b2);
@@ -78,34 +74,24 @@ LG_DEVICE void kd_minmax(const float4* pts, const int* ind, int count, float* mn
 LG_DEVICE int kd_pass(const float4* pts, int* ind, int b, int count, int d, float cv, int mode, int* tL, int* tR) {
   const int lane = kd_lane();
   int nL = 0, nR = 0;
-  // each position is a left stop (!front) or a right stop (front); four chunks' keys in flight at a time
-  for (int t0 = b; t0 < count; t0 += 256) {  // left stops ascending
-    float k4[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) k4[u] = kd_get(pts, ind[min(t0 + 64 * u + lane, count - 1)], d);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = t0 + 64 * u + lane;
-      const bool front = mode == 0 ? k4[u] < cv : k4[u] <= cv;
-      const bool ls = i < count && !front;
-      const unsigned long long m = __ballot(ls);
-      if (ls) tL[nL + kd_popc_below(m)] = i;
-      nL += __popcll(m);
-    }
+  // each position is a left stop (!front) or a right stop (front)
+  for (int t0 = b; t0 < count; t0 += 64) {  // left stops ascending
+    const int i = t0 + lane;
+    const float k = kd_get(pts, ind[min(i, count - 1)], d);
+    const bool front = mode == 0 ? k < cv : k <= cv;
+    const bool ls = i < count && !front;
+    const unsigned long long m = __ballot(ls);
+    if (ls) tL[nL + kd_popc_below(m)] = i;
+    nL += __popcll(m);
   }
-  for (int t0 = count - 1; t0 >= b; t0 -= 256) {  // right stops descending
-    float k4[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) k4[u] = kd_get(pts, ind[max(t0 - 64 * u - lane, b)], d);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = t0 - 64 * u - lane;
-      const bool front = mode == 0 ? k4[u] < cv : k4[u] <= cv;
-      const bool rs = i >= b && front;
-      const unsigned long long m = __ballot(rs);
-      if (rs) tR[nR + kd_popc_below(m)] = i;
-      nR += __popcll(m);
-    }
+  for (int t0 = count - 1; t0 >= b; t0 -= 64) {  // right stops descending
+    const int i = t0 - lane;
+    const float k = kd_get(pts, ind[max(i, b)], d);
+    const bool front = mode == 0 ? k < cv : k <= cv;
+    const bool rs = i >= b && front;
+    const unsigned long long m = __ballot(rs);
+    if (rs) tR[nR + kd_popc_below(m)] = i;
+    nR += __popcll(m);
   }
   kd_sync();
   const int K = min(nL, nR);

@@ -3344,7 +3344,9 @@ struct LmLdsT {  // kMaxQ: feature queries of one loop (V * max(cap_sharp, cap_f
   int ntie;                   // queries of this search with an exact 1-NN distance tie
   int tieq[kMaxQ];
   int kd_built;               // nanoflann's tree of this loop's Last cloud is in B.kd_*
+  int kd_n;                   // that cloud's size
   float kd_box[6];            // its root bbox
+  lgkd::KdView kdv;           // the tree's scratch (B.kd_* of this stream) and cloud
   float fred[6][16];
   int iscan[16];
   float cur[6];
@@ -3972,21 +3974,27 @@ using namespace lgkd;
 
 // Re-resolve the tied queries L.tieq[0, L.ntie) with nanoflann's tree (built on first use in this LM
 // loop).  Wave 0 only; the caller synchronises the workgroup around it.
+// (out of line, each piece on its own: k_lm's register budget sets its co-residence with the front end)
+__device__ __attribute__((noinline)) int kd_build_nl(const KdView* K, int n, float* box) { return kd_build(*K, n, box); }
+__device__ __attribute__((noinline)) int kd_nn1_nl(const KdView* K, const float* box, float4 q, bool* ovf) {
+  const int cap = (10 * K->vh) / (5 * 64);  // search frames per lane
+  float d;
+  int c;
+  kd_knn<1>(*K, box, q, K->frames + (size_t)lane_id() * cap * 5, cap, &c, &d, *ovf);
+  return c;
+}
 template <class Lds>
-LG_DEVICE void kd_resolve_ties(Lds& L, const KdView& K, int nl, int& st) {
+__device__ __attribute__((noinline)) void kd_resolve_ties(Lds& L) {
   if (!L.kd_built) {
-    if (kd_build(K, nl, L.kd_box) < 0) return;  // (a build-stack overflow keeps the grid's lowest indices)
+    if (kd_build_nl(&L.kdv, L.kd_n, L.kd_box) < 0) return;  // (a build-stack overflow keeps the grid's lowest indices)
     if (lane_id() == 0) L.kd_built = 1;
   }
-  const int cap = (10 * K.vh) / (5 * 64);  // search frames per lane
   for (int k0 = 0; k0 < L.ntie; k0 += 64) {
     const int k = k0 + lane_id();
     if (k < L.ntie) {
       const int q = L.tieq[k];
-      float d;
-      int c;
       bool ovf = false;
-      kd_knn<1>(K, L.kd_box, L.sel[q], K.frames + (size_t)lane_id() * cap * 5, cap, &c, &d, ovf);
+      const int c = kd_nn1_nl(&L.kdv, L.kd_box, L.sel[q], &ovf);
       if (!ovf) L.ind1[q] = c;  // (a stack overflow keeps the grid's lowest index)
     }
   }
@@ -3999,7 +4007,7 @@ LG_DEVICE void kd_resolve_ties(Lds& L, const KdView& K, int nl, int& st) {
 // in registers) and the workgroup meets once per block instead of three times per iteration.
 template <bool kF1, class Lds>
 LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __restrict__ feat, int nq,
-                       const float4* __restrict__ last_g, int nl, bool surf, float4* gp, int& iters, KdView Kv) {
+                       const float4* __restrict__ last_g, int nl, bool surf, float4* gp, int& iters) {
   const int tid = threadIdx.x;
   const int nw = (int)(blockDim.x >> 6);
   const bool small = nl <= LM_LAST_LDS;
@@ -4017,8 +4025,7 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
   const float4* last = small ? (const float4*)L.u.lastc : last_g;
   ring_index(L, last, nl);
   PROF_ADD(surf ? 16 : 48, t_bg0);
-  if (tid == 0) { L.iters = 0; L.kd_built = 0; }
-  Kv.pts = last;
+  if (tid == 0) { L.iters = 0; L.kd_built = 0; L.kdv.pts = last; L.kd_n = nl; }
   for (int iter = 0; iter < 25; iter += 5) {
     {  // search (all waves)
       float cur[6];
@@ -4051,7 +4058,7 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
       }
       __syncthreads();
       if (L.ntie > 0) {  // exact ties: nanoflann's choice (its first visited point), from its tree
-        if (wave_id() == 0) kd_resolve_ties(L, Kv, nl, st);
+        if (wave_id() == 0) kd_resolve_ties(L);
         __syncthreads();
       }
       PROF_ADD(surf ? 37 : 46, t_nn0);
@@ -4306,18 +4313,19 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
   } else {
     if (tid == 0 && S.tree_stale) L.status |= LEGO_ST_STALE_TREE;
     float4* gp = B.grid_pts + (size_t)s * VH;
-    KdView kv;
-    kv.pts = nullptr;
-    kv.node = B.kd_node + (size_t)s * 2 * VH;
-    kv.vind = B.kd_vind + (size_t)s * VH;
-    kv.tmp = B.kd_tmp + (size_t)s * 2 * VH;
-    kv.frames = B.kd_frames + (size_t)s * 10 * VH;
-    kv.vh = VH;
+    if (tid == 0) {  // the tie path's tree scratch (read after the loops' barriers)
+      L.kdv.pts = nullptr;
+      L.kdv.node = B.kd_node + (size_t)s * 2 * VH;
+      L.kdv.vind = B.kd_vind + (size_t)s * VH;
+      L.kdv.tmp = B.kd_tmp + (size_t)s * 2 * VH;
+      L.kdv.frames = B.kd_frames + (size_t)s * 10 * VH;
+      L.kdv.vh = VH;
+    }
     PROF_T(t_ls0);
-    lm_loop<kF1>(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, gp, it_s, kv);
+    lm_loop<kF1>(P, L, S, f_flat, n_flat, slast, S.n_surf_last, true, gp, it_s);
     PROF_ADD(17, t_ls0);
     PROF_T(t_lc0);
-    lm_loop<kF1>(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, gp, it_c, kv);
+    lm_loop<kF1>(P, L, S, f_sharp, n_sharp, clast, S.n_corner_last, false, gp, it_c);
     PROF_ADD(18, t_lc0);
   }
   __syncthreads();
@@ -4731,6 +4739,58 @@ __global__ __launch_bounds__(64) void k_sort_bench(const unsigned* keys, int n, 
   if (lane == 0) out[blockIdx.x] = L.vval[n / 2];
 }
 #endif
+
+// Counter calibration (MI355X_MICROARCH.md: FETCH_SIZE is calibrated only for 16-B-per-lane streaming
+// reads): k_project's input read patterns over S scans of points, one 1024-thread workgroup a scan,
+// nothing else read and one float a lane written.  mode 0: the scatter pass's 12-byte buffer loads;
+// 1: 16-byte loads of the same points; 2: mode 0, then every point again as a 16-byte load (the
+// column pass's re-gather, in point order).
+__global__ __launch_bounds__(1024) void k_fetch_probe(int mode, const float4* __restrict__ pts,
+                                                      const int64_t* __restrict__ offs,
+                                                      const int32_t* __restrict__ cnts, float* out) {
+  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const float4* in = pts + offs[s];
+  const int n = cnts[s];
+  float acc = 0.f;
+  constexpr int kU = 8;
+  if (mode == 1) {
+    for (int i0 = tid; i0 < n; i0 += nt * kU) {
+      float4 pk[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) pk[u] = in[min(i0 + u * nt, n - 1)];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) acc += pk[u].x + pk[u].y + pk[u].z;
+    }
+  } else {
+    const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
+    for (int i0 = tid; i0 < n; i0 += nt * kU) {
+      float3 pk[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) pk[u] = buffer_load_f3(rin, (uint32_t)(i0 + u * nt) * 16u);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) acc += pk[u].x + pk[u].y + pk[u].z;
+    }
+    if (mode == 2) {
+      __syncthreads();
+      for (int i0 = tid; i0 < n; i0 += nt * kU) {
+        float4 pk[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) pk[u] = in[min(i0 + u * nt, n - 1)];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) acc += pk[u].w;
+      }
+    }
+  }
+  out[(size_t)s * nt + tid] = acc;
+}
+
+extern "C" int lego_debug_fetch_probe(int32_t mode, int32_t S, const void* pts, const int64_t* offs,
+                                      const int32_t* cnts, float* out, void* stream) {
+  if (mode < 0 || mode > 2 || S < 1 || !pts || !offs || !cnts || !out) return LEGO_EINVAL;
+  hipLaunchKernelGGL(k_fetch_probe, dim3(S), dim3(1024), 0, (hipStream_t)stream, mode, (const float4*)pts, offs,
+                     cnts, out);
+  return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+}
 
 // Diagnostics (profile build only): time `blocks` concurrent copies of one device sort.
 extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, float* ms) {
