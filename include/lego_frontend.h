@@ -240,8 +240,7 @@ int  lego_test_libm(const float* a, const float* b, float* out, int32_t n, int32
 int  lego_test_libm_d(const double* a, const double* b, double* out, int32_t n, int32_t which);
 /* Sort (key, val) pairs by key with the device's wave-parallel std::sort emulation (n <= 2048);
  * keys are uint32 (is_float 0) or float bit patterns (1); is_float 2 runs k_extract's segment
- * sort (float keys, n <= 512: register sort when keys are distinct, else the emulation); is_float 3
- * the level-synchronous VoxelGrid sort (uint32 keys). */
+ * sort (float keys, n <= 512: register sort when keys are distinct, else the emulation). */
 int  lego_test_sort(uint32_t* keys, int32_t* vals, int32_t n, int32_t is_float);
 /* Projection cell (row * H + col, or -1 = rejected) of n points (x, y, z, w float32) by the fast path
  * of k_project (-2 = too close to a decision boundary, decided by the exact path) and by the exact

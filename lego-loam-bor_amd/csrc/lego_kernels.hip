@@ -298,58 +298,14 @@ __attribute__((noinline)) __device__ void proj_drain(float ang_bottom, float res
   const int c = proj_cell_exact(P, in[i]);
   if (c >= 0) atomicMax(&winner[c], i);
 }
-// The LDS winner image: int32 input indices (-1: empty), or with kW16 (n < 65535) 16-bit index + 1
-// (0: empty), whose atomicMax is a CAS on the containing word (the image then takes half the LDS).
-template <bool kW16>
-struct WinImg {
-  int* w;
-  LG_DEVICE void reset(int c) const { w[c] = -1; }
-  LG_DEVICE void put(int c, int i) const { atomicMax(&w[c], i); }
-  LG_DEVICE int get(int c) const { return w[c]; }
-};
-template <>
-struct WinImg<true> {
-  uint16_t* w;
-  LG_DEVICE void reset(int c) const { w[c] = 0; }
-  LG_DEVICE void put(int c, int i) const {
-    unsigned* wd = (unsigned*)w + (c >> 1);
-    const int sh = (c & 1) << 4;
-    const unsigned v = (unsigned)(i + 1);
-    unsigned old = *(volatile unsigned*)wd;
-    while (((old >> sh) & 0xffffu) < v) {
-      const unsigned got = atomicCAS(wd, old, (old & ~(0xffffu << sh)) | (v << sh));
-      if (got == old) break;
-      old = got;
-    }
-  }
-  LG_DEVICE int get(int c) const { return (int)w[c] - 1; }
-};
-template <bool kW16>
-__attribute__((noinline)) __device__ void proj_drain_img(float ang_bottom, float res_x, float res_y, int V, int H,
-                                                         const float4* in, const int* q, WinImg<kW16> img) {
-  LgParams P;
-  P.ang_bottom = ang_bottom;
-  P.ang_res_x = res_x;
-  P.ang_res_y = res_y;
-  P.V = V;
-  P.H = H;
-  const int i = q[lane_id()];
-  const int c = proj_cell_exact(P, in[i]);
-  if (c >= 0) img.put(c, i);
-}
-
-// kNT threads a scan; kW16: the 16-bit winner image.  (1024 / int32: the whole CU; 256 / 16-bit: 60 KB of
-// LDS and one wave a SIMD, so the projection can share a CU with k_lm.)
-template <int kNT, bool kW16>
-__global__ __launch_bounds__(kNT) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
-                                                 const int64_t* __restrict__ offs,
-                                                 const int32_t* __restrict__ cnts) {
+__global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
+                                                  const int64_t* __restrict__ offs,
+                                                  const int32_t* __restrict__ cnts) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, H = P.H, VH = P.VH;
   int* scratch = smem;                 // 64 ints
-  WinImg<kW16> winner;                 // LDS image: V*H cells, after the scratch and the wave queues
-  winner.w = (decltype(winner.w))(smem + 64 + (kNT / 64) * PQ_CAP);
+  int* winner = smem + 64;  // LDS image: V*H ints
   const float4* in = pts + offs[s];
   const int n = cnts[s];
   // the first batch's point loads go out before the LDS image reset (see below)
@@ -359,7 +315,7 @@ __global__ __launch_bounds__(kNT) void k_project(LgParams P, LgBufs B, const flo
 #pragma unroll
   for (int u = 0; u < kU; ++u) pk[u] = buffer_load_f3(rin, (uint32_t)(tid + u * nt) * 16u);
   PROF_T(t_p0);
-  for (int c = tid; c < VH; c += nt) winner.reset(c);
+  for (int c = tid; c < VH; c += nt) winner[c] = -1;
   __syncthreads();
   PROF_ADD(20, t_p0);
   PROF_T(t_p1);
@@ -368,7 +324,7 @@ __global__ __launch_bounds__(kNT) void k_project(LgParams P, LgBufs B, const flo
   // lane, the next batch's loads issued before the current batch is processed.  Lanes past n load
   // nothing (buffer range check).  Cells come from the fast path; the few points it cannot decide
   // queue per wave and take the exact path 64 at a time.
-  int* queue = smem + 64 + wave_id() * PQ_CAP;  // PQ_CAP ints per wave
+  int* queue = smem + 64 + VH + wave_id() * PQ_CAP;  // PQ_CAP ints per wave
   int qn = 0;
   for (int i0 = tid; i0 < n; i0 += nt * kU) {
     float3 nx[kU];
@@ -383,13 +339,13 @@ __global__ __launch_bounds__(kNT) void k_project(LgParams P, LgBufs B, const flo
         fmin = min(fmin, i);
         fmax = max(fmax, i);
         c = P.fast_proj ? proj_cell_fast(P, p) : proj_cell_exact_ni(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, p);
-        if (c >= 0) winner.put(c, i);
+        if (c >= 0) atomicMax(&winner[c], i);
       }
       const unsigned long long amb = __ballot(c == -2);
       if (c == -2) queue[qn + popc_below(amb)] = i;
       qn += __popcll(amb);
       if (qn >= 64) {  // wave-uniform, rare: the oldest 64 take the exact path
-        proj_drain_img<kW16>(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue + qn - 64, winner);
+        proj_drain(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue + qn - 64, winner);
         qn -= 64;
       }
     }
@@ -398,7 +354,7 @@ __global__ __launch_bounds__(kNT) void k_project(LgParams P, LgBufs B, const flo
   }
   if (qn > 0) {  // the rest (< 64): lanes past qn repeat entry 0 (the same max, harmless)
     if (lane_id() >= qn) queue[lane_id()] = queue[0];
-    proj_drain_img<kW16>(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue, winner);
+    proj_drain(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue, winner);
   }
   PROF_ADD(21, t_p1);
   PROF_T(t_p2);
@@ -442,7 +398,7 @@ __global__ __launch_bounds__(kNT) void k_project(LgParams P, LgBufs B, const flo
       int w[16];
       float4 pk[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) w[u] = (i0 + u < V) ? winner.get((i0 + u) * H + j) : -1;
+      for (int u = 0; u < 16; ++u) w[u] = (i0 + u < V) ? winner[(i0 + u) * H + j] : -1;
 #pragma unroll
       for (int u = 0; u < 16; ++u) pk[u] = src0[w[u] >= 0 ? w[u] : 0];
 #pragma unroll
@@ -903,7 +859,7 @@ LG_DEVICE void distort_segmented(const LgParams& P, const LgBufs& B, int s, int 
 #define SEG_DMAX 12       // row bits 0..12 of a pending root (below SEG_PEND)
 #define SEG_VH_MAX 32765  // cell indices stay below SEG_GND
 #define SEG_U 8
-#define SEG_CELLS 32768  // SEG_ROUNDS * threads * SEG_U >= V*H on this path
+#define SEG_ROUNDS 4  // 4 * 1024 * SEG_U = 32768 >= V*H on this path
 
 LG_DEVICE bool seg_eligible(int8_t g, float r) { return g != 1 && r != FLT_MAX; }  // _label_mat == 0
 
@@ -933,9 +889,7 @@ LG_DEVICE void uf_unite_rep16(uint16_t* parent, int a, int b) {  // uf_unite_rep
   }
 }
 
-template <int kNT>
-__global__ __launch_bounds__(kNT) void k_segment_lds(LgParams P, LgBufs B) {
-  constexpr int SEG_ROUNDS = SEG_CELLS / (kNT * SEG_U);
+__global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, H = P.H, VH = P.VH, G = P.G;
@@ -2281,206 +2235,6 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
   PROF_ADD(11, t_fin0);
 }
 
-// ---- level-synchronous introsort (VoxelGrid keys) ----------------------------------------------
-// __introsort_loop's ranges of one recursion depth are disjoint and each is partitioned by its own
-// pivot, so the order in which the reference's loop visits them does not matter: here every range of
-// a level is partitioned at once.  __unguarded_partition pairs the k-th left stop L_k (!(key < pivot),
-// scanning up from first + 1) with the k-th right stop R_k (!(pivot < key), scanning down from
-// last - 1), swaps while L_k < R_k and returns min(L_K, R_{K-1}) for the first crossing pair K
-// (R_{-1} = last); a swap by pair j lies outside the span (L_k, R_k) of every later valid pair k, so
-// both stop lists can be read off the array before any swap (wave_partition_stream's argument).  Per
-// level: one lane per range moves its median of three to first; one lane per 32-position block
-// classifies its positions (the stop bits) and a wave scan ranks them; the right stops are scattered by
-// rank; each left stop finds its partner R_k, swaps if L_k < R_k and counts itself valid, or offers its
-// position as L_K; one lane per range cuts and emits the children of more than 16 keys.  All ranges of
-// the level at depth 0 are heap-sorted (__partial_sort).  The final insertion sort is the register
-// sort by (key, position) (final_bitonic), so no final-block bits are kept.  n <= NMAX <= 2048.
-template <int NMAX>
-struct SortLv {
-  static constexpr int kR = NMAX / 17 + 1;  // ranges of > 16 keys at once
-  uint16_t pr[NMAX];                        // the k-th right stop (from last) of a range at [first + k]
-  int rng[2][kR];                           // this level's / the next level's ranges: first | last << 16
-  unsigned pv[kR];                          // pivots
-  int gl[kR], gr[kR], nr[kR];               // left stops before first, right stops before last, right count
-  int kv[kR], linv[kR];                     // valid pairs; the first invalid left stop (L_K)
-  unsigned ml[65], mr[65];                  // stop bits of the 32-position blocks
-  int pfl[65], pfr[65];                     // stops before each block
-};
-
-template <int NMAX>
-LG_DEVICE int lv_before(const unsigned* mk, const int* pf, int x) {  // stops at positions < x
-  return pf[x >> 5] + __popc(mk[x >> 5] & ((1u << (x & 31)) - 1u));
-}
-
-template <int NMAX>
-LG_DEVICE void voxel_std_sort(unsigned* key, uint16_t* val, int n, SortLv<NMAX>& W) {
-  const int lane = lane_id();
-  if (n <= 1) return;
-  SortView<unsigned, uint16_t> a{key, val};
-  PROF_T(t_part0);
-  int depth = 2 * floor_log2(n);
-  int cur = 0, m = 0;
-  if (n > 16) {
-    if (lane == 0) W.rng[0][0] = n << 16;
-    m = 1;
-  }
-  __syncthreads();
-  const int p0 = 32 * lane;
-  while (m > 0) {
-    const int* rng = W.rng[cur];
-    if (depth == 0) {  // __partial_sort of every remaining range
-      for (int r = 0; r < m; ++r) {
-        const int g = rng[r];
-        PROF_T(t_hs0);
-        heap_sort_wave(a, g & 0xffff, g >> 16);
-        PROF_ADD(7, t_hs0);
-#ifdef LG_PROFILE
-        if (lane == 0) atomicAdd(&PROF_SLOT(24), 1ull);
-#endif
-      }
-      break;
-    }
-    --depth;
-    for (int r = lane; r < m; r += 64) {  // __move_median_to_first(first, first + 1, mid, last - 1)
-      const int g = rng[r], f = g & 0xffff, e = g >> 16;
-      move_median_to_first(a, f, f + 1, f + (e - f) / 2, e - 1);
-      W.pv[r] = key[f];
-      W.kv[r] = 0;
-      W.linv[r] = e;
-    }
-    __syncthreads();
-    // this lane's block [p0, p0 + 32): the first range ending after p0 (ranges are sorted by position)
-    int s0 = 0;
-    {
-      int hi = m;
-      while (s0 < hi) {
-        const int mid = (s0 + hi) >> 1;
-        if ((rng[mid] >> 16) > p0) hi = mid;
-        else s0 = mid + 1;
-      }
-    }
-    unsigned mL = 0u, mR = 0u;
-    {
-      int r = s0, f = 0x10000, e = 0x10000;
-      unsigned pv = 0u;
-      if (r < m) { f = rng[r] & 0xffff; e = rng[r] >> 16; pv = W.pv[r]; }
-      const int pe = min(p0 + 32, n);
-      for (int p = p0; p < pe; ++p) {
-        while (p >= e) {
-          ++r;
-          if (r < m) { f = rng[r] & 0xffff; e = rng[r] >> 16; pv = W.pv[r]; }
-          else { f = e = 0x10000; }
-        }
-        if (p >= f) {
-          const unsigned k = key[p];
-          const unsigned bit = 1u << (p - p0);
-          if (p > f && !(k < pv)) mL |= bit;
-          if (!(pv < k)) mR |= bit;
-        }
-      }
-    }
-    const int cL = __popc(mL), cR = __popc(mR);
-    int iL = cL, iR = cR;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int uL = __shfl_up(iL, o), uR = __shfl_up(iR, o);
-      if (lane >= o) { iL += uL; iR += uR; }
-    }
-    const int xL = iL - cL, xR = iR - cR;  // stops before this block
-    W.ml[lane] = mL; W.mr[lane] = mR; W.pfl[lane] = xL; W.pfr[lane] = xR;
-    if (lane == 63) { W.ml[64] = 0u; W.mr[64] = 0u; W.pfl[64] = iL; W.pfr[64] = iR; }
-    __syncthreads();
-    for (int r = lane; r < m; r += 64) {
-      const int g = rng[r], f = g & 0xffff, e = g >> 16;
-      const int re = lv_before<NMAX>(W.mr, W.pfr, e);
-      W.gl[r] = lv_before<NMAX>(W.ml, W.pfl, f);
-      W.gr[r] = re;
-      W.nr[r] = re - lv_before<NMAX>(W.mr, W.pfr, f);
-    }
-    __syncthreads();
-    {  // right stops by rank from last
-      int r = s0, f = 0, e = 0, gr = 0;
-      unsigned bits = mR;
-      while (bits) {
-        const int i = __ffs(bits) - 1;
-        bits &= bits - 1u;
-        const int p = p0 + i;
-        while (p >= e) { f = rng[r] & 0xffff; e = rng[r] >> 16; gr = W.gr[r]; ++r; }
-        W.pr[f + gr - xR - __popc(mR & ((2u << i) - 1u))] = (uint16_t)p;
-      }
-    }
-    __syncthreads();
-    {  // left stops: partner, swap, validity (one atomic per lane and range: valid count, first invalid)
-      int r = s0, f = 0, e = 0, gl = 0, nr = 0, rr = -1, nv = 0, inv = 0x10000;
-      unsigned bits = mL;
-      while (bits) {
-        const int i = __ffs(bits) - 1;
-        bits &= bits - 1u;
-        const int p = p0 + i;
-        if (p >= e) {
-          if (rr >= 0) {
-            if (nv) atomicAdd(&W.kv[rr], nv);
-            if (inv < 0x10000) atomicMin(&W.linv[rr], inv);
-          }
-          nv = 0;
-          inv = 0x10000;
-          while (p >= e) { f = rng[r] & 0xffff; e = rng[r] >> 16; gl = W.gl[r]; nr = W.nr[r]; rr = r; ++r; }
-        }
-        const int k = xL + __popc(mL & ((1u << i) - 1u)) - gl;
-        const int q = k < nr ? (int)W.pr[f + k] : -1;
-        if (p < q) {
-          a.swap(p, q);
-          ++nv;
-        } else if (inv == 0x10000) {
-          inv = p;  // positions ascend: the lane's first invalid stop in this range
-        }
-      }
-      if (rr >= 0) {
-        if (nv) atomicAdd(&W.kv[rr], nv);
-        if (inv < 0x10000) atomicMin(&W.linv[rr], inv);
-      }
-    }
-    __syncthreads();
-    // cuts and the next level's ranges (> 16 keys), in position order
-    const int nxt = cur ^ 1;
-    int mnext = 0;
-    for (int r0 = 0; r0 < m; r0 += 64) {
-      const int r = r0 + lane;
-      int c1 = 0, c2 = 0, f = 0, e = 0, cut = 0;
-      if (r < m) {
-        f = rng[r] & 0xffff;
-        e = rng[r] >> 16;
-        const int K = W.kv[r];
-        cut = min(W.linv[r], K > 0 ? (int)W.pr[f + K - 1] : e);
-        c1 = cut - f > 16 ? 1 : 0;
-        c2 = e - cut > 16 ? 1 : 0;
-      }
-      int inc = c1 + c2;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(inc, o);
-        if (lane >= o) inc += u;
-      }
-      const int off = mnext + inc - c1 - c2;
-      if (c1) W.rng[nxt][off] = f | (cut << 16);
-      if (c2) W.rng[nxt][off + c1] = cut | (e << 16);
-      mnext += __shfl(inc, 63);
-    }
-    __syncthreads();
-    cur = nxt;
-    m = mnext;
-  }
-  PROF_ADD(6, t_part0);
-  PROF_T(t_fin0);
-  if (n <= 64) final_bitonic<1>(key, val, n);
-  else if (n <= 128) final_bitonic<2>(key, val, n);
-  else if (n <= 256) final_bitonic<4>(key, val, n);
-  else if (n <= 512) final_bitonic<8>(key, val, n);
-  else if (n <= 1024) final_bitonic<16>(key, val, n);
-  else final_bitonic<32>(key, val, n);
-  PROF_ADD(11, t_fin0);
-}
-
 struct ScanView {
   int M, VH;
   const float* curv;
@@ -2745,22 +2499,13 @@ LG_DEVICE void voxel_sort_stable(unsigned* key, uint16_t* val, int n) {
   }
 }
 
-struct VoxSortLds {  // k_voxel<0>: the level-synchronous sort's LDS (21 KB a wave)
-  union {
-    unsigned vkey[RING_MAX];
-  } u;
-  uint16_t vval[RING_MAX];
-  SortLv<RING_MAX> srt;
-};
-
-// kMode 0: voxel_tie_order 0 (libstdc++ introsort permutation, level-synchronous emulation, VoxSortLds);
-// 1 / 2: stable order, rings of at most / more than 1024 points; 3: either order, any ring (one kernel
-// for the whole step; the streaming emulation for order 0).
+// kMode 0: voxel_tie_order 0 (libstdc++ introsort permutation); 1 / 2: stable order, rings of at most /
+// more than 1024 points; 3: either order, any ring (one kernel for the whole step).
 // The ring's points are read in batches of VX_U a lane with every load of a batch issued before any is
 // used (a loop of single loads pays one memory latency per point); L.vval is the identity on entry.
 #define VX_U 8
-template <int kMode, class Lds>
-LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, Lds& L, int n, int base_pos, RingOut& o) {
+template <int kMode>
+LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, int n, int base_pos, RingOut& o) {
   const float4* fa = v.fa + base_pos;  // L.vval holds positions relative to the ring start
   const int lane = lane_id();
   o.nLF = 0;
@@ -2811,7 +2556,7 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, Lds& L, int n, i
   __syncthreads();
   PROF_T(t_vs0);
   if constexpr (kMode == 0) {
-    voxel_std_sort<RING_MAX>(L.u.vkey, L.vval, n, L.srt);
+    wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
   } else if constexpr (kMode == 3) {
     if (P.voxel_stable) voxel_sort_stable<3>(L.u.vkey, L.vval, n);
     else wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
@@ -3103,7 +2848,7 @@ LG_DEVICE int lessflat_list(const ScanView& v, int st, int en, uint16_t* list) {
 // kMode as voxel_ring: 0 for voxel_tie_order 0; 1 and 2 split the stable order's rings by size.
 template <int kMode>
 __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
-  __shared__ typename std::conditional<kMode == 0, VoxSortLds, ExtractLds>::type L;
+  __shared__ ExtractLds L;
   const int V = P.V;
   const int b = blockIdx.x, sl = b / V, s = P.s0 + sl;
   const int ring = (b % V + sl / max(P.ncu / V, 1)) % V;  // ring rotation as in k_extract
@@ -3120,7 +2865,7 @@ __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
   o.nLF = 0;
   o.status = 0;
   PROF_T(t_vox0);
-  voxel_ring<kMode>(P, v, L, n, 0, o);  // (Lds deduced)
+  voxel_ring<kMode>(P, v, L, n, 0, o);
   PROF_ADD(4, t_vox0);
   if (lane_id() == 0) {
     B.r_vcount[sb] = o.nLF;
@@ -4695,17 +4440,8 @@ int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* p
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_pw_columns, dim3((P.H + PC_NT - 1) / PC_NT, S), dim3(PC_NT), 0, st, P, B, pts, offs, cnts);
   } else {  // !wide implies the LDS images fit (lego_batch_set_wide)
-    static const int proj_nt = getenv("LEGO_PROJ_NT") ? atoi(getenv("LEGO_PROJ_NT")) : 1024;  // (experiment)
-    if (proj_nt == 256 && P.max_points < 65535) {
-      const size_t sm = (size_t)(64 + 4 * PQ_CAP) * 4 + (((size_t)P.VH * 2 + 15) & ~(size_t)15);
-      hipLaunchKernelGGL((k_project<256, true>), dim3(S), dim3(256), sm, st, P, B, pts, offs, cnts);
-    } else if (proj_nt == 512 && P.max_points < 65535) {
-      const size_t sm = (size_t)(64 + 8 * PQ_CAP) * 4 + (((size_t)P.VH * 2 + 15) & ~(size_t)15);
-      hipLaunchKernelGGL((k_project<512, true>), dim3(S), dim3(512), sm, st, P, B, pts, offs, cnts);
-    } else {
-      const size_t sm = (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4;
-      hipLaunchKernelGGL((k_project<1024, false>), dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
-    }
+    size_t sm = (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4;
+    hipLaunchKernelGGL(k_project, dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
   }
   LG_CHECK_LAUNCH();
   return LEGO_OK;
@@ -4730,10 +4466,7 @@ int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
     hipLaunchKernelGGL(k_sw_finish, dim3(S), dim3(1024), 0, st, P, B, (int)g.x);
   } else {
     size_t sm = (size_t)64 * 4 + (((size_t)P.VH * 2 + 3) & ~(size_t)3);
-    static const int seg_nt = getenv("LEGO_SEG_NT") ? atoi(getenv("LEGO_SEG_NT")) : 1024;  // (experiment)
-    if (seg_nt == 256) hipLaunchKernelGGL(k_segment_lds<256>, dim3(S), dim3(256), sm, st, P, B);
-    else if (seg_nt == 512) hipLaunchKernelGGL(k_segment_lds<512>, dim3(S), dim3(512), sm, st, P, B);
-    else hipLaunchKernelGGL(k_segment_lds<1024>, dim3(S), dim3(1024), sm, st, P, B);
+    hipLaunchKernelGGL(k_segment_lds, dim3(S), dim3(1024), sm, st, P, B);
   }
   LG_CHECK_LAUNCH();
   return LEGO_OK;
@@ -4763,10 +4496,7 @@ int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   // off the SIMDs k_lm holds, which measured faster there.  With more scans than CUs the split
   // kernels (the common one at 83 VGPRs shares SIMDs with k_lm) measured faster: 245k vs 226k
   // scans/s at S = 512.
-  static const int vox_lv = getenv("LEGO_VOX_LV") ? atoi(getenv("LEGO_VOX_LV")) : 1;  // (experiment)
-  if (!P.voxel_stable && vox_lv) {  // the level-synchronous introsort emulation
-    hipLaunchKernelGGL(k_voxel<0>, dim3(S * P.V), dim3(64), 0, st, P, B);
-  } else if (S <= P.ncu) {
+  if (S <= P.ncu) {
     hipLaunchKernelGGL(k_voxel<3>, dim3(S * P.V), dim3(64), 0, st, P, B);
   } else if (P.voxel_stable) {
     hipLaunchKernelGGL(k_voxel<1>, dim3(S * P.V), dim3(64), 0, st, P, B);
@@ -4975,15 +4705,6 @@ extern "C" int lego_test_libm_d(const double* h_a, const double* h_b, double* h_
   return rc;
 }
 
-__global__ __launch_bounds__(64) void k_sort_test_lv(unsigned* keys, int* vals, int n) {
-  __shared__ VoxSortLds L;
-  const int lane = lane_id();
-  for (int i = lane; i < n; i += 64) { L.u.vkey[i] = keys[i]; L.vval[i] = (uint16_t)vals[i]; }
-  __syncthreads();
-  voxel_std_sort<RING_MAX>(L.u.vkey, L.vval, n, L.srt);
-  for (int i = lane; i < n; i += 64) { keys[i] = L.u.vkey[i]; vals[i] = L.vval[i]; }
-}
-
 __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int n, int is_float) {
   __shared__ ExtractLds L;
   const int lane = lane_id();
@@ -5004,7 +4725,7 @@ __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int
 }
 
 extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int32_t is_float) {
-  if (n < 0 || n > RING_MAX || !h_keys || !h_vals || is_float < 0 || is_float > 3) return LEGO_EINVAL;
+  if (n < 0 || n > RING_MAX || !h_keys || !h_vals || is_float < 0 || is_float > 2) return LEGO_EINVAL;
   if (is_float == 2 && n > SEG_MAX) return LEGO_EINVAL;
   if (n == 0) return LEGO_OK;
   unsigned* k = nullptr;
@@ -5015,8 +4736,7 @@ extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int3
   if (hipMemcpy(k, h_keys, n * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(v, h_vals, n * 4, hipMemcpyHostToDevice) != hipSuccess) rc = LEGO_EDEVICE;
   if (rc == LEGO_OK) {
-    if (is_float == 3) hipLaunchKernelGGL(k_sort_test_lv, dim3(1), dim3(64), 0, 0, k, v, n);
-    else hipLaunchKernelGGL(k_sort_test, dim3(1), dim3(64), 0, 0, k, v, n, is_float);
+    hipLaunchKernelGGL(k_sort_test, dim3(1), dim3(64), 0, 0, k, v, n, is_float);
     if (hipGetLastError() != hipSuccess || hipMemcpy(h_keys, k, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(h_vals, v, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = LEGO_EDEVICE;
   }
@@ -5030,15 +4750,7 @@ __global__ __launch_bounds__(64) void k_sort_bench(const unsigned* keys, int n, 
   const int lane = lane_id();
   for (int i = lane; i < n; i += 64) { L.u.vkey[i] = keys[i]; L.vval[i] = (uint16_t)i; }
   __syncthreads();
-  wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);  // as k_voxel
-  if (lane == 0) out[blockIdx.x] = L.vval[n / 2];
-}
-__global__ __launch_bounds__(64) void k_sort_bench_lv(const unsigned* keys, int n, unsigned* out) {
-  __shared__ VoxSortLds L;
-  const int lane = lane_id();
-  for (int i = lane; i < n; i += 64) { L.u.vkey[i] = keys[i]; L.vval[i] = (uint16_t)i; }
-  __syncthreads();
-  voxel_std_sort<RING_MAX>(L.u.vkey, L.vval, n, L.srt);
+  wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
   if (lane == 0) out[blockIdx.x] = L.vval[n / 2];
 }
 #endif
@@ -5099,8 +4811,6 @@ extern "C" int lego_debug_fetch_probe(int32_t mode, int32_t S, const void* pts, 
 extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, float* ms) {
 #ifdef LG_PROFILE
   unsigned *k = nullptr, *o = nullptr;
-  const bool lv = blocks < 0;  // negative: the level-synchronous VoxelGrid sort
-  if (lv) blocks = -blocks;
   if (n < 1 || n > RING_MAX || blocks < 1) return LEGO_EINVAL;
   hipMalloc((void**)&k, n * 4);
   hipMalloc((void**)&o, blocks * 4);
@@ -5108,11 +4818,9 @@ extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t 
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  if (lv) hipLaunchKernelGGL(k_sort_bench_lv, dim3(blocks), dim3(64), 0, 0, k, n, o);
-  else hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
+  hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
   hipEventRecord(a, 0);
-  if (lv) hipLaunchKernelGGL(k_sort_bench_lv, dim3(blocks), dim3(64), 0, 0, k, n, o);
-  else hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
+  hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
   hipEventRecord(b, 0);
   hipEventSynchronize(b);
   hipEventElapsedTime(ms, a, b);

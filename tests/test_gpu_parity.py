@@ -208,8 +208,7 @@ def test_fast_projection_decides_like_the_exact_path(gpu, kind):
 
 
 def test_device_sort_matches_libstdcxx(gpu):
-    """The wave-parallel introsort (segment + voxel sorts) gives libstdc++ std::sort's permutation; every
-    unsigned case also runs the level-synchronous VoxelGrid sort (lego_test_sort mode 3)."""
+    """The wave-parallel introsort (segment + voxel sorts) gives libstdc++ std::sort's permutation."""
     import oracle as O
     rng = np.random.default_rng(7)
     fp = C.POINTER
@@ -222,12 +221,11 @@ def test_device_sort_matches_libstdcxx(gpu):
                     keys = rng.integers(0, distinct, n).astype(np.uint32)
                 vals = np.arange(n, dtype=np.int32)
                 ek, ev = O.std_sort(keys, vals, is_float)
-                for mode in ((1,) if is_float else (0, 3)):
-                    gk, gv = keys.copy(), vals.copy()
-                    rc = L.lib().lego_test_sort(gk.ctypes.data_as(fp(C.c_uint32)), gv.ctypes.data_as(fp(C.c_int32)), n,
-                                                mode)
-                    assert rc == 0
-                    assert np.array_equal(gv, ev) and np.array_equal(gk, ek), (n, distinct, mode)
+                gk, gv = keys.copy(), vals.copy()
+                rc = L.lib().lego_test_sort(gk.ctypes.data_as(fp(C.c_uint32)), gv.ctypes.data_as(fp(C.c_int32)), n,
+                                            is_float)
+                assert rc == 0
+                assert np.array_equal(gv, ev) and np.array_equal(gk, ek), (n, distinct, is_float)
     # k_extract's segment sort (is_float 2, n <= 512): distinct keys, ties, and keys whose sign bit
     # keeps it on the emulation's insertion phase.  (NaN keys are left out: they break std::sort's
     # strict-weak-ordering precondition, so the reference's own result is undefined.)
@@ -255,11 +253,10 @@ def test_device_sort_matches_libstdcxx(gpu):
             keys = keys.astype(np.uint32)
             vals = np.arange(n, dtype=np.int32)
             ek, ev = O.std_sort(keys, vals, 0)
-            for mode in (0, 3):
-                gk, gv = keys.copy(), vals.copy()
-                assert L.lib().lego_test_sort(gk.ctypes.data_as(fp(C.c_uint32)), gv.ctypes.data_as(fp(C.c_int32)), n,
-                                              mode) == 0
-                assert np.array_equal(gv, ev) and np.array_equal(gk, ek), (n, name, mode)
+            gk, gv = keys.copy(), vals.copy()
+            assert L.lib().lego_test_sort(gk.ctypes.data_as(fp(C.c_uint32)), gv.ctypes.data_as(fp(C.c_int32)), n,
+                                          0) == 0
+            assert np.array_equal(gv, ev) and np.array_equal(gk, ek), (n, name)
     # inputs that hit the introsort depth limit (heap-sort fallback), with ties
     import subprocess
     import tempfile
@@ -272,7 +269,7 @@ def test_device_sort_matches_libstdcxx(gpu):
                 out = subprocess.run([exe, str(n), str(c)], stdout=subprocess.PIPE, universal_newlines=True, check=True)
                 keys = np.array(out.stdout.split(), dtype=np.uint32)
                 vals = np.arange(n, dtype=np.int32)
-                modes = [(0, keys), (3, keys)] + ([(2, keys.astype(np.float32).view(np.uint32))] if n <= 512 else [])
+                modes = [(0, keys)] + ([(2, keys.astype(np.float32).view(np.uint32))] if n <= 512 else [])
                 for mode, kk in modes:
                     ek, ev = O.std_sort(kk, vals, min(mode, 1))
                     gk, gv = kk.copy(), vals.copy()
