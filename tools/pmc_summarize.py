@@ -38,10 +38,11 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--workload", required=True)
     ap.add_argument("--streams", type=int, default=256)
+    ap.add_argument("--note", default="", help="what was run (free text)")
     a = ap.parse_args()
     fe = per_kernel(a.fetch_dir, "FETCH_SIZE")
     wr = per_kernel(a.write_dir, "WRITE_SIZE")
-    out = {"workload": a.workload, "streams": a.streams, "unit": "bytes per dispatch",
+    out = {"workload": a.workload, "streams": a.streams, "note": a.note, "unit": "bytes per dispatch",
            "formula": "2*FETCH_SIZE + WRITE_SIZE (KiB counters x 1024); gfx950 FETCH_SIZE halves 16-B reads",
            "kernels": {}}
     for k in sorted(set(fe) | set(wr)):

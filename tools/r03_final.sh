@@ -1,0 +1,23 @@
+# Round-3 measurement set (through gpurun from the repo root):
+#  1. the whole -m gpu suite; 2. the default bench line; 3. kernel trace + stats of it; 4. C3 PMC passes
+#  (FETCH_SIZE / WRITE_SIZE separately); 5. the S = 2048 roofline pair's PMC passes; 6. C4 (HDL-64E) bench.
+set -e
+TAG=${1:-r03f}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export LEGO_REPORT_DIR=$OUT
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+if [ -z "$NO_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
+  tail -2 "$OUT/gpu_tests.log"
+fi
+timeout -k 10 300 python3 bench.py > "$OUT/bench.log" 2>&1
+tail -c 300 "$OUT/bench.log"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 bench.py --no-cpu-baseline > "$OUT/bench_traced.log" 2>&1
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-alt-order --roofline-streams 0 > "$OUT/fetch.log" 2>&1
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-alt-order --roofline-streams 0 > "$OUT/write.log" 2>&1
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch2048" -o run -- python3 tools/roofline_pmc.py 2048 > "$OUT/fetch2048.log" 2>&1
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write2048" -o run -- python3 tools/roofline_pmc.py 2048 > "$OUT/write2048.log" 2>&1
+timeout -k 10 300 python3 bench.py --kind hdl64 --no-cpu-baseline > "$OUT/bench_hdl64.log" 2>&1
+tail -c 300 "$OUT/bench_hdl64.log"
+echo done
