@@ -160,12 +160,20 @@ def pmc_traffic(args, S, kernels):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        by_base = {k.split("<")[0]: v for k, v in d.get("kernels", {}).items()}  # k_project<true, 16> -> k_project
-        if d.get("streams") == S and d.get("workload") == args.kind and all(k in by_base for k in kernels):
-            best = (f, by_base)
+        by_base = {k.split("<")[0]: v for k, v in d.get("kernels", {}).items()}  # k_pw_scatter<4> -> k_pw_scatter
+        # each entry of `kernels` names one kernel slot as "a|b": the first of its alternatives present
+        pick = [next((a for a in k.split("|") if a in by_base), None) for k in kernels]
+        if d.get("streams") == S and d.get("workload") == args.kind and all(pick):
+            best = (f, [by_base[k] for k in pick])
     if best is None:
         return None, None
-    return int(sum(best[1][k]["hbm_bytes"] for k in kernels)), os.path.relpath(best[0], REPO)
+    return int(sum(v["hbm_bytes"] for v in best[1])), os.path.relpath(best[0], REPO)
+
+
+def roofline_kernels(wide):
+    """The projection + smoothness kernels the roofline pair times: k_project (or its windowed form)
+    + k_fa_prep4 in the LDS layout, k_pw_scatter + k_pw_columns + k_fa_prep4 in the wide layout."""
+    return ("k_pw_scatter", "k_pw_columns", "k_fa_prep4") if wide else ("k_project_win|k_project", "k_fa_prep4")
 
 
 def roofline_at(args, L, A, mk_params, cfg, dev_index, stream):
@@ -202,7 +210,7 @@ def roofline_at(args, L, A, mk_params, cfg, dev_index, stream):
     del d_pts
     torch.cuda.empty_cache()
     achieved = b_tot / (ms * 1e-3) / 1e9
-    traffic, src = pmc_traffic(args, Sb, ("k_project", "k_fa_prep4"))
+    traffic, src = pmc_traffic(args, Sb, roofline_kernels(args.wide == 1 or args.kind == "hdl64"))
     return {"streams": Sb, "bytes_per_launch": int(b_tot), "launch_ms": round(ms, 4), "achieved": round(achieved, 1),
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
             "note": "%d scans per launch: working set %.2f GB, above the 256 MiB Infinity Cache" % (Sb, b_tot / 1e9)}
@@ -333,7 +341,7 @@ def main():
     b_smooth = 22.0 * float(m_last.sum())
     t_ms = pair_ms  # k_project + k_fa_prep4
     achieved = (b_proj + b_smooth) / (t_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args, S, ("k_project", "k_fa_prep4"))
+    traffic, traffic_src = pmc_traffic(args, S, roofline_kernels(args.wide == 1 or args.kind == "hdl64"))
     big = roofline_at(args, L, A, mk_params, cfg, local_dev, stream) if world == 1 and args.roofline_streams > 0 else None
     roofline = {"kernel": "k_project+k_fa_prep4 (projection+smoothness)", "bound": "hbm",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

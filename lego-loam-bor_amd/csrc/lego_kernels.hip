@@ -298,6 +298,85 @@ __attribute__((noinline)) __device__ void proj_drain(float ang_bottom, float res
   const int c = proj_cell_exact(P, in[i]);
   if (c >= 0) atomicMax(&winner[c], i);
 }
+// Column pass of column j: the lane walks the rows bottom-up.  Each chunk of CR rows first reads its
+// CR winners and gathers their points (unconditional loads, all in flight together), then writes
+// range / cloud cells, the ground pairs (i-1, i) of groundRemoval (:271-285), and row i-1's ground
+// flag and 2-D scan candidate (:312-330) as soon as pair (i-1, i) has settled it.
+template <int CR>
+LG_DEVICE void proj_column(const LgParams& P, const LgBufs& B, int s, int j, const int* winner, const float4* src0,
+                           float* range, float4* cloud, int8_t* ground) {
+  const int V = P.V, H = P.H;
+  const float qnan = __int_as_float(0x7fc00000);
+  unsigned long long gmask = 0ull;
+  float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
+  float prev_r = 0.f;
+  float min_range = 1000.f;
+  int id_min = -1;
+  const double jfrac = (double)(float)j / 10000.0;
+  auto scan = [&](int i, float r, float Z) {  // 2-D scan (:312-330), row i final
+    const int c = i * H + j;
+    const int g = (int)((gmask >> i) & 1ull);
+    ground[c] = (int8_t)g;
+    if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f && r < min_range) {
+      min_range = r;
+      id_min = c;
+    }
+  };
+  for (int i0 = 0; i0 < V; i0 += CR) {
+    int w[CR];
+    float4 pk[CR];
+#pragma unroll
+    for (int u = 0; u < CR; ++u) w[u] = (i0 + u < V) ? winner[(i0 + u) * H + j] : -1;
+#pragma unroll
+    for (int u = 0; u < CR; ++u) pk[u] = src0[w[u] >= 0 ? w[u] : 0];
+#pragma unroll
+    for (int u = 0; u < CR; ++u) {
+      const int i = i0 + u;
+      if (i >= V) continue;  // (not `break`: the loop must stay unrollable, pk[] in registers)
+      const int c = i * H + j;
+      float4 q;
+      float r;
+      if (w[u] >= 0) {
+        const float4 p = pk[u];
+        r = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+        q = make_float4(p.x, p.y, p.z, (float)((double)(float)i + jfrac));
+      } else {
+        r = FLT_MAX;
+        q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
+      }
+      st_nt(&range[c], r);  // streaming stores: the input lines stay in L2 for the gathers
+      st_nt(&cloud[c], q);
+      if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
+        const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
+        if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) gmask |= (3ull << (i - 1));
+      }
+      if (i >= 1) scan(i - 1, prev_r, prev.z);
+      prev = q;
+      prev_r = r;
+    }
+  }
+  scan(V - 1, prev_r, prev.z);
+  B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
+}
+
+// findStartEndAngle (:234-249) from the first / last finite point (thread 0)
+LG_DEVICE void proj_orient(const LgParams& P, const LgBufs& B, int s, const float4* in, int fmin, int fmax) {
+  float so = 0.f, eo = 0.f, od = 0.f;
+  if (fmax >= 0) {
+    float4 a = in[fmin], b = in[fmax];
+    so = -atan2f_g(a.y, a.x);
+    eo = (float)(-(double)atan2f_g(b.y, b.x) + 2 * M_PI);
+    if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
+    else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
+    od = eo - so;
+  }
+  B.orient[s * 4 + 0] = so;
+  B.orient[s * 4 + 1] = eo;
+  B.orient[s * 4 + 2] = od;
+  B.orient[s * 4 + 3] = (float)(fmax >= 0);
+  B.fe_state[2 * s] = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
+}
+
 __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                   const int64_t* __restrict__ offs,
                                                   const int32_t* __restrict__ cnts) {
@@ -369,87 +448,19 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
   __syncthreads();
   PROF_ADD(22, t_p2);
   PROF_T(t_p3);
-  // Column pass: one lane per column walks the rows bottom-up.  Each chunk of 16 rows first reads
-  // its 16 winners and gathers their 16 points (unconditional loads, all in flight together), then
-  // writes range / cloud cells, the ground pairs (i-1, i) of groundRemoval (:271-285), and row i-1's
-  // ground flag and 2-D scan candidate (:312-330) as soon as pair (i-1, i) has settled it.
+  // Column pass: one lane per column (proj_column)
   float* range = B.range + (size_t)s * VH;
   float4* cloud = B.cloud + (size_t)s * VH;
   int8_t* ground = B.ground + (size_t)s * VH;
-  const float qnan = __int_as_float(0x7fc00000);
   const float4* src0 = n > 0 ? in : cloud;  // any readable address for empty cells (value unused)
-  for (int j = tid; j < H; j += nt) {
-    unsigned long long gmask = 0ull;
-    float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
-    float prev_r = 0.f;
-    float min_range = 1000.f;
-    int id_min = -1;
-    const double jfrac = (double)(float)j / 10000.0;
-    auto scan = [&](int i, float r, float Z) {  // 2-D scan (:312-330), row i final
-      const int c = i * H + j;
-      const int g = (int)((gmask >> i) & 1ull);
-      ground[c] = (int8_t)g;
-      if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f && r < min_range) {
-        min_range = r;
-        id_min = c;
-      }
-    };
-    for (int i0 = 0; i0 < V; i0 += 16) {
-      int w[16];
-      float4 pk[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) w[u] = (i0 + u < V) ? winner[(i0 + u) * H + j] : -1;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) pk[u] = src0[w[u] >= 0 ? w[u] : 0];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = i0 + u;
-        if (i >= V) continue;  // (not `break`: the loop must stay unrollable, pk[] in registers)
-        const int c = i * H + j;
-        float4 q;
-        float r;
-        if (w[u] >= 0) {
-          const float4 p = pk[u];
-          r = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-          q = make_float4(p.x, p.y, p.z, (float)((double)(float)i + jfrac));
-        } else {
-          r = FLT_MAX;
-          q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
-        }
-        st_nt(&range[c], r);  // streaming stores: the input lines stay in L2 for the gathers
-        st_nt(&cloud[c], q);
-        if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
-          const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
-          if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) gmask |= (3ull << (i - 1));
-        }
-        if (i >= 1) scan(i - 1, prev_r, prev.z);
-        prev = q;
-        prev_r = r;
-      }
-    }
-    scan(V - 1, prev_r, prev.z);
-    B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
-  }
+  for (int j = tid; j < H; j += nt) proj_column<16>(P, B, s, j, winner, src0, range, cloud, ground);
   PROF_ADD(23, t_p3);
-  if (tid == 0) {  // findStartEndAngle (:234-249)
+  if (tid == 0) {
     for (int w = 1; w < (nt >> 6); ++w) {
       fmin = min(fmin, scratch[w]);
       fmax = max(fmax, scratch[32 + w]);
     }
-    float so = 0.f, eo = 0.f, od = 0.f;
-    if (fmax >= 0) {
-      float4 a = in[fmin], b = in[fmax];
-      so = -atan2f_g(a.y, a.x);
-      eo = (float)(-(double)atan2f_g(b.y, b.x) + 2 * M_PI);
-      if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
-      else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
-      od = eo - so;
-    }
-    B.orient[s * 4 + 0] = so;
-    B.orient[s * 4 + 1] = eo;
-    B.orient[s * 4 + 2] = od;
-    B.orient[s * 4 + 3] = (float)(fmax >= 0);
-    B.fe_state[2 * s] = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
+    proj_orient(P, B, s, in, fmin, fmax);
   }
 }
 
@@ -4423,7 +4434,9 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
     if (e_ != hipSuccess) return LEGO_EDEVICE;             \
   } while (0)
 
-bool lg_lds_projection(const LgParams& P) { return (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4 <= 160 * 1024; }
+bool lg_lds_projection(const LgParams& P) {
+  return (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4 <= 160 * 1024;
+}
 bool lg_lds_segment(const LgParams& P) {  // k_segment_lds packing
   return P.V <= 16 && P.VH <= SEG_VH_MAX && P.seg_valid_line <= SEG_DMAX;
 }

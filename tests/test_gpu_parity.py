@@ -623,6 +623,58 @@ def test_edge_inputs(gpu):
         fe.close()
 
 
+def test_projection_input_orders_lds_layout(gpu):
+    """The one-workgroup-a-scan layout (k_project, k_segment_lds) on inputs that are not in firing
+    order: a second sweep over the first (every cell claimed twice, the later point winning), reversed,
+    shuffled and rotated point orders, a ~400 deg sweep, and the edge clouds of test_edge_inputs (which
+    run the single-context, wide layout).  Every stream equals the oracle (projection bit-exact,
+    features, transform).  A projection that writes columns while the input still streams (measured
+    and not kept) must pass this test."""
+    import torch
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    rng = np.random.default_rng(11)
+    base = A.synth_scan(cfg, 4, 0)
+    odd = base.copy()
+    odd[rng.choice(len(odd), 500, replace=False), :3] = np.nan
+    odd[rng.choice(len(odd), 200, replace=False), 2] = 500.0
+    odd[rng.choice(len(odd), 100, replace=False), :3] = 0.01
+    variants = [
+        np.concatenate([base, base * np.float32(1.0002)]),  # every column touched again a sweep later
+        base[::-1],
+        base[rng.permutation(len(base))],
+        np.roll(base, 9000, axis=0),
+        np.concatenate([base, base[:3000] * np.float32(0.999)]),  # a sweep of ~400 deg
+        base[:40],
+        base[::37],
+        odd,
+        base[(np.arange(len(base)) % 16) != 5],
+    ]
+    S, steps = len(variants), 3
+    cap = 2 * params.num_vertical_scans * params.num_horizontal_scans
+    pts = np.zeros((S, cap, 4), np.float32)
+    cnt = np.zeros(S, np.int32)
+    for s, v in enumerate(variants):
+        pts[s, :len(v)] = v
+        cnt[s] = len(v)
+    d_pts = torch.from_numpy(pts.reshape(-1, 4)).cuda()
+    offs = torch.from_numpy(np.arange(S, dtype=np.int64) * cap).cuda()
+    cnts = torch.from_numpy(cnt).cuda()
+    b = L.Batch(params, S, cap)
+    b.set_wide(0)
+    assert b.wide() == 0
+    oracles = [oracle_for(params) for _ in range(S)]
+    for k in range(steps):  # the same cloud again: the stale-state path across scans
+        b.step(d_pts.data_ptr(), offs.data_ptr(), cnts.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        b.sync()
+        for s in range(S):
+            pr = oracles[s].cloud_handler(variants[s])
+            fr = oracles[s].feature_association()
+            pg, fg = b.read(s)
+            assert_scan_parity((k, s), pg, pr, fg, fr)
+    b.close()
+
+
 def _ring0_cropped(pts, keep):
     """Drop all but the first `keep` points of VLP-16 ring 0 (elevation -15 deg)."""
     el = np.degrees(np.arctan2(pts[:, 2], np.hypot(pts[:, 0], pts[:, 1])))
