@@ -57,6 +57,7 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
                                         // staging (features, lessFlat, VoxelGrid output) it uses
   int S;                                // streams of the batch (staging stride)
   int wide;                             // wide mode: k_pw_* / k_sw_* (many workgroups a scan)
+  unsigned wtag;                        // wide mode: launch tag in the winner image entries' top 4 bits
   int max_points;                       // input capacity per scan (wide scatter grid)
   int fp1;                              // lego_params.fp_mode == 1: unqualified libm calls in double
   double sinXd, cosXd, sinYd, cosYd;    // fp_mode 1: sin / cos(double(alpha)) of labelComponents (:463)

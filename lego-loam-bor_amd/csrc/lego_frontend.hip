@@ -150,6 +150,7 @@ struct lego_batch {
   bool timing = false;
   bool events = false;
   int epoch = 0;  // k_extract first-pass token (LgParams.epoch), never 0 after the first launch
+  int wepoch = 0;  // wide projection's launch counter 1..15 (LgParams.wtag), 0: image zeroed
   // stream groups: the S sequences split into `groups` slices, each launched on its own HIP stream
   // so one slice's long-tail kernels overlap the next slice's (fork/join on the caller's stream)
   int groups = 1;
@@ -387,9 +388,10 @@ int lego_batch_reset(lego_batch* b) {
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fe_state, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.counts, 0, S * CNT_N * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
-  // wide mode's per-scan scratch starts (and is left by every launch) reset: winner -1, first point
-  // INT_MAX, last point -1
-  if (hipMemset(B.winner, 0xff, S * VH * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
+  // wide mode's per-scan scratch: winner image zeroed (no launch tag: every cell empty); first point
+  // INT_MAX and last point -1 (every launch leaves them so)
+  b->wepoch = 0;
+  if (hipMemset(B.winner, 0, S * VH * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   {
     std::vector<int32_t> mm(2 * S);
     for (size_t s = 0; s < S; ++s) { mm[2 * s] = 0x7fffffff; mm[2 * s + 1] = -1; }
@@ -409,6 +411,20 @@ int lego_batch_set_timing(lego_batch* b, int32_t enabled) {
     b->events = true;
   }
   b->timing = enabled != 0;
+  return LEGO_OK;
+}
+
+// The next wide projection launch's tag (LgParams.wtag, k_pw_scatter): a counter 1..15 in the top 4
+// bits of the winner image's entries.  At the wrap the image is zeroed on `st`, before the launches
+// that follow there (every earlier launch is ordered before them on `st`: chain_stream / joins).
+static int next_wtag(lego_batch* b, hipStream_t st) {
+  if (!b->P.wide) return LEGO_OK;
+  if (++b->wepoch > 15) {
+    b->wepoch = 1;
+    if (hipMemsetAsync(b->B.winner, 0, (size_t)b->S * b->P.VH * sizeof(int32_t), st) != hipSuccess)
+      return LEGO_EDEVICE;
+  }
+  b->P.wtag = (unsigned)b->wepoch << 28;
   return LEGO_OK;
 }
 
@@ -628,6 +644,7 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     if (rc) return rc;
   }
   rc = chain_stream(b, st);
+  if (!rc) rc = next_wtag(b, st);
   if (rc) return rc;
   const bool ovl = G <= 1 && lag && !b->timing;
   if (ovl != b->pend_ovl && (b->pend_pub || b->pend_lm)) {  // the pending work belongs to the other schedule
@@ -736,6 +753,9 @@ int lego_batch_time_hbm_stages(lego_batch* b, int32_t reps, const lego_point* d_
   if (hipEventRecord(e0, st) != hipSuccess) rc = LEGO_EDEVICE;
   for (int r = 0; r < reps && !rc; ++r) {
     const bool alt = d_offsets_alt && d_counts_alt && ((reps - 1 - r) & 1);  // the last launch: the step's own
+    rc = next_wtag(b, st);
+    if (rc) break;
+    P.wtag = b->P.wtag;
     rc = lg_launch_project(P, b->B, b->S, (const float4*)d_points, alt ? d_offsets_alt : d_offsets,
                            alt ? d_counts_alt : d_counts, st);
     if (!rc) rc = lg_launch_fa_prep(P, b->B, b->S, st, false);
@@ -1200,6 +1220,7 @@ int lego_cloud_handler(lego_ctx* c, const void* points, int32_t n, int32_t step,
   if (hipMemcpyAsync(c->d_in, hin, ((size_t)n + 1) * sizeof(float4), hipMemcpyHostToDevice, nullptr) != hipSuccess)
     return LEGO_EDEVICE;
   int rc = chain_stream(b, nullptr);
+  if (!rc) rc = next_wtag(b, nullptr);
   if (rc) return rc;
   rc = run_projection(b, c->d_in + 1, c->d_off, (const int32_t*)c->d_in, nullptr, 0, 1);
   if (rc) return rc;

@@ -275,7 +275,8 @@ LG_DEVICE int cell_cm(int c, int V, int H) {
   return (c - i * H) * V + i;
 }
 __attribute__((noinline)) __device__ void proj_drain_cm(float ang_bottom, float res_x, float res_y, int V, int H,
-                                                        const float4* in, const int* q, int* winner) {
+                                                        const float4* in, const int* q, unsigned* winner,
+                                                        unsigned tag) {
   LgParams P;
   P.ang_bottom = ang_bottom;
   P.ang_res_x = res_x;
@@ -284,7 +285,7 @@ __attribute__((noinline)) __device__ void proj_drain_cm(float ang_bottom, float 
   P.H = H;
   const int i = q[lane_id()];
   const int c = cell_cm(proj_cell_exact(P, in[i]), V, H);
-  if (c >= 0) atomicMax(&winner[c], i);
+  if (c >= 0) atomicMax(&winner[c], tag | (unsigned)i);
 }
 __attribute__((noinline)) __device__ void proj_drain(float ang_bottom, float res_x, float res_y, int V, int H,
                                                      const float4* in, const int* q, int* winner) {
@@ -469,8 +470,11 @@ __global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const fl
 // segmentation spread over many workgroups instead of one, with the per-scan state in HBM.
 // ============================================================================================
 // k_pw_scatter: grid (point chunks of PW_PTS, scans).  "Later point wins" is a device-scope
-// atomicMax of the input index into the scan's winner image (-1 between launches: k_pw_columns
-// resets every cell it reads); the first / last finite point go to proj_mm by atomicMin / Max.  The
+// atomicMax of the input index into the scan's winner image; each entry carries the launch's tag
+// (P.wtag: a launch counter 1..15 in the top 4 bits, the index in the low 28), so entries of earlier
+// launches are smaller than any of this one and read as empty by k_pw_columns, and the image needs no
+// reset between launches (the host zeroes it when the counter wraps).  The first / last finite
+// point go to proj_mm by atomicMin / Max.  The
 // image is column-major (cell (i, j) at j * V + i): one firing's lasers are consecutive points and
 // land in consecutive words, so a wave's atomics touch a few cache lines instead of one per lane.
 // kNB batches of 8 points a lane per workgroup: 4 when many scans are in flight (fewer, longer
@@ -488,7 +492,8 @@ __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, cons
   const int n = cnts[s];
   const int c0 = blockIdx.x * PW_PTS * kNB;
   if (c0 >= n) return;
-  int* winner = B.winner + (size_t)s * P.VH;
+  unsigned* winner = (unsigned*)B.winner + (size_t)s * P.VH;
+  const unsigned tag = P.wtag;
   const float4* in = pts + offs[s];
   const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
   int* queue = queue_all + wave_id() * PQ_CAP;
@@ -515,13 +520,13 @@ __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, cons
         fmax = max(fmax, i);
         c = P.fast_proj ? proj_cell_fast<true>(P, p)
                         : cell_cm(proj_cell_exact_ni(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, p), V, H);
-        if (c >= 0) atomicMax(&winner[c], i);
+        if (c >= 0) atomicMax(&winner[c], tag | (unsigned)i);
       }
       const unsigned long long amb = __ballot(c == -2);
       if (c == -2) queue[qn + popc_below(amb)] = i;
       qn += __popcll(amb);
       if (qn >= 64) {
-        proj_drain_cm(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue + qn - 64, winner);
+        proj_drain_cm(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue + qn - 64, winner, tag);
         qn -= 64;
       }
     }
@@ -530,7 +535,7 @@ __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, cons
   }
   if (qn > 0) {
     if (lane_id() >= qn) queue[lane_id()] = queue[0];
-    proj_drain_cm(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue, winner);
+    proj_drain_cm(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, queue, winner, tag);
   }
   fmin = wave_min(fmin);
   fmax = wave_max(fmax);
@@ -541,9 +546,9 @@ __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, cons
 }
 
 // k_pw_columns: grid (column blocks of PW_NT, scans), one lane per column: the column pass of
-// k_project over the scan's winner image in HBM (each cell read once, then reset to -1), plus
-// labelComponents' initial state for k_sw_*: parent = cell (eligible: not ground, has a return) or
-// -1, component size / row mask 0 (eligible cells only: no other cell becomes a root).  Block (0, s) settles findStartEndAngle from proj_mm.
+// k_project over the scan's winner image in HBM (each cell read once; entries without this launch's
+// tag are empty cells).  labelComponents' initial state is k_sw_local's.  Block (0, s) settles
+// findStartEndAngle from proj_mm.
 #define PC_NT 128  // columns a workgroup
 __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                       const int64_t* __restrict__ offs,
@@ -560,7 +565,6 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
       int4* wg = (int4*)wsrc;
       for (int q = tid; q < (nw >> 2); q += PC_NT) {
         const int4 v = wg[q];
-        wg[q] = make_int4(-1, -1, -1, -1);
         const int e = 4 * q, jj = e / V, i = e - jj * V;
         int* d = wl + jj * (V + 1) + i;
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
@@ -568,7 +572,6 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
     } else {
       for (int e = tid; e < nw; e += PC_NT) {
         const int v = wsrc[e];
-        wsrc[e] = -1;
         const int jj = e / V;
         wl[jj * (V + 1) + e - jj * V] = v;
       }
@@ -580,9 +583,6 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
   float* range = B.range + (size_t)s * VH;
   float4* cloud = B.cloud + (size_t)s * VH;
   int8_t* ground = B.ground + (size_t)s * VH;
-  int* parent = B.cc_parent + (size_t)s * VH;
-  int* ccnt = B.cc_cnt + (size_t)s * VH;
-  unsigned long long* cmsk = B.cc_mask + (size_t)s * VH;
   const float qnan = __int_as_float(0x7fc00000);
   const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
   const int j = blockIdx.x * PC_NT + tid;
@@ -597,12 +597,6 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
       const int c = i * H + j;
       const int g = (int)((gmask >> i) & 1ull);
       ground[c] = (int8_t)g;
-      const bool elig = g != 1 && r != FLT_MAX;
-      parent[c] = elig ? c : -1;  // _label_mat == 0 (:293-300)
-      if (elig) {  // only roots (eligible cells) ever have their size / row mask read (k_sw_*)
-        ccnt[c] = 0;
-        cmsk[c] = 0ull;
-      }
       if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f && r < min_range) {
         min_range = r;
         id_min = c;
@@ -612,7 +606,10 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
       int w[16];
       float4 pk[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) w[u] = (i0 + u < V) ? wl[tid * (V + 1) + i0 + u] : -1;
+      for (int u = 0; u < 16; ++u) {
+        const unsigned v = (i0 + u < V) ? (unsigned)wl[tid * (V + 1) + i0 + u] : 0u;
+        w[u] = (v & 0xf0000000u) == P.wtag ? (int)(v & 0x0fffffffu) : -1;
+      }
 #pragma unroll
       for (int u = 0; u < 16; ++u) pk[u] = buffer_load_f4(rin, w[u] >= 0 ? (uint32_t)w[u] * 16u : 0xffffffffu);
 #pragma unroll
@@ -1199,7 +1196,7 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
 // ---- wide-mode segmentation: k_sw_* over tiles of SW_TILE cells, grid (tiles, scans) ----------
 // labelComponents' result (imageProjection.cpp:412-496, :354-356) as in k_segment_lds: components
 // of the edge relation by union-find (root = smallest member = the BFS seed), then each feasible
-// root ranked in raster order.  k_pw_columns has set parent (cell or -1), size and row mask.
+// root ranked in raster order.
 //   k_sw_local   union of the edges inside 2-D tiles in LDS (parent := tile-local root)
 //   k_sw_bound   union of the edges crossing tile borders (and the wrap), on the global parent[]
 //   k_sw_roots   full path compression; size and non-seed row mask of every root
@@ -1241,9 +1238,11 @@ LG_DEVICE void sw_unite(int* parent, int a, int b) {
   } while (!done);
 }
 
-// k_sw_local: 2-D tiles of SW_TR x SW_TC cells, grid (column tiles, row tiles, scans).  The edges
-// inside a tile are united in LDS (local indices; the smallest local index is the smallest global
-// one, rows dominating both orders) and every cell's parent becomes its tile-local root.
+// k_sw_local: 2-D tiles of SW_TR x SW_TC cells, grid (column tiles, row tiles, scans).  A cell takes
+// part when _label_mat is 0 there (:293-300: not ground, has a return).  The edges inside a tile are
+// united in LDS (local indices; the smallest local index is the smallest global one, rows dominating
+// both orders); every cell's parent becomes its tile-local root (-1 for cells that take no part), and
+// each tile-local root's component size / row mask start at 0 (every final root is a tile-local root).
 #define SW_TR 8
 #define SW_TC 128
 __global__ __launch_bounds__(SW_NT) void k_sw_local(LgParams P, LgBufs B) {
@@ -1253,19 +1252,21 @@ __global__ __launch_bounds__(SW_NT) void k_sw_local(LgParams P, LgBufs B) {
   const int i0 = blockIdx.y * SW_TR, j0 = blockIdx.x * SW_TC;
   int* parent = B.cc_parent + (size_t)s * VH;
   const float* range = B.range + (size_t)s * VH;
-  int pv[4];
+  const int8_t* ground = B.ground + (size_t)s * VH;
+  bool ev[4];
   float rv[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int t = u * SW_NT + threadIdx.x, i = i0 + t / SW_TC, j = j0 + t % SW_TC;
     const int c = min(i, V - 1) * H + min(j, H - 1);
-    pv[u] = (i < V && j < H) ? parent[c] : -1;
+    const int g = ground[c];
     rv[u] = range[c];
+    ev[u] = i < V && j < H && g != 1 && rv[u] != FLT_MAX;
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int t = u * SW_NT + threadIdx.x;
-    lp[t] = pv[u] >= 0 ? t : -1;
+    lp[t] = ev[u] ? t : -1;
     lrg[t] = rv[u];
   }
   __syncthreads();
@@ -1288,9 +1289,14 @@ __global__ __launch_bounds__(SW_NT) void k_sw_local(LgParams P, LgBufs B) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int t = u * SW_NT + threadIdx.x, i = i0 + t / SW_TC, j = j0 + t % SW_TC;
-    if (i < V && j < H && pv[u] >= 0) {
-      const int rt = uf_find(lp, t);
-      parent[i * H + j] = (i0 + rt / SW_TC) * H + j0 + rt % SW_TC;
+    if (i < V && j < H) {
+      const int c = i * H + j;
+      const int rt = ev[u] ? uf_find(lp, t) : -1;
+      parent[c] = rt >= 0 ? (i0 + rt / SW_TC) * H + j0 + rt % SW_TC : -1;
+      if (rt == t) {  // only roots ever have their size / row mask read (k_sw_roots / k_sw_count)
+        B.cc_cnt[(size_t)s * VH + c] = 0;
+        B.cc_mask[(size_t)s * VH + c] = 0ull;
+      }
     }
   }
 }
