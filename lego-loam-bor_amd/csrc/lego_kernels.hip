@@ -549,31 +549,37 @@ __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, cons
 // k_project over the scan's winner image in HBM (each cell read once; entries without this launch's
 // tag are empty cells).  labelComponents' initial state is k_sw_local's.  Block (0, s) settles
 // findStartEndAngle from proj_mm.
-#define PC_NT 128  // columns a workgroup
+// NQ lanes a column, 16 rows a lane (V <= 16 * NQ): lane q of column j holds rows 16q .. 16q + 15.
+// The pair (16q - 1, 16q) of groundRemoval is settled by lane q with lane q - 1's last point (shuffled
+// up), and its result for row 16q - 1 goes back down; the 2-D scan candidate is the (range, row)
+// minimum over the lanes (the sequential bottom-up scan with a strict `<`).  PC_NT lanes a workgroup
+// (256; 128 for V <= 16, so that one scan still spreads over many workgroups), PC_NT / NQ columns, the
+// workgroup's columns of the column-major winner image staged in LDS with a
+// (V + 1)-word column stride.  Many small workgroups keep more waves in flight than one lane a column
+// walking all rows (each lane has one chunk of 16 gathers to wait for, not V / 16 in turn).
+template <int NQ, int PC_NT>
 __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                       const int64_t* __restrict__ offs,
                                                       const int32_t* __restrict__ cnts) {
-  // the workgroup's PC_NT columns of the column-major winner image, read and reset with coalesced
-  // 16-byte accesses, staged in LDS with a (V + 1)-word column stride (conflict-free column reads)
-  __shared__ int wl[PC_NT * 65];
+  constexpr int NC = PC_NT / NQ;  // columns a workgroup
+  __shared__ int wl[NC * (16 * NQ + 1)];
   const int s = P.s0 + blockIdx.y, tid = threadIdx.x;
-  const int V = P.V, H = P.H, VH = P.VH;
+  const int V = P.V, H = P.H, VH = P.VH, VS = V + 1;
   {
-    int* wsrc = B.winner + (size_t)s * VH + (size_t)blockIdx.x * PC_NT * V;
-    const int nw = min(PC_NT, H - (int)blockIdx.x * PC_NT) * V;
+    const int* wsrc = B.winner + (size_t)s * VH + (size_t)blockIdx.x * NC * V;
+    const int nw = min(NC, H - (int)blockIdx.x * NC) * V;
     if ((V & 3) == 0) {  // 16-byte aligned, 4 words of one column at a time
-      int4* wg = (int4*)wsrc;
-      for (int q = tid; q < (nw >> 2); q += PC_NT) {
-        const int4 v = wg[q];
-        const int e = 4 * q, jj = e / V, i = e - jj * V;
-        int* d = wl + jj * (V + 1) + i;
+      const int4* wg = (const int4*)wsrc;
+      for (int q4 = tid; q4 < (nw >> 2); q4 += PC_NT) {
+        const int4 v = wg[q4];
+        const int e = 4 * q4, jj = e / V, i = e - jj * V;
+        int* d = wl + jj * VS + i;
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
       }
     } else {
       for (int e = tid; e < nw; e += PC_NT) {
-        const int v = wsrc[e];
         const int jj = e / V;
-        wl[jj * (V + 1) + e - jj * V] = v;
+        wl[jj * VS + e - jj * V] = wsrc[e];
       }
     }
   }
@@ -585,80 +591,89 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
   int8_t* ground = B.ground + (size_t)s * VH;
   const float qnan = __int_as_float(0x7fc00000);
   const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
-  const int j = blockIdx.x * PC_NT + tid;
-  if (j < H) {
-    unsigned long long gmask = 0ull;
-    float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
-    float prev_r = 0.f;
-    float min_range = 1000.f;
-    int id_min = -1;
-    const double jfrac = (double)(float)j / 10000.0;
-    auto settle = [&](int i, float r, float Z) {  // row i final: ground flag, 2-D scan (:312-330)
+  const int jj = tid / NQ, q = tid % NQ, i0 = 16 * q;
+  const int j = blockIdx.x * NC + jj;
+  const bool col = j < H;  // (whole lane groups: NQ divides 64)
+  float3 pk[16];  // x, y, z of the cell's point; NaN for an empty cell (nanPoint)
+  unsigned hm = 0u;  // bit u: row i0 + u has a point
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const unsigned v = (col && i0 + u < V) ? (unsigned)wl[jj * VS + i0 + u] : 0u;
+    const bool h = (v & 0xf0000000u) == P.wtag;
+    hm |= (unsigned)h << u;
+    pk[u] = buffer_load_f3(rin, h ? (v & 0x0fffffffu) * 16u : 0xffffffffu);
+  }
+  const float qnan3 = qnan;
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+    if (!((hm >> u) & 1u)) pk[u] = make_float3(qnan3, qnan3, qnan3);
+  const double jfrac = (double)(float)j / 10000.0;
+  // groundRemoval (:271-285): pair (i-1, i) for 1 <= i <= G marks both rows
+  unsigned gm = 0u;  // bit u: row i0 + u
+  float3 below = make_float3(0.f, 0.f, 0.f);
+  if constexpr (NQ > 1) {
+    below.x = __shfl_up(pk[15].x, 1, NQ);
+    below.y = __shfl_up(pk[15].y, 1, NQ);
+    below.z = __shfl_up(pk[15].z, 1, NQ);
+  }
+  bool down = false;  // pair (i0 - 1, i0) marks row i0 - 1, lane q - 1's last row
+  if (NQ > 1 && q > 0 && i0 <= P.G && col && i0 < V) {
+    const float dX = pk[0].x - below.x, dY = pk[0].y - below.y, dZ = pk[0].z - below.z;
+    if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) {
+      gm |= 1u;
+      down = true;
+    }
+  }
+#pragma unroll
+  for (int u = 1; u < 16; ++u) {
+    const int i = i0 + u;
+    if (col && i < V && i <= P.G) {
+      const float dX = pk[u].x - pk[u - 1].x, dY = pk[u].y - pk[u - 1].y, dZ = pk[u].z - pk[u - 1].z;
+      if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) gm |= 3u << (u - 1);
+    }
+  }
+  if constexpr (NQ > 1) {
+    const int dn = __shfl_down((int)down, 1, NQ);
+    if (q + 1 < NQ && dn) gm |= 1u << 15;
+  }
+  float min_range = 1000.f;
+  int id_min = 0x7fffffff;
+  if (col) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = i0 + u;
+      if (i >= V) continue;
       const int c = i * H + j;
-      const int g = (int)((gmask >> i) & 1ull);
+      const float3 p = pk[u];
+      const bool h = (hm >> u) & 1u;
+      const float r = h ? sqrtf(p.x * p.x + p.y * p.y + p.z * p.z) : FLT_MAX;
+      st_nt(&range[c], r);
+      st_nt(&cloud[c], make_float4(p.x, p.y, p.z, h ? (float)((double)(float)i + jfrac) : 0.f));  // nanPoint: 0
+      const int g = (int)((gm >> u) & 1u);
       ground[c] = (int8_t)g;
-      if (g != 1 && (double)Z > 0.4 && (double)Z < 1.2 && r < 40.f && r < min_range) {
+      if (g != 1 && (double)p.z > 0.4 && (double)p.z < 1.2 && r < 40.f && r < min_range) {  // 2-D scan (:312-330)
         min_range = r;
         id_min = c;
       }
-    };
-    for (int i0 = 0; i0 < V; i0 += 16) {
-      int w[16];
-      float4 pk[16];
+    }
+  }
+  if constexpr (NQ > 1) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const unsigned v = (i0 + u < V) ? (unsigned)wl[tid * (V + 1) + i0 + u] : 0u;
-        w[u] = (v & 0xf0000000u) == P.wtag ? (int)(v & 0x0fffffffu) : -1;
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) pk[u] = buffer_load_f4(rin, w[u] >= 0 ? (uint32_t)w[u] * 16u : 0xffffffffu);
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = i0 + u;
-        if (i >= V) continue;
-        const int c = i * H + j;
-        float4 q;
-        float r;
-        if (w[u] >= 0) {
-          const float4 p = pk[u];
-          r = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-          q = make_float4(p.x, p.y, p.z, (float)((double)(float)i + jfrac));
-        } else {
-          r = FLT_MAX;
-          q = make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: PCL default intensity 0
-        }
-        st_nt(&range[c], r);  // streaming stores: the input lines stay in L2 for the gathers
-        st_nt(&cloud[c], q);
-        if (i >= 1 && i <= P.G) {  // pair (i-1, i): groundRemoval :271-285
-          const float dX = q.x - prev.x, dY = q.y - prev.y, dZ = q.z - prev.z;
-          if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) gmask |= (3ull << (i - 1));
-        }
-        if (i >= 1) settle(i - 1, prev_r, prev.z);
-        prev = q;
-        prev_r = r;
+    for (int o = 1; o < NQ; o <<= 1) {
+      const float o_r = __shfl_xor(min_range, o, NQ);
+      const int o_c = __shfl_xor(id_min, o, NQ);
+      if (o_r < min_range || (o_r == min_range && o_c < id_min)) {
+        min_range = o_r;
+        id_min = o_c;
       }
     }
-    settle(V - 1, prev_r, prev.z);
-    B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
   }
+  if (col && q == 0) B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
   if (blockIdx.x == 0 && tid == 0) {  // findStartEndAngle (:234-249)
     const int fmin = B.proj_mm[2 * s], fmax = B.proj_mm[2 * s + 1];
     B.proj_mm[2 * s] = 0x7fffffff;
     B.proj_mm[2 * s + 1] = -1;
-    float so = 0.f, eo = 0.f, od = 0.f;
-    if (fmax >= 0) {
-      float4 a = in[fmin], b = in[fmax];
-      so = -atan2f_g(a.y, a.x);
-      eo = (float)(-(double)atan2f_g(b.y, b.x) + 2 * M_PI);
-      if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
-      else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
-      od = eo - so;
-    }
-    B.orient[s * 4 + 0] = so;
-    B.orient[s * 4 + 1] = eo;
-    B.orient[s * 4 + 2] = od;
-    B.orient[s * 4 + 3] = (float)(fmax >= 0);
-    B.fe_state[2 * s] = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
+    proj_orient(P, B, s, in, fmin, fmax);
   }
 }
 
@@ -4457,7 +4472,12 @@ int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* p
       hipLaunchKernelGGL(k_pw_scatter<1>, dim3((P.max_points + PW_PTS - 1) / PW_PTS, S), dim3(PW_NT), 0, st, P, B,
                          pts, offs, cnts);
     LG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_pw_columns, dim3((P.H + PC_NT - 1) / PC_NT, S), dim3(PC_NT), 0, st, P, B, pts, offs, cnts);
+    if (P.V <= 16)
+      hipLaunchKernelGGL((k_pw_columns<1, 128>), dim3((P.H + 127) / 128, S), dim3(128), 0, st, P, B, pts, offs, cnts);
+    else if (P.V <= 32)
+      hipLaunchKernelGGL((k_pw_columns<2, 256>), dim3((P.H + 127) / 128, S), dim3(256), 0, st, P, B, pts, offs, cnts);
+    else
+      hipLaunchKernelGGL((k_pw_columns<4, 256>), dim3((P.H + 63) / 64, S), dim3(256), 0, st, P, B, pts, offs, cnts);
   } else {  // !wide implies the LDS images fit (lego_batch_set_wide)
     size_t sm = (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4;
     hipLaunchKernelGGL(k_project, dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
