@@ -41,6 +41,11 @@
 #include "../include/lego_frontend.h"
 #include "nanoflann_restated.h"
 
+// Diagnostic: both LMs' normal equations summed in float in row order (see solve_normal); 0 = the model
+// the product follows.  Shared with s2m_oracle.cpp.
+int g_float_ne = 0;
+extern "C" void oracle_set_float_normal_equations(int on) { g_float_ne = on ? 1 : 0; }
+
 namespace {
 
 const double DEG_TO_RAD = M_PI / 180.0;          // utility.h:50
@@ -993,20 +998,27 @@ struct FeatureAssociation {
   float lm_sin(float x) const { return fp1 ? (float)Lm<double>::sn(x) : sinf(x); }
   float lm_cos(float x) const { return fp1 ? (float)Lm<double>::cs(x) : cosf(x); }
 
-  // AtA / AtB (Eigen GEMM, modelled) + solve + degeneracy; returns x[3]
+  // AtA / AtB (Eigen GEMM, modelled) + solve + degeneracy; returns x[3].  g_float_ne (diagnostic,
+  // oracle_set_float_normal_equations): float accumulators in row order instead, a second model of
+  // Eigen's float GEMM whose distance from the first measures how much the unpinned order can matter.
   void solve_normal(const std::vector<float>& A, const std::vector<float>& B, int iterCount, float x[3]) {
     const int n = (int)B.size();
     double ata[9] = {0}, atb[3] = {0};
+    float ataf[9] = {0}, atbf[3] = {0};
     for (int i = 0; i < n; ++i) {
       const float* a = &A[3 * i];
       for (int r = 0; r < 3; ++r) {
-        for (int c = 0; c < 3; ++c) ata[r * 3 + c] += (double)(a[r] * a[c]);
+        for (int c = 0; c < 3; ++c) {
+          ata[r * 3 + c] += (double)(a[r] * a[c]);
+          ataf[r * 3 + c] += a[r] * a[c];
+        }
         atb[r] += (double)(a[r] * B[i]);
+        atbf[r] += a[r] * B[i];
       }
     }
     float AtA[9], AtB[3];
-    for (int k = 0; k < 9; ++k) AtA[k] = (float)ata[k];
-    for (int k = 0; k < 3; ++k) AtB[k] = (float)atb[k];
+    for (int k = 0; k < 9; ++k) AtA[k] = g_float_ne ? ataf[k] : (float)ata[k];
+    for (int k = 0; k < 3; ++k) AtB[k] = g_float_ne ? atbf[k] : (float)atb[k];
     qr_solve3(AtA, AtB, x);
     if (iterCount == 0) {
       // SelfAdjointEigenSolver + :879-891: degenerate iff the largest eigenvalue < 10, and then every

@@ -38,6 +38,8 @@
 #include "../include/lego_s2m.h"
 #include "nanoflann_restated.h"
 
+extern int g_float_ne;  // lego_oracle.cpp (oracle_set_float_normal_equations)
+
 namespace s2m {
 
 struct Pt { float x, y, z, i; };
@@ -454,6 +456,18 @@ static void lm_row(const Trig& T, const Pt& p, const Pt& c, float out[7]) {
 // shuffles, a per-wave table); Eigen's float GEMM order cannot be restated without Eigen, and any
 // fixed order is the reference's sum up to rounding.  out: 21 upper-triangle AtA entries, then 6 AtB.
 static void normal_equations(const std::vector<float>& rows, const std::vector<int>& qidx, double out[27]) {
+  if (g_float_ne) {  // diagnostic model: float accumulators in row order (:1258-1259 as plain loops)
+    float f[27] = {0};
+    for (size_t i = 0; i < qidx.size(); ++i) {
+      const float* a = &rows[7 * i];
+      int k = 0;
+      for (int r = 0; r < 6; ++r)
+        for (int j = r; j < 6; ++j) f[k++] += a[r] * a[j];
+      for (int r = 0; r < 6; ++r) f[21 + r] += a[r] * a[6];
+    }
+    for (int k = 0; k < 27; ++k) out[k] = f[k];
+    return;
+  }
   constexpr int LANES = 1024, W = 64;
   std::vector<double> part((size_t)LANES * 27, 0.0);
   for (size_t i = 0; i < qidx.size(); ++i) {

@@ -230,3 +230,48 @@ def test_odometry_to_transform_matches_oracle():
         pos = rng.normal(size=3) * 100
         got, ref = M.odometry_to_transform(q, pos), O.odometry_to_transform(q, pos)
         assert np.array_equal(got.view(np.int32), ref.view(np.int32)), (q, got, ref)
+
+
+def test_normal_equation_order_gap(tmp_path):
+    """Eigen's float GEMM order for matAt * matA (featureAssociation.cpp:861-862, mapOptmization.cpp:1258-1259)
+    cannot be restated without Eigen, so the oracle and the product sum float products in double (FA) or in
+    k_s2m's fixed lane order (scan-to-map).  This measures how far a second model of the reference's order,
+    float accumulators in row order (oracle_set_float_normal_equations), moves the results: FA odometry over
+    a 30-scan sequence and the scan-to-map transform of 6 problems.  Reported (LEGO_REPORT_DIR or the test's
+    tmp dir); asserted only to stay far inside the north-star 1e-4 for a single solve's scale of change."""
+    import json
+    import lego_amd as LA
+    L = O.lib()
+    cfg = A.synth_cfg("vlp16")
+    scans = [A.synth_scan(cfg, 2, k) for k in range(30)]
+    runs = {}
+    try:
+        for mode in (0, 1):
+            L.oracle_set_float_normal_equations(mode)
+            orc = O.Oracle(LA.params_vlp16())
+            sums, frames = [], []
+            for p in scans:
+                orc.cloud_handler(p)
+                fr = orc.feature_association()
+                sums.append(np.asarray(fr["transform_sum"], np.float64))
+                frames.append(fr)
+            s2m = []
+            for k in (4, 9, 14, 19, 24, 29):
+                pr = M.build_problem(frames[:k + 1], k)
+                t, dg, info = O.scan2map(pr["corner"], pr["surf"], pr["corner_map"], pr["surf_map"], pr["transform"])
+                s2m.append(np.asarray(t, np.float64))
+            runs[mode] = (np.array(sums), np.array(s2m))
+    finally:
+        L.oracle_set_float_normal_equations(0)
+    fa_gap = np.abs(runs[0][0] - runs[1][0]).max(axis=1)
+    s2m_gap = np.abs(runs[0][1] - runs[1][1]).max(axis=1)
+    report = {"fa_transform_sum_gap_per_scan": [float(x) for x in fa_gap],
+              "fa_first_scan_over_1e-6": int(np.argmax(fa_gap > 1e-6)) if (fa_gap > 1e-6).any() else None,
+              "s2m_transform_gap_per_problem": [float(x) for x in s2m_gap]}
+    out = os.environ.get("LEGO_REPORT_DIR", str(tmp_path))
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "normal_equation_order_gap.json"), "w") as f:
+        json.dump(report, f, indent=1)
+    print(json.dumps(report))
+    assert np.all(np.isfinite(fa_gap)) and np.all(np.isfinite(s2m_gap))
+    assert fa_gap.max() < 1e-2 and s2m_gap.max() < 1e-2  # same trajectory, not a divergence
