@@ -469,18 +469,21 @@ def test_wide_many_streams_match_oracle(gpu, kind, S, steps, every):
     b.close()
 
 
-@pytest.mark.parametrize("groups,lag,alternate,steps", [(1, 1, False, 6), (3, 1, False, 6), (3, 0, False, 6),
-                                                        (2, 1, True, 6), (1, 0, True, 6), (1, 1, False, 2),
-                                                        (2, 1, False, 2)])
-def test_batch_back_to_back_matches_oracle(gpu, groups, lag, alternate, steps):
+@pytest.mark.parametrize("groups,lag,alternate,steps,order", [(1, 1, False, 6, 0), (3, 1, False, 6, 0),
+                                                              (3, 0, False, 6, 0), (2, 1, True, 6, 0),
+                                                              (1, 0, True, 6, 0), (1, 1, False, 2, 0),
+                                                              (2, 1, False, 2, 0), (1, 1, False, 6, 1),
+                                                              (1, 1, True, 6, 1), (1, 1, False, 2, 1)])
+def test_batch_back_to_back_matches_oracle(gpu, groups, lag, alternate, steps, order):
     """Steps enqueued back to back with one sync at the end: the grouped slices then issue the
     deferred k_publish / k_lm inside the next step (per group, on its own streams) rather than in a
     flush.  alternate: consecutive steps go to two different non-blocking streams without any sync
     in between (each step must order itself after the previous step's work).  The last scan and the
     accumulated poses equal S independent oracle runs.  steps = 2 checks scan 1, whose front end runs
-    before scan 0's LM with lag 1 (its outlier cloud must already be adjustOutlierCloud'ed)."""
+    before scan 0's LM with lag 1 (its outlier cloud must already be adjustOutlierCloud'ed).  order 1 (the
+    stable VoxelGrid order) takes the schedule whose k_lm starts after the next scan's segmentation."""
     import torch
-    params = L.params_vlp16()
+    params = L.params_vlp16(voxel_tie_order=order)
     cfg = A.synth_cfg("vlp16")
     S = 6
     cap = params.num_vertical_scans * params.num_horizontal_scans
