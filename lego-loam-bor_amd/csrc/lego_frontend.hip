@@ -431,12 +431,11 @@ static int next_wtag(lego_batch* b, hipStream_t st) {
 
 // Streams [s0, s0 + n) of the batch.  Stage events are recorded only for the whole batch (timing).
 static int run_projection(lego_batch* b, const float4* pts, const int64_t* offs, const int32_t* cnts, hipStream_t st,
-                          int s0, int n, hipEvent_t ev_proj = nullptr) {
+                          int s0, int n) {
   LgParams P = b->P;
   P.s0 = s0;
   int rc = lg_launch_project(P, b->B, n, pts, offs, cnts, st);
   if (rc) return rc;
-  if (ev_proj && hipEventRecord(ev_proj, st) != hipSuccess) return LEGO_EDEVICE;
   if (b->timing) hipEventRecord(b->ev[1], st);
   rc = lg_launch_segment(P, b->B, n, st);
   if (rc) return rc;
@@ -658,41 +657,30 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     rc = ensure_ls(b);
     if (rc) return rc;
     const bool pub_now = b->pend_pub;
-    // With the stable VoxelGrid order, k_publish(k-2) / k_lm(k-1) start after this scan's projection and
-    // segmentation: those whole-CU kernels (k_project 124 KB, k_segment_lds 115 KB of LDS) then get
-    // the CUs first instead of waiting for each CU's k_lm workgroup to retire, and k_lm overlaps the
-    // rest of the front end (small workgroups) and the VoxelGrid.  C3: 248-250k -> 260k scans/s.  With
-    // the reference's introsort order the heavier k_voxel(k) then meets k_lm(k-1) head-on (194k -> 167k
-    // scans/s), so that order keeps k_lm at the top of the step.
-#ifndef LG_ORDER0_SCHED
-#define LG_ORDER0_SCHED 0
-#endif
-    // 0: publish + k_lm at the top; 1: both after projection + segmentation; 2: publish at the top,
-    // k_lm after projection + segmentation; 3: publish at the top, k_lm after the projection
-#ifndef LG_ORDER1_SCHED
-#define LG_ORDER1_SCHED 1
-#endif
-    const int mode = b->P.voxel_stable ? LG_ORDER1_SCHED : LG_ORDER0_SCHED;
-    if (b->pend_pub && mode != 1) {  // publish(k-2) on ls, after its k_voxel (issue_publish waits for ev_vox)
+    // With the stable VoxelGrid order, k_lm(k-1) starts after this scan's projection and segmentation:
+    // those whole-CU kernels (k_project 124 KB, k_segment_lds 115 KB of LDS) then get the CUs first
+    // instead of waiting for each CU's k_lm workgroup to retire, and k_lm overlaps the rest of the front
+    // end (small workgroups) and the VoxelGrid.  k_publish(k-2) stays at the top of the step.  C3:
+    // 248-250k -> 265k scans/s.  With the reference's introsort order the heavier k_voxel(k) then
+    // meets k_lm(k-1) head-on (193k -> 167-177k scans/s), so that order keeps k_lm at the top too
+    // (where the measured variants are listed).
+    const bool lm_after_fe = b->P.voxel_stable;
+    if (b->pend_pub) {  // publish(k-2) on ls, after its k_voxel (issue_publish waits for ev_vox)
       rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
       if (!rc && hipEventRecord(b->ev_pub, b->ls) != hipSuccess) rc = LEGO_EDEVICE;
       if (rc) return rc;
     }
-    if (mode != 0) {
-      rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S, mode == 3 ? b->ev_fe : nullptr);
-      if (!rc && mode != 3 && hipEventRecord(b->ev_fe, st) != hipSuccess) rc = LEGO_EDEVICE;
+    if (lm_after_fe) {
+      rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+      if (!rc && hipEventRecord(b->ev_fe, st) != hipSuccess) rc = LEGO_EDEVICE;
       if (!rc && hipStreamWaitEvent(b->ls, b->ev_fe, 0) != hipSuccess) rc = LEGO_EDEVICE;
       if (rc) return rc;
     }
-    if (b->pend_pub && mode == 1) {
-      rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
-      if (!rc && hipEventRecord(b->ev_pub, b->ls) != hipSuccess) rc = LEGO_EDEVICE;
-    }
-    if (!rc && b->pend_lm) {  // k_lm(k-1) on ls, after k_concat(k-1)
+    if (b->pend_lm) {  // k_lm(k-1) on ls, after k_concat(k-1)
       if (hipStreamWaitEvent(b->ls, b->ev_cat[0], 0) != hipSuccess) return LEGO_EDEVICE;
       rc = issue_lm(b, b->ls, 0, b->S, b->lm_par);
     }
-    if (!rc && mode == 0) rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+    if (!rc && !lm_after_fe) rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
     if (!rc) rc = run_association_ovl(b, st, pub_now);
     if (rc) return rc;
     // pending now: publish(k-1) (its k_lm was just issued), k_lm(k)

@@ -2161,6 +2161,85 @@ LG_DEVICE int wave_partition_stream(const SortView<K, V>& a, int first, int last
   }
 }
 
+// The same partition with the stops held in registers (one wave): each scanned chunk's keys and values
+// are read once, its stops are packed into the queue lanes by a forward permute (stop of rank r to
+// lane r, the other lanes behind them), and a swap writes the two held elements without reading
+// them again.  A held element is exact when it is swapped: a valid pair (L_j < R_j) never meets a
+// position an earlier pair swapped (L increases, R decreases), and only valid pairs swap.  LDS
+// operations of one wave complete in order, so a later chunk read sees earlier swaps.
+template <typename T>
+LG_DEVICE T perm_push(int dst_lane, T v) {  // ds_permute_b32: v to lane dst_lane (a permutation)
+  return __builtin_bit_cast(T, __builtin_amdgcn_ds_permute(dst_lane << 2, __builtin_bit_cast(int, v)));
+}
+template <typename T>
+LG_DEVICE T shfl_any(T v, int src) {
+  return __builtin_bit_cast(T, __shfl(__builtin_bit_cast(int, v), src));
+}
+template <typename K, typename V>
+LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int last) {
+  const int lane = lane_id();
+  const K pv = a.key[first];
+  int lo = first + 1, hi = last - 1;
+  int qL = 0, qR = 0, nqL = 0, nqR = 0;
+  K kL = K(0), kR = K(0);
+  int vL = 0, vR = 0;
+  int lastR = last;
+  while (true) {
+    const bool scanL = nqL == 0, scanR = nqR == 0;
+    if (scanL && lo >= last) return min(last, lastR);  // unreachable for a median-of-3 pivot
+    if (scanL) {
+      const int pL = lo + lane;
+      const bool in = pL < last;
+      const K k = a.key[in ? pL : first];
+      const int v = (int)a.val[in ? pL : first];
+      const bool st = in && !(k < pv);
+      const unsigned long long m = __ballot(st);
+      const int ns = __popcll(m), below = popc_below(m);
+      const int dst = st ? below : ns + (lane - below);
+      qL = perm_push(dst, pL);
+      kL = perm_push(dst, k);
+      vL = perm_push(dst, v);
+      nqL = ns;
+      lo += 64;
+    }
+    if (scanR) {
+      const int pR = hi - lane;
+      const bool in = pR >= first;
+      const K k = a.key[in ? pR : first];
+      const int v = (int)a.val[in ? pR : first];
+      const bool st = in && !(pv < k);
+      const unsigned long long m = __ballot(st);
+      const int ns = __popcll(m), below = popc_below(m);
+      const int dst = st ? below : ns + (lane - below);
+      qR = perm_push(dst, pR);
+      kR = perm_push(dst, k);
+      vR = perm_push(dst, v);
+      nqR = ns;
+      hi -= 64;
+    }
+    const int np = min(nqL, nqR);
+    const bool valid = lane < np && qL < qR;
+    const int nv = __popcll(__ballot(valid));  // valid pairs form a prefix (L increasing, R decreasing)
+    if (valid) {
+      a.key[qL] = kR; a.val[qL] = (V)vR;
+      a.key[qR] = kL; a.val[qR] = (V)vL;
+    }
+    if (nv < np) {
+      const int Lk = __shfl(qL, nv);
+      const int Rk1 = nv > 0 ? __shfl(qR, nv - 1) : lastR;
+      return min(Lk, Rk1);
+    }
+    if (np > 0) {
+      lastR = __shfl(qR, np - 1);
+      const int src = min(lane + np, 63);
+      qL = __shfl(qL, src); kL = shfl_any(kL, src); vL = __shfl(vL, src);
+      qR = __shfl(qR, src); kR = shfl_any(kR, src); vR = __shfl(vR, src);
+      nqL -= np;
+      nqR -= np;
+    }
+  }
+}
+
 template <int R, typename K, typename V>
 LG_DEVICE void final_bitonic(K* key, V* val, int n);
 
@@ -2203,7 +2282,12 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
 
         if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
         __syncthreads();
-        cut = wave_partition_stream(a, first, last, tab);
+        if (blockDim.x == 64) {  // (every caller: one wave a workgroup)
+          cut = wave_partition_stream_reg(a, first, last);
+          __syncthreads();
+        } else {
+          cut = wave_partition_stream(a, first, last, tab);
+        }
       }
       if (lane == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = last; stk[3 * sp + 2] = depth; }
       ++sp;
