@@ -2045,6 +2045,14 @@ LG_DEVICE void heap_sort_wave(const SortView<K, V>& a, int first, int last) {
   PROF_ADD(36, t_pop0);
 }
 
+template <typename T>
+LG_DEVICE T perm_push(int dst_lane, T v) {  // ds_permute_b32: v to lane dst_lane (a permutation)
+  return __builtin_bit_cast(T, __builtin_amdgcn_ds_permute(dst_lane << 2, __builtin_bit_cast(int, v)));
+}
+template <typename T>
+LG_DEVICE T shfl_any(T v, int src) {
+  return __builtin_bit_cast(T, __shfl(__builtin_bit_cast(int, v), src));
+}
 // __unguarded_partition_pivot on a range of 17..64 elements held one per lane; returns the cut.
 // tab: >= 128 ints of LDS scratch.
 template <typename K, typename V>
@@ -2078,18 +2086,19 @@ LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last,
   const int nL = __popcll(bl), nR = __popcll(br);
   const int lrank = popc_below(bl);                                   // k-th left stop, from first+1 up
   const int rrank = __popcll(br & ~((2ull << lane) - 1ull));          // k-th right stop, from last-1 down
-  if (lf) tab[lrank] = lane;
-  if (rf) tab[64 + rrank] = lane;
-  __syncthreads();
+  // lane k of Ls / Rs: the k-th left / right stop (forward permutes: the stops to their ranks, the
+  // other lanes behind them)
+  const int Ls = perm_push(lf ? lrank : nL + (lane - lrank), lane);
+  const int nrb = __popcll(br & ((1ull << lane) - 1ull));             // right stops below this lane
+  const int Rs = perm_push(rf ? rrank : nR + (lane - nrb), lane);
   int partner = -1;
   bool left_swap = false;  // a pivot-equal lane is both kinds of stop: count only its left role
+  const int qr = __shfl(Rs, lf ? min(lrank, 63) : 0), ql = __shfl(Ls, rf ? min(rrank, 63) : 0);
   if (lf && lrank < nR) {
-    const int q = tab[64 + lrank];
-    if (lane < q) { partner = q; left_swap = true; }
+    if (lane < qr) { partner = qr; left_swap = true; }
   }
   if (rf && rrank < nL) {
-    const int q = tab[rrank];
-    if (q < lane) partner = q;
+    if (ql < lane) partner = ql;
   }
   const K kp = __shfl(k, partner < 0 ? lane : partner);
   const int vp = __shfl(v, partner < 0 ? lane : partner);
@@ -2167,14 +2176,6 @@ LG_DEVICE int wave_partition_stream(const SortView<K, V>& a, int first, int last
 // them again.  A held element is exact when it is swapped: a valid pair (L_j < R_j) never meets a
 // position an earlier pair swapped (L increases, R decreases), and only valid pairs swap.  LDS
 // operations of one wave complete in order, so a later chunk read sees earlier swaps.
-template <typename T>
-LG_DEVICE T perm_push(int dst_lane, T v) {  // ds_permute_b32: v to lane dst_lane (a permutation)
-  return __builtin_bit_cast(T, __builtin_amdgcn_ds_permute(dst_lane << 2, __builtin_bit_cast(int, v)));
-}
-template <typename T>
-LG_DEVICE T shfl_any(T v, int src) {
-  return __builtin_bit_cast(T, __shfl(__builtin_bit_cast(int, v), src));
-}
 template <typename K, typename V>
 LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int last) {
   const int lane = lane_id();
