@@ -155,7 +155,7 @@ def pmc_traffic(args, S, kernels):
     passes); None when no summary matches the workload."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc*.json"))):  # r03i_pmc.json, r03i_pmc_2048.json
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -171,9 +171,9 @@ def pmc_traffic(args, S, kernels):
 
 
 def roofline_kernels(wide):
-    """The projection + smoothness kernels the roofline pair times: k_project (or its windowed form)
-    + k_fa_prep4 in the LDS layout, k_pw_scatter + k_pw_columns + k_fa_prep4 in the wide layout."""
-    return ("k_pw_scatter", "k_pw_columns", "k_fa_prep4") if wide else ("k_project_win|k_project", "k_fa_prep4")
+    """The projection + smoothness kernels the roofline pair times: k_project + k_fa_prep4 in the LDS
+    layout, k_pw_scatter + k_pw_columns + k_fa_prep4 in the wide layout."""
+    return ("k_pw_scatter", "k_pw_columns", "k_fa_prep4") if wide else ("k_project", "k_fa_prep4")
 
 
 def roofline_at(args, L, A, mk_params, cfg, dev_index, stream):
