@@ -2124,54 +2124,8 @@ LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last,
 // (L_k, R_k) of every later valid pair k, so stops read in a chunk before or after such a swap are
 // the same up to the crossing, and the min() covers a left scan that has run into swapped
 // territory.  Every position is read at most once.
-template <typename K, typename V>
-LG_DEVICE int wave_partition_stream(const SortView<K, V>& a, int first, int last, int* tab) {
-  const int lane = lane_id();
-  const K pv = a.key[first];
-  int lo = first + 1, hi = last - 1;
-  int qL = 0, qR = 0, nqL = 0, nqR = 0;
-  int lastR = last;
-  while (true) {
-    const bool scanL = nqL == 0, scanR = nqR == 0;
-    if (scanL && lo >= last) {  // unreachable for a median-of-3 pivot; mirrors the unguarded end
-      __syncthreads();
-      return min(last, lastR);
-    }
-    bool stL = false, stR = false;
-    const int pL = lo + lane, pR = hi - lane;
-    if (scanL && pL < last) stL = !(a.key[pL] < pv);
-    if (scanR && pR >= first) stR = !(pv < a.key[pR]);
-    const unsigned long long mL = __ballot(stL), mR = __ballot(stR);
-    if (stL) tab[popc_below(mL)] = pL;
-    if (stR) tab[64 + popc_below(mR)] = pR;
-    __syncthreads();
-    if (scanL) { qL = tab[lane]; nqL = __popcll(mL); lo += 64; }
-    if (scanR) { qR = tab[64 + lane]; nqR = __popcll(mR); hi -= 64; }
-    __syncthreads();
-    const int np = min(nqL, nqR);
-    const bool valid = lane < np && qL < qR;
-    const int nv = __popcll(__ballot(valid));  // valid pairs form a prefix (L increasing, R decreasing)
-    if (valid) a.swap(qL, qR);
-    if (nv < np) {
-      const int Lk = __shfl(qL, nv);
-      const int Rk1 = nv > 0 ? __shfl(qR, nv - 1) : lastR;
-      __syncthreads();
-      return min(Lk, Rk1);
-    }
-    if (np > 0) {
-      lastR = __shfl(qR, np - 1);
-      const int src = min(lane + np, 63);
-      qL = __shfl(qL, src);
-      qR = __shfl(qR, src);
-      nqL -= np;
-      nqR -= np;
-    }
-    __syncthreads();
-  }
-}
-
-// The same partition with the stops held in registers (one wave): each scanned chunk's keys and values
-// are read once, its stops are packed into the queue lanes by a forward permute (stop of rank r to
+// The stops are held in registers (one wave): each scanned chunk's keys and values are read once, its
+// stops are packed into the queue lanes by a forward permute (stop of rank r to
 // lane r, the other lanes behind them), and a swap writes the two held elements without reading
 // them again.  A held element is exact when it is swapped: a valid pair (L_j < R_j) never meets a
 // position an earlier pair swapped (L increases, R decreases), and only valid pairs swap.  LDS
@@ -2283,12 +2237,8 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
 
         if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
         __syncthreads();
-        if (blockDim.x == 64) {  // (every caller: one wave a workgroup)
-          cut = wave_partition_stream_reg(a, first, last);
-          __syncthreads();
-        } else {
-          cut = wave_partition_stream(a, first, last, tab);
-        }
+        cut = wave_partition_stream_reg(a, first, last);  // (every caller: one wave a workgroup)
+        __syncthreads();
       }
       if (lane == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = last; stk[3 * sp + 2] = depth; }
       ++sp;
