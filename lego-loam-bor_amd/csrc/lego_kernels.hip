@@ -2132,17 +2132,18 @@ LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last,
 // operations of one wave complete in order, so a later chunk read sees earlier swaps.
 template <typename K, typename V>
 LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int last) {
+  // the queues: lanes [hL, hL + nqL) hold the pending left stops (position, key, value) in scan order,
+  // lanes [hR, hR + nqR) the right stops; pair i = (left lane hL + i, right lane hR + i)
   const int lane = lane_id();
   const K pv = a.key[first];
   int lo = first + 1, hi = last - 1;
-  int qL = 0, qR = 0, nqL = 0, nqR = 0;
+  int qL = 0, qR = 0, nqL = 0, nqR = 0, hL = 0, hR = 0;
   K kL = K(0), kR = K(0);
   int vL = 0, vR = 0;
   int lastR = last;
   while (true) {
-    const bool scanL = nqL == 0, scanR = nqR == 0;
-    if (scanL && lo >= last) return min(last, lastR);  // unreachable for a median-of-3 pivot
-    if (scanL) {
+    if (nqL == 0) {
+      if (lo >= last) return min(last, lastR);  // unreachable for a median-of-3 pivot
       const int pL = lo + lane;
       const bool in = pL < last;
       const K k = a.key[in ? pL : first];
@@ -2155,9 +2156,10 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
       kL = perm_push(dst, k);
       vL = perm_push(dst, v);
       nqL = ns;
+      hL = 0;
       lo += 64;
     }
-    if (scanR) {
+    if (nqR == 0) {
       const int pR = hi - lane;
       const bool in = pR >= first;
       const K k = a.key[in ? pR : first];
@@ -2170,28 +2172,32 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
       kR = perm_push(dst, k);
       vR = perm_push(dst, v);
       nqR = ns;
+      hR = 0;
       hi -= 64;
     }
     const int np = min(nqL, nqR);
-    const bool valid = lane < np && qL < qR;
+    if (np == 0) continue;  // a scanned chunk without stops
+    const int i = lane - hL;
+    const int src = min(max(hR + i, 0), 63);
+    const int rq = __shfl(qR, src);
+    const K rk = shfl_any(kR, src);
+    const int rv = __shfl(vR, src);
+    const bool valid = i >= 0 && i < np && qL < rq;
     const int nv = __popcll(__ballot(valid));  // valid pairs form a prefix (L increasing, R decreasing)
     if (valid) {
-      a.key[qL] = kR; a.val[qL] = (V)vR;
-      a.key[qR] = kL; a.val[qR] = (V)vL;
+      a.key[qL] = rk; a.val[qL] = (V)rv;
+      a.key[rq] = kL; a.val[rq] = (V)vL;
     }
     if (nv < np) {
-      const int Lk = __shfl(qL, nv);
-      const int Rk1 = nv > 0 ? __shfl(qR, nv - 1) : lastR;
+      const int Lk = __builtin_amdgcn_readlane(qL, hL + nv);
+      const int Rk1 = nv > 0 ? __builtin_amdgcn_readlane(rq, hL + nv - 1) : lastR;
       return min(Lk, Rk1);
     }
-    if (np > 0) {
-      lastR = __shfl(qR, np - 1);
-      const int src = min(lane + np, 63);
-      qL = __shfl(qL, src); kL = shfl_any(kL, src); vL = __shfl(vL, src);
-      qR = __shfl(qR, src); kR = shfl_any(kR, src); vR = __shfl(vR, src);
-      nqL -= np;
-      nqR -= np;
-    }
+    lastR = __builtin_amdgcn_readlane(rq, hL + np - 1);
+    hL += np;
+    hR += np;
+    nqL -= np;
+    nqR -= np;
   }
 }
 
