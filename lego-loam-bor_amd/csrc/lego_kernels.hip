@@ -2133,7 +2133,9 @@ LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last,
 template <typename K, typename V>
 LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int last) {
   // the queues: lanes [hL, hL + nqL) hold the pending left stops (position, key, value) in scan order,
-  // lanes [hR, hR + nqR) the right stops; pair i = (left lane hL + i, right lane hR + i)
+  // lanes [hR, hR + nqR) the right stops; pair i = (left lane hL + i, right lane hR + i).  With 16-bit
+  // values a stop's position and value travel as one word (positions < 2^16: n <= 2048 here).
+  constexpr bool kPack = sizeof(V) == 2;
   const int lane = lane_id();
   const K pv = a.key[first];
   int lo = first + 1, hi = last - 1;
@@ -2141,6 +2143,7 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
   K kL = K(0), kR = K(0);
   int vL = 0, vR = 0;
   int lastR = last;
+  auto pos_of = [](int q) { return kPack ? (q >> 16) : q; };
   while (true) {
     if (nqL == 0) {
       if (lo >= last) return min(last, lastR);  // unreachable for a median-of-3 pivot
@@ -2152,9 +2155,9 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
       const unsigned long long m = __ballot(st);
       const int ns = __popcll(m), below = popc_below(m);
       const int dst = st ? below : ns + (lane - below);
-      qL = perm_push(dst, pL);
+      qL = perm_push(dst, kPack ? (pL << 16) | v : pL);
       kL = perm_push(dst, k);
-      vL = perm_push(dst, v);
+      if (!kPack) vL = perm_push(dst, v);
       nqL = ns;
       hL = 0;
       lo += 64;
@@ -2168,9 +2171,9 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
       const unsigned long long m = __ballot(st);
       const int ns = __popcll(m), below = popc_below(m);
       const int dst = st ? below : ns + (lane - below);
-      qR = perm_push(dst, pR);
+      qR = perm_push(dst, kPack ? (pR << 16) | v : pR);
       kR = perm_push(dst, k);
-      vR = perm_push(dst, v);
+      if (!kPack) vR = perm_push(dst, v);
       nqR = ns;
       hR = 0;
       hi -= 64;
@@ -2179,17 +2182,18 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
     if (np == 0) continue;  // a scanned chunk without stops
     const int i = lane - hL;
     const int src = min(max(hR + i, 0), 63);
-    const int rq = __shfl(qR, src);
+    const int rqw = __shfl(qR, src);
     const K rk = shfl_any(kR, src);
-    const int rv = __shfl(vR, src);
-    const bool valid = i >= 0 && i < np && qL < rq;
+    const int rv = kPack ? (rqw & 0xffff) : __shfl(vR, src);
+    const int lq = pos_of(qL), rq = pos_of(rqw);
+    const bool valid = i >= 0 && i < np && lq < rq;
     const int nv = __popcll(__ballot(valid));  // valid pairs form a prefix (L increasing, R decreasing)
     if (valid) {
-      a.key[qL] = rk; a.val[qL] = (V)rv;
-      a.key[rq] = kL; a.val[rq] = (V)vL;
+      a.key[lq] = rk; a.val[lq] = (V)rv;
+      a.key[rq] = kL; a.val[rq] = (V)(kPack ? (qL & 0xffff) : vL);
     }
     if (nv < np) {
-      const int Lk = __builtin_amdgcn_readlane(qL, hL + nv);
+      const int Lk = __builtin_amdgcn_readlane(lq, hL + nv);
       const int Rk1 = nv > 0 ? __builtin_amdgcn_readlane(rq, hL + nv - 1) : lastR;
       return min(Lk, Rk1);
     }
