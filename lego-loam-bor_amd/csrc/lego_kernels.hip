@@ -378,10 +378,9 @@ LG_DEVICE void proj_orient(const LgParams& P, const LgBufs& B, int s, const floa
   B.fe_state[2 * s] = (fmax >= 0) ? LEGO_OK : LEGO_EEMPTY;
 }
 
-__global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
-                                                  const int64_t* __restrict__ offs,
-                                                  const int32_t* __restrict__ cnts) {
-  extern __shared__ __attribute__((aligned(16))) int smem[];
+// k_project's body (one 1,024-thread workgroup a scan; smem: the dynamic LDS, lg_lds_projection)
+LG_DEVICE void project_lds(const LgParams& P, const LgBufs& B, const float4* __restrict__ pts,
+                           const int64_t* __restrict__ offs, const int32_t* __restrict__ cnts, int* smem) {
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, H = P.H, VH = P.VH;
   int* scratch = smem;                 // 64 ints
@@ -912,8 +911,8 @@ LG_DEVICE void uf_unite_rep16(uint16_t* parent, int a, int b) {  // uf_unite_rep
   }
 }
 
-__global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
-  extern __shared__ __attribute__((aligned(16))) int smem[];
+// k_segment_lds's body (one 1,024-thread workgroup a scan; smem: 64 ints + V*H half-words)
+LG_DEVICE void segment_lds(const LgParams& P, const LgBufs& B, int* smem) {
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int V = P.V, H = P.H, VH = P.VH, G = P.G;
   int* scratch = smem;  // 64 ints
@@ -1208,6 +1207,16 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
   }
 }
 
+__global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
+                                                  const int64_t* __restrict__ offs,
+                                                  const int32_t* __restrict__ cnts) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  project_lds(P, B, pts, offs, cnts, smem);
+}
+__global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  segment_lds(P, B, smem);
+}
 // ---- wide-mode segmentation: k_sw_* over tiles of SW_TILE cells, grid (tiles, scans) ----------
 // labelComponents' result (imageProjection.cpp:412-496, :354-356) as in k_segment_lds: components
 // of the edge relation by union-find (root = smallest member = the BFS seed), then each feasible
