@@ -49,6 +49,8 @@ extern "C" {
 #define LEGO_ST_EMITTED         0x080  /* AssociationOut sent to mapping this cycle (fa.cpp:1432)     */
 #define LEGO_ST_VOXEL_OVERFLOW  0x100  /* PCL VoxelGrid index overflow: cloud copied unfiltered       */
 #define LEGO_ST_DEGEN_UB        0x200  /* ref UB: degenerate at iter>0 uses uninit matP (fa.cpp:894)  */
+#define LEGO_ST_TIE_UNRESOLVED  0x400  /* an exact 1-NN tie kept the grid's lowest index: the device kd-tree's
+                                        * build or search stack overflowed (not nanoflann's choice)  */
 
 /* ---- parameters: the reference's loam_config.yaml keys ------------------------- */
 typedef struct lego_params {
@@ -240,7 +242,8 @@ int  lego_test_libm(const float* a, const float* b, float* out, int32_t n, int32
 int  lego_test_libm_d(const double* a, const double* b, double* out, int32_t n, int32_t which);
 /* Sort (key, val) pairs by key with the device's wave-parallel std::sort emulation (n <= 2048);
  * keys are uint32 (is_float 0) or float bit patterns (1); is_float 2 runs k_extract's segment
- * sort (float keys, n <= 512: register sort when keys are distinct, else the emulation). */
+ * sort (float keys, n <= 512: register sort when keys are distinct, else the emulation); is_float 3
+ * runs k_voxel's level-synchronous emulation (uint32 keys, values < 2^16). */
 int  lego_test_sort(uint32_t* keys, int32_t* vals, int32_t n, int32_t is_float);
 /* Projection cell (row * H + col, or -1 = rejected) of n points (x, y, z, w float32) by the fast path
  * of k_project (-2 = too close to a decision boundary, decided by the exact path) and by the exact

@@ -43,6 +43,8 @@ extern "C" {
 #define LEGO_S2M_ST_FEW         0x04  /* an iteration had < 50 correspondences (:1208: no update)           */
 #define LEGO_S2M_ST_CONVERGED   0x08  /* LMOptimization returned true (:1308) before the 10th iteration     */
 #define LEGO_S2M_ST_SKIPPED     0x10  /* the map gate of :1316 failed: transform and state untouched        */
+#define LEGO_S2M_ST_TIE_UNRESOLVED 0x20  /* a tied query kept the grid's order: the device kd-tree's build or
+                                          * search stack overflowed (not nanoflann's choice)                 */
 
 /* Device-side batch: array i of problem p is base_i[off_i[p] .. off_i[p] + n_i[p]).  All pointers are
  * DEVICE pointers (offsets int64, counts int32, one entry per problem). */

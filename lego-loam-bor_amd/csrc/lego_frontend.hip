@@ -8,6 +8,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <new>
 #include <vector>
@@ -1278,7 +1279,9 @@ int lego_test_set_lm_state(lego_ctx* c, const float* cur6, const float* sum6, in
   lego_batch* b = c->b;
   const LgParams& P = b->P;
   const LgBufs& B = b->B;
-  if (n_corner > P.V * P.cap_lsharp || n_surf > P.VH) return LEGO_EINVAL;
+  // the corner Last cloud's kd-tree / grid scratch is sized by V*H (kd_vind, kd_tmp, kd_node, grid_pts):
+  // with H < cap_lsharp an injected cloud of V*cap_lsharp points would not fit it
+  if (n_corner > std::min(P.V * P.cap_lsharp, P.VH) || n_surf > P.VH) return LEGO_EINVAL;
   hipSetDevice(b->device);
   if (flush_pending(b) != LEGO_OK || hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
   LgState S;

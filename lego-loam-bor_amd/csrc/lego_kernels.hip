@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -2321,6 +2322,318 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
   PROF_ADD(11, t_fin0);
 }
 
+// ============================================================================================
+// Level-synchronous libstdc++ introsort (voxel_tie_order 0), one wave, n <= 64 R keys < 2^31 - 1.
+//
+// __introsort_loop's result does not depend on the order in which it visits its disjoint ranges,
+// and every range at recursion level t has depth limit d0 - t.  So all ranges of a level are
+// partitioned together, from registers: lane l holds positions [l R, l R + R) (key, value).
+// __unguarded_partition on [f, l) with the median-of-3 pivot at f, per position p in (f, l):
+//   left stop  lf(p) = !(key < pivot),  right stop rf(p) = !(pivot < key),
+//   A(p) = #lf in (f, p),  B(p) = #rf in (p, l),  D(p) = A(p) - B(p)  (non-decreasing in p).
+// Hoare's loop swaps the k-th left stop from the left with the k-th right stop from the right while
+// the left one is below the right one: left stop p (rank A) is swapped iff D(p) < 0, right stop q
+// (rank B) iff D(q) > 0, and the pair of rank k exchanges through two scratch slots (f + k and
+// l - 1 - k; 2K < l - f).  The returned cut min(L_K, R_{K-1}) is the first position p > f with
+// (lf(p) && D(p) >= 0) || (rf(p) && D(p) > 0).  Ranges still longer than 16 at depth 0 take the
+// heap sort (heap_sort_wave, as the stack emulation).  __final_insertion_sort is then the stable
+// order by key inside each final range (no element crosses a cut): each position's rank among the
+// <= 15 neighbours of its range on either side.  Range starts are one bit per position (S, R bits a
+// lane); the counts of the lanes below / above come from ballots of the per-lane totals' bits and
+// one shuffle from the lane holding the range's start (or end).
+// Bit-exact against libstdc++: test_device_sort_matches_libstdcxx (is_float 3), every voxel_tie_order
+// 0 parity test.
+// ============================================================================================
+#define LV_BUF(R) (64 * (R) + 64)
+// One position's work per scheduling region in the unrolled passes: left free, the scheduler
+// interleaves all R positions and runs out of registers.
+#define LV_SCHED() __builtin_amdgcn_sched_barrier(0)
+// An opaque copy of a per-lane mask for each pass: the per-position bits ((S >> r) & 1 ...) a pass
+// derives from it are then not shared with the other passes (which kept R of them live across all).
+LG_DEVICE unsigned lv_opaque(unsigned v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}  // padded u64 slots: position p at p + p / R (conflict-free lanes)
+
+template <int R>
+struct VoxLvlLds {  // k_voxel<4> (R = 16, rings of <= 1,024 points): 9.2 KB per wave; <5> (R = 32): 17.4 KB
+  union {
+    struct { unsigned key[64 * R]; uint16_t val[64 * R]; } nat;  // natural order (in / out)
+    unsigned long long buf[LV_BUF(R) + 64];                      // the sort's exchange buffer (+ dump slots)
+  } u;
+};
+
+// Exclusive prefix over lanes of a per-lane count < 64, and the wave total.
+LG_DEVICE void lv_lane_prefix(int c, int& ex, int& tot) {
+  const unsigned long long below = (1ull << lane_id()) - 1ull;
+  ex = 0;
+  tot = 0;
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    const unsigned long long m = __ballot((c >> b) & 1);
+    ex += __popcll(m & below) << b;
+    tot += __popcll(m) << b;
+  }
+}
+
+// The lanes holding the start of the range that runs into this lane (jb) and the end of the range
+// that runs out of it (ja, -1: none), the first position of the former (cf) and the end of the
+// latter (cl).
+template <int R>
+LG_DEVICE void lv_carry(unsigned S, int p0, int& jb, int& ja, int& cf, int& cl) {
+  const int lane = lane_id();
+  const unsigned long long Ms = __ballot(S != 0u);
+  const unsigned long long mb = Ms & ((1ull << lane) - 1ull);
+  const unsigned long long ma = Ms & ~((2ull << lane) - 1ull);  // lane 63: none
+  jb = mb ? 63 - __clzll((long long)mb) : 0;
+  ja = ma ? __ffsll((long long)ma) - 1 : -1;
+  const int lastS = S ? p0 + 31 - __clz(S) : -1;
+  const int firstS = S ? p0 + __ffs(S) - 1 : 64 * R;
+  cf = __shfl(lastS, jb);
+  const int c1 = __shfl(firstS, ja < 0 ? lane : ja);
+  cl = ja < 0 ? 64 * R : c1;
+}
+
+template <int R>
+LG_DEVICE void lvl_sort(unsigned* nkey, uint16_t* nval, unsigned long long* buf, int n) {
+  static_assert(R >= 16 && R <= 32, "final ranks need a range inside two lanes");
+  const int lane = lane_id();
+  const int p0 = lane * R;
+  if (n <= 1) return;
+  auto pad = [](int p) { return p + (int)((unsigned)p / R); };
+  uint2* eb = reinterpret_cast<uint2*>(buf);  // (value | scratch << 16, key) pairs
+  uint2* own = eb + lane * (R + 1);           // this lane's positions, padded
+  const int dump = LV_BUF(R) + lane;          // exchange slot of positions that do not swap
+  // e[r]: position p0 + r.  x: value (low 16 bits) | per-level scratch (high 16), y: key.  The
+  // element is the whole register state: range bounds and counts are rebuilt from the start bits.
+  uint2 e[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int p = p0 + r;
+    const int pc = p < n ? p : n - 1;
+    const unsigned kk = nkey[pc], vv = nval[pc];
+    e[r] = make_uint2(vv, p < n ? kk : 0x7fffffffu);
+  }
+  __syncthreads();  // buf aliases nkey / nval
+  // range starts: 0, and the padding range [n, 64 R) that never partitions
+  unsigned S = (lane == 0 ? 1u : 0u) | ((n >= p0 && n < p0 + R) ? (1u << (n - p0)) : 0u);
+  const int d0 = 2 * floor_log2(n);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  // first of the range holding position p0 + r (its start at or below it, else the carried one)
+  // (positions relative to p0 inside the passes: in-lane positions are then immediates)
+  auto first_of = [](unsigned Sx, int r, int cfr) {
+    const unsigned sm = Sx & ((2u << r) - 1u);
+    return sm ? 31 - __clz(sm) : cfr;
+  };
+  PROF_T(t_part0);
+  for (int t = 0;; ++t) {
+    int jb, ja, cf, cl;
+    lv_carry<R>(S, p0, jb, ja, cf, cl);
+    const int cfr = cf - p0, clr = cl - p0, nr = n - p0;
+    unsigned AM = 0;  // positions in ranges that still partition (> 16 positions, not padding)
+    {
+      const unsigned Sx = lv_opaque(S);
+      int l = clr;
+#pragma unroll
+      for (int r = R - 1; r >= 0; --r) {
+        const int f = first_of(Sx, r, cfr);
+        AM = (AM << 1) | ((l - f > 16 && f < nr) ? 1u : 0u);  // bit r after the remaining shifts
+        l = ((Sx >> r) & 1u) ? r : l;
+        LV_SCHED();
+      }
+    }
+    if (__ballot(AM != 0u) == 0ull) break;
+    if (t == d0) {  // depth limit: __partial_sort (heap sort) of every range still longer than 16
+      PROF_T(t_hs0);
+      unsigned* nk = nkey + p0;  // (base + immediate offsets: no per-position address registers)
+      uint16_t* nv = nval + p0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) { nk[r] = e[r].y; nv[r] = (uint16_t)e[r].x; }  // < RING_MAX
+      __syncthreads();
+      unsigned H = S & AM;
+      unsigned long long HB;
+      while ((HB = __ballot(H != 0u)) != 0ull) {
+        const int src = __ffsll((long long)HB) - 1;
+        int f = 0, l = 0;
+        if (H) {
+          const int r = __ffs(H) - 1;
+          const unsigned hi = S & ~((2u << r) - 1u);
+          f = p0 + r;
+          l = hi ? p0 + __ffs(hi) - 1 : cl;
+        }
+        f = __builtin_amdgcn_readlane(f, src);
+        l = __builtin_amdgcn_readlane(l, src);
+        if (lane == src) H &= H - 1u;
+        heap_sort_wave(SortView<unsigned, uint16_t>{nkey, nval}, f, l);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) e[r] = make_uint2(nv[r], nk[r]);
+      __syncthreads();
+      PROF_ADD(7, t_hs0);
+      break;
+    }
+    // __move_median_to_first(f, f + 1, mid, l - 1) for every partitioning range, through LDS
+#pragma unroll
+    for (int r = 0; r < R; ++r) own[r] = e[r];
+    __syncthreads();
+    {
+      unsigned H = S & AM;
+      while (H) {
+        const int r = __ffs(H) - 1;
+        H &= H - 1u;
+        const unsigned hi = S & ~((2u << r) - 1u);
+        const int f = p0 + r, l = hi ? p0 + __ffs(hi) - 1 : cl;
+        const int x = f + 1, y = f + (l - f) / 2, z = l - 1;
+        const uint2 ef = eb[pad(f)], ex = eb[pad(x)], ey = eb[pad(y)], ez = eb[pad(z)];
+        int s;
+        uint2 es;
+        if (ex.y < ey.y) {
+          if (ey.y < ez.y) { s = y; es = ey; }
+          else if (ex.y < ez.y) { s = z; es = ez; }
+          else { s = x; es = ex; }
+        } else if (ex.y < ez.y) { s = x; es = ex; }
+        else if (ey.y < ez.y) { s = z; es = ez; }
+        else { s = y; es = ey; }
+        eb[pad(f)] = es;
+        eb[pad(s)] = ef;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) e[r] = own[r];
+    // the stop flags against each range's pivot (the key now at its start)
+    unsigned lastKey = 0u;
+    {
+      const unsigned Sx = lv_opaque(S);
+#pragma unroll
+      for (int r = 0; r < R; ++r) lastKey = ((Sx >> r) & 1u) ? e[r].y : lastKey;
+    }
+    unsigned LF = 0u, RF = 0u;  // built top-down: bit r enters at bit 31 and moves down
+    {
+      const unsigned Sx = lv_opaque(S), Ax = lv_opaque(AM & ~S);
+      unsigned pv = (unsigned)__shfl((int)lastKey, jb);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        pv = ((Sx >> r) & 1u) ? e[r].y : pv;
+        const bool in = (Ax >> r) & 1u;  // partitioning, not the range's start
+        LF = (LF >> 1) | ((in && e[r].y >= pv) ? 0x80000000u : 0u);
+        RF = (RF >> 1) | ((in && e[r].y <= pv) ? 0x80000000u : 0u);
+        LV_SCHED();
+      }
+      LF >>= 32 - R;
+      RF >>= 32 - R;
+    }
+    // A(p) = #lf in (f, p), B(p) = #rf in (p, l): in-lane running counts, the lanes between from
+    // per-lane totals
+    const int tL = __popc(LF), tR = __popc(RF);
+    int PL, PR, TL, TR;
+    lv_lane_prefix(tL, PL, TL);
+    lv_lane_prefix(tR, PR, TR);
+    const int lastS = S ? p0 + 31 - __clz(S) : -1;
+    const int firstS = S ? p0 + __ffs(S) - 1 : 0;
+    const int tailL = S ? __popc(LF & ~((1u << (lastS - p0)) - 1u)) : tL;  // lf after the last start
+    const int headR = S ? __popc(RF & ((1u << (firstS - p0)) - 1u)) : tR;  // rf before the first start
+    int runA = __shfl(tailL - PL - tL, jb) + PL;                              // lf in (f, p0)
+    const int yb = __shfl(PR + headR, ja < 0 ? lane : ja);
+    int runB = (ja < 0 ? TR : yb) - PR - tR;                                  // rf in [p0 + R, l)
+    {
+      const unsigned Sx = lv_opaque(S), Lx = lv_opaque(LF);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {  // scratch: A
+        runA = ((Sx >> r) & 1u) ? 0 : runA;
+        e[r].x = __builtin_amdgcn_perm((unsigned)runA, e[r].x, 0x05040100u);  // x.lo | A << 16
+        runA += (int)((Lx >> r) & 1u);
+      }
+    }
+    // swaps: each swapped position writes itself to its pair's slot (buf is scratch now: every
+    // position is held in registers) and keeps the slot it reads back as scratch.  Branch-free:
+    // bitwise flags, both slots computed, one select each.
+    unsigned CM = 0u;  // cut candidates
+    {
+      const unsigned Sx = lv_opaque(S), Lx = lv_opaque(LF), Rx = lv_opaque(RF);
+      int l = clr;
+#pragma unroll
+      for (int r = R - 1; r >= 0; --r) {
+        const int f = first_of(Sx, r, cfr), A = (int)(e[r].x >> 16), B = runB;
+        runB += (int)((Rx >> r) & 1u);
+        runB = ((Sx >> r) & 1u) ? 0 : runB;
+        const int D = A - B;
+        const unsigned lf = (Lx >> r) & 1u, rf = (Rx >> r) & 1u;
+        const unsigned dneg = (unsigned)D >> 31, dpos = (unsigned)(-D) >> 31;  // D < 0, D > 0
+        const unsigned sw_l = lf & dneg, sw_r = rf & dpos;
+        CM = (CM << 1) | (lf & (dneg ^ 1u)) | sw_r;  // bit r after the remaining shifts
+        const int wl = p0 + (sw_l ? l - 1 - A : f + B), rl = p0 + (sw_l ? f + A : l - 1 - B);
+        const int w = (sw_l | sw_r) ? pad(wl) : dump;
+        const int rd = (sw_l | sw_r) ? pad(rl) : dump;
+        eb[w] = e[r];
+        e[r].x = __builtin_amdgcn_perm((unsigned)rd, e[r].x, 0x05040100u);  // x.lo | rd << 16
+        l = ((Sx >> r) & 1u) ? r : l;
+        LV_SCHED();
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const unsigned rd = e[r].x >> 16;
+      const uint2 x = eb[rd];
+      e[r] = rd != (unsigned)dump ? x : e[r];
+    }
+    __syncthreads();
+    // the cut of each range: its first candidate
+    const unsigned ctail = S ? (CM & ~((1u << (lastS - p0)) - 1u)) : CM;
+    const unsigned long long CT = __ballot(ctail != 0u);
+    unsigned seen = (CT & below & ~((1ull << jb) - 1ull)) != 0ull ? 1u : 0u;
+    unsigned cuts = 0u;
+    const unsigned Sx = lv_opaque(S);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      seen &= ~(Sx >> r) & 1u;
+      const unsigned c = (CM >> r) & 1u;
+      cuts = (cuts >> 1) | ((c & (seen ^ 1u)) << 31);
+      seen |= c;
+    }
+    S |= cuts >> (32 - R);
+  }
+  PROF_ADD(6, t_part0);
+  // __final_insertion_sort: the stable order by key inside each final range.  Ranges are ordered
+  // (every key of a range <= every key of the next), so the keys of other ranges within +-15 never
+  // count, and a range of > 16 positions (heap-sorted) is sorted already.  Keys are < 2^31 - 1 (the
+  // padding's 2^31 - 1 sorts last), so bit 31 of a - b is (a < b), without compare masks.
+  PROF_T(t_fin0);
+  int kp[15], kn[15];  // the previous lane's last 15 keys, the next lane's first 15
+#pragma unroll
+  for (int i = 0; i < 15; ++i) {
+    const int a = __shfl_up((int)e[R - 15 + i].y, 1);
+    const int b = __shfl_down((int)e[i].y, 1);
+    kp[i] = lane == 0 ? 0 : a;
+    kn[i] = lane == 63 ? 0x7fffffff : b;
+  }
+  __syncthreads();  // buf reads are done: nkey / nval take the output
+  // an opaque copy of p0: p0 + r here must not be shared with the loads before the loop (which
+  // would keep R positions live through it)
+  int p0o;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(p0o) : "v"(p0));
+  unsigned* nk = nkey + p0o;
+  uint16_t* nv = nval + p0o;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int kr = (int)e[r].y;
+    int pos = r;
+#pragma unroll
+    for (int d = 1; d <= 15; ++d) {
+      const int q = r - d, u = r + d;
+      const int kq = q >= 0 ? (int)e[q >= 0 ? q : 0].y : kp[q + 15 >= 0 ? q + 15 : 0];
+      const int ku = u < R ? (int)e[u < R ? u : 0].y : kn[u - R < 15 ? u - R : 0];
+      pos += (int)(((unsigned)ku - (unsigned)kr) >> 31) - (int)(((unsigned)kr - (unsigned)kq) >> 31);
+    }
+    LV_SCHED();
+    nk[pos] = (unsigned)kr;  // positions >= n keep their place (< 64 R <= RING_MAX)
+    nv[pos] = (uint16_t)e[r].x;
+  }
+  __syncthreads();
+  PROF_ADD(11, t_fin0);
+}
+
 struct ScanView {
   int M, VH;
   const float* curv;
@@ -2541,6 +2854,13 @@ LG_DEVICE float4 seg_point(const ScanView& v, int ind, int& status) {  // segmen
   return make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+LG_DEVICE unsigned* vx_key(ExtractLds& L) { return L.u.vkey; }
+LG_DEVICE uint16_t* vx_val(ExtractLds& L) { return L.vval; }
+template <int R>
+LG_DEVICE unsigned* vx_key(VoxLvlLds<R>& L) { return L.u.nat.key; }
+template <int R>
+LG_DEVICE uint16_t* vx_val(VoxLvlLds<R>& L) { return L.u.nat.val; }
+
 // PCL VoxelGrid<PointXYZI> (leaf 0.2) over the ring's lessFlat points (positions in L.vval[0..n)).
 // Ascending sort of n <= RING_MAX (key, val) pairs by (key, val), one wave, (key << 32 | val) in
 // registers.  vals are distinct ring positions appended in point order, so this is the order
@@ -2590,9 +2910,11 @@ LG_DEVICE void voxel_sort_stable(unsigned* key, uint16_t* val, int n) {
 // The ring's points are read in batches of VX_U a lane with every load of a batch issued before any is
 // used (a loop of single loads pays one memory latency per point); L.vval is the identity on entry.
 #define VX_U 8
-template <int kMode>
-LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, int n, int base_pos, RingOut& o) {
-  const float4* fa = v.fa + base_pos;  // L.vval holds positions relative to the ring start
+template <int kMode, class Lds>
+LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, Lds& L, int n, int base_pos, RingOut& o) {
+  unsigned* vkey = vx_key(L);
+  uint16_t* vval = vx_val(L);
+  const float4* fa = v.fa + base_pos;  // vval holds positions relative to the ring start
   const int lane = lane_id();
   o.nLF = 0;
   if (n == 0) return;
@@ -2616,7 +2938,7 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
   const long long dy = (long long)((mxy - mny) * inv) + 1;
   const long long dz = (long long)((mxz - mnz) * inv) + 1;
   if (dx * dy * dz > 2147483647ll) {  // PCL: "Integer indices would overflow" -> output = input
-    for (int t = lane; t < n; t += 64) o.lflat[t] = fa[L.vval[t]];
+    for (int t = lane; t < n; t += 64) o.lflat[t] = fa[vval[t]];
     o.nLF = n;
     o.status |= LEGO_ST_VOXEL_OVERFLOW;
     return;
@@ -2636,34 +2958,38 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, ExtractLds& L, i
       const int i0 = (int)(floorf(p.x * inv) - (float)minbx);
       const int i1 = (int)(floorf(p.y * inv) - (float)minby);
       const int i2 = (int)(floorf(p.z * inv) - (float)minbz);
-      if (t < n) L.u.vkey[t] = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+      if (t < n) vkey[t] = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
     }
   }
   __syncthreads();
   PROF_T(t_vs0);
-  if constexpr (kMode == 0) {
-    wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
+  if constexpr (kMode == 4) {
+    lvl_sort<16>(vkey, vval, L.u.buf, n);
+  } else if constexpr (kMode == 5) {
+    lvl_sort<32>(vkey, vval, L.u.buf, n);
+  } else if constexpr (kMode == 0) {
+    wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, true);
   } else if constexpr (kMode == 3) {
-    if (P.voxel_stable) voxel_sort_stable<3>(L.u.vkey, L.vval, n);
-    else wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);
+    if (P.voxel_stable) voxel_sort_stable<3>(vkey, vval, n);
+    else wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, true);
   } else {
-    voxel_sort_stable<kMode>(L.u.vkey, L.vval, n);
+    voxel_sort_stable<kMode>(vkey, vval, n);
   }
   PROF_ADD(5, t_vs0);
   int running = 0;
   for (int base = 0; base < n; base += 64) {
     const int t = base + lane;
-    const bool start = t < n && (t == 0 || L.u.vkey[t] != L.u.vkey[t - 1]);
+    const bool start = t < n && (t == 0 || vkey[t] != vkey[t - 1]);
     const unsigned long long m = __ballot(start);
     if (start) {  // CentroidPoint: float sums in sorted order; the run's loads VX_U at a time in flight
-      const unsigned k = L.u.vkey[t];
+      const unsigned k = vkey[t];
       int e = t + 1;
-      while (e < n && L.u.vkey[e] == k) ++e;
+      while (e < n && vkey[e] == k) ++e;
       float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
       for (int g = t; g < e; g += VX_U) {
         float4 pk[VX_U];
 #pragma unroll
-        for (int u = 0; u < VX_U; ++u) pk[u] = fa[L.vval[min(g + u, e - 1)]];
+        for (int u = 0; u < VX_U; ++u) pk[u] = fa[vval[min(g + u, e - 1)]];
 #pragma unroll
         for (int u = 0; u < VX_U; ++u)
           if (g + u < e) { sx += pk[u].x; sy += pk[u].y; sz += pk[u].z; si += pk[u].w; }
@@ -2931,10 +3257,13 @@ LG_DEVICE int lessflat_list(const ScanView& v, int st, int en, uint16_t* list) {
 // k_voxel: surfPointsLessFlatScan -> VoxelGrid (leaf 0.2) per ring, one wave per ring.  A kernel
 // of its own so the register-resident voxel sort's VGPRs do not cut k_extract's occupancy.
 // ============================================================================================
-// kMode as voxel_ring: 0 for voxel_tie_order 0; 1 and 2 split the stable order's rings by size.
+// kMode as voxel_ring: 0 for voxel_tie_order 0 by the stack emulation; 4 and 5 by the level-synchronous
+// one, split by ring size (each with its own register and LDS budget); 1 and 2 split the stable order's
+// rings by size; 3 either order.
 template <int kMode>
-__global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
-  __shared__ ExtractLds L;
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kMode == 5 ? 2 : kMode == 4 ? 3 : 1)))
+void k_voxel(LgParams P, LgBufs B) {
+  __shared__ std::conditional_t<kMode == 4, VoxLvlLds<16>, std::conditional_t<kMode == 5, VoxLvlLds<32>, ExtractLds>> L;
   const int V = P.V;
   const int b = blockIdx.x, sl = b / V, s = P.s0 + sl;
   const int ring = (b % V + sl / max(P.ncu / V, 1)) % V;  // ring rotation as in k_extract
@@ -2943,8 +3272,8 @@ __global__ __launch_bounds__(64) void k_voxel(LgParams P, LgBufs B) {
   ScanView v;
   v.fa = B.lf_stage + sb * P.H;  // the ring's lessFlat points, in surfPointsLessFlatScan order
   const int n = B.lf_count[sb];
-  if (kMode != 3 && (P.voxel_stable ? (n > 1024 ? 2 : 1) : 0) != kMode) return;
-  for (int t = lane_id(); t < n; t += 64) L.vval[t] = (uint16_t)t;
+  if (kMode != 3 && (P.voxel_stable ? (n > 1024 ? 2 : 1) : kMode >= 4 ? (n > 1024 ? 5 : 4) : 0) != kMode) return;
+  for (int t = lane_id(); t < n; t += 64) vx_val(L)[t] = (uint16_t)t;
   __syncthreads();
   RingOut o;
   o.lflat = B.r_lflat + sb * P.H;  // output half P.par too (k_publish of this scan reads it)
@@ -4087,9 +4416,13 @@ __device__ __attribute__((noinline)) int kd_nn1_nl(const KdView* K, const float*
 template <class Lds>
 __device__ __attribute__((noinline)) void kd_resolve_ties(Lds& L) {
   if (!L.kd_built) {
-    if (kd_build_nl(&L.kdv, L.kd_n, L.kd_box) < 0) return;  // (a build-stack overflow keeps the grid's lowest indices)
+    if (kd_build_nl(&L.kdv, L.kd_n, L.kd_box) < 0) {  // a build-stack overflow keeps the grid's lowest indices
+      if (lane_id() == 0) atomicOr(&L.status, LEGO_ST_TIE_UNRESOLVED);
+      return;
+    }
     if (lane_id() == 0) L.kd_built = 1;
   }
+  bool unres = false;
   for (int k0 = 0; k0 < L.ntie; k0 += 64) {
     const int k = k0 + lane_id();
     if (k < L.ntie) {
@@ -4097,8 +4430,10 @@ __device__ __attribute__((noinline)) void kd_resolve_ties(Lds& L) {
       bool ovf = false;
       const int c = kd_nn1_nl(&L.kdv, L.kd_box, L.sel[q], &ovf);
       if (!ovf) L.ind1[q] = c;  // (a stack overflow keeps the grid's lowest index)
+      unres |= ovf;
     }
   }
+  if (__ballot(unres) != 0ull && lane_id() == 0) atomicOr(&L.status, LEGO_ST_TIE_UNRESOLVED);
 }
 
 // one LM loop (surf or corner), <= 25 iterations.  The correspondence search (iterations 0, 5, 10,
@@ -4589,7 +4924,12 @@ int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   // off the SIMDs k_lm holds, which measured faster there.  With more scans than CUs the split
   // kernels (the common one at 83 VGPRs shares SIMDs with k_lm) measured faster: 245k vs 226k
   // scans/s at S = 512.
-  if (S <= P.ncu) {
+  static const bool legacy = std::getenv("LEGO_VOXEL_STACK_SORT") != nullptr;  // A/B: the stack emulation
+  if (!P.voxel_stable && !legacy) {
+    hipLaunchKernelGGL(k_voxel<4>, dim3(S * P.V), dim3(64), 0, st, P, B);
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_voxel<5>, dim3(S * P.V), dim3(64), 0, st, P, B);
+  } else if (S <= P.ncu) {
     hipLaunchKernelGGL(k_voxel<3>, dim3(S * P.V), dim3(64), 0, st, P, B);
   } else if (P.voxel_stable) {
     hipLaunchKernelGGL(k_voxel<1>, dim3(S * P.V), dim3(64), 0, st, P, B);
@@ -4798,6 +5138,16 @@ extern "C" int lego_test_libm_d(const double* h_a, const double* h_b, double* h_
   return rc;
 }
 
+template <int R>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R == 32 ? 2 : 3)))
+void k_sort_test_lvl(unsigned* keys, int* vals, int n) {  // as k_voxel<4 / 5>
+  __shared__ VoxLvlLds<R> L;
+  for (int i = lane_id(); i < n; i += 64) { L.u.nat.key[i] = keys[i]; L.u.nat.val[i] = (uint16_t)vals[i]; }
+  __syncthreads();
+  lvl_sort<R>(L.u.nat.key, L.u.nat.val, L.u.buf, n);
+  for (int i = lane_id(); i < n; i += 64) { keys[i] = L.u.nat.key[i]; vals[i] = L.u.nat.val[i]; }
+}
+
 __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int n, int is_float) {
   __shared__ ExtractLds L;
   const int lane = lane_id();
@@ -4818,8 +5168,11 @@ __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int
 }
 
 extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int32_t is_float) {
-  if (n < 0 || n > RING_MAX || !h_keys || !h_vals || is_float < 0 || is_float > 2) return LEGO_EINVAL;
+  if (n < 0 || n > RING_MAX || !h_keys || !h_vals || is_float < 0 || is_float > 3) return LEGO_EINVAL;
   if (is_float == 2 && n > SEG_MAX) return LEGO_EINVAL;
+  if (is_float == 3)
+    for (int i = 0; i < n; ++i)
+      if (h_keys[i] >= 0x7fffffffu || (uint32_t)h_vals[i] > 0xffffu) return LEGO_EINVAL;
   if (n == 0) return LEGO_OK;
   unsigned* k = nullptr;
   int* v = nullptr;
@@ -4829,7 +5182,9 @@ extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int3
   if (hipMemcpy(k, h_keys, n * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(v, h_vals, n * 4, hipMemcpyHostToDevice) != hipSuccess) rc = LEGO_EDEVICE;
   if (rc == LEGO_OK) {
-    hipLaunchKernelGGL(k_sort_test, dim3(1), dim3(64), 0, 0, k, v, n, is_float);
+    if (is_float == 3 && n > 1024) hipLaunchKernelGGL(k_sort_test_lvl<32>, dim3(1), dim3(64), 0, 0, k, v, n);
+    else if (is_float == 3) hipLaunchKernelGGL(k_sort_test_lvl<16>, dim3(1), dim3(64), 0, 0, k, v, n);
+    else hipLaunchKernelGGL(k_sort_test, dim3(1), dim3(64), 0, 0, k, v, n, is_float);
     if (hipGetLastError() != hipSuccess || hipMemcpy(h_keys, k, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(h_vals, v, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = LEGO_EDEVICE;
   }

@@ -659,7 +659,7 @@ LG_DEVICE QueryRow row_from_nb(bool is_corner, float4 ori, float4 sel, Trig T, c
 __device__ __attribute__((noinline)) void s2m_resolve_ties(const S2mScratch& Gc, const S2mScratch& Gs, GridInfo gc, GridInfo gs,
                                 const float4* cmap, int ncm, const float4* smap, int nsm, const float4* corner,
                                 const float4* surf, int nc, int ntie, const Trig& T, int* built, float* box,
-                                int max_map) {
+                                int max_map, int* status) {
   const int lane = lane_id();
   bool need0 = false, need1 = false;
   for (int k = lane; k < ntie; k += 64) {
@@ -710,7 +710,10 @@ __device__ __attribute__((noinline)) void s2m_resolve_ties(const S2mScratch& Gc,
         done = true;
       }
     }
-    if (!done) r = query_row(is_corner, ori, T, is_corner ? Gc : Gs, is_corner ? gc : gs, false);
+    if (!done) {  // the grid's order stands: not nanoflann's choice
+      r = query_row(is_corner, ori, T, is_corner ? Gc : Gs, is_corner ? gc : gs, false);
+      atomicOr(status, LEGO_S2M_ST_TIE_UNRESOLVED);
+    }
     Gc.rows[2 * q] = r.r0;
     Gc.rows[2 * q + 1] = r.r1;
   }
@@ -879,7 +882,7 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m(lego_s2m_io io, S2mScratch*
     if (L.ntie > 0) {  // (uniform)
       if (wave_id() == 0)
         s2m_resolve_ties(Gc, Gs, gc, gs, cmap, ncm, smap, nsm, corner, surf, nc, L.ntie, T, L.kd_built, &L.kd_box[0][0],
-                         max_map);
+                         max_map, &L.status);
       __syncthreads();
     }
     normal_equations(L, Gc.rows, nc + ns);
@@ -1021,7 +1024,7 @@ __global__ __launch_bounds__(S2M_THREADS) void k_s2m_solve(lego_s2m_io io, S2mSc
       s2m_resolve_ties(Gc, Gs, S->gc, S->gs, (const float4*)io.corner_map + io.corner_map_off[p], io.corner_map_n[p],
                        (const float4*)io.surf_map + io.surf_map_off[p], io.surf_map_n[p],
                        (const float4*)io.corner + io.corner_off[p], (const float4*)io.surf + io.surf_off[p],
-                       io.corner_n[p], ntie, T, S->kd_built, &S->kd_box[0][0], max_map);
+                       io.corner_n[p], ntie, T, S->kd_built, &S->kd_box[0][0], max_map, &S->status);
     }
     __syncthreads();
     if (tid == 0) S->ntie = 0;
@@ -1385,18 +1388,12 @@ struct lego_s2m {
   int wide_clouds = 0;
 };
 
-extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max_map_points, lego_s2m** out) {
-  if (!out) return LEGO_EINVAL;
-  *out = nullptr;
-  if (max_problems < 1 || max_map_points < 1 || max_map_points > LEGO_MAX_POINTS) return LEGO_EINVAL;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return LEGO_EDEVICE;
-  if (hipSetDevice(device) != hipSuccess) return LEGO_EDEVICE;
-  lego_s2m* m = new (std::nothrow) lego_s2m();
-  if (!m) return LEGO_ENOMEM;
-  m->device = device;
-  m->max_problems = max_problems;
-  m->max_map = max_map_points;
+// The LM's per-problem scratch (bucket tables, bucketed points, rows, nanoflann trees: ~200 B a map
+// point) is allocated on the first lego_s2m_run, so an engine used only for lego_map_transform /
+// lego_map_voxel (the mapper's VoxelGrid engine) never holds it.
+static int s2m_alloc_lm(lego_s2m* m) {
+  if (m->d_scratch) return LEGO_OK;
+  const int max_problems = m->max_problems, max_map_points = m->max_map;
   // per problem and map cloud: bucket table, points, indices
   const size_t tab = (size_t)(S2M_NB_MAX + 1) * 4, pts = (size_t)max_map_points * 16, idx = (size_t)max_map_points * 4;
   const size_t rows = (size_t)max_map_points * 32;
@@ -1407,16 +1404,15 @@ extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max
   const size_t kd_node = 2 * mp * sizeof(KdNode), kd_vind = mp * 4, kd_tmp = 2 * mp * 4, kd_frames = (10 * mp + S2M_KD_STACK) * 4,
                tieq = mp * 4;
   const size_t kd_per = 2 * (kd_node + kd_vind) + kd_tmp + kd_frames + tieq;
+  S2mScratch* d_scratch = nullptr;
   if (hipMalloc(&m->d_mem, per * 2 * max_problems) != hipSuccess ||
       hipMalloc(&m->d_kd, kd_per * max_problems) != hipSuccess ||
-      hipMalloc((void**)&m->d_scratch, sizeof(S2mScratch) * 2 * max_problems) != hipSuccess ||
-      hipMalloc((void**)&m->d_meta, 256) != hipSuccess ||
-      hipMalloc((void**)&m->d_state, sizeof(S2mState) * max_problems) != hipSuccess) {
-    lego_s2m_destroy(m);
+      hipMalloc((void**)&d_scratch, sizeof(S2mScratch) * 2 * max_problems) != hipSuccess) {
+    if (d_scratch) hipFree(d_scratch);
     return LEGO_ENOMEM;
   }
   S2mScratch* h = new (std::nothrow) S2mScratch[2 * max_problems];
-  if (!h) { lego_s2m_destroy(m); return LEGO_ENOMEM; }
+  if (!h) { hipFree(d_scratch); return LEGO_ENOMEM; }
   char* base = (char*)m->d_mem;
   for (int k = 0; k < 2 * max_problems; ++k) {
     char* b = base + per * k;
@@ -1431,9 +1427,30 @@ extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max
     h[k].kd_frames = (float*)(kb + 2 * (kd_node + kd_vind) + kd_tmp);
     h[k].tieq = (int*)(kb + 2 * (kd_node + kd_vind) + kd_tmp + kd_frames);
   }
-  const bool ok = hipMemcpy(m->d_scratch, h, sizeof(S2mScratch) * 2 * max_problems, hipMemcpyHostToDevice) == hipSuccess;
+  const bool ok = hipMemcpy(d_scratch, h, sizeof(S2mScratch) * 2 * max_problems, hipMemcpyHostToDevice) == hipSuccess;
   delete[] h;
-  if (!ok) { lego_s2m_destroy(m); return LEGO_EDEVICE; }
+  if (!ok) { hipFree(d_scratch); return LEGO_EDEVICE; }
+  m->d_scratch = d_scratch;
+  return LEGO_OK;
+}
+
+extern "C" int lego_s2m_create(int32_t device, int32_t max_problems, int32_t max_map_points, lego_s2m** out) {
+  if (!out) return LEGO_EINVAL;
+  *out = nullptr;
+  if (max_problems < 1 || max_map_points < 1 || max_map_points > LEGO_MAX_POINTS) return LEGO_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return LEGO_EDEVICE;
+  if (hipSetDevice(device) != hipSuccess) return LEGO_EDEVICE;
+  lego_s2m* m = new (std::nothrow) lego_s2m();
+  if (!m) return LEGO_ENOMEM;
+  m->device = device;
+  m->max_problems = max_problems;
+  m->max_map = max_map_points;
+  if (hipMalloc((void**)&m->d_meta, 256) != hipSuccess ||
+      hipMalloc((void**)&m->d_state, sizeof(S2mState) * max_problems) != hipSuccess) {
+    lego_s2m_destroy(m);
+    return LEGO_ENOMEM;
+  }
   *out = m;
   return LEGO_OK;
 }
@@ -1462,6 +1479,7 @@ extern "C" int lego_s2m_run(lego_s2m* m, int32_t n, const lego_s2m_io* io, void*
       !io->surf_map_n || !io->transform || !io->degenerate || !io->info)
     return LEGO_EINVAL;
   if (hipSetDevice(m->device) != hipSuccess) return LEGO_EDEVICE;
+  if (const int rc = s2m_alloc_lm(m)) return rc;
   hipStream_t st = (hipStream_t)hip_stream;
   const bool lat = m->layout == 1 || (m->layout < 0 && n <= S2M_LATENCY_MAX);
   if (!lat) {
@@ -1657,6 +1675,7 @@ extern "C" int lego_test_s2m_debug(lego_s2m* m, int32_t max_iters, int32_t p, in
   m->max_iters = max_iters;
   if (!nq) return LEGO_OK;
   if (hipSetDevice(m->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  if (!m->d_scratch) return LEGO_EINVAL;  // no lego_s2m_run yet: no rows
   S2mScratch g;
   if (hipMemcpy(&g, m->d_scratch + 2 * p, sizeof(g), hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(out, g.rows, (size_t)nq * 32, hipMemcpyDeviceToHost) != hipSuccess)

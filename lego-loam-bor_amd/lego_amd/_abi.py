@@ -24,8 +24,11 @@ ST_STALE_IND_OOB = 0x040
 ST_EMITTED = 0x080
 ST_VOXEL_OVERFLOW = 0x100
 ST_DEGEN_UB = 0x200
-# bits that mark reference undefined behaviour given defined behaviour here
-ST_UB_MASK = ST_STALE_TREE | ST_FWD_OOB | ST_STALE_IND_OOB | ST_DEGEN_UB  # (NN_TIE: resolved as nanoflann does)
+ST_TIE_UNRESOLVED = 0x400  # a 1-NN tie the device kd-tree could not resolve (stack overflow): not nanoflann's
+# bits that mark reference undefined behaviour given defined behaviour here, or a result not pinned to the
+# reference (NN_TIE alone is resolved as nanoflann does)
+ST_UB_MASK = ST_STALE_TREE | ST_FWD_OOB | ST_STALE_IND_OOB | ST_DEGEN_UB | ST_TIE_UNRESOLVED
+S2M_ST_TIE_UNRESOLVED = 0x20
 
 
 class LegoParams(C.Structure):

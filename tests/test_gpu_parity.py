@@ -278,6 +278,51 @@ def test_device_sort_matches_libstdcxx(gpu):
                     assert np.array_equal(gv, ev) and np.array_equal(gk, ek), ("adversary", n, c, mode)
 
 
+def test_device_level_sort_matches_libstdcxx(gpu):
+    """k_voxel's level-synchronous introsort (lego_test_sort mode 3, both register layouts: n <= 1024 and
+    n > 1024) gives libstdc++ std::sort's permutation: random keys of few / many distinct values, the
+    structured inputs, the introsort adversary (heap-sort fallbacks) and recorded VoxelGrid rings
+    (tools/data/voxel_keys_heavy.npz, one with a 1,309-key heap-sort fallback)."""
+    import subprocess
+    import tempfile
+    import oracle as O
+    rng = np.random.default_rng(11)
+    fp = C.POINTER
+    cases = []
+    for n in [0, 1, 2, 15, 16, 17, 33, 64, 65, 100, 300, 511, 512, 700, 1000, 1023, 1024, 1025, 1500, 1800, 2047,
+              2048]:
+        for distinct in [1, 2, 5, 40, 10 ** 6]:
+            cases.append(("rand", n, rng.integers(0, distinct, n)))
+    for n in [65, 129, 700, 1024, 1600, 2048]:
+        i = np.arange(n)
+        for name, keys in [("sorted", i), ("reverse", n - i), ("organ", np.minimum(i, n - i)), ("saw", i % 37),
+                           ("runs", i // 9), ("two", (i > n // 3).astype(np.int64)),
+                           ("spike", np.where(i == n // 2, 10 ** 6, 5)), ("runs_rev", (n - i) // 7)]:
+            cases.append((name, n, keys))
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "ia")
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-I" + os.path.join(REPO, "lego-loam-bor_amd", "csrc"),
+                               os.path.join(REPO, "tests", "native", "introsort_adversary.cpp"), "-o", exe])
+        for n in [100, 500, 700, 1024, 1025, 2048]:
+            for c in [1, 2]:
+                out = subprocess.run([exe, str(n), str(c)], stdout=subprocess.PIPE, universal_newlines=True, check=True)
+                cases.append(("adversary%d" % c, n, np.array(out.stdout.split(), dtype=np.int64)))
+    rec = np.load(os.path.join(REPO, "tools", "data", "voxel_keys_heavy.npz"))
+    for name in rec.files:
+        cases.append((name, len(rec[name]), rec[name].astype(np.int64)))
+    for name, n, keys in cases:
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        vals = np.arange(n, dtype=np.int32)
+        ek, ev = O.std_sort(keys, vals, 0)
+        gk, gv = keys.copy(), vals.copy()
+        assert L.lib().lego_test_sort(gk.ctypes.data_as(fp(C.c_uint32)), gv.ctypes.data_as(fp(C.c_int32)), n, 3) == 0
+        assert np.array_equal(gv, ev) and np.array_equal(gk, ek), (name, n)
+    # keys must stay below 2^31 - 1 (the padding key)
+    bad = np.array([5, 0x7fffffff], dtype=np.uint32)
+    assert L.lib().lego_test_sort(bad.ctypes.data_as(fp(C.c_uint32)), np.arange(2, dtype=np.int32).ctypes.data_as(
+        fp(C.c_int32)), 2, 3) != 0
+
+
 @pytest.mark.parametrize("fp_mode", [0, 1])
 @pytest.mark.parametrize("seq", [0, 7, 21])
 def test_vlp16_sequence_parity(gpu, seq, fp_mode):
