@@ -12,11 +12,15 @@ host, uploaded, and resident in HBM before the timed region.  Each rank owns its
 (weak scaling, no collective on the data path); after timing, the per-stream trajectories are
 all-gathered to rank 0 (RCCL), the only collective.  Rank 0 prints one JSON line.
 
-The measured path runs PCL VoxelGrid with voxel_tie_order = 1 (each voxel's points summed in point
-order) unless --voxel-tie-order 0 is given; order 0 reproduces the GCC/libstdc++-built reference bit
-for bit (its introsort tie order).  At N = 1 the other order is measured too on the same inputs and
-reported as "other_voxel_tie_order" (--no-alt-order skips it).  Labels, feature indices and the 6-DoF
-transform meet the north_star bar in both orders (tests/test_gpu_parity.py).
+The measured path runs PCL VoxelGrid with voxel_tie_order = 0: libstdc++ std::sort's permutation of
+equal leaf indices, bit-identical to the GCC-built reference (--voxel-tie-order 1: each voxel's points
+summed in point order, std::stable_sort's).  At N = 1 the other order is measured too on the same
+inputs and reported as "other_voxel_tie_order" (--no-alt-order skips it).
+
+The roofline pair's durations are reported twice: launched back to back (roofline.launch_ms, the
+kernels' own time) and inside the timed pipeline, where the previous scan's LM shares the CUs
+(roofline.in_pipeline: events around the two stages of every step of a third pass over the same
+steps, lego_batch_set_probe).
 
 The roofline pair (k_project + k_fa_prep4) is also timed at --roofline-streams scans per launch (2048:
 a working set far above the 256 MiB Infinity Cache) and reported beside the S-stream figure.
@@ -57,10 +61,10 @@ def parse():
                     help="projection / segmentation layout (lego_batch_set_wide): -1 automatic")
     ap.add_argument("--lag", type=int, default=1, choices=[0, 1],
                     help="pipeline depth (lego_batch_set_lag): 1 = a step runs the previous scan's LM")
-    ap.add_argument("--voxel-tie-order", type=int, default=1, choices=[0, 1],
-                    help="lego_params.voxel_tie_order of the measured path: 1 = VoxelGrid sums each voxel in "
-                         "point order (stable); 0 = libstdc++ std::sort order, bit-identical to the GCC-built "
-                         "reference. At N=1 the other order is measured too and reported beside the value.")
+    ap.add_argument("--voxel-tie-order", type=int, default=0, choices=[0, 1],
+                    help="lego_params.voxel_tie_order of the measured path: 0 = libstdc++ std::sort order, "
+                         "bit-identical to the GCC-built reference; 1 = VoxelGrid sums each voxel in point order "
+                         "(stable). At N=1 the other order is measured too and reported beside the value.")
     ap.add_argument("--no-alt-order", action="store_true",
                     help="skip measuring the other voxel_tie_order on the same inputs (N = 1)")
     ap.add_argument("--fp-mode", type=int, default=0, choices=[0, 1],
@@ -314,6 +318,17 @@ def main():
         alt = {"voxel_tie_order": alt_order, "value": round(total_scans / el_alt, 1),
                "ms_per_step": round(1e3 * el_alt / K, 3)}
 
+    # ---- the roofline pair inside the pipeline: the same steps again with events around k_project and
+    # k_fa_prep4 of every step (lego_batch_set_probe; not the timed pass, whose value stays event-free)
+    probe = None
+    if args.groups == 1 and args.lag == 1:
+        batch.reset()
+        batch.set_probe(True)
+        timed(batch)
+        p_ms, f_ms, p_steps = batch.probe_times()
+        batch.set_probe(False)
+        probe = (p_ms, f_ms, p_steps)
+
     # ---- per-stage kernel times (hipEvents on the launch stream), re-running the timed steps ------
     batch.reset()
     batch.set_timing(True)
@@ -357,6 +372,13 @@ def main():
                                "k_fa_prep4": {"bytes": int(b_smooth), "ms": round(stage[2], 4),
                                              "GBps": round(b_smooth / (stage[2] * 1e-3) / 1e9, 1)}},
                 "traffic_source": traffic_src,
+                "in_pipeline": None if probe is None else {
+                    "launch_ms": round(probe[0] + probe[1], 4), "project_ms": round(probe[0], 4),
+                    "fa_prep_ms": round(probe[1], 4), "steps": probe[2],
+                    "achieved": round((b_proj + b_smooth) / ((probe[0] + probe[1]) * 1e-3) / 1e9, 1),
+                    "frac": round((b_proj + b_smooth) / ((probe[0] + probe[1]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "source": "events around the projection and smoothness stages of every step of the "
+                              "overlap schedule (the previous scan's LM on the CUs), a pass over the timed steps"},
                 "note": ("%d scans per launch: working set below the 256 MiB Infinity Cache (cache-assisted)" % S
                          if b_proj + b_smooth < 256 * 2**20 else
                          "%d scans per launch: working set above the 256 MiB Infinity Cache" % S),

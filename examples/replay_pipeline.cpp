@@ -9,7 +9,8 @@
 // file.bag: a ROS bag v2.0; every sensor_msgs/PointCloud2 on `topic` (default /velodyne_points,
 // the reference's pointCloudTopic, utility.h:28) is decoded zero-copy (lego_rosbag.hpp) and replayed
 // in file order, as main.cpp:62-76 does with rosbag::View.
-// Prints one line per run: "cycles <n> status <bits> position x y z orientation x y z w".
+// Prints one line per run: "cycles <n> status <bits> position x y z orientation x y z w last <publishCloudsLast
+// publications> emitted <AssociationOut hand-offs>".
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -56,7 +57,7 @@ int main(int argc, char** argv) {
   Channel<ProjectionOut> projection_out_channel(true);
   Channel<AssociationOut> association_out_channel(mapping);  // main.cpp:38: blocking in rosbag mode
   Odometry odom;
-  int status = 0, cycles = 0, map_cycles = 0, keys = 0;
+  int status = 0, cycles = 0, map_cycles = 0, keys = 0, n_last = 0, n_emit = 0;
   Odometry aft;
   try {
     ImageProjection IP(params, projection_out_channel, device);
@@ -90,6 +91,8 @@ int main(int argc, char** argv) {
     odom = FA.last_odometry();
     status = FA.last_status();
     cycles = FA.cycles();
+    n_last = FA.clouds_last_published();
+    n_emit = FA.emitted();
     if (MO) {
       MO->finish();  // every AssociationOut FA sent has been through the mapping loop
       if (!MO->error().empty()) {
@@ -107,9 +110,9 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "error: %s\n", e.what());
     return 2;
   }
-  std::printf("cycles %d status %d position %.9g %.9g %.9g orientation %.9g %.9g %.9g %.9g\n", cycles, status,
-              odom.position[0], odom.position[1], odom.position[2], odom.orientation[0], odom.orientation[1],
-              odom.orientation[2], odom.orientation[3]);
+  std::printf("cycles %d status %d position %.9g %.9g %.9g orientation %.9g %.9g %.9g %.9g last %d emitted %d\n",
+              cycles, status, odom.position[0], odom.position[1], odom.position[2], odom.orientation[0],
+              odom.orientation[1], odom.orientation[2], odom.orientation[3], n_last, n_emit);
   if (mapping)
     std::printf("mapping cycles %d keys %d aft %.9g %.9g %.9g %.9g %.9g %.9g %.9g\n", map_cycles, keys, aft.position[0],
                 aft.position[1], aft.position[2], aft.orientation[0], aft.orientation[1], aft.orientation[2],

@@ -211,6 +211,13 @@ int  lego_batch_time_hbm_stages(lego_batch* b, int32_t reps, const lego_point* d
                                 void* hip_stream, float* ms_pair);
 /* While timing is enabled, steps run as one slice on the caller's stream (plus the VoxelGrid stream). */
 int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
+/* Measurement: while the probe is on, every overlap-schedule step records events around its projection
+ * (k_project / the wide projection) and around its smoothness stage (k_fa_prep4) on the step's stream;
+ * lego_batch_probe_times returns their mean durations inside the pipeline (ms2[0] projection, ms2[1]
+ * smoothness, over *steps steps; the concurrent LM of the previous scan included) and clears them.
+ * bench.py's in-pipeline roofline. */
+int  lego_batch_set_probe(lego_batch* b, int32_t enabled);
+int  lego_batch_probe_times(lego_batch* b, float* ms2, int32_t* steps);
 /* Split the streams into `groups` (1..LEGO_MAX_GROUPS) slices, each launched on its own internal HIP
  * stream (forked from and joined back into the step's stream), so one slice's long-tail kernels
  * overlap the others'.  Results do not depend on the grouping. */

@@ -25,6 +25,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdint>
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -124,6 +125,154 @@ inline lego_params vlp16_params() {
   return p;
 }
 
+// ---- Pieces shared by the classes below and the ROS node (ros/lego_nodes.cpp) ----------------------
+// Everything between a ROS message and the C-ABI that is not a field-by-field copy lives here, so the
+// ROS translation unit keeps only message conversion and publishing (tests/native/mirror_check.cpp,
+// tests/test_cpp_mirror.py).
+
+constexpr int kPointFieldFloat32 = 7;  // sensor_msgs::PointField::FLOAT32
+
+// fromROSMsg's x / y / z (imageProjection.cpp:159): the byte offsets of the float32 fields named x, y
+// and z in any container of fields with name / offset / datatype / count (sensor_msgs::PointField).
+// False when one is missing or the payload is big-endian.
+template <class Fields>
+bool xyz_offsets(const Fields& fields, bool big_endian, int& ox, int& oy, int& oz) {
+  ox = oy = oz = -1;
+  for (const auto& f : fields) {
+    if ((int)f.datatype != kPointFieldFloat32 || f.count != 1) continue;
+    if (f.name == "x") ox = (int)f.offset;
+    else if (f.name == "y") oy = (int)f.offset;
+    else if (f.name == "z") oz = (int)f.offset;
+  }
+  return ox >= 0 && oy >= 0 && oz >= 0 && !big_endian;
+}
+
+// A PointCloud2 payload as lego_cloud_handler takes it (width * height points of point_step bytes,
+// back to back): rows with padding (row_step > width * point_step) are packed into buf.
+inline const uint8_t* packed_rows(const uint8_t* data, uint32_t width, uint32_t height, uint32_t point_step,
+                                  uint32_t row_step, std::vector<uint8_t>& buf) {
+  const size_t row = (size_t)width * point_step;
+  if (height <= 1 || row_step == row) return data;
+  buf.resize(row * height);
+  for (uint32_t r = 0; r < height; ++r) std::memcpy(&buf[row * r], data + (size_t)row_step * r, row);
+  return buf.data();
+}
+
+// publishClouds' cloud_info (imageProjection.cpp:498-536) from the C-ABI's view into any type with the
+// cloud_info fields (cloud_msgs::cloud_info or CloudInfo): the per-point arrays either trimmed to the
+// segmented cloud or, as the reference's resetParameters leaves them (:137-139), V * H entries with a
+// zero tail.
+template <class Info>
+void fill_cloud_info(const lego_projection_out& o, int V, int VH, bool full, Info& s) {
+  s.startRingIndex.assign(o.start_ring_index, o.start_ring_index + V);
+  s.endRingIndex.assign(o.end_ring_index, o.end_ring_index + V);
+  s.startOrientation = o.start_orientation;
+  s.endOrientation = o.end_orientation;
+  s.orientationDiff = o.orientation_diff;
+  const int n = full ? VH : o.n_segmented;
+  s.segmentedCloudGroundFlag.assign(n, 0);
+  s.segmentedCloudColInd.assign(n, 0);
+  s.segmentedCloudRange.assign(n, 0);
+  for (int i = 0; i < o.n_segmented && i < n; ++i) {
+    s.segmentedCloudGroundFlag[i] = o.segmented_cloud_ground_flag[i] != 0;
+    s.segmentedCloudColInd[i] = o.segmented_cloud_col_ind[i];
+    s.segmentedCloudRange[i] = o.segmented_cloud_range[i];
+  }
+}
+
+// runFeatureAssociation's input (featureAssociation.cpp:1394-1407): a ProjectionOut's clouds and
+// cloud_info as the C-ABI's view (lego_feature_association_from).  False for a malformed cloud_info
+// (arrays shorter than the segmented cloud, ring indices shorter than V): the scan is dropped.
+template <class Info>
+bool projection_in(const lego_point* seg, int M, const lego_point* outl, int n_outlier, const lego_point* scan,
+                   int n_scan, const Info& si, int V, lego_projection_out& in) {
+  if ((int)si.segmentedCloudGroundFlag.size() < M || (int)si.segmentedCloudColInd.size() < M ||
+      (int)si.segmentedCloudRange.size() < M || (int)si.startRingIndex.size() < V || (int)si.endRingIndex.size() < V)
+    return false;
+  in.n_segmented = M;
+  in.n_outlier = n_outlier;
+  in.n_scan = n_scan;
+  in.segmented_cloud = seg;
+  in.outlier_cloud = outl;
+  in.scan_msg = scan;
+  in.start_ring_index = si.startRingIndex.data();
+  in.end_ring_index = si.endRingIndex.data();
+  in.start_orientation = si.startOrientation;
+  in.end_orientation = si.endOrientation;
+  in.orientation_diff = si.orientationDiff;
+  in.segmented_cloud_ground_flag = reinterpret_cast<const uint8_t*>(si.segmentedCloudGroundFlag.data());
+  in.segmented_cloud_col_ind = si.segmentedCloudColInd.data();
+  in.segmented_cloud_range = si.segmentedCloudRange.data();
+  in.label_mat = nullptr;
+  in.ground_mat = nullptr;
+  in.range_mat = nullptr;
+  return true;
+}
+
+// What one runFeatureAssociation cycle (featureAssociation.cpp:1408-1450) publishes after the GPU
+// association, from its status bits: the feature clouds always (:1410), nothing else on the
+// initialisation scan (checkSystemInitialization, :1413-1416), otherwise the odometry (:1422),
+// publishCloudsLast's clouds every skipFrameNum + 1-th time (:1362-1382, frameCount starting at
+// skipFrameNum = 1) and the AssociationOut on mapping cycles (:1431-1448, LEGO_ST_EMITTED).
+class FeatureAssociationCycle {
+ public:
+  struct Decision {
+    bool init, odometry, clouds_last, emit;
+  };
+  Decision next(int status) {
+    Decision d;
+    d.init = (status & LEGO_ST_INIT) != 0;
+    d.odometry = !d.init;
+    d.clouds_last = false;
+    if (!d.init && ++_frame_count >= kSkipFrameNum + 1) {
+      _frame_count = 0;
+      d.clouds_last = true;
+    }
+    d.emit = !d.init && (status & LEGO_ST_EMITTED) != 0;
+    return d;
+  }
+
+ private:
+  static constexpr int kSkipFrameNum = 1;  // featureAssociation.cpp:132
+  int _frame_count = kSkipFrameNum;
+};
+
+// runFeatureAssociation's loop (featureAssociation.cpp:1386-1450) over a Channel of ProjectionOut-like
+// items, for the C++ mirror and the ROS node alike.  The sink converts and publishes:
+//   bool end(const In&)                                  the destructor's empty item ends the loop
+//   bool view(const In&, lego_projection_out&)           the C-ABI view (projection_in); false: drop
+//   void dropped(const char* why, int rc)
+//   void features(const In&, const lego_association_out&)     publishClouds (:1410)
+//   void odometry(const In&, const lego_association_out&)     publishOdometry (:1422)
+//   void clouds_last(const In&, const lego_association_out&)  publishCloudsLast's publication (:1424)
+//   void emit(const In&, const lego_association_out&)         the AssociationOut hand-off (:1448)
+template <class In, class Chan, class Sink>
+void run_feature_association(lego_ctx* ctx, Chan& input, Sink& sink) {
+  FeatureAssociationCycle cycle;
+  while (true) {
+    In projection;
+    input.receive(projection);
+    if (sink.end(projection)) break;
+    lego_projection_out in;
+    if (!sink.view(projection, in)) {
+      sink.dropped("malformed cloud_info", LEGO_EINVAL);
+      continue;
+    }
+    lego_association_out o;
+    const int rc = lego_feature_association_from(ctx, &in, &o);
+    if (rc != LEGO_OK) {
+      sink.dropped("lego_feature_association_from", rc);
+      continue;
+    }
+    const FeatureAssociationCycle::Decision d = cycle.next(o.status);
+    sink.features(projection, o);
+    if (d.init) continue;
+    sink.odometry(projection, o);
+    if (d.clouds_last) sink.clouds_last(projection, o);
+    if (d.emit) sink.emit(projection, o);
+  }
+}
+
 class ImageProjection {
  public:
   ImageProjection(const lego_params& params, Channel<ProjectionOut>& output_channel, int device = 0)
@@ -144,16 +293,8 @@ class ImageProjection {
     out.segmented_cloud.assign(o.segmented_cloud, o.segmented_cloud + o.n_segmented);
     out.outlier_cloud.assign(o.outlier_cloud, o.outlier_cloud + o.n_outlier);
     out.scan_msg.assign(o.scan_msg, o.scan_msg + o.n_scan);
-    CloudInfo& ci = out.seg_msg;
-    ci.stamp = msg.stamp;
-    ci.startRingIndex.assign(o.start_ring_index, o.start_ring_index + _V);
-    ci.endRingIndex.assign(o.end_ring_index, o.end_ring_index + _V);
-    ci.startOrientation = o.start_orientation;
-    ci.endOrientation = o.end_orientation;
-    ci.orientationDiff = o.orientation_diff;
-    ci.segmentedCloudGroundFlag.assign(o.segmented_cloud_ground_flag, o.segmented_cloud_ground_flag + o.n_segmented);
-    ci.segmentedCloudColInd.assign(o.segmented_cloud_col_ind, o.segmented_cloud_col_ind + o.n_segmented);
-    ci.segmentedCloudRange.assign(o.segmented_cloud_range, o.segmented_cloud_range + o.n_segmented);
+    out.seg_msg.stamp = msg.stamp;
+    fill_cloud_info(o, _V, 0, false, out.seg_msg);
     _output_channel.send(std::move(out));
   }
 
@@ -167,7 +308,7 @@ class FeatureAssociation {
  public:
   FeatureAssociation(const lego_params& params, Channel<ProjectionOut>& input_channel,
                      Channel<AssociationOut>& output_channel, int device = 0)
-      : _input_channel(input_channel), _output_channel(output_channel) {
+      : _input_channel(input_channel), _output_channel(output_channel), _V(params.num_vertical_scans) {
     check(lego_ctx_create(&params, device, &_ctx), "lego_ctx_create (FeatureAssociation)");
     _run_thread = std::thread(&FeatureAssociation::runFeatureAssociation, this);
   }
@@ -192,70 +333,76 @@ class FeatureAssociation {
     std::lock_guard<std::mutex> g(_m);
     return _n;
   }
+  // publishCloudsLast publications and AssociationOut hand-offs so far
+  int clouds_last_published() {
+    std::lock_guard<std::mutex> g(_m);
+    return _n_last;
+  }
+  int emitted() {
+    std::lock_guard<std::mutex> g(_m);
+    return _n_emit;
+  }
   std::string error() {
     std::lock_guard<std::mutex> g(_m);
     return _error;
   }
 
  private:
-  void runFeatureAssociation() {  // featureAssociation.cpp:1386-1450
-    while (true) {
-      ProjectionOut projection;
-      _input_channel.receive(projection);
-      if (!projection.valid) break;
-      lego_projection_out in;
-      const CloudInfo& ci = projection.seg_msg;
-      in.n_segmented = (int32_t)projection.segmented_cloud.size();
-      in.n_outlier = (int32_t)projection.outlier_cloud.size();
-      in.n_scan = (int32_t)projection.scan_msg.size();
-      in.segmented_cloud = projection.segmented_cloud.data();
-      in.outlier_cloud = projection.outlier_cloud.data();
-      in.scan_msg = projection.scan_msg.data();
-      in.start_ring_index = ci.startRingIndex.data();
-      in.end_ring_index = ci.endRingIndex.data();
-      in.start_orientation = ci.startOrientation;
-      in.end_orientation = ci.endOrientation;
-      in.orientation_diff = ci.orientationDiff;
-      in.segmented_cloud_ground_flag = ci.segmentedCloudGroundFlag.data();
-      in.segmented_cloud_col_ind = ci.segmentedCloudColInd.data();
-      in.segmented_cloud_range = ci.segmentedCloudRange.data();
-      in.label_mat = nullptr;
-      in.ground_mat = nullptr;
-      in.range_mat = nullptr;
-      lego_association_out o;
-      const int rc = lego_feature_association_from(_ctx, &in, &o);
-      std::lock_guard<std::mutex> g(_m);
-      if (rc != LEGO_OK) {
-        _error = "lego_feature_association_from rc=" + std::to_string(rc);
-        continue;
-      }
-      _status = o.status;
-      ++_n;
-      if (o.status & LEGO_ST_INIT) continue;  // checkSystemInitialization: no odometry (:1414-1417)
-      _odom.stamp = ci.stamp;
-      for (int k = 0; k < 4; ++k) _odom.orientation[k] = o.odom_orientation[k];
-      for (int k = 0; k < 3; ++k) _odom.position[k] = o.odom_position[k];
-      if (o.status & LEGO_ST_EMITTED) {
-        AssociationOut out;
-        out.valid = true;
-        out.cloud_corner_last.assign(o.cloud_corner_last, o.cloud_corner_last + o.n_corner_last);
-        out.cloud_surf_last.assign(o.cloud_surf_last, o.cloud_surf_last + o.n_surf_last);
-        out.cloud_outlier_last.assign(o.cloud_outlier_last, o.cloud_outlier_last + o.n_outlier_last);
-        out.laser_odometry = _odom;
-        out.scan_msg = projection.scan_msg;
-        _output_channel.send(std::move(out));
-      }
+  struct Sink {  // this mirror's conversions: the clouds are std::vector<lego_point> already
+    FeatureAssociation& fa;
+    bool end(const ProjectionOut& p) { return !p.valid; }
+    bool view(const ProjectionOut& p, lego_projection_out& in) {
+      return projection_in(p.segmented_cloud.data(), (int)p.segmented_cloud.size(), p.outlier_cloud.data(),
+                           (int)p.outlier_cloud.size(), p.scan_msg.data(), (int)p.scan_msg.size(), p.seg_msg, fa._V, in);
     }
+    void dropped(const char* why, int rc) {
+      std::lock_guard<std::mutex> g(fa._m);
+      fa._error = std::string(why) + " rc=" + std::to_string(rc);
+    }
+    void features(const ProjectionOut&, const lego_association_out& o) {
+      std::lock_guard<std::mutex> g(fa._m);
+      fa._status = o.status;
+      ++fa._n;
+    }
+    void odometry(const ProjectionOut& p, const lego_association_out& o) {
+      std::lock_guard<std::mutex> g(fa._m);
+      fa._odom.stamp = p.seg_msg.stamp;
+      for (int k = 0; k < 4; ++k) fa._odom.orientation[k] = o.odom_orientation[k];
+      for (int k = 0; k < 3; ++k) fa._odom.position[k] = o.odom_position[k];
+    }
+    void clouds_last(const ProjectionOut&, const lego_association_out&) {
+      std::lock_guard<std::mutex> g(fa._m);
+      ++fa._n_last;
+    }
+    void emit(const ProjectionOut& p, const lego_association_out& o) {
+      AssociationOut out;
+      out.valid = true;
+      out.cloud_corner_last.assign(o.cloud_corner_last, o.cloud_corner_last + o.n_corner_last);
+      out.cloud_surf_last.assign(o.cloud_surf_last, o.cloud_surf_last + o.n_surf_last);
+      out.cloud_outlier_last.assign(o.cloud_outlier_last, o.cloud_outlier_last + o.n_outlier_last);
+      {
+        std::lock_guard<std::mutex> g(fa._m);
+        out.laser_odometry = fa._odom;
+        ++fa._n_emit;
+      }
+      out.scan_msg = p.scan_msg;
+      fa._output_channel.send(std::move(out));
+    }
+  };
+  void runFeatureAssociation() {  // featureAssociation.cpp:1386-1450
+    Sink sink{*this};
+    run_feature_association<ProjectionOut>(_ctx, _input_channel, sink);
   }
 
   lego_ctx* _ctx = nullptr;
   Channel<ProjectionOut>& _input_channel;
   Channel<AssociationOut>& _output_channel;
+  int _V;
   std::thread _run_thread;
   std::mutex _m;
   Odometry _odom;
   int _status = 0;
-  int _n = 0;
+  int _n = 0, _n_last = 0, _n_emit = 0;
   std::string _error;
 };
 

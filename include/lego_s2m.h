@@ -23,6 +23,16 @@
  * calls on different streams must be ordered by the caller, as the reference's single mapping
  * thread orders them.  There is no CPU fallback: without a usable HIP device
  * lego_s2m_create returns LEGO_EDEVICE.
+ *
+ * libm model: the mapping half implements lego_params.fp_mode 0 only (GCC >= 6 builds of the reference:
+ * mapOptmization.cpp's unqualified sin / cos / sqrt on floats resolve to the float overloads).  k_s2m's
+ * pointAssociateToMap / LMOptimization trig and sqrt(sqrt(.)) weights, transformPointCloud
+ * (lego_map_transform) and transformAssociateToMap (lego_map_associate, lego_mapper_step) run the float
+ * libm (glibc's sinf / cosf / asinf / atan2f restated); none of these entry points takes an fp_mode.  A
+ * front end configured with fp_mode 1 (the GCC 4.8 / 5 double-overload model) feeding this mapping half
+ * is therefore a mixed model: its scan-to-map results stay within the scan-to-map bar of a GCC >= 6
+ * reference, not bit-identical to a GCC 4.8 / 5 one.  tests/test_s2m_cpu.py
+ * (test_mapping_half_is_fp_mode_0) pins this.
  */
 #ifndef LEGO_S2M_H
 #define LEGO_S2M_H
@@ -84,8 +94,11 @@ int  lego_s2m_run_host(lego_s2m* m, const lego_point* corner, int32_t n_corner, 
  *                       of :909-913 / :982-986);
  *   lego_map_voxel      pcl::VoxelGrid<PointXYZI>::filter (PCL 1.7/1.8 applyFilter; leaves :71-78) of
  *                       cloud c with leaf[c]: one centroid per occupied leaf in ascending leaf order,
- *                       each the float sum of its points in input order (std::stable_sort's tie order,
- *                       lego_params.voxel_tie_order = 1) divided by their count.  status[c] =
+ *                       each the float sum of its points in the order of PCL's std::sort of the (leaf
+ *                       index, point index) pairs (voxel_tie_order 0, the default: libstdc++'s introsort
+ *                       permutation, bit-identical to the reference) or, after
+ *                       lego_s2m_set_voxel_tie_order(m, 1), in input order (std::stable_sort's) divided
+ *                       by their count.  status[c] =
  *                       LEGO_ST_VOXEL_OVERFLOW when the leaf indices would overflow int32 (PCL's warning
  *                       path: the cloud is copied unfiltered).  Clouds hold at most max_map_points
  *                       points (larger: out_n = -1). */
@@ -105,6 +118,11 @@ int  lego_map_transform(lego_s2m* m, int32_t n, const lego_map_transform_io* io,
 /* scratch for the call's n clouds of max_map_points each is allocated on first use (and regrown for a
  * larger n, after a device synchronize) */
 int  lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* io, void* hip_stream);
+/* lego_map_voxel's tie order, as lego_params.voxel_tie_order: 0 (default) libstdc++ std::sort's
+ * permutation (PCL's applyFilter, the reference: a level-synchronous introsort emulation, which
+ * synchronizes hip_stream once per level of ranges longer than 2,048 points), 1 std::stable_sort's
+ * (rocPRIM radix sort, asynchronous). */
+int  lego_s2m_set_voxel_tie_order(lego_s2m* m, int32_t order);
 
 /* ---- MapOptimization's loop body (loop closure off: loam_config.yaml:24) --------------------------------
  * One mapping sequence: MapOptimization::run (mapOptmization.cpp:1521-1570) per AssociationOut, with the
@@ -129,6 +147,8 @@ int  lego_mapper_step(lego_mapper* m, const lego_point* corner_last, int32_t n_c
                       float* transform_aft_mapped, int32_t* info);
 /* key poses so far, (roll, pitch, yaw, x, y, z) each (cloudKeyPoses6D); *n = their count */
 int  lego_mapper_key_poses(const lego_mapper* m, float* out, int32_t cap, int32_t* n);
+/* the tie order of the mapper's VoxelGrids (lego_s2m_set_voxel_tie_order): 0 (default) the reference's */
+int  lego_mapper_set_voxel_tie_order(lego_mapper* m, int32_t order);
 /* Launch layout of lego_s2m_run: 0 = one 1024-thread workgroup a problem (throughput: hundreds of
  * problems), 1 = latency (a problem's grids built by two workgroups, each LM iteration's queries spread
  * over up to 256 / n workgroups, normal equations and solve in one; 21 launches), -1 (default) = latency

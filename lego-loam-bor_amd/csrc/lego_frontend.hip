@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cstdlib>
 #include <new>
 #include <vector>
 
@@ -187,6 +188,13 @@ struct lego_batch {
   bool pend_ovl = false;     // the pending work belongs to the overlap schedule
   hipStream_t ls = nullptr;
   hipEvent_t ev_pub = nullptr, ev_ls = nullptr, ev_fe = nullptr;
+  // Probe (lego_batch_set_probe): events around k_project and around k_fa_prep in the overlap
+  // schedule, four per step, so the HBM-bound pair's durations inside the pipeline can be read
+  // (lego_batch_probe_times) beside the back-to-back figure of lego_batch_time_hbm_stages.
+  bool probe = false;
+  std::vector<hipEvent_t> pev;
+  int probe_n = 0;
+  hipEvent_t* probe_cur = nullptr;  // this step's four events while it is being enqueued
   // pinned host mirrors for lego_batch_read / the single-context outputs
   Pinned h_seg, h_out, h_scan, h_sharp, h_lsharp, h_flat, h_lflat, h_clast, h_slast, h_olast;
   Pinned h_rs, h_re, h_label, h_sharp_ind, h_lsharp_ind, h_flat_ind, h_gflag, h_col, h_range_seg, h_range, h_ground;
@@ -197,6 +205,7 @@ struct lego_batch {
     for (void* p : owned) hipFree(p);
     if (events)
       for (int i = 0; i < 8; ++i) hipEventDestroy(ev[i]);
+    for (hipEvent_t e : pev) hipEventDestroy(e);
     for (int g = 0; g < LEGO_MAX_GROUPS; ++g) {
       if (gs[g]) hipStreamDestroy(gs[g]);
       if (join[g]) hipEventDestroy(join[g]);
@@ -435,8 +444,10 @@ static int run_projection(lego_batch* b, const float4* pts, const int64_t* offs,
                           int s0, int n) {
   LgParams P = b->P;
   P.s0 = s0;
+  if (b->probe_cur) hipEventRecord(b->probe_cur[0], st);
   int rc = lg_launch_project(P, b->B, n, pts, offs, cnts, st);
   if (rc) return rc;
+  if (b->probe_cur) hipEventRecord(b->probe_cur[1], st);
   if (b->timing) hipEventRecord(b->ev[1], st);
   rc = lg_launch_segment(P, b->B, n, st);
   if (rc) return rc;
@@ -553,7 +564,9 @@ static int run_association_ovl(lego_batch* b, hipStream_t st, bool wait_pub) {
   P.s0 = 0;
   P.epoch = b->epoch;
   P.par = b->par;
+  if (b->probe_cur) hipEventRecord(b->probe_cur[2], st);
   int rc = lg_launch_fa_prep(P, b->B, b->S, st, false);
+  if (b->probe_cur) hipEventRecord(b->probe_cur[3], st);
   if (!rc) rc = lg_launch_extract(P, b->B, b->S, st);
   if (rc) return rc;
   if (wait_pub && hipStreamWaitEvent(st, b->ev_pub, 0) != hipSuccess) return LEGO_EDEVICE;
@@ -657,6 +670,14 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   if (ovl) {
     rc = ensure_ls(b);
     if (rc) return rc;
+    if (b->probe) {  // four events of this step (lego_batch_probe_times)
+      while ((int)b->pev.size() < 4 * (b->probe_n + 1)) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return LEGO_EDEVICE;
+        b->pev.push_back(e);
+      }
+      b->probe_cur = &b->pev[4 * b->probe_n++];
+    }
     const bool pub_now = b->pend_pub;
     // With the stable VoxelGrid order, k_lm(k-1) starts after this scan's projection and segmentation:
     // those whole-CU kernels (k_project 124 KB, k_segment_lds 115 KB of LDS) then get the CUs first
@@ -665,7 +686,8 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     // 248-250k -> 265k scans/s.  With the reference's introsort order the heavier k_voxel(k) then
     // meets k_lm(k-1) head-on (193k -> 167-177k scans/s), so that order keeps k_lm at the top too
     // (where the measured variants are listed).
-    const bool lm_after_fe = b->P.voxel_stable;
+    static const int sched_env = std::getenv("LEGO_SCHED_LM_AFTER_FE") ? std::atoi(std::getenv("LEGO_SCHED_LM_AFTER_FE")) : -1;
+    const bool lm_after_fe = sched_env >= 0 ? sched_env != 0 : b->P.voxel_stable;  // (A/B override)
     if (b->pend_pub) {  // publish(k-2) on ls, after its k_voxel (issue_publish waits for ev_vox)
       rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
       if (!rc && hipEventRecord(b->ev_pub, b->ls) != hipSuccess) rc = LEGO_EDEVICE;
@@ -693,6 +715,7 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     b->pend_ovl = true;
     b->last_par = b->par;
     b->par ^= 1;
+    b->probe_cur = nullptr;
     return LEGO_OK;
   }
   if (G <= 1) {
@@ -713,6 +736,33 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   }
   if (rc) return rc;
   advance_pipeline(b, lag, G);
+  return LEGO_OK;
+}
+
+int lego_batch_set_probe(lego_batch* b, int32_t enabled) {
+  if (!b) return LEGO_EINVAL;
+  b->probe = enabled != 0;
+  b->probe_n = 0;
+  return LEGO_OK;
+}
+
+int lego_batch_probe_times(lego_batch* b, float* ms2, int32_t* steps) {
+  if (!b || !ms2 || !steps) return LEGO_EINVAL;
+  hipSetDevice(b->device);
+  double a = 0.0, f = 0.0;
+  for (int k = 0; k < b->probe_n; ++k) {
+    hipEvent_t* e = &b->pev[4 * k];
+    float x = 0.f, y = 0.f;
+    if (hipEventSynchronize(e[3]) != hipSuccess || hipEventElapsedTime(&x, e[0], e[1]) != hipSuccess ||
+        hipEventElapsedTime(&y, e[2], e[3]) != hipSuccess)
+      return LEGO_EDEVICE;
+    a += x;
+    f += y;
+  }
+  *steps = b->probe_n;
+  ms2[0] = b->probe_n ? (float)(a / b->probe_n) : 0.f;
+  ms2[1] = b->probe_n ? (float)(f / b->probe_n) : 0.f;
+  b->probe_n = 0;
   return LEGO_OK;
 }
 

@@ -188,6 +188,7 @@ struct lego_mapper {
   float t_sum[6] = {0}, t_tobe[6] = {0}, t_bef[6] = {0}, t_aft[6] = {0};
   float prev_pos[3] = {0, 0, 0};
   int degenerate = 0;
+  int voxel_tie_order = 0;  // the VoxelGrids' tie order (lego_mapper_set_voxel_tie_order)
 };
 
 extern "C" void lego_mapper_destroy(lego_mapper* m) {
@@ -205,8 +206,8 @@ extern "C" void lego_mapper_destroy(lego_mapper* m) {
 
 namespace {
 // an s2m engine (LM or VoxelGrid) for clouds of at least `need` points: recreated larger when needed
-int ensure_engine(int device, lego_s2m** e, int* cap, int64_t need) {
-  if (need <= *cap && *e) return LEGO_OK;
+int ensure_engine(int device, lego_s2m** e, int* cap, int64_t need, int voxel_tie_order = 0) {
+  if (need <= *cap && *e) return lego_s2m_set_voxel_tie_order(*e, voxel_tie_order);
   if (need > LEGO_MAX_POINTS) return LEGO_EINVAL;
   const int64_t nc = std::min<int64_t>(LEGO_MAX_POINTS, std::max<int64_t>(need, 2 * (int64_t)*cap));
   if (*e) {
@@ -218,7 +219,7 @@ int ensure_engine(int device, lego_s2m** e, int* cap, int64_t need) {
   const int rc = lego_s2m_create(device, 1, (int32_t)nc, e);
   if (rc != LEGO_OK) return rc;
   *cap = (int)nc;
-  return LEGO_OK;
+  return lego_s2m_set_voxel_tie_order(*e, voxel_tie_order);
 }
 int ensure_parts(lego_mapper* m, size_t np) {  // part lists of np parts (and >= 8 VoxelGrid clouds)
   np = std::max<size_t>(np, 8);
@@ -245,7 +246,7 @@ extern "C" int lego_mapper_create(int32_t device, int32_t max_map_points, int64_
     return LEGO_EDEVICE;
   }
   int rc = ensure_engine(device, &m->s2m, &m->lm_cap, max_map_points);
-  if (rc == LEGO_OK) rc = ensure_engine(device, &m->vox, &m->vox_cap, 2 * (int64_t)max_map_points);
+  if (rc == LEGO_OK) rc = ensure_engine(device, &m->vox, &m->vox_cap, 2 * (int64_t)max_map_points, m->voxel_tie_order);
   if (rc != LEGO_OK) {
     lego_mapper_destroy(m);
     return rc;
@@ -266,6 +267,12 @@ extern "C" int lego_mapper_create(int32_t device, int32_t max_map_points, int64_
 // OdometryToTransform (utility.h:96-110): the mapping thread's transformSum from the odometry message,
 // through tf::Matrix3x3(tf::Quaternion(q.z, -q.x, -q.y, q.w)).getRPY (tf/LinearMath/Matrix3x3.h:
 // setRotation, getEulerYPR with solution 1) in double, then transform = (-pitch, -yaw, roll, position).
+extern "C" int lego_mapper_set_voxel_tie_order(lego_mapper* m, int32_t order) {
+  if (!m || order < 0 || order > 1) return LEGO_EINVAL;
+  m->voxel_tie_order = order;
+  return m->vox ? lego_s2m_set_voxel_tie_order(m->vox, order) : LEGO_OK;
+}
+
 extern "C" int lego_map_odometry_to_transform(const double* orientation, const double* position, float* transform) {
   if (!orientation || !position || !transform) return LEGO_EINVAL;
   const double qx = orientation[2], qy = -orientation[0], qz = -orientation[1], qw = orientation[3];
@@ -387,7 +394,7 @@ extern "C" int lego_mapper_step(lego_mapper* m, const lego_point* corner_last, i
   const int64_t big = std::max<int64_t>(std::max<int64_t>(ncm, nsm), (int64_t)n_corner + n_surf + n_outlier);
   if ((rc = grow(&m->d_raw, (size_t)n_raw, &m->raw_cap, 0)) || (rc = grow(&m->d_vox, (size_t)n_raw, &m->vox_buf_cap, 0)) ||
       (rc = grow(&m->d_tot, (size_t)2 * (n_surf + n_outlier), &m->tot_cap, 0)) ||
-      (rc = ensure_engine(m->device, &m->vox, &m->vox_cap, big)))
+      (rc = ensure_engine(m->device, &m->vox, &m->vox_cap, big, m->voxel_tie_order)))
     return rc;
   // the scan's clouds after the map's
   if (n_corner) MCHECK(hipMemcpy(m->d_raw + base_sc, corner_last, (size_t)n_corner * sizeof(lego_point), hipMemcpyHostToDevice));

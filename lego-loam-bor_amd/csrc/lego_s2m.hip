@@ -31,6 +31,7 @@
 #include "../../include/lego_s2m.h"
 #include "lego_device.h"
 #include "lego_kdtree.h"
+#include "lego_wavesort.h"  // lvl_sort / heap_sort_wave: the map clouds' std::sort order
 
 using namespace lg;
 
@@ -1357,6 +1358,227 @@ __global__ __launch_bounds__(S2M_THREADS) void k_vxf_emit(lego_map_voxel_io io, 
   out[slot] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
 }
 
+// ---- VoxelGrid with PCL's std::sort tie order (voxel_tie_order 0) for map clouds -----------------------
+// libstdc++'s introsort over every cloud's (leaf index, point index) pairs, as the front end's VoxelGrid
+// (lego_wavesort.h: lvl_sort) but device-wide while ranges are large: all ranges of a recursion level
+// longer than VXS_SMALL are partitioned together, a range in chunks of VXS_CH positions (k_vxs_*), each
+// Hoare stop's rank from per-chunk counts; ranges of at most VXS_SMALL positions then finish on one wave
+// each with lvl_sort from their own depth limit (k_vxs_small), ranges still longer than VXS_SMALL at depth
+// 0 take the heap sort (k_vxs_heap).  The pairs are sorted in place in m->d_keys / d_vals.
+constexpr int VXS_SMALL = 2048;       // ranges finished by one wave (lvl_sort<32>)
+constexpr int VXS_TPB = 256;          // threads per chunk block
+constexpr int VXS_EPT = 16;           // positions per thread
+constexpr int VXS_CH = VXS_TPB * VXS_EPT;
+
+struct VxsSeg {  // a range [f, l) of the key arrays at depth limit d
+  int f, l, d;
+};
+
+// grid (big ranges): __move_median_to_first(f, f + 1, mid, l - 1); the pivot key; the cut reset to l
+__global__ __launch_bounds__(64) void k_vxs_median(const VxsSeg* segs, const int* nseg, unsigned* keys,
+                                                    unsigned* vals, unsigned* pivot, int* cut) {
+  const int s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= *nseg) return;
+  const VxsSeg g = segs[s];
+  const int x = g.f + 1, y = g.f + (g.l - g.f) / 2, z = g.l - 1;
+  const unsigned kx = keys[x], ky = keys[y], kz = keys[z];
+  int sel;
+  if (kx < ky) sel = ky < kz ? y : (kx < kz ? z : x);
+  else sel = kx < kz ? x : (ky < kz ? z : y);
+  const unsigned kf = keys[g.f], vf = vals[g.f], ks = keys[sel], vs = vals[sel];
+  keys[g.f] = ks; vals[g.f] = vs;
+  keys[sel] = kf; vals[sel] = vf;
+  pivot[s] = ks;
+  cut[s] = g.l;
+}
+
+// Block-wide exclusive scan of a packed (lf | rf << 16) count per thread (VXS_TPB threads).
+LG_DEVICE int vxs_block_scan(int v, int* sh, int& total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int k = 0; k < VXS_TPB / 64; ++k) {
+    if (k < w) off += sh[k];
+    tot += sh[k];
+  }
+  __syncthreads();
+  total = tot;
+  return off + x - v;
+}
+
+// the stop flags of position p of range g (p > f) against pivot pv: lf | rf << 16
+LG_DEVICE int vxs_flags(unsigned k, unsigned pv) { return (k >= pv ? 1 : 0) | ((k <= pv ? 1 : 0) << 16); }
+
+// grid (chunks, big ranges): per chunk the counts of left / right stops (packed lf | rf << 16)
+__global__ __launch_bounds__(VXS_TPB) void k_vxs_count(const VxsSeg* segs, const int* nseg, const unsigned* keys,
+                                                       const unsigned* pivot, int* cnt, int maxch) {
+  __shared__ int sh[VXS_TPB / 64];
+  const int s = blockIdx.y, c = blockIdx.x;
+  if (s >= *nseg) return;
+  const VxsSeg g = segs[s];
+  const int c0 = g.f + c * VXS_CH;
+  if (c0 >= g.l) return;
+  const unsigned pv = pivot[s];
+  int v = 0;
+  const int p0 = c0 + threadIdx.x * VXS_EPT;
+#pragma unroll
+  for (int e = 0; e < VXS_EPT; ++e) {
+    const int p = p0 + e;
+    if (p > g.f && p < g.l) v += vxs_flags(keys[p], pv);
+  }
+  int total;
+  vxs_block_scan(v, sh, total);
+  if (threadIdx.x == 0) cnt[(size_t)s * maxch + c] = total;
+}
+
+// grid (chunks, big ranges): each stop's rank, Hoare's swaps through the scratch slots (f + k for the
+// k-th right stop, l - 1 - k for the k-th left stop), the read-back slot of every swapped position and
+// the cut (the first left stop with D >= 0 or right stop with D > 0)
+__global__ __launch_bounds__(VXS_TPB) void k_vxs_exchange(const VxsSeg* segs, const int* nseg, const unsigned* keys,
+                                                          const unsigned* vals, const unsigned* pivot, const int* cnt,
+                                                          int maxch, unsigned* xk, unsigned* xv, int* rds, int* cut) {
+  __shared__ int sh[VXS_TPB / 64];
+  const int s = blockIdx.y, c = blockIdx.x;
+  if (s >= *nseg) return;
+  const VxsSeg g = segs[s];
+  const int c0 = g.f + c * VXS_CH;
+  if (c0 >= g.l) return;
+  const unsigned pv = pivot[s];
+  const int nch = (g.l - g.f + VXS_CH - 1) / VXS_CH;
+  int before = 0, totR = 0;  // stops of the chunks before this one; right stops of the whole range
+  for (int q = 0; q < nch; ++q) {
+    const int t = cnt[(size_t)s * maxch + q];
+    if (q < c) before += t;
+    totR += t >> 16;
+  }
+  const int p0 = c0 + threadIdx.x * VXS_EPT;
+  unsigned k[VXS_EPT];
+  int v = 0;
+#pragma unroll
+  for (int e = 0; e < VXS_EPT; ++e) {
+    const int p = p0 + e;
+    k[e] = (p > g.f && p < g.l) ? keys[p] : 0u;
+    if (p > g.f && p < g.l) v += vxs_flags(k[e], pv);
+  }
+  int total;
+  int run = vxs_block_scan(v, sh, total) + before;  // lf | rf << 16 in (f, p)
+  int best = 0x7fffffff;
+#pragma unroll
+  for (int e = 0; e < VXS_EPT; ++e) {
+    const int p = p0 + e;
+    if (!(p > g.f && p < g.l)) continue;
+    const int fl = vxs_flags(k[e], pv);
+    const int A = run & 0xffff;                        // left stops in (f, p)
+    const int B = totR - (run >> 16) - (fl >> 16);     // right stops in (p, l)
+    run += fl;
+    const bool lf = fl & 1, rf = fl >> 16;
+    const int D = A - B;
+    int rd = -1;
+    if (lf && D < 0) {
+      xk[g.l - 1 - A] = k[e]; xv[g.l - 1 - A] = vals[p];
+      rd = g.f + A;
+    } else if (rf && D > 0) {
+      xk[g.f + B] = k[e]; xv[g.f + B] = vals[p];
+      rd = g.l - 1 - B;
+    }
+    rds[p] = rd;
+    if ((lf && D >= 0) || (rf && D > 0)) best = min(best, p);
+  }
+  for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o));
+  if ((threadIdx.x & 63) == 0 && best != 0x7fffffff) atomicMin(&cut[s], best);
+}
+
+// grid (chunks, big ranges): swapped positions take their pair's element
+__global__ __launch_bounds__(VXS_TPB) void k_vxs_readback(const VxsSeg* segs, const int* nseg, unsigned* keys,
+                                                          unsigned* vals, const unsigned* xk, const unsigned* xv,
+                                                          const int* rds) {
+  const int s = blockIdx.y, c = blockIdx.x;
+  if (s >= *nseg) return;
+  const VxsSeg g = segs[s];
+  const int c0 = g.f + c * VXS_CH;
+  if (c0 >= g.l) return;
+  const int p0 = c0 + threadIdx.x * VXS_EPT;
+#pragma unroll
+  for (int e = 0; e < VXS_EPT; ++e) {
+    const int p = p0 + e;
+    if (p > g.f && p < g.l) {
+      const int rd = rds[p];
+      if (rd >= 0) { keys[p] = xk[rd]; vals[p] = xv[rd]; }
+    }
+  }
+}
+
+// grid (big ranges): the two sub-ranges [f, cut) and [cut, l) at depth d - 1: longer than VXS_SMALL into
+// the next level's list (or, at depth 0, the heap-sort list), the others into the small list
+__global__ __launch_bounds__(64) void k_vxs_split(const VxsSeg* segs, const int* nseg, const int* cut, VxsSeg* next,
+                                                  int* nnext, VxsSeg* small, int* nsmall, VxsSeg* heap, int* nheap) {
+  const int s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= *nseg) return;
+  const VxsSeg g = segs[s];
+  const int m = cut[s];
+  const VxsSeg h[2] = {{g.f, m, g.d - 1}, {m, g.l, g.d - 1}};
+  for (int i = 0; i < 2; ++i) {
+    const int len = h[i].l - h[i].f;
+    if (len <= VXS_SMALL) small[atomicAdd(nsmall, 1)] = h[i];
+    else if (h[i].d == 0) heap[atomicAdd(nheap, 1)] = h[i];
+    else next[atomicAdd(nnext, 1)] = h[i];
+  }
+}
+
+// grid (clouds): every cloud's whole range, into the big (> VXS_SMALL) or small list at depth
+// 2 floor(log2 n) (nothing for n <= 1 or an overflowed cloud)
+__global__ __launch_bounds__(64) void k_vxs_init(const int* seg_b, const int* seg_e, int n_clouds, VxsSeg* big,
+                                                 int* nbig, VxsSeg* small, int* nsmall) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= n_clouds) return;
+  const int f = seg_b[c], l = seg_e[c], n = l - f;
+  if (n <= 1) return;
+  const VxsSeg g = {f, l, 2 * lg::floor_log2(n)};
+  if (n <= VXS_SMALL) small[atomicAdd(nsmall, 1)] = g;
+  else big[atomicAdd(nbig, 1)] = g;
+}
+
+// grid (small ranges): one wave each, the level-synchronous emulation from the range's depth limit in LDS
+// (R = 16 for ranges of at most 1,024 positions, else 32: two kernels, each with its register budget)
+// The point indices may exceed lvl_sort's 16-bit values: the sort carries range positions, and the
+// indices follow through the scratch copy xv of the range.
+template <int R>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R == 32 ? 2 : 3)))
+void k_vxs_small(const VxsSeg* segs, const int* nseg, unsigned* keys, unsigned* vals, unsigned* xv) {
+  __shared__ lgws::VoxLvlLds<R> L;
+  const int s = blockIdx.x;
+  if (s >= *nseg) return;
+  const VxsSeg g = segs[s];
+  const int n = g.l - g.f;
+  if ((n > 1024) != (R == 32) || n <= 1) return;
+  for (int i = threadIdx.x; i < n; i += 64) {
+    L.u.nat.key[i] = keys[g.f + i];
+    L.u.nat.val[i] = (uint16_t)i;
+    xv[g.f + i] = vals[g.f + i];
+  }
+  __syncthreads();
+  lgws::lvl_sort<R>(L.u.nat.key, L.u.nat.val, L.u.buf, n, g.d);
+  for (int i = threadIdx.x; i < n; i += 64) {
+    keys[g.f + i] = L.u.nat.key[i];
+    vals[g.f + i] = xv[g.f + L.u.nat.val[i]];
+  }
+}
+
+// grid (heap ranges): __partial_sort of a range longer than VXS_SMALL at depth 0, one wave, in HBM
+__global__ __launch_bounds__(64) void k_vxs_heap(const VxsSeg* segs, const int* nseg, unsigned* keys,
+                                                 unsigned* vals) {
+  const int s = blockIdx.x;
+  if (s >= *nseg) return;
+  const VxsSeg g = segs[s];
+  lgws::heap_sort_wave(lg::SortView<unsigned, unsigned>{keys, vals}, g.f, g.l);
+}
+
 }  // namespace
 
 struct lego_s2m {
@@ -1386,6 +1608,14 @@ struct lego_s2m {
   void* d_wide_tmp = nullptr;
   size_t wide_tmp_bytes = 0;
   int wide_clouds = 0;
+  // voxel_tie_order 0 (PCL's std::sort order, the reference): the level-synchronous emulation's scratch
+  // for vxs_clouds clouds: exchange slots, read-back slots, range lists and their counters
+  int voxel_tie_order = 0;
+  int vxs_clouds = 0;
+  unsigned *d_xk = nullptr, *d_xv = nullptr, *d_pivot = nullptr;
+  int *d_rds = nullptr, *d_cut = nullptr, *d_cnt = nullptr, *d_ctr = nullptr, *h_ctr = nullptr;
+  VxsSeg *d_big = nullptr, *d_next = nullptr, *d_small = nullptr, *d_heap = nullptr;
+  int cap_big = 0, cap_small = 0, vxs_maxch = 0;
 };
 
 // The LM's per-problem scratch (bucket tables, bucketed points, rows, nanoflann trees: ~200 B a map
@@ -1467,8 +1697,11 @@ extern "C" void lego_s2m_destroy(lego_s2m* m) {
   if (m->d_state) hipFree(m->d_state);
   for (void* p : {(void*)m->d_keys, (void*)m->d_vals, (void*)m->d_keys2, (void*)m->d_vals2, (void*)m->d_seg,
                   (void*)m->d_ovf, m->d_sort_tmp, (void*)m->d_k64, (void*)m->d_k64b, (void*)m->d_wv, (void*)m->d_wv2,
-                  (void*)m->d_wseg, (void*)m->d_wovf, (void*)m->d_wbounds, (void*)m->d_wtcount, m->d_wide_tmp})
+                  (void*)m->d_wseg, (void*)m->d_wovf, (void*)m->d_wbounds, (void*)m->d_wtcount, m->d_wide_tmp,
+                  (void*)m->d_xk, (void*)m->d_xv, (void*)m->d_pivot, (void*)m->d_rds, (void*)m->d_cut, (void*)m->d_cnt,
+                  (void*)m->d_ctr, (void*)m->d_big, (void*)m->d_next, (void*)m->d_small, (void*)m->d_heap})
     if (p) hipFree(p);
+  if (m->h_ctr) hipHostFree(m->h_ctr);
   delete m;
 }
 
@@ -1555,6 +1788,15 @@ extern "C" int lego_map_transform(lego_s2m* m, int32_t n, const lego_map_transfo
   return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }
 
+static int ensure_vox_scratch(lego_s2m* m, int n);
+static int map_voxel_std_order(lego_s2m* m, int n, const lego_map_voxel_io* io, hipStream_t st);
+
+extern "C" int lego_s2m_set_voxel_tie_order(lego_s2m* m, int32_t order) {
+  if (!m || order < 0 || order > 1) return LEGO_EINVAL;
+  m->voxel_tie_order = order;
+  return LEGO_OK;
+}
+
 extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* io, void* hip_stream) {
   if (!m || !io || n < 1 || !io->in || !io->in_off || !io->in_n || !io->leaf ||
       !io->out || !io->out_off || !io->out_n || !io->status)
@@ -1562,6 +1804,7 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
   if (hipSetDevice(m->device) != hipSuccess) return LEGO_EDEVICE;
   const int cap = m->max_map;
   hipStream_t st = (hipStream_t)hip_stream;
+  if (m->voxel_tie_order == 0) return map_voxel_std_order(m, n, io, st);
   if ((size_t)n * cap <= S2M_WIDE_MAX && n < 64) {
     // few clouds (the mapping thread's five): the tiled kernels and one device-wide stable radix sort
     // over the clouds' points (their counts read back first: this path synchronizes the stream)
@@ -1626,7 +1869,28 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
                        (const int*)m->d_wtcount, tiles);
     return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
   }
-  if (n > m->vox_clouds) {  // scratch for n clouds of up to max_map_points (grows, never shrinks)
+  const int rc = ensure_vox_scratch(m, n);
+  if (rc) return rc;
+  int* seg_b = m->d_seg;
+  int* seg_e = m->d_seg + m->vox_clouds;
+  hipLaunchKernelGGL(k_vox_keys, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys, m->d_vals, seg_b, seg_e, m->d_ovf,
+                     cap);
+  if (hipGetLastError() != hipSuccess) return LEGO_EDEVICE;
+  // stable LSD radix sort of every cloud's (leaf index, point index) pairs: std::stable_sort's order
+  size_t tmp = m->sort_tmp_bytes;
+  if (rocprim::segmented_radix_sort_pairs(m->d_sort_tmp, tmp, m->d_keys, m->d_keys2, m->d_vals, m->d_vals2,
+                                          (unsigned)((size_t)n * cap), (unsigned)n, seg_b, seg_e, 0, 32, st) !=
+      hipSuccess)
+    return LEGO_EDEVICE;
+  hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys2, m->d_vals2, m->d_ovf, cap);
+  return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+}
+
+// scratch for n clouds of up to max_map_points: keys / values in and sorted, segments, overflow flags,
+// rocPRIM's temporary storage (grows, never shrinks)
+static int ensure_vox_scratch(lego_s2m* m, int n) {
+  const int cap = m->max_map;
+  if (n > m->vox_clouds) {
     const int nc = n;
     const size_t e = (size_t)nc * cap;
     if (e >= (1ull << 32)) return LEGO_EINVAL;
@@ -1651,18 +1915,95 @@ extern "C" int lego_map_voxel(lego_s2m* m, int32_t n, const lego_map_voxel_io* i
     m->sort_tmp_bytes = tmp;
     m->vox_clouds = nc;
   }
+  return LEGO_OK;
+}
+
+// PCL's std::sort order (voxel_tie_order 0): k_vox_keys, the level-synchronous introsort emulation in place
+// (device-wide levels while ranges exceed VXS_SMALL, then one wave a range), k_vox_reduce.  Synchronizes
+// the stream once per device-wide level (the count of ranges still longer than VXS_SMALL).
+static int map_voxel_std_order(lego_s2m* m, int n, const lego_map_voxel_io* io, hipStream_t st) {
+  int rc = ensure_vox_scratch(m, n);
+  if (rc) return rc;
+  const int cap = m->max_map;
+  const size_t e = (size_t)n * cap;
+  if (n > m->vxs_clouds) {
+    hipDeviceSynchronize();  // earlier calls may still use the old scratch
+    for (void* p : {(void*)m->d_xk, (void*)m->d_xv, (void*)m->d_pivot, (void*)m->d_rds, (void*)m->d_cut,
+                    (void*)m->d_cnt, (void*)m->d_ctr, (void*)m->d_big, (void*)m->d_next, (void*)m->d_small,
+                    (void*)m->d_heap})
+      if (p) hipFree(p);
+    m->d_xk = m->d_xv = m->d_pivot = nullptr;
+    m->d_rds = m->d_cut = m->d_cnt = m->d_ctr = nullptr;
+    m->d_big = m->d_next = m->d_small = m->d_heap = nullptr;
+    m->vxs_clouds = 0;
+    m->cap_big = (int)(e / VXS_SMALL) + n + 16;    // ranges longer than VXS_SMALL at one level
+    m->cap_small = (int)(e / 16) + 2 * n + 16;     // every finished range (> 16 positions but the last ones)
+    m->vxs_maxch = (cap + VXS_CH - 1) / VXS_CH;
+    if (hipMalloc((void**)&m->d_xk, e * 4) != hipSuccess || hipMalloc((void**)&m->d_xv, e * 4) != hipSuccess ||
+        hipMalloc((void**)&m->d_rds, e * 4) != hipSuccess ||
+        hipMalloc((void**)&m->d_pivot, (size_t)m->cap_big * 4) != hipSuccess ||
+        hipMalloc((void**)&m->d_cut, (size_t)m->cap_big * 4) != hipSuccess ||
+        hipMalloc((void**)&m->d_cnt, (size_t)m->cap_big * m->vxs_maxch * 4) != hipSuccess ||
+        hipMalloc((void**)&m->d_ctr, 64) != hipSuccess ||
+        hipMalloc((void**)&m->d_big, (size_t)m->cap_big * sizeof(VxsSeg)) != hipSuccess ||
+        hipMalloc((void**)&m->d_next, (size_t)m->cap_big * sizeof(VxsSeg)) != hipSuccess ||
+        hipMalloc((void**)&m->d_heap, (size_t)m->cap_big * sizeof(VxsSeg)) != hipSuccess ||
+        hipMalloc((void**)&m->d_small, (size_t)m->cap_small * sizeof(VxsSeg)) != hipSuccess)
+      return LEGO_ENOMEM;
+    if (!m->h_ctr && hipHostMalloc((void**)&m->h_ctr, 64) != hipSuccess) return LEGO_ENOMEM;
+    m->vxs_clouds = n;
+  }
   int* seg_b = m->d_seg;
   int* seg_e = m->d_seg + m->vox_clouds;
+  int* ctr = m->d_ctr;  // [0] big ranges, [1] next level's, [2] small, [3] heap-sort
+  if (hipMemsetAsync(ctr, 0, 16, st) != hipSuccess) return LEGO_EDEVICE;
   hipLaunchKernelGGL(k_vox_keys, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys, m->d_vals, seg_b, seg_e, m->d_ovf,
                      cap);
+  hipLaunchKernelGGL(k_vxs_init, dim3((n + 63) / 64), dim3(64), 0, st, (const int*)seg_b, (const int*)seg_e, n,
+                     m->d_big, ctr, m->d_small, ctr + 2);
   if (hipGetLastError() != hipSuccess) return LEGO_EDEVICE;
-  // stable LSD radix sort of every cloud's (leaf index, point index) pairs: std::stable_sort's order
-  size_t tmp = m->sort_tmp_bytes;
-  if (rocprim::segmented_radix_sort_pairs(m->d_sort_tmp, tmp, m->d_keys, m->d_keys2, m->d_vals, m->d_vals2,
-                                          (unsigned)((size_t)n * cap), (unsigned)n, seg_b, seg_e, 0, 32, st) !=
-      hipSuccess)
+  VxsSeg *cur = m->d_big, *nxt = m->d_next;
+  for (int level = 0;; ++level) {
+    if (hipMemcpyAsync(m->h_ctr, ctr, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return LEGO_EDEVICE;
+    const int nbig = m->h_ctr[0];
+    if (nbig == 0) break;
+    if (nbig > m->cap_big || nbig > 65535 || level > 64) return LEGO_EDEVICE;  // (bounded by construction)
+    const int g64 = (nbig + 63) / 64;
+    const dim3 gch(m->vxs_maxch, nbig);
+    if (hipMemsetAsync(ctr + 1, 0, 4, st) != hipSuccess) return LEGO_EDEVICE;
+    hipLaunchKernelGGL(k_vxs_median, dim3(g64), dim3(64), 0, st, (const VxsSeg*)cur, (const int*)ctr, m->d_keys,
+                       m->d_vals, m->d_pivot, m->d_cut);
+    hipLaunchKernelGGL(k_vxs_count, gch, dim3(VXS_TPB), 0, st, (const VxsSeg*)cur, (const int*)ctr,
+                       (const unsigned*)m->d_keys, (const unsigned*)m->d_pivot, m->d_cnt, m->vxs_maxch);
+    hipLaunchKernelGGL(k_vxs_exchange, gch, dim3(VXS_TPB), 0, st, (const VxsSeg*)cur, (const int*)ctr,
+                       (const unsigned*)m->d_keys, (const unsigned*)m->d_vals, (const unsigned*)m->d_pivot,
+                       (const int*)m->d_cnt, m->vxs_maxch, m->d_xk, m->d_xv, m->d_rds, m->d_cut);
+    hipLaunchKernelGGL(k_vxs_readback, gch, dim3(VXS_TPB), 0, st, (const VxsSeg*)cur, (const int*)ctr, m->d_keys,
+                       m->d_vals, (const unsigned*)m->d_xk, (const unsigned*)m->d_xv, (const int*)m->d_rds);
+    hipLaunchKernelGGL(k_vxs_split, dim3(g64), dim3(64), 0, st, (const VxsSeg*)cur, (const int*)ctr,
+                       (const int*)m->d_cut, nxt, ctr + 1, m->d_small, ctr + 2, m->d_heap, ctr + 3);
+    if (hipGetLastError() != hipSuccess) return LEGO_EDEVICE;
+    std::swap(cur, nxt);
+    if (hipMemcpyAsync(ctr, ctr + 1, 4, hipMemcpyDeviceToDevice, st) != hipSuccess) return LEGO_EDEVICE;
+  }
+  if (hipMemcpyAsync(m->h_ctr, ctr, 16, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
     return LEGO_EDEVICE;
-  hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, m->d_keys2, m->d_vals2, m->d_ovf, cap);
+  const int nsmall = m->h_ctr[2], nheap = m->h_ctr[3];
+  if (nsmall > m->cap_small || nheap > m->cap_big) return LEGO_EDEVICE;
+  if (nsmall > 0) {
+    hipLaunchKernelGGL(k_vxs_small<16>, dim3(nsmall), dim3(64), 0, st, (const VxsSeg*)m->d_small, (const int*)(ctr + 2),
+                       m->d_keys, m->d_vals, m->d_xv);
+    hipLaunchKernelGGL(k_vxs_small<32>, dim3(nsmall), dim3(64), 0, st, (const VxsSeg*)m->d_small, (const int*)(ctr + 2),
+                       m->d_keys, m->d_vals, m->d_xv);
+  }
+  if (nheap > 0)
+    hipLaunchKernelGGL(k_vxs_heap, dim3(nheap), dim3(64), 0, st, (const VxsSeg*)m->d_heap, (const int*)(ctr + 3),
+                       m->d_keys, m->d_vals);
+  hipLaunchKernelGGL(k_vox_reduce, dim3(n), dim3(S2M_THREADS), 0, st, *io, (const unsigned*)m->d_keys,
+                     (const unsigned*)m->d_vals, m->d_ovf, cap);
   return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
 }
 

@@ -83,6 +83,8 @@ def lib():
                                                  C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_float)]
         L.lego_batch_set_groups.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_lag.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_batch_set_probe.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_batch_probe_times.argtypes = [C.c_void_p, P(C.c_float), P(C.c_int32)]
         L.lego_batch_set_wide.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_wide.argtypes = [C.c_void_p]
         L.lego_batch_read_counts.argtypes = [C.c_void_p, P(C.c_int32)]
@@ -97,6 +99,8 @@ def lib():
         L.lego_map_transform.argtypes = [C.c_void_p, C.c_int32, P(LegoMapTransformIo), C.c_void_p]
         L.lego_map_voxel.argtypes = [C.c_void_p, C.c_int32, P(LegoMapVoxelIo), C.c_void_p]
         L.lego_s2m_set_layout.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_s2m_set_voxel_tie_order.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_mapper_set_voxel_tie_order.argtypes = [C.c_void_p, C.c_int32]
         L.lego_mapper_create.argtypes = [C.c_int32, C.c_int32, C.c_int64, P(C.c_void_p)]
         L.lego_mapper_destroy.argtypes = [C.c_void_p]
         L.lego_mapper_step.argtypes = [C.c_void_p] + [C.c_void_p, C.c_int32] * 3 + [P(C.c_float), P(C.c_float),
@@ -236,6 +240,17 @@ class Batch:
         """Launch the streams as `groups` slices on separate HIP streams (overlapping kernel tails)."""
         _check(lib().lego_batch_set_groups(self.h, int(groups)), "lego_batch_set_groups")
 
+    def set_probe(self, on=True):
+        """Events around the projection and smoothness stages of every overlap-schedule step."""
+        _check(lib().lego_batch_set_probe(self.h, int(bool(on))), "lego_batch_set_probe")
+
+    def probe_times(self):
+        """(projection ms, smoothness ms, steps): mean in-pipeline durations since set_probe; clears them."""
+        ms = (C.c_float * 2)()
+        n = C.c_int32()
+        _check(lib().lego_batch_probe_times(self.h, ms, C.byref(n)), "lego_batch_probe_times")
+        return float(ms[0]), float(ms[1]), int(n.value)
+
     def set_lag(self, lag):
         """Pipeline depth: 0 = a step runs its own scan's LM, 1 (default) = the previous scan's."""
         _check(lib().lego_batch_set_lag(self.h, int(lag)), "lego_batch_set_lag")
@@ -331,8 +346,13 @@ class ScanToMap:
         _check(lib().lego_map_transform(self.h, int(n), C.byref(io), C.c_void_p(stream)), "lego_map_transform")
 
     def map_voxel(self, n, io, stream=0):
-        """pcl::VoxelGrid::filter of n clouds (LegoMapVoxelIo of device pointers); asynchronous."""
+        """pcl::VoxelGrid::filter of n clouds (LegoMapVoxelIo of device pointers); asynchronous (tie order 1;
+        order 0 synchronizes `stream` once per device-wide sort level)."""
         _check(lib().lego_map_voxel(self.h, int(n), C.byref(io), C.c_void_p(stream)), "lego_map_voxel")
+
+    def set_voxel_tie_order(self, order):
+        """map_voxel's tie order: 0 (default) PCL's std::sort permutation (the reference), 1 std::stable_sort's."""
+        _check(lib().lego_s2m_set_voxel_tie_order(self.h, int(order)), "lego_s2m_set_voxel_tie_order")
 
 
 class Mapper:
@@ -340,11 +360,12 @@ class Mapper:
     sequence: step() takes one AssociationOut's clouds and transformSum and returns transformAftMapped;
     the key frames' downsampled clouds stay in device memory (lego_mapper_*, include/lego_s2m.h)."""
 
-    def __init__(self, max_map_points=200000, max_key_points=50_000_000, device=0):
+    def __init__(self, max_map_points=200000, max_key_points=50_000_000, device=0, voxel_tie_order=0):
         h = C.c_void_p()
         _check(lib().lego_mapper_create(int(device), int(max_map_points), int(max_key_points), C.byref(h)),
                "lego_mapper_create")
         self.h = h
+        _check(lib().lego_mapper_set_voxel_tie_order(self.h, int(voxel_tie_order)), "lego_mapper_set_voxel_tie_order")
 
     def close(self):
         if getattr(self, "h", None):

@@ -1,16 +1,22 @@
 // lego_nodes.cpp — ImageProjection / FeatureAssociation over the MI355X C-ABI (see lego_nodes.h).
 //
-// ImageProjection::cloudHandler (imageProjection.cpp:153-174) hands the PointCloud2 payload to
-// lego_cloud_handler (fromROSMsg + removeNaN + projection + ground removal + segmentation on the GPU) and
-// sends the reference's ProjectionOut (utility.h:64-70) on the channel, as publishClouds does (:498-548).
-// FeatureAssociation::runFeatureAssociation (featureAssociation.cpp:1386-1450) receives it and runs one
-// lego_feature_association_from (adjustDistortion ... publishCloudsLast on the GPU), then publishes the
-// odometry (:1286-1306) and the clouds, and sends AssociationOut every mapping_frequency_divider cycles.
+// A thin ROS layer over include/lego_loam_amd.hpp: every decision between a message and the C-ABI is
+// the GPU-tested mirror's (tests/test_cpp_mirror.py, tests/native/mirror_check.cpp):
+//   * ImageProjection::cloudHandler (imageProjection.cpp:153-174): xyz_offsets + packed_rows hand the
+//     PointCloud2 payload to lego_cloud_handler (fromROSMsg + removeNaN + projection + ground removal +
+//     segmentation on the GPU); fill_cloud_info builds the cloud_info of the ProjectionOut (utility.h:64-70)
+//     sent on the channel, as publishClouds does (:498-548);
+//   * FeatureAssociation::runFeatureAssociation (featureAssociation.cpp:1386-1450) is the mirror's
+//     run_feature_association loop (projection_in, lego_feature_association_from, FeatureAssociationCycle's
+//     publication decisions) with a sink that converts PCL <-> lego_point and publishes.
+// What remains here is message conversion and publishing.
 #include "lego_nodes.h"
 
 #include <cstring>
 #include <stdexcept>
 #include <string>
+
+#include "lego_loam_amd.hpp"
 
 namespace {
 
@@ -93,28 +99,15 @@ ImageProjection::ImageProjection(ros::NodeHandle& nh, Channel<ProjectionOut>& ou
 ImageProjection::~ImageProjection() { lego_ctx_destroy(_gpu); }
 
 void ImageProjection::cloudHandler(const sensor_msgs::PointCloud2ConstPtr& msg) {
-  int ox = -1, oy = -1, oz = -1;  // the float32 x, y, z fields (fromROSMsg, :159)
-  for (const auto& fld : msg->fields) {
-    if (fld.datatype != sensor_msgs::PointField::FLOAT32 || fld.count != 1) continue;
-    if (fld.name == "x") ox = fld.offset;
-    else if (fld.name == "y") oy = fld.offset;
-    else if (fld.name == "z") oz = fld.offset;
-  }
-  if (ox < 0 || oy < 0 || oz < 0 || msg->is_bigendian) {
+  int ox, oy, oz;  // the float32 x, y, z fields (fromROSMsg, :159)
+  if (!lego_amd::xyz_offsets(msg->fields, msg->is_bigendian, ox, oy, oz)) {
     ROS_ERROR_THROTTLE(1.0, "lidar PointCloud2 without little-endian float32 x, y, z fields");
     return;
   }
-  const int n = (int)(msg->width * msg->height);
-  const uint8_t* data = msg->data.data();
-  if (msg->height > 1 && msg->row_step != msg->width * msg->point_step) {  // padded rows: pack them
-    _packed.resize((size_t)n * msg->point_step);
-    for (uint32_t r = 0; r < msg->height; ++r)
-      std::memcpy(&_packed[(size_t)r * msg->width * msg->point_step], data + (size_t)r * msg->row_step,
-                  (size_t)msg->width * msg->point_step);
-    data = _packed.data();
-  }
+  const uint8_t* data =
+      lego_amd::packed_rows(msg->data.data(), msg->width, msg->height, msg->point_step, msg->row_step, _packed);
   lego_projection_out o;
-  const int rc = lego_cloud_handler(_gpu, data, n, (int)msg->point_step, ox, oy, oz, &o);
+  const int rc = lego_cloud_handler(_gpu, data, (int)(msg->width * msg->height), (int)msg->point_step, ox, oy, oz, &o);
   if (rc != LEGO_OK) {  // an empty or all-NaN cloud (UB in the reference's findStartEndAngle)
     ROS_WARN_THROTTLE(1.0, "lego_cloud_handler rc=%d: scan dropped", rc);
     return;
@@ -129,26 +122,12 @@ void ImageProjection::publishClouds(const lego_projection_out& o, const std_msgs
   out.segmented_cloud = to_pcl(o.segmented_cloud, o.n_segmented);
   out.outlier_cloud = to_pcl(o.outlier_cloud, o.n_outlier);
   out.scan_msg = to_pcl(o.scan_msg, o.n_scan);
-  cloud_msgs::cloud_info& s = out.seg_msg;
-  s.header = header;
-  s.startRingIndex.assign(o.start_ring_index, o.start_ring_index + V);
-  s.endRingIndex.assign(o.end_ring_index, o.end_ring_index + V);
-  s.startOrientation = o.start_orientation;
-  s.endOrientation = o.end_orientation;
-  s.orientationDiff = o.orientation_diff;
-  // sized V*H with a zero tail, as resetParameters leaves them (imageProjection.cpp:137-139)
-  s.segmentedCloudGroundFlag.assign(VH, false);
-  s.segmentedCloudColInd.assign(VH, 0);
-  s.segmentedCloudRange.assign(VH, 0);
-  for (int i = 0; i < o.n_segmented; ++i) {
-    s.segmentedCloudGroundFlag[i] = o.segmented_cloud_ground_flag[i] != 0;
-    s.segmentedCloudColInd[i] = o.segmented_cloud_col_ind[i];
-    s.segmentedCloudRange[i] = o.segmented_cloud_range[i];
-  }
+  out.seg_msg.header = header;
+  lego_amd::fill_cloud_info(o, V, VH, true, out.seg_msg);  // V*H entries with a zero tail (:137-139)
   publish_cloud(_pub_outlier_cloud, out.outlier_cloud, header.stamp, "base_link");
   publish_cloud(_pub_segmented_cloud, out.segmented_cloud, header.stamp, "base_link");
   publish_cloud(_pub_laser, out.scan_msg, header.stamp, "base_link");
-  if (_pub_segmented_cloud_info.getNumSubscribers() != 0) _pub_segmented_cloud_info.publish(s);
+  if (_pub_segmented_cloud_info.getNumSubscribers() != 0) _pub_segmented_cloud_info.publish(out.seg_msg);
 }
 
 // ---- FeatureAssociation -----------------------------------------------------------------------------
@@ -182,59 +161,36 @@ FeatureAssociation::~FeatureAssociation() {
   lego_ctx_destroy(_gpu);
 }
 
-void FeatureAssociation::runFeatureAssociation() {
+// run_feature_association's sink: PCL <-> lego_point conversion and the publishers
+struct FeatureAssociation::Sink {
+  FeatureAssociation& fa;
   std::vector<lego_point> seg, outl;
-  std::vector<uint8_t> gflag;
-  while (ros::ok()) {
-    ProjectionOut projection;
-    _input_channel.receive(projection);
-    if (!ros::ok() || !projection.segmented_cloud) break;
-    const cloud_msgs::cloud_info& si = projection.seg_msg;
-    cloudHeader = si.header;
-    from_pcl(projection.segmented_cloud, seg);
-    from_pcl(projection.outlier_cloud, outl);
-    const int M = (int)seg.size();
-    if ((int)si.segmentedCloudGroundFlag.size() < M || (int)si.segmentedCloudColInd.size() < M ||
-        (int)si.segmentedCloudRange.size() < M || (int)si.startRingIndex.size() < _params.num_vertical_scans ||
-        (int)si.endRingIndex.size() < _params.num_vertical_scans) {
-      ROS_ERROR("malformed cloud_info: scan dropped");
-      continue;
-    }
-    gflag.assign(si.segmentedCloudGroundFlag.begin(), si.segmentedCloudGroundFlag.begin() + M);
-    lego_projection_out in;
-    std::memset(&in, 0, sizeof(in));
-    in.n_segmented = M;
-    in.n_outlier = (int)outl.size();
-    in.segmented_cloud = seg.data();
-    in.outlier_cloud = outl.data();
-    in.start_ring_index = si.startRingIndex.data();
-    in.end_ring_index = si.endRingIndex.data();
-    in.start_orientation = si.startOrientation;
-    in.end_orientation = si.endOrientation;
-    in.orientation_diff = si.orientationDiff;
-    in.segmented_cloud_ground_flag = gflag.data();
-    in.segmented_cloud_col_ind = si.segmentedCloudColInd.data();
-    in.segmented_cloud_range = si.segmentedCloudRange.data();
-    lego_association_out o;
-    const int rc = lego_feature_association_from(_gpu, &in, &o);
-    if (rc != LEGO_OK) {
-      ROS_ERROR("lego_feature_association_from rc=%d: scan dropped", rc);
-      continue;
-    }
-    publishClouds(o);                     // :1410 (visualization)
-    if (o.status & LEGO_ST_INIT) continue;  // checkSystemInitialization (:1413-1416)
-    publishOdometry(o);                   // :1422
-    publishCloudsLast(o);                 // :1424
-    if (o.status & LEGO_ST_EMITTED) {     // _cycle_count == _mapping_frequency_div (:1431-1448)
-      AssociationOut out;
-      out.cloud_corner_last = to_pcl(o.cloud_corner_last, o.n_corner_last);
-      out.cloud_surf_last = to_pcl(o.cloud_surf_last, o.n_surf_last);
-      out.cloud_outlier_last = to_pcl(o.cloud_outlier_last, o.n_outlier_last);
-      out.laser_odometry = laserOdometry;
-      out.scan_msg = projection.scan_msg ? projection.scan_msg : pcl::PointCloud<PointType>::Ptr(new pcl::PointCloud<PointType>());
-      _output_channel.send(std::move(out));
-    }
+  bool end(const ProjectionOut& p) { return !ros::ok() || !p.segmented_cloud; }  // the dtor's empty item
+  bool view(const ProjectionOut& p, lego_projection_out& in) {
+    fa.cloudHeader = p.seg_msg.header;
+    from_pcl(p.segmented_cloud, seg);
+    from_pcl(p.outlier_cloud, outl);
+    return lego_amd::projection_in(seg.data(), (int)seg.size(), outl.data(), (int)outl.size(), nullptr, 0, p.seg_msg,
+                                   fa._params.num_vertical_scans, in);
   }
+  void dropped(const char* why, int rc) { ROS_ERROR("%s (rc=%d): scan dropped", why, rc); }
+  void features(const ProjectionOut&, const lego_association_out& o) { fa.publishClouds(o); }      // :1410
+  void odometry(const ProjectionOut&, const lego_association_out& o) { fa.publishOdometry(o); }    // :1422
+  void clouds_last(const ProjectionOut&, const lego_association_out& o) { fa.publishCloudsLast(o); }  // :1424
+  void emit(const ProjectionOut& p, const lego_association_out& o) {  // :1431-1448
+    AssociationOut out;
+    out.cloud_corner_last = to_pcl(o.cloud_corner_last, o.n_corner_last);
+    out.cloud_surf_last = to_pcl(o.cloud_surf_last, o.n_surf_last);
+    out.cloud_outlier_last = to_pcl(o.cloud_outlier_last, o.n_outlier_last);
+    out.laser_odometry = fa.laserOdometry;
+    out.scan_msg = p.scan_msg ? p.scan_msg : pcl::PointCloud<PointType>::Ptr(new pcl::PointCloud<PointType>());
+    fa._output_channel.send(std::move(out));
+  }
+};
+
+void FeatureAssociation::runFeatureAssociation() {
+  Sink sink{*this, {}, {}};
+  lego_amd::run_feature_association<ProjectionOut>(_gpu, _input_channel, sink);
 }
 
 void FeatureAssociation::publishOdometry(const lego_association_out& o) {  // :1286-1306
@@ -266,10 +222,8 @@ void FeatureAssociation::publishClouds(const lego_association_out& o) {  // publ
     publish_cloud(pubSurfPointsLessFlat, to_pcl(o.surf_points_less_flat, o.n_less_flat), t, "/camera");
 }
 
-void FeatureAssociation::publishCloudsLast(const lego_association_out& o) {  // :1362-1382 (every 2nd frame)
-  frameCount++;
-  if (frameCount < 2) return;  // frameCount >= skipFrameNum + 1
-  frameCount = 0;
+void FeatureAssociation::publishCloudsLast(const lego_association_out& o) {
+  // :1362-1382's publications; FeatureAssociationCycle decides the every-second-frame gate
   const ros::Time t = cloudHeader.stamp;
   if (_pub_outlier_cloudLast.getNumSubscribers())
     publish_cloud(_pub_outlier_cloudLast, to_pcl(o.cloud_outlier_last, o.n_outlier_last), t, "/camera");

@@ -62,6 +62,7 @@ class FeatureAssociation {
   void runFeatureAssociation();
 
  private:
+  struct Sink;  // lego_amd::run_feature_association's conversions and publishers (lego_nodes.cpp)
   void publishOdometry(const lego_association_out& o);
   void publishClouds(const lego_association_out& o);
   void publishCloudsLast(const lego_association_out& o);
@@ -77,7 +78,6 @@ class FeatureAssociation {
   nav_msgs::Odometry laserOdometry;
   tf::StampedTransform laserOdometryTrans;
   tf::TransformBroadcaster tfBroadcaster;
-  int frameCount = 1;  // skipFrameNum (featureAssociation.cpp:132,156)
 
   ros::Publisher pubCornerPointsSharp;
   ros::Publisher pubCornerPointsLessSharp;

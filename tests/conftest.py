@@ -40,3 +40,13 @@ def gpu(has_gpu):
     if not has_gpu:
         pytest.fail("no HIP device visible: -m gpu tests must run on the MI355X box")
     return 0
+
+
+def pytest_terminal_summary(terminalreporter):
+    """How many scans' Last clouds took assert_scan_parity's 1e-3 fallback (transform_cur not bit-identical
+    to the oracle's); every other parity scan compared them bit for bit."""
+    mod = sys.modules.get("test_gpu_parity")
+    if mod is not None and getattr(mod, "LAST_CLOUD_CHECKS", [0])[0]:
+        terminalreporter.write_line("Last-cloud parity: %d of %d scans compared at 1e-3 (transform within the bar, "
+                                    "not bit-identical), the rest bit-exact"
+                                    % (len(mod.LAST_CLOUD_FALLBACKS), mod.LAST_CLOUD_CHECKS[0]))

@@ -28,6 +28,18 @@ def write_scans(path, scans):
             f.write(p.tobytes())
 
 
+def test_mirror_message_helpers(tmp_path):
+    """The mirror's helpers between a ROS message and the C-ABI, which ros/lego_nodes.cpp uses as they are
+    (xyz_offsets, packed_rows, fill_cloud_info, projection_in, FeatureAssociationCycle): CPU checks."""
+    exe = str(tmp_path / "mirror_check")
+    lib = os.path.join(REPO, "lego-loam-bor_amd", "lego_amd")
+    subprocess.check_call(["g++", "-std=c++14", "-O2", "-Wall", "-Werror", "-I" + os.path.join(REPO, "include"),
+                           os.path.join(REPO, "tests", "native", "mirror_check.cpp"), "-o", exe, "-L" + lib,
+                           "-llego_frontend", "-Wl,-rpath," + lib, "-pthread"])
+    r = subprocess.run([exe], stdout=subprocess.PIPE, universal_newlines=True)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout
+
+
 def test_mirror_builds_and_fails_loudly_without_device(tmp_path):
     build()
     import lego_amd
@@ -56,12 +68,24 @@ def test_mirror_pipeline_matches_oracle(gpu, tmp_path):
     pos = np.array([float(x) for x in tok[5:8]])
     quat = np.array([float(x) for x in tok[9:13]])
     orc = O.Oracle(MG.params_for("vlp16"))
+    n_last = n_emit = 0
+    frame_count = 1  # publishCloudsLast's skip counter (featureAssociation.cpp:132, :1362-1382)
     for p in scans:
         orc.cloud_handler(p)
         fa = orc.feature_association()
+        if fa["status"] & A.ST_INIT:
+            continue
+        frame_count += 1
+        if frame_count >= 2:
+            frame_count = 0
+            n_last += 1
+        n_emit += bool(fa["status"] & A.ST_EMITTED)
     assert cycles == len(scans)
     np.testing.assert_allclose(pos, fa["odom_position"], atol=Hs.TF_TOL, rtol=0)
     np.testing.assert_allclose(quat, fa["odom_orientation"], atol=Hs.TF_TOL, rtol=0)
+    # run_feature_association's publication decisions (shared with ros/lego_nodes.cpp)
+    assert tok[13] == "last" and int(tok[14]) == n_last and tok[15] == "emitted" and int(tok[16]) == n_emit, tok
+    assert n_emit >= 1 and n_last >= 3
 
 
 @pytest.mark.gpu

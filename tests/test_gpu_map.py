@@ -2,9 +2,9 @@
 
 MapOptimization builds the clouds scan2MapOptimization consumes with transformPointCloud
 (mapOptmization.cpp:443-473) and pcl::VoxelGrid (leaves :71-78; extractSurroundingKeyFrames :857-996,
-downsampleCurrentScan :999-1026).  Bar: bit-exact against the oracle's restatements (VoxelGrid with
-std::stable_sort's tie order), then the whole GPU-prepared problem through the scan-to-map LM within
-1e-4 of the oracle-prepared one.
+downsampleCurrentScan :999-1026).  Bar: bit-exact against the oracle's restatements (VoxelGrid in both
+tie orders: PCL's std::sort permutation, the reference's, and std::stable_sort's), then the whole
+GPU-prepared problem through the scan-to-map LM within 1e-4 of the oracle-prepared one.
 """
 import numpy as np
 import pytest
@@ -61,7 +61,9 @@ def _gpu_voxel(s2m, clouds, leaves):
     return [(o[off[i]:off[i] + max(on[i], 0)], int(on[i]), int(so[i])) for i in range(len(cl))]
 
 
-def test_voxel_matches_oracle(s2m, sequences):
+@pytest.mark.parametrize("order", [0, 1])
+def test_voxel_matches_oracle(s2m, sequences, order):
+    s2m.set_voxel_tie_order(order)
     fr = sequences[0]
     rng = np.random.default_rng(11)
     big = np.concatenate([M.associate_to_map(np.concatenate([f["surf_last"], f["outlier_last"]]), f["transform_sum"])
@@ -73,14 +75,16 @@ def test_voxel_matches_oracle(s2m, sequences):
     for leaf in (0.2, 0.4, 1.0):
         got = _gpu_voxel(s2m, clouds, [leaf] * len(clouds))
         for c, (o, on, st) in zip(clouds, got):
-            ref, rst = O.voxel_grid(c, leaf, stable=True)
+            ref, rst = O.voxel_grid(c, leaf, stable=order == 1)
             assert st == rst and on == len(ref), (leaf, len(c), on, len(ref))
             assert np.array_equal(o.view(np.int32), ref.view(np.int32)), (leaf, len(c))
 
 
-def test_voxel_both_sort_layouts(s2m, sequences):
-    """Few clouds take one device-wide radix sort (64-bit cloud|leaf keys), many clouds rocPRIM's
-    segmented sort; the same clouds through both give the oracle's output."""
+@pytest.mark.parametrize("order", [0, 1])
+def test_voxel_both_sort_layouts(s2m, sequences, order):
+    """Order 1: few clouds take one device-wide radix sort (64-bit cloud|leaf keys), many clouds rocPRIM's
+    segmented sort; order 0: one range list over all clouds.  The same clouds give the oracle's output."""
+    s2m.set_voxel_tie_order(order)
     fr = sequences[1]
     rng = np.random.default_rng(17)
     base = [fr[4]["corner_last"], fr[4]["surf_last"], np.zeros((0, 4), np.float32),
@@ -89,26 +93,30 @@ def test_voxel_both_sort_layouts(s2m, sequences):
     for clouds in (base, many):  # 4 clouds: device-wide; 70 clouds: segmented
         got = _gpu_voxel(s2m, clouds, [0.4] * len(clouds))
         for c, (o, on, st) in zip(clouds, got):
-            ref, rst = O.voxel_grid(c, 0.4, stable=True)
+            ref, rst = O.voxel_grid(c, 0.4, stable=order == 1)
             assert st == rst and on == len(ref) and np.array_equal(o.view(np.int32), ref.view(np.int32)), len(clouds)
 
 
-def test_voxel_limits(s2m):
+@pytest.mark.parametrize("order", [0, 1])
+def test_voxel_limits(s2m, order):
+    s2m.set_voxel_tie_order(order)
     rng = np.random.default_rng(12)
     wide = rng.uniform(-1000, 1000, (2000, 4)).astype(np.float32)  # 1e-3 leaves: indices overflow int32
     huge = np.zeros((130000, 4), np.float32)                       # above max_map_points
     got = _gpu_voxel(s2m, [wide, huge], [1e-3, 0.2])
-    ref, rst = O.voxel_grid(wide, 1e-3, stable=True)
+    ref, rst = O.voxel_grid(wide, 1e-3, stable=order == 1)
     assert got[0][2] == rst == 0x100 and got[0][1] == len(wide)    # LEGO_ST_VOXEL_OVERFLOW: copied
     assert np.array_equal(got[0][0], ref)
     assert got[1][1] == -1
 
 
-def test_voxel_overflow_then_normal_clouds(s2m, sequences):
+@pytest.mark.parametrize("order", [0, 1])
+def test_voxel_overflow_then_normal_clouds(s2m, sequences, order):
     """An overflowing cloud (PCL's int32 leaf-index warning path: copied unfiltered) FOLLOWED by normal
     clouds, through the few-clouds layout (one device-wide sort of cloud|leaf keys): the later clouds'
     sorted ranges must not shift, so each equals the oracle (the overflowed slots once
     sorted past every cloud)."""
+    s2m.set_voxel_tie_order(order)
     fr = sequences[2]
     rng = np.random.default_rng(21)
     wide = rng.uniform(-1000, 1000, (3000, 4)).astype(np.float32)
@@ -117,10 +125,49 @@ def test_voxel_overflow_then_normal_clouds(s2m, sequences):
     leaves = [1e-3, 0.2, 0.4, 0.4, 1e-3]
     got = _gpu_voxel(s2m, clouds, leaves)
     for c, leaf, (o, on, st) in zip(clouds, leaves, got):
-        ref, rst = O.voxel_grid(c, leaf, stable=True)
+        ref, rst = O.voxel_grid(c, leaf, stable=order == 1)
         assert st == rst and on == len(ref), (leaf, len(c), on, len(ref), st, rst)
         assert np.array_equal(o.view(np.int32), ref.view(np.int32)), (leaf, len(c))
     assert got[0][2] == 0x100 and got[4][2] == 0x100
+
+
+def test_voxel_std_order_key_sequences(s2m):
+    """voxel_tie_order 0 on clouds whose leaf indices are chosen key sequences (points at x = key + 0.5, leaf 1):
+    tie-heavy random keys up to 100k points (several device-wide levels, then one wave a range), sorted,
+    reversed, organ-pipe and run sequences, and the introsort adversary (ranges longer than 2,048 reaching
+    the depth limit: the device-wide heap sort), each against the oracle's std::sort VoxelGrid; the
+    intensities differ per point, so any other summation order shows."""
+    import os
+    import subprocess
+    import tempfile
+    s2m.set_voxel_tie_order(0)
+    rng = np.random.default_rng(31)
+
+    def cloud(keys):
+        keys = np.asarray(keys, np.int64)
+        p = np.zeros((len(keys), 4), np.float32)
+        p[:, 0] = keys + 0.5
+        p[:, 3] = rng.uniform(0, 100, len(keys)).astype(np.float32)
+        return p
+    seqs = [rng.integers(0, d, n) for n, d in [(3000, 5), (20000, 300), (100000, 2000), (60000, 60000), (2049, 2),
+                                                 (4096, 1)]]
+    i = np.arange(30000)
+    seqs += [i, i[::-1], np.minimum(i, 30000 - i), i // 7, (i * 7919) % 4001]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "ia")
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-I" + os.path.join(repo, "lego-loam-bor_amd", "csrc"),
+                               os.path.join(repo, "tests", "native", "introsort_adversary.cpp"), "-o", exe])
+        for n, c in [(3000, 1), (8192, 2), (50000, 1)]:
+            out = subprocess.run([exe, str(n), str(c)], stdout=subprocess.PIPE, universal_newlines=True, check=True)
+            seqs.append(np.array(out.stdout.split(), dtype=np.int64))
+    clouds = [cloud(k) for k in seqs]
+    for batch in (clouds[:6], clouds[6:]):
+        got = _gpu_voxel(s2m, batch, [1.0] * len(batch))
+        for c, (o, on, st) in zip(batch, got):
+            ref, rst = O.voxel_grid(c, 1.0, stable=False)
+            assert st == rst and on == len(ref), (len(c), on, len(ref))
+            assert np.array_equal(o.view(np.int32), ref.view(np.int32)), len(c)
 
 
 def test_transform_matches_oracle(s2m, sequences):
@@ -146,26 +193,28 @@ def test_transform_matches_oracle(s2m, sequences):
         assert np.array_equal(o[off[i]:off[i] + n[i]].view(np.int32), ref.view(np.int32)), i
 
 
-def _oracle_problem(frames, k, n_keys=10, perturb=(0.002, 0.002, 0.004, 0.03, 0.01, 0.03)):
-    """build_problem with the oracle's transformPointCloud and VoxelGrid (stable tie order)."""
+def _oracle_problem(frames, k, n_keys=10, perturb=(0.002, 0.002, 0.004, 0.03, 0.01, 0.03), order=0):
+    """build_problem with the oracle's transformPointCloud and VoxelGrid (in the given tie order)."""
     cparts, sparts, (c, s, o) = M._parts(frames, k, n_keys)
     cm = np.concatenate([O.transform_cloud(x, t) for x, t in cparts])
     sm = np.concatenate([O.transform_cloud(x, t) for x, t in sparts])
-    vg = lambda x, leaf: O.voxel_grid(x, leaf, stable=True)[0]  # noqa: E731
+    vg = lambda x, leaf: O.voxel_grid(x, leaf, stable=order == 1)[0]  # noqa: E731
     return {"corner_map": vg(cm, 0.2), "surf_map": vg(sm, 0.4), "corner": vg(c, 0.2),
             "surf": vg(np.concatenate([vg(s, 0.4), vg(o, 0.4)]), 0.4),
             "transform": (np.asarray(frames[k]["transform_sum"], np.float32) + np.asarray(perturb, np.float32))}
 
 
-def test_prepared_problems_match_oracle(s2m, sequences):
+@pytest.mark.parametrize("order", [0, 1])
+def test_prepared_problems_match_oracle(s2m, sequences, order):
     import torch
+    s2m.set_voxel_tie_order(order)
     k = 5
     io, keep, tr, dg, info, v = M.prepare_gpu(s2m, sequences, k)
     torch.cuda.synchronize()
     P_ = len(sequences)
     vo, oo, on = v["v_out"].cpu().numpy(), v["out_off"], v["out_n"].cpu().numpy()
     to, toff, tn = v["tot_out"].cpu().numpy(), v["tot_off"], v["tot_n"].cpu().numpy()
-    refs = [_oracle_problem(seq, k) for seq in sequences]
+    refs = [_oracle_problem(seq, k, order=order) for seq in sequences]
     for p, ref in enumerate(refs):
         got = {"corner_map": vo[oo[p]:oo[p] + on[p]], "surf_map": vo[oo[P_ + p]:oo[P_ + p] + on[P_ + p]],
                "corner": vo[oo[2 * P_ + 3 * p]:oo[2 * P_ + 3 * p] + on[2 * P_ + 3 * p]],

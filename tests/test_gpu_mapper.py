@@ -17,21 +17,24 @@ from test_gpu_mapping_loop import _emitted, mapping_step_oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("seq,max_map,max_key", [(3, 150000, 4_000_000), (8, 150000, 4_000_000), (3, 1500, 2000)])
-def test_mapper_matches_oracle_loop(gpu, seq, max_map, max_key):
-    """(3, 1500, 2000): initial capacities far below the sequence's raw map, scan clouds and key-frame
-    store, so every buffer of the mapper grows on demand (the reference has no such limits)
-    and the results stay identical."""
+@pytest.mark.parametrize("seq,max_map,max_key,order", [(3, 150000, 4_000_000, 0), (8, 150000, 4_000_000, 0),
+                                                        (3, 1500, 2000, 0), (3, 150000, 4_000_000, 1),
+                                                        (8, 150000, 4_000_000, 1)])
+def test_mapper_matches_oracle_loop(gpu, seq, max_map, max_key, order):
+    """Both VoxelGrid tie orders (0: PCL's std::sort permutation, the reference's; 1: stable), each
+    against the oracle's VoxelGrid in the same order.  (3, 1500, 2000): initial capacities far below the
+    sequence's raw map, scan clouds and key-frame store, so every buffer of the mapper grows on demand
+    (the reference has no such limits) and the results stay identical."""
     import lego_amd as LA
     stream = _emitted(seq, 61)
     assert len(stream) >= 5
-    mp = LA.Mapper(max_map_points=max_map, max_key_points=max_key, device=gpu)
+    mp = LA.Mapper(max_map_points=max_map, max_key_points=max_key, device=gpu, voxel_tie_order=order)
     r = M.MapSequence(associate=O.associate_to_map, odometry=O.odometry_to_transform)
     ran = 0
     for k, a in enumerate(stream):
         tg, ig = mp.step(a["corner_last"], a["surf_last"], a["outlier_last"],
                              M.odometry_to_transform(a["odom_orientation"], a["odom_position"]))
-        (_, _, ir), = mapping_step_oracle([r], [a])
+        (_, _, ir), = mapping_step_oracle([r], [a], order)
         assert np.array_equal(tg.view(np.int32), r.t_aft.view(np.int32)), (k, tg, r.t_aft)
         assert np.array_equal(ig, ir), (k, ig, ir)
         ran += int(ig[0] == 1)

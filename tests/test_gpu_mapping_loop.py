@@ -33,11 +33,13 @@ def _emitted(seq, n_scans):
     return out
 
 
-def mapping_step_oracle(seqs, assocs):
+def mapping_step_oracle(seqs, assocs, voxel_tie_order=0):
+    """One mapping cycle around the oracle's operations; VoxelGrid in the given tie order (0: PCL's
+    std::sort permutation, the reference's; 1: std::stable_sort's)."""
     res = []
     for sq, a in zip(seqs, assocs):
         cparts, sparts, (c, s, o), t0 = sq.begin(a)
-        vg = lambda x, leaf: O.voxel_grid(x, leaf, stable=True)[0]  # noqa: E731
+        vg = lambda x, leaf: O.voxel_grid(x, leaf, stable=voxel_tie_order == 1)[0]  # noqa: E731
         cat = lambda xs: np.concatenate(xs) if xs else np.zeros((0, 4), np.float32)  # noqa: E731
         cm = vg(cat([O.transform_cloud(x, t) for x, t in cparts]), 0.2)
         sm = vg(cat([O.transform_cloud(x, t) for x, t in sparts]), 0.4)
@@ -49,18 +51,20 @@ def mapping_step_oracle(seqs, assocs):
     return res
 
 
-def test_mapping_loop_matches_oracle(gpu):
+@pytest.mark.parametrize("order", [0, 1])
+def test_mapping_loop_matches_oracle(gpu, order):
     import lego_amd as LA
     streams = [_emitted(seq, 31) for seq in (3, 6, 8)]
     n = min(len(s) for s in streams)
     assert n >= 5
     s2m = LA.ScanToMap(max_problems=len(streams), max_map_points=150000, device=gpu)
+    s2m.set_voxel_tie_order(order)
     g = [M.MapSequence() for _ in streams]
     r = [M.MapSequence(associate=O.associate_to_map, odometry=O.odometry_to_transform) for _ in streams]
     ran = 0
     for k in range(n):
         out_g = M.mapping_step_gpu(s2m, g, [s[k] for s in streams])
-        out_r = mapping_step_oracle(r, [s[k] for s in streams])
+        out_r = mapping_step_oracle(r, [s[k] for s in streams], order)
         for p, ((tg, dgg, ig), (tr, dgr, ir)) in enumerate(zip(out_g, out_r)):
             assert np.abs(tg - tr).max() <= 1e-4, (k, p, tg, tr)
             assert dgg == dgr and ig[0] == ir[0] and ig[1] == ir[1], (k, p, ig, ir)

@@ -38,6 +38,12 @@ def run_pair(params, cfg, seq, nscans, scans=None):
     return results
 
 
+# scans whose transformed Last clouds were compared at 1e-3 because transform_cur differed (within the
+# north-star bar) from the oracle's; printed by the session fixture in conftest.py
+LAST_CLOUD_FALLBACKS = []
+LAST_CLOUD_CHECKS = [0]
+
+
 def assert_scan_parity(k, pg, pr, fg, fr, tf_tol=Hs.TF_TOL):
     bad = Hs.diff_report(Hs.PROJ_KEYS, pg, pr)
     assert not bad, ("projection", k, bad)
@@ -47,9 +53,17 @@ def assert_scan_parity(k, pg, pr, fg, fr, tf_tol=Hs.TF_TOL):
     assert (fg["lm_iter_surf"], fg["lm_iter_corner"]) == (fr["lm_iter_surf"], fr["lm_iter_corner"]), k
     np.testing.assert_allclose(fg["transform_cur"], fr["transform_cur"], atol=tf_tol, rtol=0)
     np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=tf_tol, rtol=0)
-    np.testing.assert_allclose(fg["corner_last"][:, :3], fr["corner_last"][:, :3], atol=1e-3, rtol=0)
     assert Hs.bits_equal(fg["corner_last"][:, 3], fr["corner_last"][:, 3])
-    np.testing.assert_allclose(fg["surf_last"][:, :3], fr["surf_last"][:, :3], atol=1e-3, rtol=0)
+    assert Hs.bits_equal(fg["surf_last"][:, 3], fr["surf_last"][:, 3])
+    LAST_CLOUD_CHECKS[0] += 1
+    if Hs.bits_equal(fg["transform_cur"], fr["transform_cur"]):
+        # TransformToEnd of bit-identical features with a bit-identical transform: bit-identical clouds
+        assert Hs.bits_equal(fg["corner_last"], fr["corner_last"]), k
+        assert Hs.bits_equal(fg["surf_last"], fr["surf_last"]), k
+    else:  # the transform differs within the bar: the clouds it moved differ by as much
+        LAST_CLOUD_FALLBACKS.append(k)
+        np.testing.assert_allclose(fg["corner_last"][:, :3], fr["corner_last"][:, :3], atol=1e-3, rtol=0)
+        np.testing.assert_allclose(fg["surf_last"][:, :3], fr["surf_last"][:, :3], atol=1e-3, rtol=0)
     assert Hs.bits_equal(fg["outlier_last"], fr["outlier_last"])
 
 

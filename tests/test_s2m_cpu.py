@@ -158,7 +158,8 @@ def test_s2m_abi_exports():
                      "lego_map_transform",
                      "lego_map_voxel", "lego_map_associate", "lego_map_odometry_to_transform", "lego_mapper_create",
                      "lego_mapper_destroy",
-                     "lego_mapper_step", "lego_mapper_key_poses"}
+                     "lego_mapper_step", "lego_mapper_key_poses", "lego_s2m_set_voxel_tie_order",
+                     "lego_mapper_set_voxel_tie_order"}
     assert "lego_test_s2m_debug" in hdr
     names.add("lego_test_s2m_debug")
     lib = C.CDLL(A.LIB_FRONTEND)
@@ -275,3 +276,78 @@ def test_normal_equation_order_gap(tmp_path):
     print(json.dumps(report))
     assert np.all(np.isfinite(fa_gap)) and np.all(np.isfinite(s2m_gap))
     assert fa_gap.max() < 1e-2 and s2m_gap.max() < 1e-2  # same trajectory, not a divergence
+
+
+def _associate_double_libm(S, B, A):
+    """transformAssociateToMap (mapOptmization.cpp:264-387) as a GCC 4.8 / 5 build evaluates it
+    (lego_params.fp_mode 1): unqualified sin / cos / asin / atan2 on floats are the double functions, each
+    expression evaluated in double and rounded where it is stored to a float."""
+    import math
+    f = np.float32
+    d = lambda x: float(x)  # noqa: E731
+    c, s = math.cos, math.sin
+    S, B, A = [[f(v) for v in t] for t in (S, B, A)]
+    x1 = f(c(d(S[1])) * d(f(B[3] - S[3])) - s(d(S[1])) * d(f(B[5] - S[5])))
+    y1 = f(B[4] - S[4])
+    z1 = f(s(d(S[1])) * d(f(B[3] - S[3])) + c(d(S[1])) * d(f(B[5] - S[5])))
+    y2 = f(c(d(S[0])) * d(y1) + s(d(S[0])) * d(z1))
+    z2 = f(-s(d(S[0])) * d(y1) + c(d(S[0])) * d(z1))
+    inc3 = f(c(d(S[2])) * d(x1) + s(d(S[2])) * d(y2))
+    inc4 = f(-s(d(S[2])) * d(x1) + c(d(S[2])) * d(y2))
+    inc5 = z2
+    tr = [f(g(d(v))) for v in (S[0], S[1], S[2], B[0], B[1], B[2], A[0], A[1], A[2]) for g in (s, c)]
+    sbcx, cbcx, sbcy, cbcy, sbcz, cbcz, sblx, cblx, sbly, cbly, sblz, cblz, salx, calx, saly, caly, salz, calz = tr
+    p1 = salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz
+    p2 = calx * calz * (cbly * sblz - cblz * sblx * sbly) - calx * salz * (cbly * cblz + sblx * sbly * sblz) + \
+        cblx * salx * sbly
+    p3 = calx * salz * (cblz * sbly - cbly * sblx * sblz) - calx * calz * (sbly * sblz + cbly * cblz * sblx) + \
+        cblx * cbly * salx
+    srx = -sbcx * p1 - cbcx * sbcy * p2 - cbcx * cbcy * p3
+    T = [f(0)] * 6
+    T[0] = f(-math.asin(d(srx)))
+    q1, q2 = caly * calz + salx * saly * salz, caly * salz - calz * salx * saly
+    q3, q4 = saly * salz + caly * calz * salx, calz * saly - caly * salx * salz
+    srycrx = sbcx * (cblx * cblz * q2 - cblx * sblz * q1 + calx * saly * sblx) - \
+        cbcx * cbcy * (q1 * (cblz * sbly - cbly * sblx * sblz) + q2 * (sbly * sblz + cbly * cblz * sblx) -
+                       calx * cblx * cbly * saly) + \
+        cbcx * sbcy * (q1 * (cbly * cblz + sblx * sbly * sblz) + q2 * (cbly * sblz - cblz * sblx * sbly) +
+                       calx * cblx * saly * sbly)
+    crycrx = sbcx * (cblx * sblz * q4 - cblx * cblz * q3 + calx * caly * sblx) + \
+        cbcx * cbcy * (q3 * (sbly * sblz + cbly * cblz * sblx) + q4 * (cblz * sbly - cbly * sblx * sblz) +
+                       calx * caly * cblx * cbly) - \
+        cbcx * sbcy * (q3 * (cbly * sblz - cblz * sblx * sbly) + q4 * (cbly * cblz + sblx * sbly * sblz) -
+                       calx * caly * cblx * sbly)
+    T[1] = f(math.atan2(d(srycrx) / c(d(T[0])), d(crycrx) / c(d(T[0]))))
+    srzcrx = (cbcz * sbcy - cbcy * sbcx * sbcz) * p3 - (cbcy * cbcz + sbcx * sbcy * sbcz) * p2 + cbcx * sbcz * p1
+    crzcrx = (cbcy * sbcz - cbcz * sbcx * sbcy) * p2 - (sbcy * sbcz + cbcy * cbcz * sbcx) * p3 + cbcx * cbcz * p1
+    T[2] = f(math.atan2(d(srzcrx) / c(d(T[0])), d(crzcrx) / c(d(T[0]))))
+    x1 = f(c(d(T[2])) * d(inc3) - s(d(T[2])) * d(inc4))
+    y1 = f(s(d(T[2])) * d(inc3) + c(d(T[2])) * d(inc4))
+    z1 = inc5
+    y2 = f(c(d(T[0])) * d(y1) - s(d(T[0])) * d(z1))
+    z2 = f(s(d(T[0])) * d(y1) + c(d(T[0])) * d(z1))
+    T[3] = f(d(A[3]) - (c(d(T[1])) * d(x1) + s(d(T[1])) * d(z2)))
+    T[4] = f(A[4] - y2)
+    T[5] = f(d(A[5]) - (-s(d(T[1])) * d(x1) + c(d(T[1])) * d(z2)))
+    return np.array(T, np.float32)
+
+
+def test_mapping_half_is_fp_mode_0():
+    """The mapping half implements lego_params.fp_mode 0 only (include/lego_s2m.h): no
+    lego_s2m / lego_map / lego_mapper entry point takes an fp_mode, and transformAssociateToMap
+    (lego_map_associate, the mapping loop's) is the float-libm evaluation bit for bit, which a GCC 4.8 / 5
+    build's double-libm evaluation (fp_mode 1) is not on a measurable share of poses."""
+    import re
+    from lego_amd import mapping as M
+    hdr = open(os.path.join(REPO, "include", "lego_s2m.h")).read()
+    decls = re.findall(r"int\s+lego_(?:s2m|map|mapper)_\w+\s*\([^;]*\);", hdr)
+    assert decls and not any("fp_mode" in d for d in decls)
+    rng = np.random.default_rng(5)
+    differ = 0
+    for _ in range(400):
+        t = rng.uniform(-1, 1, (3, 6)).astype(np.float32)
+        t[:, 3:] *= 50
+        got = M.transform_associate_to_map(t[0], t[1], t[2])
+        assert np.array_equal(got.view(np.int32), O.associate_to_map(t[0], t[1], t[2]).view(np.int32))
+        differ += not np.array_equal(got.view(np.int32), _associate_double_libm(t[0], t[1], t[2]).view(np.int32))
+    assert differ >= 20, differ  # the two libm models are distinguishable: the test discriminates
