@@ -2512,7 +2512,8 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, Lds& L, int n, i
   __syncthreads();
   PROF_T(t_vs0);
   if constexpr (kMode == 4) {
-    lvl_sort<16>(vkey, vval, L.u.buf, n);
+    if (n <= 512) lvl_sort<8>(vkey, vval, L.u.buf, n);
+    else lvl_sort<16>(vkey, vval, L.u.buf, n);
   } else if constexpr (kMode == 5) {
     lvl_sort<32>(vkey, vval, L.u.buf, n);
   } else if constexpr (kMode == 0) {
@@ -4731,7 +4732,8 @@ extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int3
       hipMemcpy(v, h_vals, n * 4, hipMemcpyHostToDevice) != hipSuccess) rc = LEGO_EDEVICE;
   if (rc == LEGO_OK) {
     if (is_float == 3 && n > 1024) hipLaunchKernelGGL(k_sort_test_lvl<32>, dim3(1), dim3(64), 0, 0, k, v, n);
-    else if (is_float == 3) hipLaunchKernelGGL(k_sort_test_lvl<16>, dim3(1), dim3(64), 0, 0, k, v, n);
+    else if (is_float == 3 && n > 512) hipLaunchKernelGGL(k_sort_test_lvl<16>, dim3(1), dim3(64), 0, 0, k, v, n);
+    else if (is_float == 3) hipLaunchKernelGGL(k_sort_test_lvl<8>, dim3(1), dim3(64), 0, 0, k, v, n);
     else hipLaunchKernelGGL(k_sort_test, dim3(1), dim3(64), 0, 0, k, v, n, is_float);
     if (hipGetLastError() != hipSuccess || hipMemcpy(h_keys, k, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(h_vals, v, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = LEGO_EDEVICE;

@@ -1451,10 +1451,12 @@ __global__ __launch_bounds__(VXS_TPB) void k_vxs_exchange(const VxsSeg* segs, co
   if (c0 >= g.l) return;
   const unsigned pv = pivot[s];
   const int nch = (g.l - g.f + VXS_CH - 1) / VXS_CH;
-  int before = 0, totR = 0;  // stops of the chunks before this one; right stops of the whole range
+  // left / right stops of the chunks before this one, right stops of the whole range (a chunk's packed
+  // counts fit 16 bits each; a range's do not)
+  int beforeL = 0, beforeR = 0, totR = 0;
   for (int q = 0; q < nch; ++q) {
     const int t = cnt[(size_t)s * maxch + q];
-    if (q < c) before += t;
+    if (q < c) { beforeL += t & 0xffff; beforeR += t >> 16; }
     totR += t >> 16;
   }
   const int p0 = c0 + threadIdx.x * VXS_EPT;
@@ -1467,16 +1469,18 @@ __global__ __launch_bounds__(VXS_TPB) void k_vxs_exchange(const VxsSeg* segs, co
     if (p > g.f && p < g.l) v += vxs_flags(k[e], pv);
   }
   int total;
-  int run = vxs_block_scan(v, sh, total) + before;  // lf | rf << 16 in (f, p)
+  const int pre = vxs_block_scan(v, sh, total);  // lf | rf << 16 before this thread's positions, in the block
+  int runL = (pre & 0xffff) + beforeL, runR = (pre >> 16) + beforeR;  // lf / rf in (f, p)
   int best = 0x7fffffff;
 #pragma unroll
   for (int e = 0; e < VXS_EPT; ++e) {
     const int p = p0 + e;
     if (!(p > g.f && p < g.l)) continue;
     const int fl = vxs_flags(k[e], pv);
-    const int A = run & 0xffff;                        // left stops in (f, p)
-    const int B = totR - (run >> 16) - (fl >> 16);     // right stops in (p, l)
-    run += fl;
+    const int A = runL;                            // left stops in (f, p)
+    const int B = totR - runR - (fl >> 16);        // right stops in (p, l)
+    runL += fl & 0xffff;
+    runR += fl >> 16;
     const bool lf = fl & 1, rf = fl >> 16;
     const int D = A - B;
     int rd = -1;

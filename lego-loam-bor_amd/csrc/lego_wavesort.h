@@ -244,7 +244,7 @@ LG_DEVICE void lv_carry(unsigned S, int p0, int& jb, int& ja, int& cf, int& cl) 
 
 template <int R>
 LG_DEVICE void lvl_sort(unsigned* nkey, uint16_t* nval, unsigned long long* buf, int n, int depth = -1) {
-  static_assert(R >= 16 && R <= 32, "final ranks need a range inside two lanes");
+  static_assert(R >= 8 && R <= 32, "final ranks reach two lanes either side; masks are 32 bits");
   const int lane = ws_lane();
   const int p0 = lane * R;
   if (n <= 1) return;
@@ -448,13 +448,17 @@ LG_DEVICE void lvl_sort(unsigned* nkey, uint16_t* nval, unsigned long long* buf,
   // count, and a range of > 16 positions (heap-sorted) is sorted already.  Keys are < 2^31 - 1 (the
   // padding's 2^31 - 1 sorts last), so bit 31 of a - b is (a < b), without compare masks.
   PROF_T(t_fin0);
-  int kp[15], kn[15];  // the previous lane's last 15 keys, the next lane's first 15
+  int kp[15], kn[15];  // the keys of positions p0 - 15 .. p0 - 1 and p0 + R .. p0 + R + 14 (lanes within 2)
 #pragma unroll
   for (int i = 0; i < 15; ++i) {
-    const int a = __shfl_up((int)e[R - 15 + i].y, 1);
-    const int b = __shfl_down((int)e[i].y, 1);
-    kp[i] = lane == 0 ? 0 : a;
-    kn[i] = lane == 63 ? 0x7fffffff : b;
+    const int qb = i - 15, qa = R + i;             // offsets from p0
+    const int db = (qb - (R - 1)) / R;             // floor(qb / R) (qb < 0): -1 or -2 lanes
+    const int da = qa / R;                         // +1 or +2 lanes
+    const int rb = qb - db * R, ra = qa - da * R;  // the register in that lane
+    const int a = __shfl_up((int)e[rb].y, -db);
+    const int b = __shfl_down((int)e[ra].y, da);
+    kp[i] = lane < -db ? 0 : a;
+    kn[i] = lane > 63 - da ? 0x7fffffff : b;
   }
   __syncthreads();  // buf reads are done: nkey / nval take the output
   // an opaque copy of p0: p0 + r here must not be shared with the loads before the loop (which
