@@ -272,8 +272,9 @@ int  lego_test_kd_knn(const float* cloud, int32_t n, const float* queries, int32
 /* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
  * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */
 int  lego_debug_prof(uint64_t* out256, int32_t reset);
-/* Kernel time of `blocks` concurrent one-wave copies of the device sort of h_keys (profile build). */
-int  lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, float* ms);
+/* Kernel time of `blocks` concurrent one-wave copies of the device sort of h_keys (profile build);
+ * mode 0 the stack emulation, 1 the level-synchronous one (n <= 2048). */
+int  lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, int32_t mode, float* ms);
 /* Counter calibration: k_project's input read patterns (mode 0 12-byte buffer loads, 1 16-byte loads,
  * 2 both passes) over S scans of device points (offs / cnts as lego_batch_run's), out[S * 1024]. */
 int  lego_debug_fetch_probe(int32_t mode, int32_t S, const void* pts, const int64_t* offs, const int32_t* cnts,

@@ -188,6 +188,7 @@ struct lego_batch {
   bool pend_ovl = false;     // the pending work belongs to the overlap schedule
   hipStream_t ls = nullptr;
   hipEvent_t ev_pub = nullptr, ev_ls = nullptr, ev_fe = nullptr;
+
   // Probe (lego_batch_set_probe): events around k_project and around k_fa_prep in the overlap
   // schedule, four per step, so the HBM-bound pair's durations inside the pipeline can be read
   // (lego_batch_probe_times) beside the back-to-back figure of lego_batch_time_hbm_stages.
@@ -573,10 +574,15 @@ static int run_association_ovl(lego_batch* b, hipStream_t st, bool wait_pub) {
   rc = lg_launch_concat(P, b->B, b->S, st);
   if (rc) return rc;
   if (hipEventRecord(b->ev_cat[0], st) != hipSuccess) return LEGO_EDEVICE;
-  if (hipStreamWaitEvent(b->vs[0], b->ev_cat[0], 0) != hipSuccess) return LEGO_EDEVICE;
-  rc = lg_launch_voxel(P, b->B, b->S, b->vs[0]);
+  // A/B (LEGO_VOXEL_TWO_STREAMS): odd scans' VoxelGrid on gs[0] (idle in this schedule), so k_voxel(k)
+  // may still run while k_voxel(k + 1) starts; a stream of its own measured slower for both orders
+  // (212k vs 268k scans/s with the stable order): one more stream than the 4 hardware queues.
+  static const bool two_vs = std::getenv("LEGO_VOXEL_TWO_STREAMS") != nullptr;
+  hipStream_t vst = (P.par && two_vs) ? b->gs[0] : b->vs[0];
+  if (hipStreamWaitEvent(vst, b->ev_cat[0], 0) != hipSuccess) return LEGO_EDEVICE;
+  rc = lg_launch_voxel(P, b->B, b->S, vst);
   if (rc) return rc;
-  if (hipEventRecord(b->ev_vox[0][P.par], b->vs[0]) != hipSuccess) return LEGO_EDEVICE;
+  if (hipEventRecord(b->ev_vox[0][P.par], vst) != hipSuccess) return LEGO_EDEVICE;
   return LEGO_OK;
 }
 

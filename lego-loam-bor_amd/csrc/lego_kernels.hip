@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -2809,10 +2810,23 @@ LG_DEVICE int lessflat_list(const ScanView& v, int st, int en, uint16_t* list) {
 // kMode as voxel_ring: 0 for voxel_tie_order 0 by the stack emulation; 4 and 5 by the level-synchronous
 // one, split by ring size (each with its own register and LDS budget); 1 and 2 split the stable order's
 // rings by size; 3 either order.
+// 6: voxel_tie_order 0, rings of at most 1024 points by the level-synchronous sort, larger ones by the
+// stack emulation (one launch; LDS the union of both layouts).
+union VoxMixLds {
+  ExtractLds e;
+  VoxLvlLds<16> l;
+};
+template <int kM, class Lds>
+LG_DEVICE void voxel_wave(const LgParams& P, const ScanView& v, Lds& L, int n, RingOut& o) {
+  for (int t = lane_id(); t < n; t += 64) vx_val(L)[t] = (uint16_t)t;
+  __syncthreads();
+  voxel_ring<kM>(P, v, L, n, 0, o);
+}
 template <int kMode>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kMode == 5 ? 2 : kMode == 4 ? 3 : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kMode == 5 ? 2 : (kMode == 4 || kMode == 6) ? 3 : 1)))
 void k_voxel(LgParams P, LgBufs B) {
-  __shared__ std::conditional_t<kMode == 4, VoxLvlLds<16>, std::conditional_t<kMode == 5, VoxLvlLds<32>, ExtractLds>> L;
+  __shared__ std::conditional_t<kMode == 4, VoxLvlLds<16>, std::conditional_t<kMode == 5, VoxLvlLds<32>,
+             std::conditional_t<kMode == 6, VoxMixLds, ExtractLds>>> L;
   const int V = P.V;
   const int b = blockIdx.x, sl = b / V, s = P.s0 + sl;
   const int ring = (b % V + sl / max(P.ncu / V, 1)) % V;  // ring rotation as in k_extract
@@ -2821,15 +2835,19 @@ void k_voxel(LgParams P, LgBufs B) {
   ScanView v;
   v.fa = B.lf_stage + sb * P.H;  // the ring's lessFlat points, in surfPointsLessFlatScan order
   const int n = B.lf_count[sb];
-  if (kMode != 3 && (P.voxel_stable ? (n > 1024 ? 2 : 1) : kMode >= 4 ? (n > 1024 ? 5 : 4) : 0) != kMode) return;
-  for (int t = lane_id(); t < n; t += 64) vx_val(L)[t] = (uint16_t)t;
-  __syncthreads();
+  if (kMode != 3 && kMode != 6 && (P.voxel_stable ? (n > 1024 ? 2 : 1) : kMode >= 4 ? (n > 1024 ? 5 : 4) : 0) != kMode)
+    return;
   RingOut o;
   o.lflat = B.r_lflat + sb * P.H;  // output half P.par too (k_publish of this scan reads it)
   o.nLF = 0;
   o.status = 0;
   PROF_T(t_vox0);
-  voxel_ring<kMode>(P, v, L, n, 0, o);
+  if constexpr (kMode == 6) {
+    if (n <= 1024) voxel_wave<4>(P, v, L.l, n, o);
+    else voxel_wave<0>(P, v, L.e, n, o);
+  } else {
+    voxel_wave<kMode>(P, v, L, n, o);
+  }
   PROF_ADD(4, t_vox0);
   if (lane_id() == 0) {
     B.r_vcount[sb] = o.nLF;
@@ -4050,6 +4068,8 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
       PROF_T(t_rs0);
       // ring-limited 2nd / 3rd points (fa.cpp:514-564, 652-713).  Larger clouds: one wave per query
       // over the index ranges the per-ring first / last indices give, 8 loads in flight per lane.
+      // (Visiting the 1-NN grid's cells instead, tpq lanes a query pruned by the lanes' bests, is exact
+      // too but measured slower: 251k vs 271k scans/s, 239k with the staged clouds as well.)
       if (!small) for (int q = wave_id(); q < nq; q += nw) {
         const int c = L.ind1[q];
         int o2 = -1, o3 = -1;
@@ -4473,8 +4493,15 @@ int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   // off the SIMDs k_lm holds, which measured faster there.  With more scans than CUs the split
   // kernels (the common one at 83 VGPRs shares SIMDs with k_lm) measured faster: 245k vs 226k
   // scans/s at S = 512.
-  static const bool legacy = std::getenv("LEGO_VOXEL_STACK_SORT") != nullptr;  // A/B: the stack emulation
-  if (!P.voxel_stable && !legacy) {
+  // voxel_tie_order 0 takes the stack emulation here: the level-synchronous sort (k_voxel<4> / <5>, or <6>
+  // for rings of at most 1024 points) has the lower latency on one ring but more instructions, and in the
+  // pipeline, where the VoxelGrid shares the CUs with k_lm and the next front end, it measured slower
+  // (C3: 143-151k / 164k vs 176-195k scans/s).  LEGO_VOXEL_SORT=level / mix selects them (A/B).
+  static const char* sort_env = std::getenv("LEGO_VOXEL_SORT");
+  static const int variant = !sort_env ? 0 : !strcmp(sort_env, "level") ? 1 : !strcmp(sort_env, "mix") ? 2 : 0;
+  if (!P.voxel_stable && variant == 2) {
+    hipLaunchKernelGGL(k_voxel<6>, dim3(S * P.V), dim3(64), 0, st, P, B);
+  } else if (!P.voxel_stable && variant == 1) {
     hipLaunchKernelGGL(k_voxel<4>, dim3(S * P.V), dim3(64), 0, st, P, B);
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_voxel<5>, dim3(S * P.V), dim3(64), 0, st, P, B);
@@ -4751,6 +4778,15 @@ __global__ __launch_bounds__(64) void k_sort_bench(const unsigned* keys, int n, 
   wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
   if (lane == 0) out[blockIdx.x] = L.vval[n / 2];
 }
+template <int R>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R == 32 ? 2 : 3)))
+void k_sort_bench_lvl(const unsigned* keys, int n, unsigned* out) {
+  __shared__ VoxLvlLds<R> L;
+  for (int i = lane_id(); i < n; i += 64) { L.u.nat.key[i] = keys[i]; L.u.nat.val[i] = (uint16_t)i; }
+  __syncthreads();
+  lvl_sort<R>(L.u.nat.key, L.u.nat.val, L.u.buf, n);
+  if (lane_id() == 0) out[blockIdx.x] = L.u.nat.val[n / 2];
+}
 #endif
 
 // Counter calibration (MI355X_MICROARCH.md: FETCH_SIZE is calibrated only for 16-B-per-lane streaming
@@ -4806,19 +4842,26 @@ extern "C" int lego_debug_fetch_probe(int32_t mode, int32_t S, const void* pts, 
 }
 
 // Diagnostics (profile build only): time `blocks` concurrent copies of one device sort.
-extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, float* ms) {
+// mode 0: the stack emulation (wave_std_sort), 1: the level-synchronous one (lvl_sort, R by size)
+extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, int32_t mode, float* ms) {
 #ifdef LG_PROFILE
   unsigned *k = nullptr, *o = nullptr;
-  if (n < 1 || n > RING_MAX || blocks < 1) return LEGO_EINVAL;
+  if (n < 1 || n > RING_MAX || blocks < 1 || (mode == 1 && n > 2048)) return LEGO_EINVAL;
   hipMalloc((void**)&k, n * 4);
   hipMalloc((void**)&o, blocks * 4);
   hipMemcpy(k, h_keys, n * 4, hipMemcpyHostToDevice);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
+  auto launch = [&]() {
+    if (mode == 0) hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
+    else if (n > 1024) hipLaunchKernelGGL(k_sort_bench_lvl<32>, dim3(blocks), dim3(64), 0, 0, k, n, o);
+    else if (n > 512) hipLaunchKernelGGL(k_sort_bench_lvl<16>, dim3(blocks), dim3(64), 0, 0, k, n, o);
+    else hipLaunchKernelGGL(k_sort_bench_lvl<8>, dim3(blocks), dim3(64), 0, 0, k, n, o);
+  };
+  launch();
   hipEventRecord(a, 0);
-  hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
+  launch();
   hipEventRecord(b, 0);
   hipEventSynchronize(b);
   hipEventElapsedTime(ms, a, b);
@@ -4828,7 +4871,7 @@ extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t 
   hipFree(o);
   return LEGO_OK;
 #else
-  (void)h_keys; (void)n; (void)blocks; (void)ms;
+  (void)h_keys; (void)n; (void)blocks; (void)mode; (void)ms;
   return LEGO_ENOTSUP;
 #endif
 }

@@ -1,5 +1,5 @@
-# Round-4 quick GPU check: selected parity tests, then bench lines (order 0 with the level-synchronous
-# VoxelGrid sort, the stack emulation for A/B, and order 1).
+# Round-4 quick GPU check: selected parity tests, then bench lines (order 0 with the stack emulation of
+# the VoxelGrid sort, the level-synchronous sort for A/B, and order 1).
 #   tools/r04_check.sh TAG "pytest -k expression"
 set -e
 TAG=$1; KEXPR=$2
@@ -12,6 +12,6 @@ if [ -n "$KEXPR" ]; then
 fi
 timeout -k 10 300 python3 bench.py --voxel-tie-order 0 --no-cpu-baseline --roofline-streams 0 > "$OUT/bench0.log" 2>&1
 tail -c 600 "$OUT/bench0.log"
-LEGO_VOXEL_STACK_SORT=1 timeout -k 10 300 python3 bench.py --voxel-tie-order 0 --no-cpu-baseline --roofline-streams 0 --no-alt-order > "$OUT/bench0_stack.log" 2>&1
-tail -c 300 "$OUT/bench0_stack.log"
+LEGO_VOXEL_SORT=level timeout -k 10 300 python3 bench.py --voxel-tie-order 0 --no-cpu-baseline --roofline-streams 0 --no-alt-order > "$OUT/bench0_level.log" 2>&1
+tail -c 300 "$OUT/bench0_level.log"
 echo done

@@ -5,7 +5,8 @@
 tools/data/voxel_keys_heavy.npz holds VoxelGrid key sequences of single rings recorded from the CPU
 oracle on synthetic VLP-16 scans (c110 drives libstdc++'s introsort into a 1309-element heap-sort
 fallback; c10 is an ordinary ring).  Each set is sorted by 1 block (latency) and by 256*11 blocks
-(one per wave slot of the chip, throughput).
+(one per wave slot of the chip, throughput), with the stack emulation (wave_std_sort) and the
+level-synchronous one (lvl_sort).
 """
 import ctypes as C
 import os
@@ -20,15 +21,19 @@ import lego_amd as L  # noqa: E402
 
 def main():
     lib = L.lib()
-    lib.lego_debug_sort_bench.argtypes = [C.POINTER(C.c_uint32), C.c_int32, C.c_int32, C.POINTER(C.c_float)]
+    lib.lego_debug_sort_bench.argtypes = [C.POINTER(C.c_uint32), C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_float)]
     d = np.load(os.path.join(REPO, "tools", "data", "voxel_keys_heavy.npz"))
     for name in d.files:
         k = np.ascontiguousarray(d[name].astype(np.uint32))
-        for blocks in (1, 256 * 11):
-            ms = C.c_float()
-            rc = lib.lego_debug_sort_bench(k.ctypes.data_as(C.POINTER(C.c_uint32)), len(k), blocks, C.byref(ms))
-            assert rc == 0, rc
-            print("%-5s n=%5d blocks=%5d  %.3f ms" % (name, len(k), blocks, ms.value))
+        for mode in (0, 1):
+            for blocks in (1, 256 * 11):
+                ms = C.c_float()
+                rc = lib.lego_debug_sort_bench(k.ctypes.data_as(C.POINTER(C.c_uint32)), len(k), blocks, mode,
+                                               C.byref(ms))
+                if rc != 0:
+                    print("%-5s n=%5d mode %d: rc %d" % (name, len(k), mode, rc))
+                    continue
+                print("%-5s n=%5d %-6s blocks=%5d  %.3f ms" % (name, len(k), ("stack", "level")[mode], blocks, ms.value))
 
 
 if __name__ == "__main__":
