@@ -77,6 +77,9 @@ LG_DEVICE K rdlane(K v, int l) {
 }
 
 // __sort_heap (= repeated __pop_heap + __adjust_heap from the root) with the whole wave.
+// (Round 4 measured a variant with two ballots and the descent as a branch-free walk on the scalar
+// unit: bit-exact but slower, 1.40 vs 1.03 ms on the heaviest recorded ring, 157-161k vs 195k scans/s
+// for order 0: ~75 dependent scalar operations a window cost more than the vector chain they replace.)
 // Each pop's hole descent depends on keys only.  A window is the 5-level subtree below a window
 // root x: lane l holds the key and value of one of its 62 nodes (level L = 1..5 at lanes
 // [2^L - 2, 2^(L+1) - 2), siblings in lanes l, l ^ 1), read with one LDS round trip.  A node is on
