@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--groups", type=int, default=1, help="stream slices launched on separate HIP streams")
     ap.add_argument("--wide", type=int, default=-1, choices=[-1, 0, 1],
                     help="projection / segmentation layout (lego_batch_set_wide): -1 automatic")
-    ap.add_argument("--lag", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--lag", type=int, default=1, choices=[0, 1, 2],
                     help="pipeline depth (lego_batch_set_lag): 1 = a step runs the previous scan's LM")
     ap.add_argument("--voxel-tie-order", type=int, default=0, choices=[0, 1],
                     help="lego_params.voxel_tie_order of the measured path: 0 = libstdc++ std::sort order, "

@@ -53,8 +53,8 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int epoch;                            // per-launch token for k_extract's first-pass flags
   float inv_res_x, inv_res_y;           // (float)(1 / ang_res_*) for the fast projection path
   int fast_proj;                        // the fast path's margins hold for these resolutions
-  int par;                              // parity of the launch's scan: the half of the double-buffered
-                                        // staging (features, lessFlat, VoxelGrid output) it uses
+  int par;                              // staging slot of the launch's scan (scan index mod LG_SLOTS):
+                                        // its features, lessFlat and VoxelGrid output
   int S;                                // streams of the batch (staging stride)
   int wide;                             // wide mode: k_pw_* / k_sw_* (many workgroups a scan)
   unsigned wtag;                        // wide mode: launch tag in the winner image entries' top 4 bits
@@ -94,6 +94,10 @@ struct KdNode {
   int pad;
 };
 
+// Staging slots of the front end -> VoxelGrid -> LM pipeline: scan k uses slot k mod LG_SLOTS, whose
+// previous user (scan k - LG_SLOTS) has published before scan k's k_concat refills it.
+#define LG_SLOTS 3
+
 struct LgBufs {  // device buffers, all indexed [stream][...]
   // ImageProjection
   float* range;          // [S][VH]
@@ -132,18 +136,18 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   float4* r_flat; int32_t* r_flat_ind;      // [S][V][cap_flat]
   int32_t* r_counts;                        // [S][V][4]   sharp, lessSharp, flat (k_extract), unused
   int32_t* r_status;                        // [S][V]      k_extract status bits
-  // [2][...]: halves by scan parity (LgParams.par), so scan k's VoxelGrid / publish / LM may run
-  // while scan k+1's front end fills the other half
-  float4* lf_stage;                         // [2][S][V][H] surfPointsLessFlatScan per ring (k_concat)
-  int32_t* lf_count;                        // [2][S][V]
-  float4* r_lflat;                          // [2][S][V][H] VoxelGrid output per ring (k_voxel)
-  int32_t* r_vcount;                        // [2][S][V]    its point count
-  int32_t* r_vstatus;                       // [2][S][V]    k_voxel status bits
+  // [LG_SLOTS][...]: slots by scan (LgParams.par = scan index mod LG_SLOTS), so scan k's VoxelGrid /
+  // publish / LM may run while scans k+1 and k+2 fill the other slots (pipeline lag up to 2)
+  float4* lf_stage;                         // [LG_SLOTS][S][V][H] surfPointsLessFlatScan per ring (k_concat)
+  int32_t* lf_count;                        // [LG_SLOTS][S][V]
+  float4* r_lflat;                          // [LG_SLOTS][S][V][H] VoxelGrid output per ring (k_voxel)
+  int32_t* r_vcount;                        // [LG_SLOTS][S][V]    its point count
+  int32_t* r_vstatus;                       // [LG_SLOTS][S][V]    k_voxel status bits
   // concatenated features
-  float4* f_sharp; int32_t* f_sharp_ind;    // [2][S][V*cap_sharp]
-  float4* f_lsharp; int32_t* f_lsharp_ind;  // [2][S][V*cap_lsharp]
-  float4* f_flat; int32_t* f_flat_ind;      // [2][S][V*cap_flat]
-  int32_t* fcnt;                            // [2][S][4]  sharp, lessSharp, flat counts, status (k_lm)
+  float4* f_sharp; int32_t* f_sharp_ind;    // [LG_SLOTS][S][V*cap_sharp]
+  float4* f_lsharp; int32_t* f_lsharp_ind;  // [LG_SLOTS][S][V*cap_lsharp]
+  float4* f_flat; int32_t* f_flat_ind;      // [LG_SLOTS][S][V*cap_flat]
+  int32_t* fcnt;                            // [LG_SLOTS][S][4]  sharp, lessSharp, flat counts, status (k_lm)
   float4* f_lflat;                          // [S][VH]
   // Last clouds, double-buffered
   float4* corner_last;   // [S][2][V*cap_lsharp]

@@ -169,16 +169,24 @@ struct lego_batch {
   //   lag 0: step k runs k_publish(k-1), then k_lm(k);  k_publish(k) stays pending.
   //   lag 1: step k runs k_publish(k-2), then k_lm(k-1); k_publish(k-1) and k_lm(k) stay pending,
   //          so k_voxel(k) has two steps of other work to hide behind.
+  //   lag 2 (overlap schedule only; the others run it as lag 1): step k runs k_publish(k-3), then
+  //          k_lm(k-2); k_voxel(k) starts a whole step before k_lm(k) and is due only at k_publish(k),
+  //          and consecutive VoxelGrid launches alternate between two streams, so one launch's
+  //          slowest ring no longer holds the next one back.
   // lego_batch_flush (and every read) issues what is pending.
   int lag = 1;
   hipStream_t vs[LEGO_MAX_GROUPS] = {};
-  hipEvent_t ev_cat[LEGO_MAX_GROUPS] = {}, ev_vox[LEGO_MAX_GROUPS][2] = {};
-  int par = 0;               // parity of the next front-end scan
-  int last_par = 0;          // parity of the last front-end scan (reads)
-  bool pend_pub = false;     // k_publish of a scan whose k_lm has run (parity pub_par)
+  hipEvent_t ev_cat[LEGO_MAX_GROUPS] = {}, ev_vox[LEGO_MAX_GROUPS][LG_SLOTS] = {};
+  hipEvent_t ev_cats[LG_SLOTS] = {};  // overlap schedule: k_concat of the scan in each slot
+  int vox_alt = 0;           // lag 2: the stream of the next VoxelGrid launch (vs[0] / gs[0])
+  int par = 0;               // staging slot of the next front-end scan
+  int last_par = 0;          // slot of the last front-end scan (reads)
+  bool pend_pub = false;     // k_publish of a scan whose k_lm has run (slot pub_par)
   int pub_par = 0;
-  bool pend_lm = false;      // k_lm of the last front-end scan (lag 1; parity lm_par)
+  bool pend_lm = false;      // k_lm of the last front-end scan (lag >= 1; slot lm_par)
   int lm_par = 0;
+  bool pend_lm_old = false;  // lag 2: k_lm of the scan before it (slot lm_par_old)
+  int lm_par_old = 0;
   int pend_groups = 1;       // slicing of the pending work
   // Overlap schedule (one slice, lag 1, timing off): k_publish(k-2) and k_lm(k-1) go to the internal
   // LM stream ls at the start of step k, ordered after k_concat(k-1) (ev_cat) and k_voxel(k-2)
@@ -212,9 +220,11 @@ struct lego_batch {
       if (join[g]) hipEventDestroy(join[g]);
       if (vs[g]) hipStreamDestroy(vs[g]);
       if (ev_cat[g]) hipEventDestroy(ev_cat[g]);
-      for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < LG_SLOTS; ++h)
         if (ev_vox[g][h]) hipEventDestroy(ev_vox[g][h]);
     }
+    for (int h = 0; h < LG_SLOTS; ++h)
+      if (ev_cats[h]) hipEventDestroy(ev_cats[h]);
     if (fork) hipEventDestroy(fork);
     if (ev_chain) hipEventDestroy(ev_chain);
     if (ls) hipStreamDestroy(ls);
@@ -355,11 +365,11 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   A(r_lsharp, S * V * P.cap_lsharp); A(r_lsharp_ind, S * V * P.cap_lsharp);
   A(r_flat, S * V * P.cap_flat); A(r_flat_ind, S * V * P.cap_flat);
   A(r_counts, S * V * 4); A(r_status, S * V);
-  A(lf_stage, 2 * S * V * H); A(lf_count, 2 * S * V);
-  A(r_lflat, 2 * S * V * H); A(r_vcount, 2 * S * V); A(r_vstatus, 2 * S * V);
-  A(f_sharp, 2 * S * V * P.cap_sharp); A(f_sharp_ind, 2 * S * V * P.cap_sharp);
-  A(f_lsharp, 2 * S * V * P.cap_lsharp); A(f_lsharp_ind, 2 * S * V * P.cap_lsharp);
-  A(f_flat, 2 * S * V * P.cap_flat); A(f_flat_ind, 2 * S * V * P.cap_flat); A(fcnt, 2 * S * 4);
+  A(lf_stage, LG_SLOTS * S * V * H); A(lf_count, LG_SLOTS * S * V);
+  A(r_lflat, LG_SLOTS * S * V * H); A(r_vcount, LG_SLOTS * S * V); A(r_vstatus, LG_SLOTS * S * V);
+  A(f_sharp, LG_SLOTS * S * V * P.cap_sharp); A(f_sharp_ind, LG_SLOTS * S * V * P.cap_sharp);
+  A(f_lsharp, LG_SLOTS * S * V * P.cap_lsharp); A(f_lsharp_ind, LG_SLOTS * S * V * P.cap_lsharp);
+  A(f_flat, LG_SLOTS * S * V * P.cap_flat); A(f_flat_ind, LG_SLOTS * S * V * P.cap_flat); A(fcnt, LG_SLOTS * S * 4);
   A(f_lflat, S * VH);
   A(corner_last, S * 2 * V * P.cap_lsharp); A(surf_last, S * 2 * VH); A(grid_pts, S * VH);
   A(state, S); A(fe_state, S * 2);
@@ -395,7 +405,7 @@ int lego_batch_reset(lego_batch* b) {
   if (hipMemset(B.smooth, 0, S * VH * sizeof(int2)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fp_sync, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   b->epoch = 0;
-  b->pend_pub = b->pend_lm = b->pend_ovl = false;
+  b->pend_pub = b->pend_lm = b->pend_lm_old = b->pend_ovl = false;
   b->par = b->last_par = 0;
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fe_state, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
@@ -517,7 +527,7 @@ static void advance_pipeline(lego_batch* b, bool lag, int groups) {
   }
   b->pend_groups = groups;
   b->last_par = b->par;
-  b->par ^= 1;
+  b->par = (b->par + 1) % LG_SLOTS;
 }
 
 static int ensure_streams(lego_batch* b, int groups) {
@@ -529,7 +539,7 @@ static int ensure_streams(lego_batch* b, int groups) {
     if (!b->vs[g] && hipStreamCreateWithFlags(&b->vs[g], hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
     if (!b->ev_cat[g] && hipEventCreateWithFlags(&b->ev_cat[g], hipEventDisableTiming) != hipSuccess)
       return LEGO_EDEVICE;
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < LG_SLOTS; ++h)
       if (!b->ev_vox[g][h] && hipEventCreateWithFlags(&b->ev_vox[g][h], hipEventDisableTiming) != hipSuccess)
         return LEGO_EDEVICE;
   }
@@ -555,6 +565,9 @@ static int ensure_ls(lego_batch* b) {
   if (!b->ev_pub && hipEventCreateWithFlags(&b->ev_pub, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_ls && hipEventCreateWithFlags(&b->ev_ls, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_fe && hipEventCreateWithFlags(&b->ev_fe, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
+  for (int h = 0; h < LG_SLOTS; ++h)
+    if (!b->ev_cats[h] && hipEventCreateWithFlags(&b->ev_cats[h], hipEventDisableTiming) != hipSuccess)
+      return LEGO_EDEVICE;
   return ensure_streams(b, 1);
 }
 
@@ -573,13 +586,17 @@ static int run_association_ovl(lego_batch* b, hipStream_t st, bool wait_pub) {
   if (wait_pub && hipStreamWaitEvent(st, b->ev_pub, 0) != hipSuccess) return LEGO_EDEVICE;
   rc = lg_launch_concat(P, b->B, b->S, st);
   if (rc) return rc;
-  if (hipEventRecord(b->ev_cat[0], st) != hipSuccess) return LEGO_EDEVICE;
-  // A/B (LEGO_VOXEL_TWO_STREAMS): odd scans' VoxelGrid on gs[0] (idle in this schedule), so k_voxel(k)
-  // may still run while k_voxel(k + 1) starts; a stream of its own measured slower for both orders
-  // (212k vs 268k scans/s with the stable order): one more stream than the 4 hardware queues.
+  if (hipEventRecord(b->ev_cats[P.par], st) != hipSuccess) return LEGO_EDEVICE;
+  // Lag 2 (and A/B at lag 1, LEGO_VOXEL_TWO_STREAMS): every other scan's VoxelGrid on gs[0] (idle in
+  // this schedule), so k_voxel(k) may still run while k_voxel(k + 1) starts; a stream of its own
+  // measured slower for both orders (212k vs 268k scans/s with the stable order): one more stream than
+  // the 4 hardware queues.  LEGO_VOXEL_ONE_STREAM keeps lag 2 on vs[0] (A/B).
   static const bool two_vs = std::getenv("LEGO_VOXEL_TWO_STREAMS") != nullptr;
-  hipStream_t vst = (P.par && two_vs) ? b->gs[0] : b->vs[0];
-  if (hipStreamWaitEvent(vst, b->ev_cat[0], 0) != hipSuccess) return LEGO_EDEVICE;
+  static const bool one_vs = std::getenv("LEGO_VOXEL_ONE_STREAM") != nullptr;
+  const bool alt = b->lag >= 2 ? !one_vs : two_vs;
+  hipStream_t vst = (alt && b->vox_alt) ? b->gs[0] : b->vs[0];
+  b->vox_alt ^= 1;
+  if (hipStreamWaitEvent(vst, b->ev_cats[P.par], 0) != hipSuccess) return LEGO_EDEVICE;
   rc = lg_launch_voxel(P, b->B, b->S, vst);
   if (rc) return rc;
   if (hipEventRecord(b->ev_vox[0][P.par], vst) != hipSuccess) return LEGO_EDEVICE;
@@ -590,18 +607,22 @@ static int run_association_ovl(lego_batch* b, hipStream_t st, bool wait_pub) {
 // call that left them, in the pending work's slicing.
 static int flush_pending(lego_batch* b) {
   if (!b->pend_pub && !b->pend_lm) return LEGO_OK;
-  if (b->pend_ovl) {  // on ls: publish(k-1), k_lm(k), publish(k); then the last step's stream waits for ls
+  if (b->pend_ovl) {  // on ls: publish(k-1), [k_lm(k-1), publish(k-1),] k_lm(k), publish(k); then the
+                      // last step's stream waits for ls
     int rc = LEGO_OK;
     if (b->pend_pub) rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
-    if (!rc && b->pend_lm) {
-      if (hipStreamWaitEvent(b->ls, b->ev_cat[0], 0) != hipSuccess) return LEGO_EDEVICE;
-      rc = issue_lm(b, b->ls, 0, b->S, b->lm_par);
-      if (!rc) rc = issue_publish(b, b->ls, 0, 0, b->S, b->lm_par);
+    for (int q = 0; q < 2 && !rc; ++q) {
+      const bool has = q == 0 ? b->pend_lm_old : b->pend_lm;
+      const int lp = q == 0 ? b->lm_par_old : b->lm_par;
+      if (!has) continue;
+      if (hipStreamWaitEvent(b->ls, b->ev_cats[lp], 0) != hipSuccess) return LEGO_EDEVICE;
+      rc = issue_lm(b, b->ls, 0, b->S, lp);
+      if (!rc) rc = issue_publish(b, b->ls, 0, 0, b->S, lp);
     }
     if (rc) return rc;
     if (hipEventRecord(b->ev_ls, b->ls) != hipSuccess) return LEGO_EDEVICE;
     if (hipStreamWaitEvent(b->last_stream, b->ev_ls, 0) != hipSuccess) return LEGO_EDEVICE;
-    b->pend_pub = b->pend_lm = b->pend_ovl = false;
+    b->pend_pub = b->pend_lm = b->pend_lm_old = b->pend_ovl = false;
     return LEGO_OK;
   }
   const int G = b->pend_groups;
@@ -631,7 +652,7 @@ int lego_batch_set_groups(lego_batch* b, int32_t groups) {
 }
 
 int lego_batch_set_lag(lego_batch* b, int32_t lag) {
-  if (!b || lag < 0 || lag > 1) return LEGO_EINVAL;
+  if (!b || lag < 0 || lag > 2) return LEGO_EINVAL;
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   int rc = flush_pending(b);  // the pending work belongs to the old schedule
   if (rc) return rc;
@@ -705,22 +726,30 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
       if (!rc && hipStreamWaitEvent(b->ls, b->ev_fe, 0) != hipSuccess) rc = LEGO_EDEVICE;
       if (rc) return rc;
     }
-    if (b->pend_lm) {  // k_lm(k-1) on ls, after k_concat(k-1)
-      if (hipStreamWaitEvent(b->ls, b->ev_cat[0], 0) != hipSuccess) return LEGO_EDEVICE;
-      rc = issue_lm(b, b->ls, 0, b->S, b->lm_par);
+    // the LM issued now: lag 1, k_lm(k-1) (the newest pending); lag 2, k_lm(k-2) (the older one)
+    const bool deep = b->lag >= 2;
+    const bool lm_now = deep ? b->pend_lm_old : b->pend_lm;
+    const int lm_slot = deep ? b->lm_par_old : b->lm_par;
+    if (lm_now) {  // on ls, after that scan's k_concat
+      if (hipStreamWaitEvent(b->ls, b->ev_cats[lm_slot], 0) != hipSuccess) return LEGO_EDEVICE;
+      rc = issue_lm(b, b->ls, 0, b->S, lm_slot);
     }
     if (!rc && !lm_after_fe) rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
     if (!rc) rc = run_association_ovl(b, st, pub_now);
     if (rc) return rc;
-    // pending now: publish(k-1) (its k_lm was just issued), k_lm(k)
-    b->pend_pub = b->pend_lm;
-    b->pub_par = b->lm_par;
+    // pending now: the publish of the LM just issued, then (lag 2) k_lm(k-1), and k_lm(k)
+    b->pend_pub = lm_now;
+    b->pub_par = lm_slot;
+    if (deep) {
+      b->pend_lm_old = b->pend_lm;
+      b->lm_par_old = b->lm_par;
+    }
     b->pend_lm = true;
     b->lm_par = b->par;
     b->pend_groups = 1;
     b->pend_ovl = true;
     b->last_par = b->par;
-    b->par ^= 1;
+    b->par = (b->par + 1) % LG_SLOTS;
     b->probe_cur = nullptr;
     return LEGO_OK;
   }

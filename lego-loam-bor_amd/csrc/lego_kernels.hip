@@ -2977,50 +2977,48 @@ __global__ __launch_bounds__(64) void k_extract(LgParams P, LgBufs B) {
 // ============================================================================================
 // k_concat: ring-ordered concatenation (cornerPointsSharp etc. are appended ring by ring)
 // ============================================================================================
-__global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
-  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+// One wave a ring (grid S * V, 64-lane workgroups: a whole-scan workgroup waited for 16 free wave slots
+// of one CU behind the VoxelGrid's waves); each ring's offsets are prefix sums over the ring counts.
+__global__ __launch_bounds__(64) void k_concat(LgParams P, LgBufs B) {
   const int V = P.V;
-  __shared__ int cnt3[3][65], off[3][65], stat[65];
-  if (tid < V) {  // per-ring counts and status, one thread a ring
-    const int32_t* rc = B.r_counts + ((size_t)s * V + tid) * 4;
-    cnt3[0][tid] = rc[0]; cnt3[1][tid] = rc[1]; cnt3[2][tid] = rc[2];
-    stat[tid] = B.r_status[(size_t)s * V + tid];
+  const int s = P.s0 + blockIdx.x / V, r = blockIdx.x % V, l = lane_id();
+  int c0 = 0, c1 = 0, c2 = 0, stat = 0;
+  if (l < V) {  // per-ring counts and status, one lane a ring
+    const int32_t* rc = B.r_counts + ((size_t)s * V + l) * 4;
+    c0 = rc[0]; c1 = rc[1]; c2 = rc[2];
+    stat = B.r_status[(size_t)s * V + l];
   }
-  __syncthreads();
-  if (tid == 0) {
-    int a[3] = {0, 0, 0};
-    int status = 0;
-    for (int r = 0; r < V; ++r) {
-      for (int k = 0; k < 3; ++k) { off[k][r] = a[k]; a[k] += cnt3[k][r]; }
-      status |= stat[r];
+  const int o0 = wave_sum(l < r ? c0 : 0), o1 = wave_sum(l < r ? c1 : 0), o2 = wave_sum(l < r ? c2 : 0);
+  const int n0 = __shfl(c0, r), n1 = __shfl(c1, r), n2 = __shfl(c2, r);
+  if (r == 0) {
+    const int a0 = wave_sum(c0), a1 = wave_sum(c1), a2 = wave_sum(c2), status = wave_or(stat);
+    if (l == 0) {
+      int32_t* cnt = B.counts + (size_t)s * CNT_N;
+      cnt[CNT_SHARP] = a0; cnt[CNT_LSHARP] = a1; cnt[CNT_FLAT] = a2;
+      cnt[CNT_STATUS] = status;
+      int32_t* fc = B.fcnt + ((size_t)P.par * P.S + s) * 4;  // k_lm's copy, slot P.par
+      fc[0] = a0; fc[1] = a1; fc[2] = a2; fc[3] = status;
+      B.fe_state[2 * s + 1] += 1;  // read by the next scan's front end (adjustOutlierCloud)
     }
-    int32_t* cnt = B.counts + (size_t)s * CNT_N;
-    cnt[CNT_SHARP] = a[0]; cnt[CNT_LSHARP] = a[1]; cnt[CNT_FLAT] = a[2];
-    cnt[CNT_STATUS] = status;
-    int32_t* fc = B.fcnt + ((size_t)P.par * P.S + s) * 4;  // k_lm's copy, half P.par
-    fc[0] = a[0]; fc[1] = a[1]; fc[2] = a[2]; fc[3] = status;
-    B.fe_state[2 * s + 1] += 1;  // read by the next scan's front end (adjustOutlierCloud)
   }
-  __syncthreads();
-  // feature clouds into half P.par: k_lm of this scan may run after the next scan's k_concat
+  // feature clouds into slot P.par: k_lm of this scan may run after the next scans' k_concat
   const size_t hs = (size_t)P.par * P.S + s;
-  for (int r = wave_id(); r < V; r += nt >> 6) {  // one wave a ring: ring-ordered concatenation
+  {  // ring-ordered concatenation
     const size_t rb = (size_t)s * V + r;
-    const int l = lane_id();
-    for (int t = l; t < cnt3[0][r]; t += 64) {
-      B.f_sharp[hs * V * P.cap_sharp + off[0][r] + t] = B.r_sharp[rb * P.cap_sharp + t];
-      B.f_sharp_ind[hs * V * P.cap_sharp + off[0][r] + t] = B.r_sharp_ind[rb * P.cap_sharp + t];
+    for (int t = l; t < n0; t += 64) {
+      B.f_sharp[hs * V * P.cap_sharp + o0 + t] = B.r_sharp[rb * P.cap_sharp + t];
+      B.f_sharp_ind[hs * V * P.cap_sharp + o0 + t] = B.r_sharp_ind[rb * P.cap_sharp + t];
     }
-    for (int t = l; t < cnt3[1][r]; t += 64) {
-      B.f_lsharp[hs * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp[rb * P.cap_lsharp + t];
-      B.f_lsharp_ind[hs * V * P.cap_lsharp + off[1][r] + t] = B.r_lsharp_ind[rb * P.cap_lsharp + t];
+    for (int t = l; t < n1; t += 64) {
+      B.f_lsharp[hs * V * P.cap_lsharp + o1 + t] = B.r_lsharp[rb * P.cap_lsharp + t];
+      B.f_lsharp_ind[hs * V * P.cap_lsharp + o1 + t] = B.r_lsharp_ind[rb * P.cap_lsharp + t];
     }
-    for (int t = l; t < cnt3[2][r]; t += 64) {
-      B.f_flat[hs * V * P.cap_flat + off[2][r] + t] = B.r_flat[rb * P.cap_flat + t];
-      B.f_flat_ind[hs * V * P.cap_flat + off[2][r] + t] = B.r_flat_ind[rb * P.cap_flat + t];
+    for (int t = l; t < n2; t += 64) {
+      B.f_flat[hs * V * P.cap_flat + o2 + t] = B.r_flat[rb * P.cap_flat + t];
+      B.f_flat_ind[hs * V * P.cap_flat + o2 + t] = B.r_flat_ind[rb * P.cap_flat + t];
     }
   }
-  // surfPointsLessFlatScan of every ring (:370-374) into staging half P.par, one wave per ring: the
+  // surfPointsLessFlatScan of the ring (:370-374) into staging slot P.par: the
   // VoxelGrid (k_voxel) reads only this copy, so it may overlap the next scan's front end
   ScanView v;
   v.M = B.counts[(size_t)s * CNT_N + CNT_M];
@@ -3032,7 +3030,7 @@ __global__ __launch_bounds__(1024) void k_concat(LgParams P, LgBufs B) {
   // with sp >= ep are skipped (their positions are not lessFlat candidates).  Eight chunks of 64
   // positions per batch: label loads issued together, point loads buffer-masked.
   const __amdgpu_buffer_rsrc_t rs_fa = buffer_rsrc(fa, (uint32_t)P.VH * 16u);
-  for (int r = wave_id(); r < V; r += nt >> 6) {
+  {
     const size_t rb = (size_t)s * V + r;
     const size_t sb = (size_t)P.par * P.S * V + rb;
     float4* dst = B.lf_stage + sb * P.H;
@@ -4214,62 +4212,48 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
 // k_lm has just produced (untransformed on the initialisation scan, :1181-1209).  Runs after both
 // k_lm and k_voxel of its scan, before the next scan's k_lm.
 // ============================================================================================
+// One wave a ring (grid S * V, 64-lane workgroups): a workgroup of a whole scan needed 16 wave slots of
+// one CU at once and waited behind the VoxelGrid / segmentation waves for most of their duration (the
+// trace showed 450-700 us a launch for < 20 us of work), with the next k_lm queued behind it.
 template <bool kF1>
-__global__ __launch_bounds__(1024) void k_publish(LgParams P, LgBufs B) {
-  const int s = P.s0 + blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+__global__ __launch_bounds__(64) void k_publish(LgParams P, LgBufs B) {
   const int V = P.V, VH = P.VH;
-  __shared__ int off[65], cnt[65], vst[65];
-  __shared__ float cur[6];
-  __shared__ int copy, nb;
-  const size_t hb = ((size_t)P.par * P.S + s) * V;  // k_voxel's output half of this scan
-  if (tid < V) {
-    cnt[tid] = B.r_vcount[hb + tid];
-    vst[tid] = B.r_vstatus[hb + tid];
-  }
-  if (tid == 64) {
-    const LgState& S = B.state[s];
-    for (int k = 0; k < 6; ++k) cur[k] = S.cur[k];
-    copy = S.pub_copy;
-    nb = S.last_buf;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int a = 0;
-    for (int r = 0; r < V; ++r) { off[r] = a; a += cnt[r]; }
-    off[V] = a;
-  }
-  __syncthreads();
+  const int s = P.s0 + blockIdx.x / V, r = blockIdx.x % V, lane = lane_id();
+  const size_t hb = ((size_t)P.par * P.S + s) * V;  // k_voxel's output slot of this scan
+  const int c = lane < V ? B.r_vcount[hb + lane] : 0;
+  const int o = wave_sum(lane < r ? c : 0);  // the ring's offset: the lessFlat rings in ring order
+  const int n_lflat = wave_sum(c);
+  const int n = __shfl(c, r);
+  const LgState& S0 = B.state[s];
   float c6[6];
-  for (int k = 0; k < 6; ++k) c6[k] = cur[k];
+  for (int k = 0; k < 6; ++k) c6[k] = S0.cur[k];
+  const int copy = S0.pub_copy, nb = S0.last_buf;
   const EndTrig<kF1> E = end_trig<kF1>(c6);
   float4* sl = B.surf_last + (size_t)s * 2 * VH + (size_t)nb * VH;
   float4* fl = B.f_lflat + (size_t)s * VH;
-  for (int r = wave_id(); r < V; r += nt >> 6) {  // one wave a ring
-    const float4* src = B.r_lflat + (hb + r) * P.H;
-    const int n = cnt[r], o = off[r];
-    for (int t0 = lane_id(); t0 < n; t0 += 64 * 4) {
-      float4 p4[4];
+  const float4* src = B.r_lflat + (hb + r) * P.H;
+  for (int t0 = lane; t0 < n; t0 += 64 * 4) {
+    float4 p4[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) p4[u] = src[min(t0 + 64 * u, n - 1)];
+    for (int u = 0; u < 4; ++u) p4[u] = src[min(t0 + 64 * u, n - 1)];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int t = t0 + 64 * u;
-        if (t < n) {
-          fl[o + t] = p4[u];
-          sl[o + t] = copy ? p4[u] : transform_to_end_t<kF1>(p4[u], c6, E);
-        }
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 64 * u;
+      if (t < n) {
+        fl[o + t] = p4[u];
+        sl[o + t] = copy ? p4[u] : transform_to_end_t<kF1>(p4[u], c6, E);
       }
     }
   }
-  if (tid == 0) {
-    int st = 0;
-    for (int r = 0; r < V; ++r) st |= vst[r];
-    const int n_lflat = off[V];
-    LgState& S = B.state[s];
-    S.n_surf_last = n_lflat;
-    S.tree_stale = copy ? 0 : !(S.n_corner_last > 10 && n_lflat > 100);
-    S.status |= st;
-    B.counts[(size_t)s * CNT_N + CNT_LFLAT] = n_lflat;
+  if (r == 0) {
+    const int st = wave_or(lane < V ? B.r_vstatus[hb + lane] : 0);
+    if (lane == 0) {
+      LgState& S = B.state[s];
+      S.n_surf_last = n_lflat;
+      S.tree_stale = copy ? 0 : !(S.n_corner_last > 10 && n_lflat > 100);
+      S.status |= st;
+      B.counts[(size_t)s * CNT_N + CNT_LFLAT] = n_lflat;
+    }
   }
 }
 
@@ -4520,15 +4504,15 @@ int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
 
 int lg_launch_publish(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   if (P.fp1)
-    hipLaunchKernelGGL(k_publish<true>, dim3(S), dim3(1024), 0, st, P, B);
+    hipLaunchKernelGGL(k_publish<true>, dim3(S * P.V), dim3(64), 0, st, P, B);
   else
-    hipLaunchKernelGGL(k_publish<false>, dim3(S), dim3(1024), 0, st, P, B);
+    hipLaunchKernelGGL(k_publish<false>, dim3(S * P.V), dim3(64), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
 
 int lg_launch_concat(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  hipLaunchKernelGGL(k_concat, dim3(S), dim3(1024), 0, st, P, B);
+  hipLaunchKernelGGL(k_concat, dim3(S * P.V), dim3(64), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }

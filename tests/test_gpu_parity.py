@@ -532,7 +532,10 @@ def test_wide_many_streams_match_oracle(gpu, kind, S, steps, every):
                                                               (3, 0, False, 6, 0), (2, 1, True, 6, 0),
                                                               (1, 0, True, 6, 0), (1, 1, False, 2, 0),
                                                               (2, 1, False, 2, 0), (1, 1, False, 6, 1),
-                                                              (1, 1, True, 6, 1), (1, 1, False, 2, 1)])
+                                                              (1, 1, True, 6, 1), (1, 1, False, 2, 1),
+                                                              (1, 2, False, 6, 0), (1, 2, True, 7, 0),
+                                                              (1, 2, False, 2, 0), (1, 2, False, 3, 0),
+                                                              (1, 2, False, 6, 1), (3, 2, False, 5, 0)])
 def test_batch_back_to_back_matches_oracle(gpu, groups, lag, alternate, steps, order):
     """Steps enqueued back to back with one sync at the end: the grouped slices then issue the
     deferred k_publish / k_lm inside the next step (per group, on its own streams) rather than in a
@@ -540,7 +543,9 @@ def test_batch_back_to_back_matches_oracle(gpu, groups, lag, alternate, steps, o
     in between (each step must order itself after the previous step's work).  The last scan and the
     accumulated poses equal S independent oracle runs.  steps = 2 checks scan 1, whose front end runs
     before scan 0's LM with lag 1 (its outlier cloud must already be adjustOutlierCloud'ed).  order 1 (the
-    stable VoxelGrid order) takes the schedule whose k_lm starts after the next scan's segmentation."""
+    stable VoxelGrid order) takes the schedule whose k_lm starts after the next scan's segmentation.  lag 2:
+    k_lm(k-2) in step k, three staging slots in use, the VoxelGrid launches alternating between two
+    streams (groups > 1 runs it as lag 1)."""
     import torch
     params = L.params_vlp16(voxel_tie_order=order)
     cfg = A.synth_cfg("vlp16")
