@@ -196,6 +196,11 @@ struct lego_batch {
   bool pend_ovl = false;     // the pending work belongs to the overlap schedule
   hipStream_t ls = nullptr;
   hipEvent_t ev_pub = nullptr, ev_ls = nullptr, ev_fe = nullptr;
+  // Phased overlap schedule (lag 1): the front end of scan k starts after k_lm(k-2) and k_lm(k-1) after
+  // scan k's k_concat, so the whole-CU front-end kernels never share the GPU with k_lm; the VoxelGrid
+  // (two alternating streams) fills the LM's spare CU resources.
+  hipEvent_t ev_lmdone = nullptr;
+  bool lm_ev_valid = false;
 
   // Probe (lego_batch_set_probe): events around k_project and around k_fa_prep in the overlap
   // schedule, four per step, so the HBM-bound pair's durations inside the pipeline can be read
@@ -231,6 +236,7 @@ struct lego_batch {
     if (ev_pub) hipEventDestroy(ev_pub);
     if (ev_ls) hipEventDestroy(ev_ls);
     if (ev_fe) hipEventDestroy(ev_fe);
+    if (ev_lmdone) hipEventDestroy(ev_lmdone);
   }
 };
 
@@ -530,13 +536,39 @@ static void advance_pipeline(lego_batch* b, bool lag, int groups) {
   b->par = (b->par + 1) % LG_SLOTS;
 }
 
+// Internal side streams (A/B switches, read once): LEGO_SIDE_PRIO=low creates the LM / VoxelGrid streams
+// at the lowest priority (the caller's stream, which carries the front end, keeps its own);
+// LEGO_VOX_CUMASK=k (1..7) restricts the VoxelGrid streams to k of every 8 CUs (hipExtStreamCreateWithCUMask),
+// so the front end's whole-CU workgroups find CUs without VoxelGrid waves.
+static hipError_t make_side_stream(hipStream_t* st, bool vox) {
+  static const char* pe = std::getenv("LEGO_SIDE_PRIO");
+  static const char* me = std::getenv("LEGO_VOX_CUMASK");
+  const int keep = me ? std::atoi(me) : 0;
+  if (vox && keep > 0 && keep < 8) {
+    uint32_t mask[16];
+    for (int w = 0; w < 16; ++w) {
+      uint32_t m = 0;
+      for (int b = 0; b < 32; ++b)
+        if (((w * 32 + b) & 7) < keep) m |= 1u << b;
+      mask[w] = m;
+    }
+    return hipExtStreamCreateWithCUMask(st, 16, mask);
+  }
+  if (pe && !strcmp(pe, "low")) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return hipErrorUnknown;
+    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, least);
+  }
+  return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
 static int ensure_streams(lego_batch* b, int groups) {
   if (!b->fork && hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_chain && hipEventCreateWithFlags(&b->ev_chain, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   for (int g = 0; g < groups; ++g) {
-    if (!b->gs[g] && hipStreamCreateWithFlags(&b->gs[g], hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
+    if (!b->gs[g] && make_side_stream(&b->gs[g], true) != hipSuccess) return LEGO_EDEVICE;
     if (!b->join[g] && hipEventCreateWithFlags(&b->join[g], hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
-    if (!b->vs[g] && hipStreamCreateWithFlags(&b->vs[g], hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
+    if (!b->vs[g] && make_side_stream(&b->vs[g], true) != hipSuccess) return LEGO_EDEVICE;
     if (!b->ev_cat[g] && hipEventCreateWithFlags(&b->ev_cat[g], hipEventDisableTiming) != hipSuccess)
       return LEGO_EDEVICE;
     for (int h = 0; h < LG_SLOTS; ++h)
@@ -561,14 +593,21 @@ static int chain_stream(lego_batch* b, hipStream_t st) {
 }
 
 static int ensure_ls(lego_batch* b) {
-  if (!b->ls && hipStreamCreateWithFlags(&b->ls, hipStreamNonBlocking) != hipSuccess) return LEGO_EDEVICE;
+  if (!b->ls && make_side_stream(&b->ls, false) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_pub && hipEventCreateWithFlags(&b->ev_pub, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_ls && hipEventCreateWithFlags(&b->ev_ls, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_fe && hipEventCreateWithFlags(&b->ev_fe, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
+  if (!b->ev_lmdone && hipEventCreateWithFlags(&b->ev_lmdone, hipEventDisableTiming) != hipSuccess)
+    return LEGO_EDEVICE;
   for (int h = 0; h < LG_SLOTS; ++h)
     if (!b->ev_cats[h] && hipEventCreateWithFlags(&b->ev_cats[h], hipEventDisableTiming) != hipSuccess)
       return LEGO_EDEVICE;
   return ensure_streams(b, 1);
+}
+
+static bool sched_phased() {
+  static const bool on = std::getenv("LEGO_SCHED_PHASED") && std::atoi(std::getenv("LEGO_SCHED_PHASED")) != 0;
+  return on;
 }
 
 // The front end of the overlap schedule after the projection: smoothness, extraction, then (after
@@ -593,7 +632,7 @@ static int run_association_ovl(lego_batch* b, hipStream_t st, bool wait_pub) {
   // the 4 hardware queues.  LEGO_VOXEL_ONE_STREAM keeps lag 2 on vs[0] (A/B).
   static const bool two_vs = std::getenv("LEGO_VOXEL_TWO_STREAMS") != nullptr;
   static const bool one_vs = std::getenv("LEGO_VOXEL_ONE_STREAM") != nullptr;
-  const bool alt = b->lag >= 2 ? !one_vs : two_vs;
+  const bool alt = (b->lag >= 2 || sched_phased()) ? !one_vs : two_vs;
   hipStream_t vst = (alt && b->vox_alt) ? b->gs[0] : b->vs[0];
   b->vox_alt ^= 1;
   if (hipStreamWaitEvent(vst, b->ev_cats[P.par], 0) != hipSuccess) return LEGO_EDEVICE;
@@ -714,7 +753,8 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     // meets k_lm(k-1) head-on (193k -> 167-177k scans/s), so that order keeps k_lm at the top too
     // (where the measured variants are listed).
     static const int sched_env = std::getenv("LEGO_SCHED_LM_AFTER_FE") ? std::atoi(std::getenv("LEGO_SCHED_LM_AFTER_FE")) : -1;
-    const bool lm_after_fe = sched_env >= 0 ? sched_env != 0 : b->P.voxel_stable;  // (A/B override)
+    const bool phased = sched_phased() && b->lag == 1;
+    const bool lm_after_fe = !phased && (sched_env >= 0 ? sched_env != 0 : b->P.voxel_stable);  // (A/B override)
     if (b->pend_pub) {  // publish(k-2) on ls, after its k_voxel (issue_publish waits for ev_vox)
       rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
       if (!rc && hipEventRecord(b->ev_pub, b->ls) != hipSuccess) rc = LEGO_EDEVICE;
@@ -730,13 +770,27 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     const bool deep = b->lag >= 2;
     const bool lm_now = deep ? b->pend_lm_old : b->pend_lm;
     const int lm_slot = deep ? b->lm_par_old : b->lm_par;
-    if (lm_now) {  // on ls, after that scan's k_concat
-      if (hipStreamWaitEvent(b->ls, b->ev_cats[lm_slot], 0) != hipSuccess) return LEGO_EDEVICE;
-      rc = issue_lm(b, b->ls, 0, b->S, lm_slot);
+    if (phased) {  // front end(k) after k_lm(k-2); k_lm(k-1) after k_concat(k)
+      if (b->lm_ev_valid && hipStreamWaitEvent(st, b->ev_lmdone, 0) != hipSuccess) return LEGO_EDEVICE;
+      rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+      if (!rc) rc = run_association_ovl(b, st, pub_now);
+      if (rc) return rc;
+      if (lm_now) {
+        if (hipStreamWaitEvent(b->ls, b->ev_cats[b->par], 0) != hipSuccess) return LEGO_EDEVICE;
+        rc = issue_lm(b, b->ls, 0, b->S, lm_slot);
+        if (!rc && hipEventRecord(b->ev_lmdone, b->ls) != hipSuccess) rc = LEGO_EDEVICE;
+        if (rc) return rc;
+        b->lm_ev_valid = true;
+      }
+    } else {
+      if (lm_now) {  // on ls, after that scan's k_concat
+        if (hipStreamWaitEvent(b->ls, b->ev_cats[lm_slot], 0) != hipSuccess) return LEGO_EDEVICE;
+        rc = issue_lm(b, b->ls, 0, b->S, lm_slot);
+      }
+      if (!rc && !lm_after_fe) rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+      if (!rc) rc = run_association_ovl(b, st, pub_now);
+      if (rc) return rc;
     }
-    if (!rc && !lm_after_fe) rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
-    if (!rc) rc = run_association_ovl(b, st, pub_now);
-    if (rc) return rc;
     // pending now: the publish of the LM just issued, then (lag 2) k_lm(k-1), and k_lm(k)
     b->pend_pub = lm_now;
     b->pub_par = lm_slot;
