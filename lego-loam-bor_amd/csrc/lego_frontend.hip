@@ -345,6 +345,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
   b->P.ncu = ncu;
+  b->P.lm_prio = std::getenv("LEGO_LM_PRIO") ? std::atoi(std::getenv("LEGO_LM_PRIO")) : 0;  // (A/B)
   b->P.S = n_streams;
   b->S = n_streams;
   b->max_points = max_points;
@@ -754,7 +755,9 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     // (where the measured variants are listed).
     static const int sched_env = std::getenv("LEGO_SCHED_LM_AFTER_FE") ? std::atoi(std::getenv("LEGO_SCHED_LM_AFTER_FE")) : -1;
     const bool phased = sched_phased() && b->lag == 1;
-    const bool lm_after_fe = !phased && (sched_env >= 0 ? sched_env != 0 : b->P.voxel_stable);  // (A/B override)
+    // With more scans than CUs the reference order takes it too (S = 1024: 239k vs 226k scans/s; at S = 256
+    // 188k vs 195k, so not there; round 4, profiles/r04_streams_sweep.txt).
+    const bool lm_after_fe = !phased && (sched_env >= 0 ? sched_env != 0 : (b->P.voxel_stable || b->S > b->P.ncu));  // (A/B override)
     if (b->pend_pub) {  // publish(k-2) on ls, after its k_voxel (issue_publish waits for ev_vox)
       rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
       if (!rc && hipEventRecord(b->ev_pub, b->ls) != hipSuccess) rc = LEGO_EDEVICE;

@@ -4263,6 +4263,9 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
   __shared__ LgState S;
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x;
   const int V = P.V, VH = P.VH;
+  if (P.lm_prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (P.lm_prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (P.lm_prio == 3) __builtin_amdgcn_s_setprio(3);
   // the scan's features: half P.par (k_concat), which the next scan's front end does not touch
   const size_t hs = (size_t)P.par * P.S + s;
   const int32_t* fc = B.fcnt + hs * 4;
