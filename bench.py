@@ -57,10 +57,11 @@ def parse():
     ap.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (test rehearsal)")
     ap.add_argument("--groups", type=int, default=1, help="stream slices launched on separate HIP streams")
-    ap.add_argument("--wide", type=int, default=-1, choices=[-1, 0, 1],
+    ap.add_argument("--wide", type=int, default=-1, choices=[-1, 0, 1, 2],
                     help="projection / segmentation layout (lego_batch_set_wide): -1 automatic")
-    ap.add_argument("--lag", type=int, default=1, choices=[0, 1, 2],
-                    help="pipeline depth (lego_batch_set_lag): 1 = a step runs the previous scan's LM")
+    ap.add_argument("--lag", type=int, default=None, choices=[0, 1, 2],
+                    help="pipeline depth (lego_batch_set_lag): 1 = a step runs the previous scan's LM, 2 = the one "
+                         "before; default 2 for voxel_tie_order 0, 1 for order 1 (the faster of each, DESIGN §4)")
     ap.add_argument("--voxel-tie-order", type=int, default=0, choices=[0, 1],
                     help="lego_params.voxel_tie_order of the measured path: 0 = libstdc++ std::sort order, "
                          "bit-identical to the GCC-built reference; 1 = VoxelGrid sums each voxel in point order "
@@ -174,6 +175,12 @@ def pmc_traffic(args, S, kernels):
     return int(sum(v["hbm_bytes"] for v in best[1])), os.path.relpath(best[0], REPO)
 
 
+def lag_for(args, order):
+    """The pipeline depth of a batch with this VoxelGrid order: --lag, else 2 for the reference's order (its
+    VoxelGrid gets two steps before its publish) and 1 for the stable order."""
+    return args.lag if args.lag is not None else (2 if order == 0 else 1)
+
+
 def roofline_kernels(wide):
     """The projection + smoothness kernels the roofline pair times: k_project + k_fa_prep4 in the LDS
     layout, k_pw_scatter + k_pw_columns + k_fa_prep4 in the wide layout."""
@@ -199,8 +206,9 @@ def roofline_at(args, L, A, mk_params, cfg, dev_index, stream):
     d_off = torch.from_numpy((np.arange(2 * Sb, dtype=np.int64) * cap).reshape(2, Sb)).to(d_pts.device)
     d_cnt = torch.from_numpy(cnt.reshape(2, Sb).astype(np.int32)).to(d_pts.device)
     b = L.Batch(params, Sb, cap, device=dev_index)
-    b.set_lag(args.lag)
+    b.set_lag(lag_for(args, args.voxel_tie_order))
     b.set_wide(args.wide)
+    wide_b = b.wide() == 1
     for k in range(2):
         b.step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
     b.flush()
@@ -214,8 +222,8 @@ def roofline_at(args, L, A, mk_params, cfg, dev_index, stream):
     del d_pts
     torch.cuda.empty_cache()
     achieved = b_tot / (ms * 1e-3) / 1e9
-    traffic, src = pmc_traffic(args, Sb, roofline_kernels(args.wide == 1 or args.kind == "hdl64"))
-    return {"streams": Sb, "bytes_per_launch": int(b_tot), "launch_ms": round(ms, 4), "achieved": round(achieved, 1),
+    traffic, src = pmc_traffic(args, Sb, roofline_kernels(wide_b))
+    return {"streams": Sb, "kernels": "+".join(roofline_kernels(wide_b)), "bytes_per_launch": int(b_tot), "launch_ms": round(ms, 4), "achieved": round(achieved, 1),
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
             "note": "%d scans per launch: working set %.2f GB, above the 256 MiB Infinity Cache" % (Sb, b_tot / 1e9)}
 
@@ -259,9 +267,11 @@ def main():
     d_off = torch.from_numpy(offs).to(dev)
     d_cnt = torch.from_numpy(host_cnt.astype(np.int32)).to(dev)
     batch = L.Batch(params, S, cap, device=local_dev)
+    lag = lag_for(args, args.voxel_tie_order)
     batch.set_groups(args.groups)
-    batch.set_lag(args.lag)
+    batch.set_lag(lag)
     batch.set_wide(args.wide)
+    wide_pw = batch.wide() == 1  # the projection's kernels: k_pw_scatter + k_pw_columns (else k_project)
     stream = torch.cuda.current_stream(dev)
 
     def step(k, b=None):
@@ -311,7 +321,7 @@ def main():
         params_alt = mk_params(voxel_tie_order=alt_order, fp_mode=args.fp_mode)
         batch_alt = L.Batch(params_alt, S, cap, device=local_dev)
         batch_alt.set_groups(args.groups)
-        batch_alt.set_lag(args.lag)
+        batch_alt.set_lag(lag_for(args, alt_order))
         batch_alt.set_wide(args.wide)
         el_alt = timed(batch_alt)
         batch_alt.close()
@@ -321,7 +331,7 @@ def main():
     # ---- the roofline pair inside the pipeline: the same steps again with events around k_project and
     # k_fa_prep4 of every step (lego_batch_set_probe; not the timed pass, whose value stays event-free)
     probe = None
-    if args.groups == 1 and args.lag == 1:
+    if args.groups == 1 and lag >= 1:
         batch.reset()
         batch.set_probe(True)
         timed(batch)
@@ -356,18 +366,19 @@ def main():
     b_smooth = 22.0 * float(m_last.sum())
     t_ms = pair_ms  # k_project + k_fa_prep4
     achieved = (b_proj + b_smooth) / (t_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args, S, roofline_kernels(args.wide == 1 or args.kind == "hdl64"))
+    traffic, traffic_src = pmc_traffic(args, S, roofline_kernels(wide_pw))
+    pk = "+".join(roofline_kernels(wide_pw)[:-1])  # the projection's kernel(s)
     big = roofline_at(args, L, A, mk_params, cfg, local_dev, stream) if world == 1 and args.roofline_streams > 0 else None
-    roofline = {"kernel": "k_project+k_fa_prep4 (projection+smoothness)", "bound": "hbm",
+    roofline = {"kernel": "%s+k_fa_prep4 (projection+smoothness)" % pk, "bound": "hbm",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "bytes_per_launch": int(b_proj + b_smooth), "launch_ms": round(t_ms, 4),
-                "launch_ms_source": "%d back-to-back k_project + k_fa_prep4 pairs between two hipEvents on the "
+                "launch_ms_source": "%d back-to-back %s + k_fa_prep4 pairs between two hipEvents on the "
                                     "launch stream (projection inputs alternating between the last two steps')"
-                                    % args.roofline_reps,
+                                    % (args.roofline_reps, pk),
                 "launch_ms_stage_events": round(stage[0] + stage[2], 4),
                 "frac_stage_events": round((b_proj + b_smooth) / ((stage[0] + stage[2]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "per_kernel": {"k_project": {"bytes": int(b_proj), "ms": round(stage[0], 4),
+                "per_kernel": {pk: {"bytes": int(b_proj), "ms": round(stage[0], 4),
                                              "GBps": round(b_proj / (stage[0] * 1e-3) / 1e9, 1)},
                                "k_fa_prep4": {"bytes": int(b_smooth), "ms": round(stage[2], 4),
                                              "GBps": round(b_smooth / (stage[2] * 1e-3) / 1e9, 1)}},
@@ -391,7 +402,7 @@ def main():
         "config": {"workload": "%s: batched synthetic %s sweeps, %d independent sequences per GPU x 1 scan per step"
                                % ("C3" if args.kind == "vlp16" else "C4", args.kind.upper(), S),
                    "V": V, "H": H, "points_per_scan": round(n_mean, 1), "streams_per_gpu": S,
-                   "parallelism": "sequence-sharded x%d" % world, "stream_groups": args.groups, "lag": args.lag,
+                   "parallelism": "sequence-sharded x%d" % world, "stream_groups": args.groups, "lag": lag,
                    "voxel_tie_order": args.voxel_tie_order, "fp_mode": args.fp_mode, "wide": int(batch.wide())},
         "roofline": roofline,
         "stages_ms": {"project": round(stage[0], 4), "segment": round(stage[1], 4), "fa_prep": round(stage[2], 4),

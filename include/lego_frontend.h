@@ -224,15 +224,17 @@ int  lego_batch_probe_times(lego_batch* b, float* ms2, int32_t* steps);
 #define LEGO_MAX_GROUPS 4
 int  lego_batch_set_groups(lego_batch* b, int32_t groups);
 /* Pipeline depth of lego_batch_step: 0 = a step runs its own scan's LM, 1 (default) = the previous
- * scan's (see lego_batch_step).  Results do not depend on it. */
+ * scan's, 2 = the one before (the VoxelGrid of a scan gets two steps before its publish; one stream
+ * group and timing off, else run as 1; see lego_batch_step).  Results do not depend on it. */
 int  lego_batch_set_lag(lego_batch* b, int32_t lag);
 /* Kernel layout of the projection and segmentation: 1 = wide (a scan's work over many workgroups,
  * per-scan images in HBM), 0 = one workgroup a scan with its images in LDS (only where they fit:
- * V <= 16, V*H < 32768; else LEGO_EINVAL), -1 (default) = automatic: wide where the images do not
- * fit LDS or where fewer than (compute units / 8) streams are in flight.  Results do not depend on
- * it. */
+ * V <= 16, V*H < 32768; else LEGO_EINVAL), 2 = the one-workgroup projection with the wide
+ * segmentation (where the projection's image fits LDS), -1 (default) = automatic: wide where the images
+ * do not fit LDS, where fewer than (compute units / 8) streams are in flight, or with voxel_tie_order 0
+ * and at most 2 streams a compute unit; else 0.  Results do not depend on it. */
 int  lego_batch_set_wide(lego_batch* b, int32_t mode);
-/* The layout in effect (1 wide, 0 one workgroup a scan), or LEGO_EINVAL. */
+/* The layout in effect (0, 1 or 2 as lego_batch_set_wide), or LEGO_EINVAL. */
 int  lego_batch_wide(const lego_batch* b);
 
 /* ---- test hooks ------------------------------------------------------------------ */

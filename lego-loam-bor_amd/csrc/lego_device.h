@@ -56,7 +56,7 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int par;                              // staging slot of the launch's scan (scan index mod LG_SLOTS):
                                         // its features, lessFlat and VoxelGrid output
   int S;                                // streams of the batch (staging stride)
-  int wide;                             // wide mode: k_pw_* / k_sw_* (many workgroups a scan)
+  int wide;                             // 1: k_pw_* / k_sw_* (many workgroups a scan); 2: k_project, k_sw_*
   unsigned wtag;                        // wide mode: launch tag in the winner image entries' top 4 bits
   int max_points;                       // input capacity per scan (wide scatter grid)
   int fp1;                              // lego_params.fp_mode == 1: unqualified libm calls in double

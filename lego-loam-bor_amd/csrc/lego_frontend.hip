@@ -135,8 +135,14 @@ bool lg_lds_segment(const LgParams& P);
 // Wide mode (k_pw_* / k_sw_*: a scan's projection and segmentation over many workgroups) where one
 // workgroup a scan cannot hold the images in LDS, and where too few scans are in flight to fill
 // the device with one workgroup each.
+// The wide layout (many small workgroups a scan) where the one-workgroup-a-scan kernels cannot hold the
+// scan in LDS, for few scans, and with the reference's VoxelGrid order up to 2 scans a CU: there the
+// VoxelGrid's and k_lm's long-lived waves sit on every CU, and a whole-CU k_project / k_segment_lds
+// workgroup waited for them to drain (C3 order 0, lag 2: 210-215k vs 194-199k scans/s with both
+// kernels whole-CU, 184k with only the projection so, mode 2).
 static int lg_wide_auto(const LgParams& P, int S) {
-  return (!lg_lds_projection(P) || !lg_lds_segment(P) || S * 8 <= P.ncu) ? 1 : 0;
+  if (!lg_lds_projection(P) || !lg_lds_segment(P) || S * 8 <= P.ncu) return 1;
+  return (!P.voxel_stable && S <= 2 * P.ncu) ? 1 : 0;
 }
 
 struct lego_batch {
@@ -447,7 +453,7 @@ int lego_batch_set_timing(lego_batch* b, int32_t enabled) {
 // bits of the winner image's entries.  At the wrap the image is zeroed on `st`, before the launches
 // that follow there (every earlier launch is ordered before them on `st`: chain_stream / joins).
 static int next_wtag(lego_batch* b, hipStream_t st) {
-  if (!b->P.wide) return LEGO_OK;
+  if (b->P.wide != 1) return LEGO_OK;
   if (++b->wepoch > 15) {
     b->wepoch = 1;
     if (hipMemsetAsync(b->B.winner, 0, (size_t)b->S * b->P.VH * sizeof(int32_t), st) != hipSuccess)
@@ -701,8 +707,9 @@ int lego_batch_set_lag(lego_batch* b, int32_t lag) {
 }
 
 int lego_batch_set_wide(lego_batch* b, int32_t mode) {
-  if (!b || mode < -1 || mode > 1) return LEGO_EINVAL;
+  if (!b || mode < -1 || mode > 2) return LEGO_EINVAL;
   if (mode == 0 && (!lg_lds_projection(b->P) || !lg_lds_segment(b->P))) return LEGO_EINVAL;
+  if (mode == 2 && !lg_lds_projection(b->P)) return LEGO_EINVAL;
   // both layouts keep the persistent state alike and leave their scratch reset: switchable at any step
   b->wide_req = mode;
   b->P.wide = mode < 0 ? lg_wide_auto(b->P, b->S) : mode;
@@ -756,8 +763,10 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     static const int sched_env = std::getenv("LEGO_SCHED_LM_AFTER_FE") ? std::atoi(std::getenv("LEGO_SCHED_LM_AFTER_FE")) : -1;
     const bool phased = sched_phased() && b->lag == 1;
     // With more scans than CUs the reference order takes it too (S = 1024: 239k vs 226k scans/s; at S = 256
-    // 188k vs 195k, so not there; round 4, profiles/r04_streams_sweep.txt).
-    const bool lm_after_fe = !phased && (sched_env >= 0 ? sched_env != 0 : (b->P.voxel_stable || b->S > b->P.ncu));  // (A/B override)
+    // 188k vs 195k with lag 1, so not there), and so does lag 2 (k_lm(k-2)'s inputs are ready long before:
+    // 214.6k vs 210.8k; round 4, profiles/r04_schedule_ab.txt).
+    const bool lm_after_fe = !phased && (sched_env >= 0 ? sched_env != 0 :
+                                         (b->P.voxel_stable || b->S > b->P.ncu || b->lag >= 2));  // (A/B override)
     if (b->pend_pub) {  // publish(k-2) on ls, after its k_voxel (issue_publish waits for ev_vox)
       rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
       if (!rc && hipEventRecord(b->ev_pub, b->ls) != hipSuccess) rc = LEGO_EDEVICE;

@@ -4409,7 +4409,7 @@ bool lg_lds_segment(const LgParams& P) {  // k_segment_lds packing
 
 int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
                       const int32_t* cnts, hipStream_t st) {
-  if (P.wide) {
+  if (P.wide == 1) {  // (mode 2: the one-workgroup projection, the wide segmentation)
     if (S >= 64)
       hipLaunchKernelGGL(k_pw_scatter<4>, dim3((P.max_points + 4 * PW_PTS - 1) / (4 * PW_PTS), S), dim3(PW_NT), 0, st,
                          P, B, pts, offs, cnts);
@@ -4432,7 +4432,8 @@ int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* p
 }
 
 int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  if (P.wide) {
+  if (P.wide) {  // modes 1 and 2: both projections leave the same range / cloud / ground images, 2-D scan
+                 // candidates and orientation, which are all the k_sw_* kernels read
     const dim3 g((P.VH + SW_TILE - 1) / SW_TILE, S);
     const dim3 g2((P.H + SW_TC - 1) / SW_TC, (P.V + SW_TR - 1) / SW_TR, S);
     hipLaunchKernelGGL(k_sw_local, g2, dim3(SW_NT), 0, st, P, B);

@@ -252,16 +252,17 @@ class Batch:
         return float(ms[0]), float(ms[1]), int(n.value)
 
     def set_lag(self, lag):
-        """Pipeline depth: 0 = a step runs its own scan's LM, 1 (default) = the previous scan's."""
+        """Pipeline depth: 0 = a step runs its own scan's LM, 1 (default) = the previous scan's, 2 = the one before."""
         _check(lib().lego_batch_set_lag(self.h, int(lag)), "lego_batch_set_lag")
 
     def set_wide(self, mode):
         """Projection / segmentation layout: 1 wide (many workgroups a scan), 0 one workgroup a scan
-        (LDS images), -1 automatic."""
+        (LDS images), 2 one-workgroup projection + wide segmentation, -1 automatic."""
         _check(lib().lego_batch_set_wide(self.h, int(mode)), "lego_batch_set_wide")
 
     def wide(self):
-        return bool(lib().lego_batch_wide(self.h))
+        """The layout in effect: 0, 1 or 2 (set_wide)."""
+        return int(lib().lego_batch_wide(self.h))
 
     def counts(self):
         """[S, 7] int32: segmented, outlier, scan_msg, sharp, less sharp, flat, less flat counts."""

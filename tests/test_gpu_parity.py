@@ -496,10 +496,13 @@ def test_batch_streams_match_oracle(gpu, groups, wide, fp_mode):
     b.close()
 
 
-@pytest.mark.parametrize("kind,S,steps,every", [("vlp16", 64, 3, 1), ("hdl64", 64, 2, 8)])
-def test_wide_many_streams_match_oracle(gpu, kind, S, steps, every):
+@pytest.mark.parametrize("kind,S,steps,every,mode", [("vlp16", 64, 3, 1, 1), ("hdl64", 64, 2, 8, 1),
+                                                    ("vlp16", 64, 3, 1, 2)])
+def test_wide_many_streams_match_oracle(gpu, kind, S, steps, every, mode):
     """The wide layout with many scans in flight (k_pw_scatter's multi-batch workgroups, S >= 64;
-    HDL-64E's bench layout) equals independent oracle runs (every `every`-th stream checked)."""
+    HDL-64E's bench layout) equals independent oracle runs (every `every`-th stream checked).  mode 2:
+    the one-workgroup projection feeding the wide segmentation (the VLP-16 bench layout with
+    voxel_tie_order 0)."""
     import torch
     params = L.params_vlp16() if kind == "vlp16" else L.params_hdl64()
     cfg = A.synth_cfg(kind)
@@ -511,8 +514,8 @@ def test_wide_many_streams_match_oracle(gpu, kind, S, steps, every):
     offs = torch.from_numpy((np.arange(S * steps, dtype=np.int64) * cap).reshape(steps, S)).cuda()
     cnts = torch.from_numpy(cnt.reshape(steps, S).astype(np.int32)).cuda()
     b = L.Batch(params, S, cap)
-    b.set_wide(1)
-    assert b.wide() == 1
+    b.set_wide(mode)
+    assert b.wide() == mode
     for k in range(steps):
         b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), torch.cuda.current_stream().cuda_stream)
     b.sync()
@@ -578,7 +581,43 @@ def test_batch_back_to_back_matches_oracle(gpu, groups, lag, alternate, steps, o
     b.close()
 
 
-@pytest.mark.parametrize("wide", [0, 1])
+@pytest.mark.parametrize("wide,order", [(0, 0), (1, 0), (2, 0), (2, 1), (-1, 0)])
+def test_lag2_layouts_match_oracle(gpu, wide, order):
+    """Lag 2 (k_lm(k-2) in step k, three staging slots, alternating VoxelGrid streams, k_lm after the
+    front end's segmentation) in every projection / segmentation layout, steps on two alternating
+    caller streams without a sync: the last scan and the poses equal S independent oracle runs."""
+    import torch
+    params = L.params_vlp16(voxel_tie_order=order)
+    cfg = A.synth_cfg("vlp16")
+    S, steps = 5, 7
+    cap = params.num_vertical_scans * params.num_horizontal_scans
+    seqs = np.repeat(np.arange(S)[None, :] + 300, steps, 0).reshape(-1)
+    scans = np.repeat(np.arange(steps)[:, None], S, 1).reshape(-1)
+    pts, cnt = A.synth_batch(cfg, seqs, scans)
+    d_pts = torch.from_numpy(pts).cuda()
+    offs = torch.from_numpy((np.arange(S * steps, dtype=np.int64) * cap).reshape(steps, S)).cuda()
+    cnts = torch.from_numpy(cnt.reshape(steps, S).astype(np.int32)).cuda()
+    torch.cuda.synchronize()
+    b = L.Batch(params, S, cap)
+    b.set_lag(2)
+    b.set_wide(wide)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for k in range(steps):
+        b.step(d_pts.data_ptr(), offs[k].data_ptr(), cnts[k].data_ptr(), streams[k % 2].cuda_stream)
+    b.sync()
+    poses, st = b.poses()
+    for s in range(S):
+        orc = oracle_for(params)
+        for k in range(steps):
+            pr = orc.cloud_handler(pts[k * S + s, :cnt[k * S + s]])
+            fr = orc.feature_association()
+        pg, fg = b.read(s)
+        assert_scan_parity(steps - 1, pg, pr, fg, fr)
+        np.testing.assert_allclose(poses[s, 6:], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
+    b.close()
+
+
+@pytest.mark.parametrize("wide", [0, 1, 2])
 def test_hbm_stage_timing_leaves_results(gpu, wide):
     """bench.py's roofline timing (k_project + k_fa_prep launched back to back, the projections
     alternating between two steps' inputs and ending on the last step's) leaves every scan's results

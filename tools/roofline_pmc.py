@@ -1,6 +1,6 @@
 """The roofline pair alone at S scans per launch (bench.py's roofline_at), for a rocprofv3 PMC pass whose
 per-dispatch figures then match bench.py's `roofline.at_roofline_streams` (tools/pmc_summarize.py
---streams S).  python tools/roofline_pmc.py [S]"""
+--streams S).  python tools/roofline_pmc.py [S] [vlp16|hdl64]"""
 import os
 import sys
 
@@ -15,7 +15,8 @@ def main():
     import lego_amd as L
     from lego_amd import _abi as A
     S = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
-    sys.argv = [sys.argv[0], "--roofline-streams", str(S), "--roofline-reps", "3"]
+    kind = sys.argv[2] if len(sys.argv) > 2 else "vlp16"
+    sys.argv = [sys.argv[0], "--roofline-streams", str(S), "--roofline-reps", "3", "--kind", kind]
     args = bench.parse()
     cfg = A.synth_cfg(args.kind)
     stream = torch.cuda.Stream()

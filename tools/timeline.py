@@ -5,7 +5,8 @@
 Prints, per step of the timed region, each kernel's start and end relative to the step's k_project
 start (microseconds), so it shows which launch a step waits for: e.g. whether k_publish(k-2) starts
 at k_voxel(k-2)'s end (the VoxelGrid on the critical path) or at k_lm(k-3)'s.  The throughput pass
-is the first W + K launches of k_project (bench.py's later passes follow it).
+is the first W + K launches of k_project (k_pw_scatter in the wide layout; bench.py's later passes
+follow it).
 """
 import argparse
 import csv
@@ -24,7 +25,7 @@ def main():
             continue
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
-    proj = [r for r in rows if r[2] == "k_project"]
+    proj = [r for r in rows if r[2] == "k_project"] or [r for r in rows if r[2].startswith("k_pw_scatter")]
     per = a.steps + a.warmup
     starts = [p[0] for p in proj[:per + 1]]
     t_end = proj[per][0] if len(proj) > per else rows[-1][1]
