@@ -2517,8 +2517,10 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, Lds& L, int n, i
     else lvl_sort<16>(vkey, vval, L.u.buf, n);
   } else if constexpr (kMode == 5) {
     lvl_sort<32>(vkey, vval, L.u.buf, n);
-  } else if constexpr (kMode == 0) {
-    wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, true);
+  } else if constexpr (kMode == 0 || kMode == 7) {
+    // 7 (A/B, LEGO_VOXEL_SORT=ins): __final_insertion_sort as per-block insertion sorts in LDS (54 VGPRs
+    // instead of 132: the register sort's 2,048 (key, position) pairs are 64 VGPRs)
+    wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, kMode == 0);
   } else if constexpr (kMode == 3) {
     if (P.voxel_stable) voxel_sort_stable<3>(vkey, vval, n);
     else wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, true);
@@ -2835,7 +2837,8 @@ void k_voxel(LgParams P, LgBufs B) {
   ScanView v;
   v.fa = B.lf_stage + sb * P.H;  // the ring's lessFlat points, in surfPointsLessFlatScan order
   const int n = B.lf_count[sb];
-  if (kMode != 3 && kMode != 6 && (P.voxel_stable ? (n > 1024 ? 2 : 1) : kMode >= 4 ? (n > 1024 ? 5 : 4) : 0) != kMode)
+  if (kMode != 3 && kMode != 6 && kMode != 7 &&
+      (P.voxel_stable ? (n > 1024 ? 2 : 1) : kMode >= 4 ? (n > 1024 ? 5 : 4) : 0) != kMode)
     return;
   RingOut o;
   o.lflat = B.r_lflat + sb * P.H;  // output half P.par too (k_publish of this scan reads it)
@@ -4486,8 +4489,13 @@ int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   // pipeline, where the VoxelGrid shares the CUs with k_lm and the next front end, it measured slower
   // (C3: 143-151k / 164k vs 176-195k scans/s).  LEGO_VOXEL_SORT=level / mix selects them (A/B).
   static const char* sort_env = std::getenv("LEGO_VOXEL_SORT");
-  static const int variant = !sort_env ? 0 : !strcmp(sort_env, "level") ? 1 : !strcmp(sort_env, "mix") ? 2 : 0;
-  if (!P.voxel_stable && variant == 2) {
+  static const int variant = !sort_env ? 0 : !strcmp(sort_env, "level") ? 1 : !strcmp(sort_env, "mix") ? 2 :
+                             !strcmp(sort_env, "ins") ? 3 : !strcmp(sort_env, "stack0") ? 4 : 0;
+  if (!P.voxel_stable && variant == 4) {
+    hipLaunchKernelGGL(k_voxel<0>, dim3(S * P.V), dim3(64), 0, st, P, B);
+  } else if (!P.voxel_stable && variant == 3) {
+    hipLaunchKernelGGL(k_voxel<7>, dim3(S * P.V), dim3(64), 0, st, P, B);
+  } else if (!P.voxel_stable && variant == 2) {
     hipLaunchKernelGGL(k_voxel<6>, dim3(S * P.V), dim3(64), 0, st, P, B);
   } else if (!P.voxel_stable && variant == 1) {
     hipLaunchKernelGGL(k_voxel<4>, dim3(S * P.V), dim3(64), 0, st, P, B);
