@@ -207,6 +207,11 @@ struct lego_batch {
   // (two alternating streams) fills the LM's spare CU resources.
   hipEvent_t ev_lmdone = nullptr;
   bool lm_ev_valid = false;
+  // Deferred VoxelGrid (lag 2, A/B LEGO_VOX_DEFER): scan k's k_voxel is issued in step k+1 after that
+  // step's segmentation (ev_fe), so the projection and segmentation start on CUs the VoxelGrid's waves
+  // do not hold; its publish is two steps later still.
+  bool vox_pend = false;
+  int vox_pend_par = 0;
 
   // Probe (lego_batch_set_probe): events around k_project and around k_fa_prep in the overlap
   // schedule, four per step, so the HBM-bound pair's durations inside the pipeline can be read
@@ -418,7 +423,7 @@ int lego_batch_reset(lego_batch* b) {
   if (hipMemset(B.smooth, 0, S * VH * sizeof(int2)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fp_sync, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   b->epoch = 0;
-  b->pend_pub = b->pend_lm = b->pend_lm_old = b->pend_ovl = false;
+  b->pend_pub = b->pend_lm = b->pend_lm_old = b->pend_ovl = b->vox_pend = false;
   b->par = b->last_par = 0;
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fe_state, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
@@ -612,6 +617,22 @@ static int ensure_ls(lego_batch* b) {
   return ensure_streams(b, 1);
 }
 
+// k_voxel of the scan in slot par on the VoxelGrid stream (alternating with gs[0] when alt), after that
+// scan's k_concat and, when given, the event `after`.
+static int launch_vox(lego_batch* b, int par, bool alt, hipEvent_t after) {
+  LgParams P = b->P;
+  P.s0 = 0;
+  P.par = par;
+  hipStream_t vst = (alt && b->vox_alt) ? b->gs[0] : b->vs[0];
+  b->vox_alt ^= 1;
+  if (hipStreamWaitEvent(vst, b->ev_cats[par], 0) != hipSuccess) return LEGO_EDEVICE;
+  if (after && hipStreamWaitEvent(vst, after, 0) != hipSuccess) return LEGO_EDEVICE;
+  int rc = lg_launch_voxel(P, b->B, b->S, vst);
+  if (rc) return rc;
+  if (hipEventRecord(b->ev_vox[0][par], vst) != hipSuccess) return LEGO_EDEVICE;
+  return LEGO_OK;
+}
+
 static bool sched_phased() {
   static const bool on = std::getenv("LEGO_SCHED_PHASED") && std::atoi(std::getenv("LEGO_SCHED_PHASED")) != 0;
   return on;
@@ -640,13 +661,13 @@ static int run_association_ovl(lego_batch* b, hipStream_t st, bool wait_pub) {
   static const bool two_vs = std::getenv("LEGO_VOXEL_TWO_STREAMS") != nullptr;
   static const bool one_vs = std::getenv("LEGO_VOXEL_ONE_STREAM") != nullptr;
   const bool alt = (b->lag >= 2 || sched_phased()) ? !one_vs : two_vs;
-  hipStream_t vst = (alt && b->vox_alt) ? b->gs[0] : b->vs[0];
-  b->vox_alt ^= 1;
-  if (hipStreamWaitEvent(vst, b->ev_cats[P.par], 0) != hipSuccess) return LEGO_EDEVICE;
-  rc = lg_launch_voxel(P, b->B, b->S, vst);
-  if (rc) return rc;
-  if (hipEventRecord(b->ev_vox[0][P.par], vst) != hipSuccess) return LEGO_EDEVICE;
-  return LEGO_OK;
+  static const bool defer = std::getenv("LEGO_VOX_DEFER") && std::atoi(std::getenv("LEGO_VOX_DEFER")) != 0;
+  if (defer && b->lag >= 2) {
+    b->vox_pend = true;
+    b->vox_pend_par = P.par;
+    return LEGO_OK;
+  }
+  return launch_vox(b, P.par, alt, nullptr);
 }
 
 // Issue the pending k_publish / k_lm (each publish joined with its k_voxel) on the stream of the
@@ -656,6 +677,11 @@ static int flush_pending(lego_batch* b) {
   if (b->pend_ovl) {  // on ls: publish(k-1), [k_lm(k-1), publish(k-1),] k_lm(k), publish(k); then the
                       // last step's stream waits for ls
     int rc = LEGO_OK;
+    if (b->vox_pend) {  // the deferred VoxelGrid first (its publish follows)
+      b->vox_pend = false;
+      rc = launch_vox(b, b->vox_pend_par, true, nullptr);
+      if (rc) return rc;
+    }
     if (b->pend_pub) rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
     for (int q = 0; q < 2 && !rc; ++q) {
       const bool has = q == 0 ? b->pend_lm_old : b->pend_lm;
@@ -776,6 +802,15 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
       rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
       if (!rc && hipEventRecord(b->ev_fe, st) != hipSuccess) rc = LEGO_EDEVICE;
       if (!rc && hipStreamWaitEvent(b->ls, b->ev_fe, 0) != hipSuccess) rc = LEGO_EDEVICE;
+      if (!rc && b->vox_pend) {  // the previous scan's deferred VoxelGrid, after this segmentation
+        b->vox_pend = false;
+        rc = launch_vox(b, b->vox_pend_par, true, b->ev_fe);
+      }
+      if (rc) return rc;
+    }
+    if (b->vox_pend) {  // (no segmentation event this step: the deferred VoxelGrid goes now)
+      b->vox_pend = false;
+      rc = launch_vox(b, b->vox_pend_par, true, nullptr);
       if (rc) return rc;
     }
     // the LM issued now: lag 1, k_lm(k-1) (the newest pending); lag 2, k_lm(k-2) (the older one)

@@ -15,12 +15,12 @@ if [ "$WHAT" = tests ]; then
   tail -2 "$OUT/smoke.log"
 fi
 if [ "$WHAT" = bench ]; then
-  timeout -k 10 300 python3 bench.py > "$OUT/bench.log" 2>&1
+  timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > "$OUT/bench.log" 2>&1
   tail -c 300 "$OUT/bench.log"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 bench.py --no-cpu-baseline --no-alt-order > "$OUT/bench_traced.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-alt-order > "$OUT/bench_traced.log" 2>&1
   find "$OUT/stats" -name '*kernel_trace.csv' -exec cp {} "$OUT/kernel_trace.csv" \;
   find "$OUT/stats" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
-  timeout -k 10 300 python3 bench.py --kind hdl64 --no-cpu-baseline > "$OUT/bench_hdl64.log" 2>&1
+  timeout -k 10 300 python3 bench.py --kind hdl64 --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/bench_hdl64.log" 2>&1
   tail -c 300 "$OUT/bench_hdl64.log"
   for S in 256 512 1024; do
     for O in 0 1; do

@@ -25,7 +25,8 @@ def main():
             continue
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
-    proj = [r for r in rows if r[2] == "k_project"] or [r for r in rows if r[2].startswith("k_pw_scatter")]
+    first = next(r[2] for r in rows if r[2] == "k_project" or r[2].startswith("k_pw_scatter"))
+    proj = [r for r in rows if r[2] == first]  # the layout of the throughput pass (the first launches)
     per = a.steps + a.warmup
     starts = [p[0] for p in proj[:per + 1]]
     t_end = proj[per][0] if len(proj) > per else rows[-1][1]
