@@ -2329,9 +2329,14 @@ LG_DEVICE void final_bitonic(K* key, V* val, int n) {
 }
 
 // (curvature bits << 32 | ring index) in registers; returns false (and leaves LDS untouched) when a
-// key tie, a NaN or a sign bit makes the order depend on the sort algorithm (*anomaly: NaN / sign).
-template <int R>
-LG_DEVICE bool seg_sort_distinct(float* key, int* val, int n, bool* anomaly) {
+// key tie, a NaN or a sign bit makes the order depend on the sort algorithm (*anomaly: NaN / sign) --
+// unless tie_ok(a) accepts the (key, index) order for the ties found (harmless ties, below).
+struct NoTieOk {
+  template <int R>
+  LG_DEVICE bool operator()(const unsigned long long (&)[R], int) const { return false; }
+};
+template <int R, class TieOk = NoTieOk>
+LG_DEVICE bool seg_sort_distinct(float* key, int* val, int n, bool* anomaly, const TieOk& tie_ok = TieOk()) {
   const int lane = lane_id();
   unsigned long long a[R];
   bool bad = false;
@@ -2355,7 +2360,7 @@ LG_DEVICE bool seg_sort_distinct(float* key, int* val, int n, bool* anomaly) {
     const unsigned kn = (r + 1 < R) ? (unsigned)(a[r + 1 < R ? r + 1 : r] >> 32) : nxt;
     if (e + 1 < n && (unsigned)(a[r] >> 32) == kn) bad = true;
   }
-  if (__ballot(bad) != 0ull) return false;
+  if (__ballot(bad) != 0ull && (*anomaly || !tie_ok(a, n))) return false;
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -2369,17 +2374,104 @@ LG_DEVICE bool seg_sort_distinct(float* key, int* val, int n, bool* anomaly) {
   return true;
 }
 
+// Harmless ties of extractFeatures' segment sort (:285-286).  std::sort's order among equal curvature
+// values reaches the outputs only through (a) the greedy passes, which walk the sorted entries and act
+// on the eligible ones -- sharp: not picked, curvature > edge threshold, not ground; flat: not picked,
+// curvature < surf threshold, ground (:289-349) -- and (b) the stale slot 4, which keeps the entry sorted
+// into it for the next scan (ring 0's first segment).  When no run of equal values holds two entries
+// eligible for the same pass (eligibility now includes every later one: picks only ever set picked[]),
+// each pass meets its eligible entries in one order whatever the tie order, and when the entry sorted
+// into slot 4 has a value of its own, every output equals the reference's; the sort by (value, index)
+// is then as good as the introsort emulation.
+LG_DEVICE unsigned long long shfl_up_u64(unsigned long long v, int o) {
+  return ((unsigned long long)(unsigned)__shfl_up((int)(v >> 32), o) << 32) | (unsigned)__shfl_up((int)(unsigned)v, o);
+}
+struct SegTieOk {
+  const float* curv;
+  const uint8_t* picked;
+  const uint8_t* gflag;
+  int M, sp;
+  float edge_thr, surf_thr;
+  template <int R>
+  LG_DEVICE bool operator()(const unsigned long long (&a)[R], int n) const {
+    const int lane = lane_id();
+    unsigned esm = 0u, efm = 0u;  // per position: sharp / flat eligible
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int e = lane * R + r;
+      if (e < n) {
+        const int ind = (int)(unsigned)a[r];
+        const float c = curv[ind];
+        const bool pk = picked[ind] != 0;
+        const bool g = ind < M ? gflag[ind] != 0 : false;
+        esm |= (unsigned)(!pk && c > edge_thr && !g) << r;
+        efm |= (unsigned)(!pk && c < surf_thr && g) << r;
+      }
+    }
+    // the previous eligible entry's value for every eligible entry: within the lane in order, across
+    // lanes the last eligible value of the lanes below (a "last set" scan)
+    bool clash = false;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const unsigned m = pass ? efm : esm;
+      unsigned long long last = ~0ull;  // (has << 32 | value bits); ~0: none
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if ((m >> r) & 1u) last = a[r] >> 32;
+      // inclusive "last eligible value" scan over the lanes (a higher lane's own value wins), then
+      // shifted up by one lane: the last eligible value of the lanes below
+      unsigned long long y = last;
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = shfl_up_u64(y, o);
+        if (lane >= o && y == ~0ull) y = t;
+      }
+      const unsigned long long yb = shfl_up_u64(y, 1);  // (every lane shuffles: lane 0 is a source)
+      const unsigned long long below = lane > 0 ? yb : ~0ull;
+      unsigned long long prev = below;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if ((m >> r) & 1u) {
+          const unsigned long long kv = a[r] >> 32;
+          if (prev == kv) clash = true;
+          prev = kv;
+        }
+      }
+    }
+    // slot 4: the entry sorted to position 4 - sp must be alone with its value
+    const int p4 = 4 - sp;
+    if (p4 >= 0 && p4 < n) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = lane * R + r;
+        if (e == p4) {
+          const unsigned k = (unsigned)(a[r] >> 32);
+          const unsigned kp = r > 0 ? (unsigned)(a[r > 0 ? r - 1 : 0] >> 32) : ~0u;
+          const unsigned kn = r + 1 < R ? (unsigned)(a[r + 1 < R ? r + 1 : r] >> 32) : ~0u;
+          if ((e > 0 && r > 0 && kp == k) || (e + 1 < n && r + 1 < R && kn == k)) clash = true;
+        }
+      }
+      // neighbours across a lane boundary
+      const unsigned klast = (unsigned)(a[R - 1] >> 32), kfirst = (unsigned)(a[0] >> 32);
+      const unsigned from_below = (unsigned)__shfl_up((int)klast, 1), from_above = (unsigned)__shfl_down((int)kfirst, 1);
+      if (p4 == lane * R && p4 > 0 && lane > 0 && from_below == kfirst) clash = true;
+      if (p4 == lane * R + R - 1 && p4 + 1 < n && lane < 63 && from_above == klast) clash = true;
+    }
+    return __ballot(clash) == 0ull;
+  }
+};
+
 // Sort [0, n) of (key, val): all-distinct keys -> register bitonic sort (any correct sort gives the
-// same permutation); any tie -> exact libstdc++ introsort emulation.
-template <class Lds>
-LG_DEVICE void sort_segment(Lds& L, int n) {
+// same permutation); ties that tie_ok accepts -> the same sort (by key, then val); other ties -> exact
+// libstdc++ introsort emulation.
+template <class Lds, class TieOk = NoTieOk>
+LG_DEVICE void sort_segment(Lds& L, int n, const TieOk& tie_ok = TieOk()) {
   float* key = L.u.seg.skey;
   int* val = L.u.seg.sval;
   bool ok, anomaly = true;
-  if (n <= 64) ok = seg_sort_distinct<1>(key, val, n, &anomaly);
-  else if (n <= 128) ok = seg_sort_distinct<2>(key, val, n, &anomaly);
-  else if (n <= 256) ok = seg_sort_distinct<4>(key, val, n, &anomaly);
-  else ok = seg_sort_distinct<8>(key, val, n, &anomaly);
+  if (n <= 64) ok = seg_sort_distinct<1>(key, val, n, &anomaly, tie_ok);
+  else if (n <= 128) ok = seg_sort_distinct<2>(key, val, n, &anomaly, tie_ok);
+  else if (n <= 256) ok = seg_sort_distinct<4>(key, val, n, &anomaly, tie_ok);
+  else ok = seg_sort_distinct<8>(key, val, n, &anomaly, tie_ok);
   if (!ok) {
 #ifdef LG_PROFILE
     if (lane_id() == 0) atomicAdd(&PROF_SLOT(14), 1ull);
@@ -2883,7 +2975,15 @@ __global__ __launch_bounds__(64) void k_sortseg(LgParams P, LgBufs B) {
     }
     __syncthreads();
     PROF_T(t_rs0);
-    sort_segment(L, n);
+    SegTieOk tie_ok;
+    tie_ok.curv = B.curv + (size_t)s * P.VH;
+    tie_ok.picked = B.picked + (size_t)s * P.VH;
+    tie_ok.gflag = B.seg_ground + (size_t)s * P.VH;
+    tie_ok.M = B.counts[(size_t)s * CNT_N + CNT_M];
+    tie_ok.sp = sp;
+    tie_ok.edge_thr = P.edge_thr;
+    tie_ok.surf_thr = P.surf_thr;
+    sort_segment(L, n, tie_ok);
     PROF_ADD(13, t_rs0);
     for (int t = lane_id(); t < n; t += 64) smooth[t] = make_int2(__float_as_int(L.u.seg.skey[t]), L.u.seg.sval[t]);
   }

@@ -865,3 +865,33 @@ def test_full_size_batch_properties(gpu, S, order):
         pg, fg = b.read(s)
         assert_scan_parity(steps - 1, pg, pr, fg, fr)
     b.close()
+
+
+def test_segment_sort_ties_match_oracle(gpu):
+    """Curvature ties everywhere: the injected ProjectionOut's ranges quantised to 5 cm (many equal
+    smoothness values in every segment, flat and sharp eligible ones among them).  Segments whose ties
+    cannot change what the greedy passes pick take the (value, index) register sort instead of the
+    introsort emulation (SegTieOk); features, labels and transforms must stay the oracle's, and the
+    stale slot 4 carried between scans too."""
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    import oracle as O
+    src = O.Oracle(params)
+    projs = []
+    for k in range(6):
+        pr = src.cloud_handler(A.synth_scan(cfg, 17, k))
+        src.feature_association()
+        r = np.asarray(pr["segmented_cloud_range"], np.float32)
+        pr["segmented_cloud_range"] = (np.round(r / 0.05) * 0.05).astype(np.float32)
+        projs.append(pr)
+    fe = L.Frontend(params)
+    orc = oracle_for(params)
+    for k, pr in enumerate(projs):
+        fr = orc.feature_association(pr)
+        fg = fe.feature_association(pr)
+        bad = Hs.diff_report(Hs.FEAT_KEYS, fg, fr)
+        assert not bad, (k, bad)
+        assert fg["status"] == fr["status"], (k, hex(fg["status"]), hex(fr["status"]))
+        np.testing.assert_allclose(fg["transform_cur"], fr["transform_cur"], atol=Hs.TF_TOL, rtol=0)
+        np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
+    fe.close()
