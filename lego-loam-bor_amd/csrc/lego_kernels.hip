@@ -1601,7 +1601,10 @@ __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
   }
 }
 
-__global__ __launch_bounds__(1024) void k_sw_finish(LgParams P, LgBufs B, int tiles) {
+// kNT threads a scan: 1,024 fills a CU's register file (128 VGPRs x 16 waves), 256 (four waves at <= 128 VGPRs)
+// shares a CU with k_lm's and k_voxel's waves.
+template <int kNT>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k_sw_finish(LgParams P, LgBufs B, int tiles) {
   __shared__ int scratch[64];
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x, V = P.V, H = P.H, VH = P.VH;
   __shared__ int tot[2];
@@ -4551,7 +4554,11 @@ int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_sw_emit, g, dim3(SW_NT), 0, st, P, B);
     LG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_sw_finish, dim3(S), dim3(1024), 0, st, P, B, (int)g.x);
+    static const int swf_env = std::getenv("LEGO_SWF_NT") ? std::atoi(std::getenv("LEGO_SWF_NT")) : 0;  // (A/B)
+    if (swf_env == 256)
+      hipLaunchKernelGGL(k_sw_finish<256>, dim3(S), dim3(256), 0, st, P, B, (int)g.x);
+    else
+      hipLaunchKernelGGL(k_sw_finish<1024>, dim3(S), dim3(1024), 0, st, P, B, (int)g.x);
   } else {
     size_t sm = (size_t)64 * 4 + (((size_t)P.VH * 2 + 3) & ~(size_t)3);
     hipLaunchKernelGGL(k_segment_lds, dim3(S), dim3(1024), sm, st, P, B);
