@@ -62,7 +62,6 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   int fp1;                              // lego_params.fp_mode == 1: unqualified libm calls in double
   double sinXd, cosXd, sinYd, cosYd;    // fp_mode 1: sin / cos(double(alpha)) of labelComponents (:463)
   int lm_prio;                          // k_lm's wave priority (s_setprio 0..3; A/B: LEGO_LM_PRIO)
-  int lm_mw;                            // k_lm: iteration blocks on every wave above this many queries (0: wave 0)
 };
 
 struct LgState {  // FeatureAssociation members that persist across scans (featureAssociation.h)

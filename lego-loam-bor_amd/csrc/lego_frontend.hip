@@ -357,7 +357,6 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
   b->P.ncu = ncu;
   b->P.lm_prio = std::getenv("LEGO_LM_PRIO") ? std::atoi(std::getenv("LEGO_LM_PRIO")) : 0;  // (A/B)
-  b->P.lm_mw = std::getenv("LEGO_LM_MW") ? std::atoi(std::getenv("LEGO_LM_MW")) : 0;  // (A/B; 0 = wave 0 only)
   b->P.S = n_streams;
   b->S = n_streams;
   b->max_points = max_points;

@@ -3449,7 +3449,6 @@ struct LmLdsT {  // kMaxQ: feature queries of one loop (V * max(cap_sharp, cap_f
   float kd_box[6];            // its root bbox
   lgkd::KdView kdv;           // the tree's scratch (B.kd_* of this stream) and cloud
   float fred[6][16];
-  double dred[16][10];  // per-wave partial normal equations (the all-waves iteration blocks)
   int iscan[16];
   float cur[6];
   int flag;      // 1 = keep iterating
@@ -4260,50 +4259,7 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
       PROF_ADD(9, t_srch0);
     }
     PROF_T(t_acc0);
-    // More than 3 queries a lane (HDL-64E-sized feature sets): every wave takes a share of the rows, the
-    // per-wave sums meet in LDS and every thread adds them in wave order and solves (identical values
-    // everywhere).  The float cast of each double sum hides the changed summation order.
-    if (P.lm_mw > 0 && nq > P.lm_mw) {
-      float cur[6];
-      for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
-      int deg = S.is_degenerate, status = 0, run = L.iters;
-      bool keep = true;
-      for (int it = iter; it < iter + 5 && it < 25; ++it) {
-        const LmTrig T = lm_trig<kF1>(cur);
-        double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int q = tid; q < nq; q += (int)blockDim.x) {
-          const float4 po = L.featl[q];
-          const float4 sel = it == iter ? L.sel[q] : transform_to_start<kF1>(po, cur);
-          float4 cf;
-          const bool ok = surf ? (L.ind2[q] >= 0 && L.ind3[q] >= 0 && surf_coeff_pl<kF1>(L.plane[q], sel, it, cf))
-                               : corner_coeff(last, L.ind1[q], L.ind2[q], sel, it, cf);
-          if (ok) {
-            if (surf) accumulate_surf_row(T, po, cf, acc);
-            else accumulate_corner_row(T, po, cf, acc);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 10; ++k)
-          for (int o = 32; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o);
-        if (lane_id() == 0)
-          for (int k = 0; k < 10; ++k) L.dred[wave_id()][k] = acc[k];
-        __syncthreads();
-        double tot[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int w = 0; w < nw; ++w)
-          for (int k = 0; k < 10; ++k) tot[k] += L.dred[w][k];
-        __syncthreads();  // dred is rewritten by the next iteration
-        run = it + 1;
-        if (tot[9] < 10.0) continue;  // too few correspondences: `continue`
-        if (!lm_solve_reg(cur, deg, status, tot, it, surf)) { keep = false; break; }
-      }
-      if (tid == 0) {
-        for (int k = 0; k < 6; ++k) L.cur[k] = cur[k];
-        S.is_degenerate = deg;
-        if (status) L.status |= status;
-        L.iters = run;
-        L.flag = keep ? 1 : 0;
-      }
-    } else if (wave_id() == 0) {  // iterations iter .. iter + 4 on wave 0
+    if (wave_id() == 0) {  // iterations iter .. iter + 4 on wave 0
       const int lane = lane_id();
       float cur[6];
       for (int k = 0; k < 6; ++k) cur[k] = L.cur[k];
