@@ -24,6 +24,11 @@ steps, lego_batch_set_probe).
 
 The roofline pair (k_project + k_fa_prep4) is also timed at --roofline-streams scans per launch (2048:
 a working set far above the 256 MiB Infinity Cache) and reported beside the S-stream figure.
+
+BASELINE's configs:  --config c3 (default) is the headline: S streams per GPU, weak scaling.  Every line
+also carries "c5": BASELINE config C5, the 20k-scan synthetic dataset (80 sequences x 250 scans) sharded
+by sequence over the N ranks (80 / N sequences each, strong scaling), every scan of it timed; --config
+c5 makes that the headline value (--c5-sequences / --c5-scans shrink it for tests; --no-c5 skips it).
 """
 import argparse
 import json
@@ -74,6 +79,13 @@ def parse():
     ap.add_argument("--roofline-streams", type=int, default=2048,
                     help="also time the roofline pair at this many scans per launch (0: skip)")
     ap.add_argument("--dump-poses", default="", help="rank 0: write the gathered trajectories (.npy) here")
+    ap.add_argument("--config", default="c3", choices=["c3", "c5"],
+                    help="headline workload: c3 = S streams per GPU (weak scaling); c5 = the 20k-scan dataset "
+                         "sharded over the ranks (strong scaling)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 measurement (config c3)")
+    ap.add_argument("--c5-sequences", type=int, default=80, help="C5: sequences in the dataset")
+    ap.add_argument("--c5-scans", type=int, default=250, help="C5: scans per sequence")
+    ap.add_argument("--dump-c5", default="", help="rank 0: write C5's gathered per-scan odometry (.npy) here")
     return ap.parse_args()
 
 
@@ -175,10 +187,20 @@ def pmc_traffic(args, S, kernels):
     return int(sum(v["hbm_bytes"] for v in best[1])), os.path.relpath(best[0], REPO)
 
 
-def lag_for(args, order):
-    """The pipeline depth of a batch with this VoxelGrid order: --lag, else 2 for the reference's order (its
-    VoxelGrid gets two steps before its publish) and 1 for the stable order."""
-    return args.lag if args.lag is not None else (2 if order == 0 else 1)
+def default_lag(order):
+    return 2 if order == 0 else 1
+
+
+def configure_batch(b, order, lag=None, wide=-1, groups=1):
+    """The schedule every measured batch runs (and tests/test_gpu_bench_config.py pins against the
+    oracle): `groups` stream slices, pipeline depth `lag` (default: 2 for the reference's VoxelGrid
+    order, 1 for the stable one), projection / segmentation layout `wide` (-1: lego_batch_set_wide's
+    automatic choice).  Returns the lag set."""
+    lag = default_lag(order) if lag is None else lag
+    b.set_groups(groups)
+    b.set_lag(lag)
+    b.set_wide(wide)
+    return lag
 
 
 def roofline_kernels(wide):
@@ -206,8 +228,7 @@ def roofline_at(args, L, A, mk_params, cfg, dev_index, stream):
     d_off = torch.from_numpy((np.arange(2 * Sb, dtype=np.int64) * cap).reshape(2, Sb)).to(d_pts.device)
     d_cnt = torch.from_numpy(cnt.reshape(2, Sb).astype(np.int32)).to(d_pts.device)
     b = L.Batch(params, Sb, cap, device=dev_index)
-    b.set_lag(lag_for(args, args.voxel_tie_order))
-    b.set_wide(args.wide)
+    configure_batch(b, args.voxel_tie_order, args.lag, args.wide)
     wide_b = b.wide() == 1
     for k in range(2):
         b.step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
@@ -226,6 +247,81 @@ def roofline_at(args, L, A, mk_params, cfg, dev_index, stream):
     return {"streams": Sb, "kernels": "+".join(roofline_kernels(wide_b)), "bytes_per_launch": int(b_tot), "launch_ms": round(ms, 4), "achieved": round(achieved, 1),
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
             "note": "%d scans per launch: working set %.2f GB, above the 256 MiB Infinity Cache" % (Sb, b_tot / 1e9)}
+
+
+C5_SEQ0 = 100000  # C5's sequence ids: a dataset of its own, apart from C3's 0 .. S * N - 1
+
+
+def run_c5(args, L, A, mk_params, cfg, rank, world, dev_index, stream, dist, coll_dev):
+    """BASELINE config C5: the synthetic dataset of --c5-sequences x --c5-scans VLP-16 scans (80 x 250 =
+    20k), sequences sharded over the ranks in contiguous blocks (no collective on the data path).  Each
+    rank runs its sequences as the streams of one batch, every scan of the dataset in the timed region
+    (inputs resident in HBM before it; barrier + sync on both sides, max over ranks), the per-scan
+    odometry recorded on the device (lego_batch_set_trajectory) and all-gathered to rank 0 afterwards,
+    the path's only collective.  Returns (summary dict, gathered odometry [sequences, scans, 12] or
+    None off rank 0)."""
+    import torch
+    n_seq, K = args.c5_sequences, args.c5_scans
+    per = (n_seq + world - 1) // world  # the gather's padded shard size
+    lo, hi = min(rank * per, n_seq), min((rank + 1) * per, n_seq)
+    S = hi - lo
+    params = mk_params(voxel_tie_order=args.voxel_tie_order, fp_mode=args.fp_mode)
+    cap = params.num_vertical_scans * params.num_horizontal_scans
+    dev = torch.device("cuda", dev_index)
+    el, t_gen, lag, wide = 0.0, 0.0, None, None
+    traj = torch.zeros((per, K, 12), dtype=torch.float32, device=dev)
+    if S > 0:
+        t0 = time.time()
+        seqs = np.repeat(np.arange(C5_SEQ0 + lo, C5_SEQ0 + hi, dtype=np.int32)[None, :], K, 0).reshape(-1)
+        scans = np.repeat(np.arange(K, dtype=np.int32)[:, None], S, 1).reshape(-1)
+        pts, cnt = A.synth_batch(cfg, seqs, scans, nthreads=args.threads)
+        t_gen = time.time() - t0
+        d_pts = torch.from_numpy(pts).to(dev)
+        del pts
+        d_off = torch.from_numpy((np.arange(K * S, dtype=np.int64) * cap).reshape(K, S)).to(dev)
+        d_cnt = torch.from_numpy(cnt.reshape(K, S).astype(np.int32)).to(dev)
+        b = L.Batch(params, S, cap, device=dev_index)
+        lag = configure_batch(b, args.voxel_tie_order, args.lag, args.wide, args.groups)
+        wide = int(b.wide())
+        b.set_trajectory(traj.data_ptr(), K)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if S > 0:
+        for k in range(K):
+            b.step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
+        b.flush()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    status = 0
+    if S > 0:
+        status = int(np.bitwise_or.reduce(b.poses()[1]))
+        b.close()
+        del d_pts
+        torch.cuda.empty_cache()
+    out = traj.to(coll_dev)
+    if world > 1:
+        parts = [torch.empty_like(out) for _ in range(world)]
+        dist.all_gather(parts, out)
+        out = torch.cat(parts)
+    gathered = out[:n_seq].cpu().numpy() if rank == 0 else None
+    summary = {"workload": "C5: synthetic %s dataset, %d sequences x %d scans = %d scans, sharded by sequence "
+                           "over %d rank(s) (%d sequences a rank), every scan timed"
+                           % (args.kind.upper(), n_seq, K, n_seq * K, world, per),
+               "value": round(n_seq * K / el, 1), "unit": "scans/s", "n_gpus": world, "elapsed_s": round(el, 4),
+               "ms_per_step": round(1e3 * el / K, 3), "scaling": "strong", "sequences": n_seq,
+               "scans_per_sequence": K, "sequences_per_rank": per, "lag": lag, "wide": wide,
+               "lm_status_bits_rank0": status, "input_gen_s": round(t_gen, 2)}
+    return summary, gathered
 
 
 def main():
@@ -267,10 +363,7 @@ def main():
     d_off = torch.from_numpy(offs).to(dev)
     d_cnt = torch.from_numpy(host_cnt.astype(np.int32)).to(dev)
     batch = L.Batch(params, S, cap, device=local_dev)
-    lag = lag_for(args, args.voxel_tie_order)
-    batch.set_groups(args.groups)
-    batch.set_lag(lag)
-    batch.set_wide(args.wide)
+    lag = configure_batch(batch, args.voxel_tie_order, args.lag, args.wide, args.groups)
     wide_pw = batch.wide() == 1  # the projection's kernels: k_pw_scatter + k_pw_columns (else k_project)
     stream = torch.cuda.current_stream(dev)
 
@@ -320,9 +413,7 @@ def main():
         alt_order = 1 - args.voxel_tie_order
         params_alt = mk_params(voxel_tie_order=alt_order, fp_mode=args.fp_mode)
         batch_alt = L.Batch(params_alt, S, cap, device=local_dev)
-        batch_alt.set_groups(args.groups)
-        batch_alt.set_lag(lag_for(args, alt_order))
-        batch_alt.set_wide(args.wide)
+        configure_batch(batch_alt, alt_order, args.lag, args.wide, args.groups)
         el_alt = timed(batch_alt)
         batch_alt.close()
         alt = {"voxel_tie_order": alt_order, "value": round(total_scans / el_alt, 1),
@@ -413,6 +504,18 @@ def main():
         "trajectories_gathered": int(traj_all.shape[0]),
         "input_gen_s": round(t_gen, 2),
     }
+    if args.config == "c5" or not args.no_c5:
+        del d_pts
+        torch.cuda.empty_cache()
+        c5, c5_traj = run_c5(args, L, A, mk_params, cfg, rank, world, local_dev, stream, dist, coll_dev)
+        if rank == 0 and args.dump_c5:
+            np.save(args.dump_c5, c5_traj)
+        if args.config == "c5":  # the headline is C5; C3's line moves under "c3"
+            out["c3"] = {k: out[k] for k in ("value", "ms_per_step", "scaling", "config")}
+            out["value"], out["ms_per_step"], out["scaling"] = c5["value"], c5["ms_per_step"], "strong"
+            out["config"] = dict(out["config"], workload=c5["workload"], streams_per_gpu=c5["sequences_per_rank"],
+                                 lag=c5["lag"], wide=c5["wide"])
+        out["c5"] = c5
     if world == 1 and not args.no_cpu_baseline:  # N = 1 only; the reference's own VoxelGrid order (std::sort)
         params_ref = mk_params(voxel_tie_order=0, fp_mode=args.fp_mode)
         out["cpu_baseline"] = cpu_baseline(params_ref, cfg, host_pts, host_cnt, args.cpu_seconds)

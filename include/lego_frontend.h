@@ -191,6 +191,13 @@ int  lego_batch_sync(lego_batch* b);
 int  lego_batch_read(lego_batch* b, int32_t s, lego_projection_out* proj, lego_association_out* assoc);
 /* Poses of all streams: out[s*12 + 0..5] = transformCur, [6..11] = transformSum; status[s]. */
 int  lego_batch_read_poses(lego_batch* b, float* out, int32_t* status);
+/* Per-scan odometry of every stream (publishOdometry runs every scan, featureAssociation.cpp:1286-1298):
+ * while set, each association of stream s writes d_traj[(s * max_scans + k) * 12 + 0..5] = transformCur
+ * and [6..11] = transformSum after it, k = the stream's association count since lego_batch_reset (0:
+ * the initialising scan); associations past max_scans are not recorded.  d_traj is a DEVICE array of
+ * n_streams * max_scans * 12 floats, written asynchronously by the LM kernel (read it after
+ * lego_batch_sync).  d_traj NULL / max_scans 0 stops recording. */
+int  lego_batch_set_trajectory(lego_batch* b, float* d_traj, int32_t max_scans);
 /* Sizes of the last step per stream: out[s*7 + 0..6] = segmented, outlier, scan_msg, sharp,
  * less sharp, flat, less flat point counts. */
 int  lego_batch_read_counts(lego_batch* b, int32_t* out);
@@ -277,8 +284,9 @@ int  lego_debug_prof(uint64_t* out256, int32_t reset);
 /* Kernel time of `blocks` concurrent one-wave copies of the device sort of h_keys (profile build);
  * mode 0 the stack emulation, 1 the level-synchronous one (n <= 2048). */
 int  lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, int32_t mode, float* ms);
-/* Counter calibration: k_project's input read patterns (mode 0 12-byte buffer loads, 1 16-byte loads,
- * 2 both passes) over S scans of device points (offs / cnts as lego_batch_run's), out[S * 1024]. */
+/* Counter calibration (profile build; LEGO_ENOTSUP in the shipped library): k_project's input read
+ * patterns (mode 0 12-byte buffer loads, 1 16-byte loads, 2 both passes) over S scans of device points
+ * (offs / cnts as lego_batch_run's), out[S * 1024]. */
 int  lego_debug_fetch_probe(int32_t mode, int32_t S, const void* pts, const int64_t* offs, const int32_t* cnts,
                             float* out, void* stream);
 

@@ -32,14 +32,27 @@ def _stale(target, deps):
 
 
 def build_frontend(force=False, profile=False):
+    """One object per translation unit, compiled in parallel (no device code crosses a TU: each kernel is
+    launched from the file that defines it), then one shared-library link."""
     target = os.path.join(OUT, "liblego_frontend_prof.so" if profile else "liblego_frontend.so")
     deps = [os.path.join(CSRC, f) for f in FRONTEND_DEPS] + [os.path.join(REPO, "include", h)
                                                           for h in ("lego_frontend.h", "lego_s2m.h")]
     if force or _stale(target, deps):
-        cmd = [HIPCC] + HIP_FLAGS + (["-DLG_PROFILE"] if profile else []) + \
-            [os.path.join(CSRC, f) for f in FRONTEND_SRC] + ["-o", target]
-        print(" ".join(cmd), flush=True)
-        subprocess.check_call(cmd)
+        import tempfile
+        from concurrent.futures import ThreadPoolExecutor
+        flags = [f for f in HIP_FLAGS if f != "-shared"] + (["-DLG_PROFILE"] if profile else [])
+        with tempfile.TemporaryDirectory() as tmp:
+            objs = [os.path.join(tmp, f + ".o") for f in FRONTEND_SRC]
+
+            def compile_one(i):
+                cmd = [HIPCC] + flags + ["-c", os.path.join(CSRC, FRONTEND_SRC[i]), "-o", objs[i]]
+                print(" ".join(cmd), flush=True)
+                subprocess.check_call(cmd)
+            with ThreadPoolExecutor(max_workers=len(FRONTEND_SRC)) as ex:
+                list(ex.map(compile_one, range(len(FRONTEND_SRC))))
+            cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", target]
+            print(" ".join(cmd), flush=True)
+            subprocess.check_call(cmd)
     return target
 
 

@@ -60,8 +60,8 @@ struct LgParams {  // ImageProjection / FeatureAssociation ctor constants (host-
   unsigned wtag;                        // wide mode: launch tag in the winner image entries' top 4 bits
   int max_points;                       // input capacity per scan (wide scatter grid)
   int fp1;                              // lego_params.fp_mode == 1: unqualified libm calls in double
+  int traj_cap;                         // scans a stream's trajectory record holds (0: none; LgBufs.traj)
   double sinXd, cosXd, sinYd, cosYd;    // fp_mode 1: sin / cos(double(alpha)) of labelComponents (:463)
-  int lm_prio;                          // k_lm's wave priority (s_setprio 0..3; A/B: LEGO_LM_PRIO)
 };
 
 struct LgState {  // FeatureAssociation members that persist across scans (featureAssociation.h)
@@ -76,6 +76,8 @@ struct LgState {  // FeatureAssociation members that persist across scans (featu
   int status;            // LEGO_ST_* of the last association
   int iters_surf, iters_corner;
   int pub_copy;          // k_publish stores the lessFlat cloud untransformed (checkSystemInitialization)
+  int n_assoc;           // associations run on this stream since the reset (the trajectory record's index)
+  int pad_;
   double quat[4];
   double pos[3];
 };
@@ -155,6 +157,8 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   float4* surf_last;     // [S][2][VH]
   float4* grid_pts;      // [S][VH]  LM scratch: Last cloud bucketed by grid cell (xyz, index bits)
   LgState* state;        // [S]      written by k_lm / k_publish only (k_lm stores it whole)
+  float* traj;           // [S][traj_cap][12]  optional (lego_batch_set_trajectory): transformCur and
+                         //          transformSum after each association of the stream, by k_lm
   // nanoflann tree of a Last cloud, built by k_lm only when a 1-NN has an exact distance tie
   KdNode* kd_node;       // [S][2*VH]
   int32_t* kd_vind;      // [S][VH]

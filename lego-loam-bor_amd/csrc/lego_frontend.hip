@@ -145,6 +145,8 @@ static int lg_wide_auto(const LgParams& P, int S) {
   return (!P.voxel_stable && S <= 2 * P.ncu) ? 1 : 0;
 }
 
+#define LG_PROBE_MAX 64  // probe events kept: the last LG_PROBE_MAX steps (lego_batch_probe_times)
+
 struct lego_batch {
   lego_params params;
   LgParams P;
@@ -202,20 +204,11 @@ struct lego_batch {
   bool pend_ovl = false;     // the pending work belongs to the overlap schedule
   hipStream_t ls = nullptr;
   hipEvent_t ev_pub = nullptr, ev_ls = nullptr, ev_fe = nullptr;
-  // Phased overlap schedule (lag 1): the front end of scan k starts after k_lm(k-2) and k_lm(k-1) after
-  // scan k's k_concat, so the whole-CU front-end kernels never share the GPU with k_lm; the VoxelGrid
-  // (two alternating streams) fills the LM's spare CU resources.
-  hipEvent_t ev_lmdone = nullptr;
-  bool lm_ev_valid = false;
-  // Deferred VoxelGrid (lag 2, A/B LEGO_VOX_DEFER): scan k's k_voxel is issued in step k+1 after that
-  // step's segmentation (ev_fe), so the projection and segmentation start on CUs the VoxelGrid's waves
-  // do not hold; its publish is two steps later still.
-  bool vox_pend = false;
-  int vox_pend_par = 0;
 
   // Probe (lego_batch_set_probe): events around k_project and around k_fa_prep in the overlap
   // schedule, four per step, so the HBM-bound pair's durations inside the pipeline can be read
-  // (lego_batch_probe_times) beside the back-to-back figure of lego_batch_time_hbm_stages.
+  // (lego_batch_probe_times) beside the back-to-back figure of lego_batch_time_hbm_stages.  A ring of
+  // LG_PROBE_MAX steps: a probe left on reuses the oldest events instead of growing the list.
   bool probe = false;
   std::vector<hipEvent_t> pev;
   int probe_n = 0;
@@ -247,7 +240,6 @@ struct lego_batch {
     if (ev_pub) hipEventDestroy(ev_pub);
     if (ev_ls) hipEventDestroy(ev_ls);
     if (ev_fe) hipEventDestroy(ev_fe);
-    if (ev_lmdone) hipEventDestroy(ev_lmdone);
   }
 };
 
@@ -356,7 +348,6 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
   b->P.ncu = ncu;
-  b->P.lm_prio = std::getenv("LEGO_LM_PRIO") ? std::atoi(std::getenv("LEGO_LM_PRIO")) : 0;  // (A/B)
   b->P.S = n_streams;
   b->S = n_streams;
   b->max_points = max_points;
@@ -423,7 +414,7 @@ int lego_batch_reset(lego_batch* b) {
   if (hipMemset(B.smooth, 0, S * VH * sizeof(int2)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fp_sync, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   b->epoch = 0;
-  b->pend_pub = b->pend_lm = b->pend_lm_old = b->pend_ovl = b->vox_pend = false;
+  b->pend_pub = b->pend_lm = b->pend_lm_old = b->pend_ovl = false;
   b->par = b->last_par = 0;
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fe_state, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
@@ -548,39 +539,17 @@ static void advance_pipeline(lego_batch* b, bool lag, int groups) {
   b->par = (b->par + 1) % LG_SLOTS;
 }
 
-// Internal side streams (A/B switches, read once): LEGO_SIDE_PRIO=low creates the LM / VoxelGrid streams
-// at the lowest priority (the caller's stream, which carries the front end, keeps its own);
-// LEGO_VOX_CUMASK=k (1..7) restricts the VoxelGrid streams to k of every 8 CUs (hipExtStreamCreateWithCUMask),
-// so the front end's whole-CU workgroups find CUs without VoxelGrid waves.
-static hipError_t make_side_stream(hipStream_t* st, bool vox) {
-  static const char* pe = std::getenv("LEGO_SIDE_PRIO");
-  static const char* me = std::getenv("LEGO_VOX_CUMASK");
-  const int keep = me ? std::atoi(me) : 0;
-  if (vox && keep > 0 && keep < 8) {
-    uint32_t mask[16];
-    for (int w = 0; w < 16; ++w) {
-      uint32_t m = 0;
-      for (int b = 0; b < 32; ++b)
-        if (((w * 32 + b) & 7) < keep) m |= 1u << b;
-      mask[w] = m;
-    }
-    return hipExtStreamCreateWithCUMask(st, 16, mask);
-  }
-  if (pe && !strcmp(pe, "low")) {
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return hipErrorUnknown;
-    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, least);
-  }
-  return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-}
+// Internal side streams: non-blocking, default priority, every CU (lower priorities and CU masks for the
+// VoxelGrid streams were measured and not kept).
+static hipError_t make_side_stream(hipStream_t* st) { return hipStreamCreateWithFlags(st, hipStreamNonBlocking); }
 
 static int ensure_streams(lego_batch* b, int groups) {
   if (!b->fork && hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_chain && hipEventCreateWithFlags(&b->ev_chain, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   for (int g = 0; g < groups; ++g) {
-    if (!b->gs[g] && make_side_stream(&b->gs[g], true) != hipSuccess) return LEGO_EDEVICE;
+    if (!b->gs[g] && make_side_stream(&b->gs[g]) != hipSuccess) return LEGO_EDEVICE;
     if (!b->join[g] && hipEventCreateWithFlags(&b->join[g], hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
-    if (!b->vs[g] && make_side_stream(&b->vs[g], true) != hipSuccess) return LEGO_EDEVICE;
+    if (!b->vs[g] && make_side_stream(&b->vs[g]) != hipSuccess) return LEGO_EDEVICE;
     if (!b->ev_cat[g] && hipEventCreateWithFlags(&b->ev_cat[g], hipEventDisableTiming) != hipSuccess)
       return LEGO_EDEVICE;
     for (int h = 0; h < LG_SLOTS; ++h)
@@ -605,12 +574,10 @@ static int chain_stream(lego_batch* b, hipStream_t st) {
 }
 
 static int ensure_ls(lego_batch* b) {
-  if (!b->ls && make_side_stream(&b->ls, false) != hipSuccess) return LEGO_EDEVICE;
+  if (!b->ls && make_side_stream(&b->ls) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_pub && hipEventCreateWithFlags(&b->ev_pub, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_ls && hipEventCreateWithFlags(&b->ev_ls, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
   if (!b->ev_fe && hipEventCreateWithFlags(&b->ev_fe, hipEventDisableTiming) != hipSuccess) return LEGO_EDEVICE;
-  if (!b->ev_lmdone && hipEventCreateWithFlags(&b->ev_lmdone, hipEventDisableTiming) != hipSuccess)
-    return LEGO_EDEVICE;
   for (int h = 0; h < LG_SLOTS; ++h)
     if (!b->ev_cats[h] && hipEventCreateWithFlags(&b->ev_cats[h], hipEventDisableTiming) != hipSuccess)
       return LEGO_EDEVICE;
@@ -633,11 +600,6 @@ static int launch_vox(lego_batch* b, int par, bool alt, hipEvent_t after) {
   return LEGO_OK;
 }
 
-static bool sched_phased() {
-  static const bool on = std::getenv("LEGO_SCHED_PHASED") && std::atoi(std::getenv("LEGO_SCHED_PHASED")) != 0;
-  return on;
-}
-
 // The front end of the overlap schedule after the projection: smoothness, extraction, then (after
 // publish(k-2) on ls when one was issued) k_concat and the side stream's k_voxel.
 static int run_association_ovl(lego_batch* b, hipStream_t st, bool wait_pub) {
@@ -654,20 +616,10 @@ static int run_association_ovl(lego_batch* b, hipStream_t st, bool wait_pub) {
   rc = lg_launch_concat(P, b->B, b->S, st);
   if (rc) return rc;
   if (hipEventRecord(b->ev_cats[P.par], st) != hipSuccess) return LEGO_EDEVICE;
-  // Lag 2 (and A/B at lag 1, LEGO_VOXEL_TWO_STREAMS): every other scan's VoxelGrid on gs[0] (idle in
-  // this schedule), so k_voxel(k) may still run while k_voxel(k + 1) starts; a stream of its own
-  // measured slower for both orders (212k vs 268k scans/s with the stable order): one more stream than
-  // the 4 hardware queues.  LEGO_VOXEL_ONE_STREAM keeps lag 2 on vs[0] (A/B).
-  static const bool two_vs = std::getenv("LEGO_VOXEL_TWO_STREAMS") != nullptr;
-  static const bool one_vs = std::getenv("LEGO_VOXEL_ONE_STREAM") != nullptr;
-  const bool alt = (b->lag >= 2 || sched_phased()) ? !one_vs : two_vs;
-  static const bool defer = std::getenv("LEGO_VOX_DEFER") && std::atoi(std::getenv("LEGO_VOX_DEFER")) != 0;
-  if (defer && b->lag >= 2) {
-    b->vox_pend = true;
-    b->vox_pend_par = P.par;
-    return LEGO_OK;
-  }
-  return launch_vox(b, P.par, alt, nullptr);
+  // Lag 2: every other scan's VoxelGrid on gs[0] (idle in this schedule), so k_voxel(k) may still run
+  // while k_voxel(k + 1) starts; a stream of its own measured slower for both orders (212k vs 268k
+  // scans/s with the stable order): one more stream than the 4 hardware queues.
+  return launch_vox(b, P.par, b->lag >= 2, nullptr);
 }
 
 // Issue the pending k_publish / k_lm (each publish joined with its k_voxel) on the stream of the
@@ -677,11 +629,6 @@ static int flush_pending(lego_batch* b) {
   if (b->pend_ovl) {  // on ls: publish(k-1), [k_lm(k-1), publish(k-1),] k_lm(k), publish(k); then the
                       // last step's stream waits for ls
     int rc = LEGO_OK;
-    if (b->vox_pend) {  // the deferred VoxelGrid first (its publish follows)
-      b->vox_pend = false;
-      rc = launch_vox(b, b->vox_pend_par, true, nullptr);
-      if (rc) return rc;
-    }
     if (b->pend_pub) rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
     for (int q = 0; q < 2 && !rc; ++q) {
       const bool has = q == 0 ? b->pend_lm_old : b->pend_lm;
@@ -749,6 +696,7 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   if (!b || !d_points || !d_offsets || !d_counts) return LEGO_EINVAL;
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   hipStream_t st = (hipStream_t)hip_stream;
+  b->probe_cur = nullptr;  // set again below for an overlap-schedule step while the probe is on
   b->epoch = b->epoch == 0x7fffffff ? 1 : b->epoch + 1;
   const bool lag = b->lag != 0;
   // timing: per-stage events on the caller's stream, one slice (the pipelined path itself)
@@ -770,13 +718,15 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   if (ovl) {
     rc = ensure_ls(b);
     if (rc) return rc;
-    if (b->probe) {  // four events of this step (lego_batch_probe_times)
-      while ((int)b->pev.size() < 4 * (b->probe_n + 1)) {
+    if (b->probe) {  // four events of this step (lego_batch_probe_times), a ring of LG_PROBE_MAX steps
+      const int slot = b->probe_n % LG_PROBE_MAX;
+      while ((int)b->pev.size() < 4 * (slot + 1)) {
         hipEvent_t e;
         if (hipEventCreate(&e) != hipSuccess) return LEGO_EDEVICE;
         b->pev.push_back(e);
       }
-      b->probe_cur = &b->pev[4 * b->probe_n++];
+      b->probe_cur = &b->pev[4 * slot];
+      ++b->probe_n;
     }
     const bool pub_now = b->pend_pub;
     // With the stable VoxelGrid order, k_lm(k-1) starts after this scan's projection and segmentation:
@@ -786,13 +736,10 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     // 248-250k -> 265k scans/s.  With the reference's introsort order the heavier k_voxel(k) then
     // meets k_lm(k-1) head-on (193k -> 167-177k scans/s), so that order keeps k_lm at the top too
     // (where the measured variants are listed).
-    static const int sched_env = std::getenv("LEGO_SCHED_LM_AFTER_FE") ? std::atoi(std::getenv("LEGO_SCHED_LM_AFTER_FE")) : -1;
-    const bool phased = sched_phased() && b->lag == 1;
     // With more scans than CUs the reference order takes it too (S = 1024: 239k vs 226k scans/s; at S = 256
     // 188k vs 195k with lag 1, so not there), and so does lag 2 (k_lm(k-2)'s inputs are ready long before:
     // 214.6k vs 210.8k; round 4, profiles/r04_schedule_ab.txt).
-    const bool lm_after_fe = !phased && (sched_env >= 0 ? sched_env != 0 :
-                                         (b->P.voxel_stable || b->S > b->P.ncu || b->lag >= 2));  // (A/B override)
+    const bool lm_after_fe = b->P.voxel_stable || b->S > b->P.ncu || b->lag >= 2;
     if (b->pend_pub) {  // publish(k-2) on ls, after its k_voxel (issue_publish waits for ev_vox)
       rc = issue_publish(b, b->ls, 0, 0, b->S, b->pub_par);
       if (!rc && hipEventRecord(b->ev_pub, b->ls) != hipSuccess) rc = LEGO_EDEVICE;
@@ -802,42 +749,20 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
       rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
       if (!rc && hipEventRecord(b->ev_fe, st) != hipSuccess) rc = LEGO_EDEVICE;
       if (!rc && hipStreamWaitEvent(b->ls, b->ev_fe, 0) != hipSuccess) rc = LEGO_EDEVICE;
-      if (!rc && b->vox_pend) {  // the previous scan's deferred VoxelGrid, after this segmentation
-        b->vox_pend = false;
-        rc = launch_vox(b, b->vox_pend_par, true, b->ev_fe);
-      }
-      if (rc) return rc;
-    }
-    if (b->vox_pend) {  // (no segmentation event this step: the deferred VoxelGrid goes now)
-      b->vox_pend = false;
-      rc = launch_vox(b, b->vox_pend_par, true, nullptr);
       if (rc) return rc;
     }
     // the LM issued now: lag 1, k_lm(k-1) (the newest pending); lag 2, k_lm(k-2) (the older one)
     const bool deep = b->lag >= 2;
     const bool lm_now = deep ? b->pend_lm_old : b->pend_lm;
     const int lm_slot = deep ? b->lm_par_old : b->lm_par;
-    if (phased) {  // front end(k) after k_lm(k-2); k_lm(k-1) after k_concat(k)
-      if (b->lm_ev_valid && hipStreamWaitEvent(st, b->ev_lmdone, 0) != hipSuccess) return LEGO_EDEVICE;
-      rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
-      if (!rc) rc = run_association_ovl(b, st, pub_now);
-      if (rc) return rc;
-      if (lm_now) {
-        if (hipStreamWaitEvent(b->ls, b->ev_cats[b->par], 0) != hipSuccess) return LEGO_EDEVICE;
-        rc = issue_lm(b, b->ls, 0, b->S, lm_slot);
-        if (!rc && hipEventRecord(b->ev_lmdone, b->ls) != hipSuccess) rc = LEGO_EDEVICE;
-        if (rc) return rc;
-        b->lm_ev_valid = true;
-      }
-    } else {
-      if (lm_now) {  // on ls, after that scan's k_concat
-        if (hipStreamWaitEvent(b->ls, b->ev_cats[lm_slot], 0) != hipSuccess) return LEGO_EDEVICE;
-        rc = issue_lm(b, b->ls, 0, b->S, lm_slot);
-      }
-      if (!rc && !lm_after_fe) rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
-      if (!rc) rc = run_association_ovl(b, st, pub_now);
-      if (rc) return rc;
+    if (lm_now) {  // on ls, after that scan's k_concat
+      if (hipStreamWaitEvent(b->ls, b->ev_cats[lm_slot], 0) != hipSuccess) rc = LEGO_EDEVICE;
+      if (!rc) rc = issue_lm(b, b->ls, 0, b->S, lm_slot);
     }
+    if (!rc && !lm_after_fe) rc = run_projection(b, (const float4*)d_points, d_offsets, d_counts, st, 0, b->S);
+    if (!rc) rc = run_association_ovl(b, st, pub_now);
+    b->probe_cur = nullptr;
+    if (rc) return rc;
     // pending now: the publish of the LM just issued, then (lag 2) k_lm(k-1), and k_lm(k)
     b->pend_pub = lm_now;
     b->pub_par = lm_slot;
@@ -851,7 +776,6 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     b->pend_ovl = true;
     b->last_par = b->par;
     b->par = (b->par + 1) % LG_SLOTS;
-    b->probe_cur = nullptr;
     return LEGO_OK;
   }
   if (G <= 1) {
@@ -875,6 +799,16 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   return LEGO_OK;
 }
 
+int lego_batch_set_trajectory(lego_batch* b, float* d_traj, int32_t max_scans) {
+  if (!b || max_scans < 0 || (max_scans > 0 && !d_traj)) return LEGO_EINVAL;
+  if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
+  int rc = flush_pending(b);  // pending LMs record where the caller asked when it issued them
+  if (rc) return rc;
+  b->B.traj = max_scans > 0 ? d_traj : nullptr;
+  b->P.traj_cap = max_scans > 0 ? max_scans : 0;
+  return LEGO_OK;
+}
+
 int lego_batch_set_probe(lego_batch* b, int32_t enabled) {
   if (!b) return LEGO_EINVAL;
   b->probe = enabled != 0;
@@ -886,7 +820,8 @@ int lego_batch_probe_times(lego_batch* b, float* ms2, int32_t* steps) {
   if (!b || !ms2 || !steps) return LEGO_EINVAL;
   hipSetDevice(b->device);
   double a = 0.0, f = 0.0;
-  for (int k = 0; k < b->probe_n; ++k) {
+  const int n = b->probe_n < LG_PROBE_MAX ? b->probe_n : LG_PROBE_MAX;  // the ring's last n steps
+  for (int k = 0; k < n; ++k) {
     hipEvent_t* e = &b->pev[4 * k];
     float x = 0.f, y = 0.f;
     if (hipEventSynchronize(e[3]) != hipSuccess || hipEventElapsedTime(&x, e[0], e[1]) != hipSuccess ||
@@ -895,9 +830,9 @@ int lego_batch_probe_times(lego_batch* b, float* ms2, int32_t* steps) {
     a += x;
     f += y;
   }
-  *steps = b->probe_n;
-  ms2[0] = b->probe_n ? (float)(a / b->probe_n) : 0.f;
-  ms2[1] = b->probe_n ? (float)(f / b->probe_n) : 0.f;
+  *steps = n;
+  ms2[0] = n ? (float)(a / n) : 0.f;
+  ms2[1] = n ? (float)(f / n) : 0.f;
   b->probe_n = 0;
   return LEGO_OK;
 }

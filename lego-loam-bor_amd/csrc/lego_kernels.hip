@@ -2607,15 +2607,8 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, Lds& L, int n, i
   }
   __syncthreads();
   PROF_T(t_vs0);
-  if constexpr (kMode == 4) {
-    if (n <= 512) lvl_sort<8>(vkey, vval, L.u.buf, n);
-    else lvl_sort<16>(vkey, vval, L.u.buf, n);
-  } else if constexpr (kMode == 5) {
-    lvl_sort<32>(vkey, vval, L.u.buf, n);
-  } else if constexpr (kMode == 0 || kMode == 7) {
-    // 7 (A/B, LEGO_VOXEL_SORT=ins): __final_insertion_sort as per-block insertion sorts in LDS (54 VGPRs
-    // instead of 132: the register sort's 2,048 (key, position) pairs are 64 VGPRs)
-    wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, kMode == 0);
+  if constexpr (kMode == 0) {
+    wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, true);
   } else if constexpr (kMode == 3) {
     if (P.voxel_stable) voxel_sort_stable<3>(vkey, vval, n);
     else wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, true);
@@ -2904,15 +2897,8 @@ LG_DEVICE int lessflat_list(const ScanView& v, int st, int en, uint16_t* list) {
 // k_voxel: surfPointsLessFlatScan -> VoxelGrid (leaf 0.2) per ring, one wave per ring.  A kernel
 // of its own so the register-resident voxel sort's VGPRs do not cut k_extract's occupancy.
 // ============================================================================================
-// kMode as voxel_ring: 0 for voxel_tie_order 0 by the stack emulation; 4 and 5 by the level-synchronous
-// one, split by ring size (each with its own register and LDS budget); 1 and 2 split the stable order's
+// kMode as voxel_ring: 0 for voxel_tie_order 0 by the stack emulation; 1 and 2 split the stable order's
 // rings by size; 3 either order.
-// 6: voxel_tie_order 0, rings of at most 1024 points by the level-synchronous sort, larger ones by the
-// stack emulation (one launch; LDS the union of both layouts).
-union VoxMixLds {
-  ExtractLds e;
-  VoxLvlLds<16> l;
-};
 template <int kM, class Lds>
 LG_DEVICE void voxel_wave(const LgParams& P, const ScanView& v, Lds& L, int n, RingOut& o) {
   for (int t = lane_id(); t < n; t += 64) vx_val(L)[t] = (uint16_t)t;
@@ -2920,10 +2906,9 @@ LG_DEVICE void voxel_wave(const LgParams& P, const ScanView& v, Lds& L, int n, R
   voxel_ring<kM>(P, v, L, n, 0, o);
 }
 template <int kMode>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kMode == 5 ? 2 : (kMode == 4 || kMode == 6) ? 3 : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
 void k_voxel(LgParams P, LgBufs B) {
-  __shared__ std::conditional_t<kMode == 4, VoxLvlLds<16>, std::conditional_t<kMode == 5, VoxLvlLds<32>,
-             std::conditional_t<kMode == 6, VoxMixLds, ExtractLds>>> L;
+  __shared__ ExtractLds L;
   const int V = P.V;
   const int b = blockIdx.x, sl = b / V, s = P.s0 + sl;
   const int ring = (b % V + sl / max(P.ncu / V, 1)) % V;  // ring rotation as in k_extract
@@ -2932,20 +2917,13 @@ void k_voxel(LgParams P, LgBufs B) {
   ScanView v;
   v.fa = B.lf_stage + sb * P.H;  // the ring's lessFlat points, in surfPointsLessFlatScan order
   const int n = B.lf_count[sb];
-  if (kMode != 3 && kMode != 6 && kMode != 7 &&
-      (P.voxel_stable ? (n > 1024 ? 2 : 1) : kMode >= 4 ? (n > 1024 ? 5 : 4) : 0) != kMode)
-    return;
+  if (kMode != 3 && (P.voxel_stable ? (n > 1024 ? 2 : 1) : 0) != kMode) return;
   RingOut o;
   o.lflat = B.r_lflat + sb * P.H;  // output half P.par too (k_publish of this scan reads it)
   o.nLF = 0;
   o.status = 0;
   PROF_T(t_vox0);
-  if constexpr (kMode == 6) {
-    if (n <= 1024) voxel_wave<4>(P, v, L.l, n, o);
-    else voxel_wave<0>(P, v, L.e, n, o);
-  } else {
-    voxel_wave<kMode>(P, v, L, n, o);
-  }
+  voxel_wave<kMode>(P, v, L, n, o);
   PROF_ADD(4, t_vox0);
   if (lane_id() == 0) {
     B.r_vcount[sb] = o.nLF;
@@ -4363,15 +4341,25 @@ __global__ __launch_bounds__(64) void k_publish(LgParams P, LgBufs B) {
   }
 }
 
+// The stream's per-scan odometry record (lego_batch_set_trajectory): transformCur and transformSum after
+// this association (publishOdometry, :1286-1298, runs every scan), at the stream's association count.
+LG_DEVICE void lm_record(const LgParams& P, const LgBufs& B, int s, LgState& S) {
+  if (B.traj && S.n_assoc < P.traj_cap) {
+    float* r = B.traj + ((size_t)s * P.traj_cap + S.n_assoc) * 12;
+    for (int k = 0; k < 6; ++k) {
+      r[k] = S.cur[k];
+      r[6 + k] = S.sum[k];
+    }
+  }
+  S.n_assoc++;
+}
+
 template <int kNT, int kMaxQ, bool kF1>
 __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
   __shared__ LmLdsT<kMaxQ> L;
   __shared__ LgState S;
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x;
   const int V = P.V, VH = P.VH;
-  if (P.lm_prio == 1) __builtin_amdgcn_s_setprio(1);
-  else if (P.lm_prio == 2) __builtin_amdgcn_s_setprio(2);
-  else if (P.lm_prio == 3) __builtin_amdgcn_s_setprio(3);
   // the scan's features: half P.par (k_concat), which the next scan's front end does not touch
   const size_t hs = (size_t)P.par * P.S + s;
   const int32_t* fc = B.fcnt + hs * 4;
@@ -4398,6 +4386,7 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
       S.tree_stale = 0;
       S.status = L.status | LEGO_ST_INIT;
       S.iters_surf = S.iters_corner = 0;
+      lm_record(P, B, s, S);
       B.state[s] = S;
     }
     return;
@@ -4493,6 +4482,7 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
       L.status |= LEGO_ST_EMITTED;
     }
     S.status = L.status;
+    lm_record(P, B, s, S);
     B.state[s] = S;
   }
 }
@@ -4554,11 +4544,7 @@ int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_sw_emit, g, dim3(SW_NT), 0, st, P, B);
     LG_CHECK_LAUNCH();
-    static const int swf_env = std::getenv("LEGO_SWF_NT") ? std::atoi(std::getenv("LEGO_SWF_NT")) : 0;  // (A/B)
-    if (swf_env == 256)
-      hipLaunchKernelGGL(k_sw_finish<256>, dim3(S), dim3(256), 0, st, P, B, (int)g.x);
-    else
-      hipLaunchKernelGGL(k_sw_finish<1024>, dim3(S), dim3(1024), 0, st, P, B, (int)g.x);
+    hipLaunchKernelGGL(k_sw_finish<1024>, dim3(S), dim3(1024), 0, st, P, B, (int)g.x);
   } else {
     size_t sm = (size_t)64 * 4 + (((size_t)P.VH * 2 + 3) & ~(size_t)3);
     hipLaunchKernelGGL(k_segment_lds, dim3(S), dim3(1024), sm, st, P, B);
@@ -4591,24 +4577,11 @@ int lg_launch_voxel(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   // off the SIMDs k_lm holds, which measured faster there.  With more scans than CUs the split
   // kernels (the common one at 83 VGPRs shares SIMDs with k_lm) measured faster: 245k vs 226k
   // scans/s at S = 512.
-  // voxel_tie_order 0 takes the stack emulation here: the level-synchronous sort (k_voxel<4> / <5>, or <6>
-  // for rings of at most 1024 points) has the lower latency on one ring but more instructions, and in the
-  // pipeline, where the VoxelGrid shares the CUs with k_lm and the next front end, it measured slower
-  // (C3: 143-151k / 164k vs 176-195k scans/s).  LEGO_VOXEL_SORT=level / mix selects them (A/B).
-  static const char* sort_env = std::getenv("LEGO_VOXEL_SORT");
-  static const int variant = !sort_env ? 0 : !strcmp(sort_env, "level") ? 1 : !strcmp(sort_env, "mix") ? 2 :
-                             !strcmp(sort_env, "ins") ? 3 : !strcmp(sort_env, "stack0") ? 4 : 0;
-  if (!P.voxel_stable && variant == 4) {
-    hipLaunchKernelGGL(k_voxel<0>, dim3(S * P.V), dim3(64), 0, st, P, B);
-  } else if (!P.voxel_stable && variant == 3) {
-    hipLaunchKernelGGL(k_voxel<7>, dim3(S * P.V), dim3(64), 0, st, P, B);
-  } else if (!P.voxel_stable && variant == 2) {
-    hipLaunchKernelGGL(k_voxel<6>, dim3(S * P.V), dim3(64), 0, st, P, B);
-  } else if (!P.voxel_stable && variant == 1) {
-    hipLaunchKernelGGL(k_voxel<4>, dim3(S * P.V), dim3(64), 0, st, P, B);
-    LG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_voxel<5>, dim3(S * P.V), dim3(64), 0, st, P, B);
-  } else if (S <= P.ncu) {
+  // voxel_tie_order 0 takes the stack emulation: the level-synchronous sort (lvl_sort) has the lower
+  // latency on one ring but more instructions, and in the pipeline, where the VoxelGrid shares the CUs
+  // with k_lm and the next front end, it measured slower (C3: 143-151k / 164k vs 176-195k scans/s;
+  // DESIGN §4).  It serves the map clouds (lego_s2m.hip).
+  if (S <= P.ncu) {
     hipLaunchKernelGGL(k_voxel<3>, dim3(S * P.V), dim3(64), 0, st, P, B);
   } else if (P.voxel_stable) {
     hipLaunchKernelGGL(k_voxel<1>, dim3(S * P.V), dim3(64), 0, st, P, B);
@@ -4892,8 +4865,9 @@ void k_sort_bench_lvl(const unsigned* keys, int n, unsigned* out) {
 }
 #endif
 
-// Counter calibration (MI355X_MICROARCH.md: FETCH_SIZE is calibrated only for 16-B-per-lane streaming
-// reads): k_project's input read patterns over S scans of points, one 1024-thread workgroup a scan,
+#ifdef LG_PROFILE
+// Counter calibration (profile build only; MI355X_MICROARCH.md: FETCH_SIZE is calibrated only for
+// 16-B-per-lane streaming reads): k_project's input read patterns over S scans of points, one 1024-thread workgroup a scan,
 // nothing else read and one float a lane written.  mode 0: the scatter pass's 12-byte buffer loads;
 // 1: 16-byte loads of the same points; 2: mode 0, then every point again as a 16-byte load (the
 // column pass's re-gather, in point order).
@@ -4936,12 +4910,19 @@ __global__ __launch_bounds__(1024) void k_fetch_probe(int mode, const float4* __
   out[(size_t)s * nt + tid] = acc;
 }
 
+#endif
+
 extern "C" int lego_debug_fetch_probe(int32_t mode, int32_t S, const void* pts, const int64_t* offs,
                                       const int32_t* cnts, float* out, void* stream) {
+#ifdef LG_PROFILE
   if (mode < 0 || mode > 2 || S < 1 || !pts || !offs || !cnts || !out) return LEGO_EINVAL;
   hipLaunchKernelGGL(k_fetch_probe, dim3(S), dim3(1024), 0, (hipStream_t)stream, mode, (const float4*)pts, offs,
                      cnts, out);
   return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
+#else
+  (void)mode; (void)S; (void)pts; (void)offs; (void)cnts; (void)out; (void)stream;
+  return LEGO_ENOTSUP;
+#endif
 }
 
 // Diagnostics (profile build only): time `blocks` concurrent copies of one device sort.

@@ -1415,11 +1415,12 @@ LG_DEVICE int vxs_block_scan(int v, int* sh, int& total) {
 // the stop flags of position p of range g (p > f) against pivot pv: lf | rf << 16
 LG_DEVICE int vxs_flags(unsigned k, unsigned pv) { return (k >= pv ? 1 : 0) | ((k <= pv ? 1 : 0) << 16); }
 
-// grid (chunks, big ranges): per chunk the counts of left / right stops (packed lf | rf << 16)
+// grid (big ranges x maxch chunks, one dimension: block b is chunk b % maxch of range b / maxch): per
+// chunk the counts of left / right stops (packed lf | rf << 16)
 __global__ __launch_bounds__(VXS_TPB) void k_vxs_count(const VxsSeg* segs, const int* nseg, const unsigned* keys,
                                                        const unsigned* pivot, int* cnt, int maxch) {
   __shared__ int sh[VXS_TPB / 64];
-  const int s = blockIdx.y, c = blockIdx.x;
+  const int s = blockIdx.x / maxch, c = blockIdx.x % maxch;
   if (s >= *nseg) return;
   const VxsSeg g = segs[s];
   const int c0 = g.f + c * VXS_CH;
@@ -1437,14 +1438,14 @@ __global__ __launch_bounds__(VXS_TPB) void k_vxs_count(const VxsSeg* segs, const
   if (threadIdx.x == 0) cnt[(size_t)s * maxch + c] = total;
 }
 
-// grid (chunks, big ranges): each stop's rank, Hoare's swaps through the scratch slots (f + k for the
+// grid (as k_vxs_count): each stop's rank, Hoare's swaps through the scratch slots (f + k for the
 // k-th right stop, l - 1 - k for the k-th left stop), the read-back slot of every swapped position and
 // the cut (the first left stop with D >= 0 or right stop with D > 0)
 __global__ __launch_bounds__(VXS_TPB) void k_vxs_exchange(const VxsSeg* segs, const int* nseg, const unsigned* keys,
                                                           const unsigned* vals, const unsigned* pivot, const int* cnt,
                                                           int maxch, unsigned* xk, unsigned* xv, int* rds, int* cut) {
   __shared__ int sh[VXS_TPB / 64];
-  const int s = blockIdx.y, c = blockIdx.x;
+  const int s = blockIdx.x / maxch, c = blockIdx.x % maxch;
   if (s >= *nseg) return;
   const VxsSeg g = segs[s];
   const int c0 = g.f + c * VXS_CH;
@@ -1498,11 +1499,11 @@ __global__ __launch_bounds__(VXS_TPB) void k_vxs_exchange(const VxsSeg* segs, co
   if ((threadIdx.x & 63) == 0 && best != 0x7fffffff) atomicMin(&cut[s], best);
 }
 
-// grid (chunks, big ranges): swapped positions take their pair's element
+// grid (as k_vxs_count): swapped positions take their pair's element
 __global__ __launch_bounds__(VXS_TPB) void k_vxs_readback(const VxsSeg* segs, const int* nseg, unsigned* keys,
                                                           unsigned* vals, const unsigned* xk, const unsigned* xv,
-                                                          const int* rds) {
-  const int s = blockIdx.y, c = blockIdx.x;
+                                                          const int* rds, int maxch) {
+  const int s = blockIdx.x / maxch, c = blockIdx.x % maxch;
   if (s >= *nseg) return;
   const VxsSeg g = segs[s];
   const int c0 = g.f + c * VXS_CH;
@@ -1552,25 +1553,46 @@ __global__ __launch_bounds__(64) void k_vxs_init(const int* seg_b, const int* se
 // (R = 16 for ranges of at most 1,024 positions, else 32: two kernels, each with its register budget)
 // The point indices may exceed lvl_sort's 16-bit values: the sort carries range positions, and the
 // indices follow through the scratch copy xv of the range.
+// lvl_sort takes keys below 2^31 - 1.  k_vox_keys' leaf indices can reach that: PCL's overflow gate
+// multiplies the truncated extents (hi - lo) / leaf + 1, the index uses floor(hi / leaf) - floor(lo / leaf)
+// + 1 per axis, which can be one larger.  A range holding such a key sorts the number of its keys below
+// each key instead (order- and tie-preserving, < 2,048), and the keys come back through the scratch xk.
 template <int R>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R == 32 ? 2 : 3)))
-void k_vxs_small(const VxsSeg* segs, const int* nseg, unsigned* keys, unsigned* vals, unsigned* xv) {
+void k_vxs_small(const VxsSeg* segs, const int* nseg, unsigned* keys, unsigned* vals, unsigned* xk, unsigned* xv) {
   __shared__ lgws::VoxLvlLds<R> L;
   const int s = blockIdx.x;
   if (s >= *nseg) return;
   const VxsSeg g = segs[s];
   const int n = g.l - g.f;
   if ((n > 1024) != (R == 32) || n <= 1) return;
+  unsigned big = 0u;
   for (int i = threadIdx.x; i < n; i += 64) {
-    L.u.nat.key[i] = keys[g.f + i];
+    const unsigned k = keys[g.f + i];
+    big |= k >= 0x7fffffffu ? 1u : 0u;
+    L.u.nat.key[i] = k;
     L.u.nat.val[i] = (uint16_t)i;
     xv[g.f + i] = vals[g.f + i];
   }
   __syncthreads();
+  const bool ranked = __ballot(big != 0u) != 0ull;
+  if (ranked) {  // (pathological extents only) keys -> count of smaller keys, O(n^2 / 64) a lane
+    for (int i = threadIdx.x; i < n; i += 64) xk[g.f + i] = L.u.nat.key[i];
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      const int i = i0 + (int)threadIdx.x;
+      const unsigned k = i < n ? xk[g.f + i] : 0u;
+      unsigned r = 0u;
+      for (int j = 0; j < n; ++j) r += xk[g.f + j] < k ? 1u : 0u;
+      if (i < n) L.u.nat.key[i] = r;
+    }
+    __syncthreads();
+  }
   lgws::lvl_sort<R>(L.u.nat.key, L.u.nat.val, L.u.buf, n, g.d);
   for (int i = threadIdx.x; i < n; i += 64) {
-    keys[g.f + i] = L.u.nat.key[i];
-    vals[g.f + i] = xv[g.f + L.u.nat.val[i]];
+    const int from = L.u.nat.val[i];
+    keys[g.f + i] = ranked ? xk[g.f + from] : L.u.nat.key[i];
+    vals[g.f + i] = xv[g.f + from];
   }
 }
 
@@ -1638,23 +1660,28 @@ static int s2m_alloc_lm(lego_s2m* m) {
   const size_t kd_node = 2 * mp * sizeof(KdNode), kd_vind = mp * 4, kd_tmp = 2 * mp * 4, kd_frames = (10 * mp + S2M_KD_STACK) * 4,
                tieq = mp * 4;
   const size_t kd_per = 2 * (kd_node + kd_vind) + kd_tmp + kd_frames + tieq;
+  // into locals: m keeps nothing of a partial failure (the next call allocates again from scratch)
   S2mScratch* d_scratch = nullptr;
-  if (hipMalloc(&m->d_mem, per * 2 * max_problems) != hipSuccess ||
-      hipMalloc(&m->d_kd, kd_per * max_problems) != hipSuccess ||
-      hipMalloc((void**)&d_scratch, sizeof(S2mScratch) * 2 * max_problems) != hipSuccess) {
+  void *d_mem = nullptr, *d_kd = nullptr;
+  auto fail = [&](int rc) {
     if (d_scratch) hipFree(d_scratch);
-    return LEGO_ENOMEM;
-  }
+    if (d_kd) hipFree(d_kd);
+    if (d_mem) hipFree(d_mem);
+    return rc;
+  };
+  if (hipMalloc(&d_mem, per * 2 * max_problems) != hipSuccess || hipMalloc(&d_kd, kd_per * max_problems) != hipSuccess ||
+      hipMalloc((void**)&d_scratch, sizeof(S2mScratch) * 2 * max_problems) != hipSuccess)
+    return fail(LEGO_ENOMEM);
   S2mScratch* h = new (std::nothrow) S2mScratch[2 * max_problems];
-  if (!h) { hipFree(d_scratch); return LEGO_ENOMEM; }
-  char* base = (char*)m->d_mem;
+  if (!h) return fail(LEGO_ENOMEM);
+  char* base = (char*)d_mem;
   for (int k = 0; k < 2 * max_problems; ++k) {
     char* b = base + per * k;
     h[k].start = (int*)b;
     h[k].pts = (float4*)(b + ((tab + 255) & ~(size_t)255));
     h[k].idx = (int*)(b + ((tab + 255) & ~(size_t)255) + pts);
     h[k].rows = (float4*)(b + ((tab + 255) & ~(size_t)255) + pts + ((idx + 255) & ~(size_t)255));
-    char* kb = (char*)m->d_kd + kd_per * (k / 2);
+    char* kb = (char*)d_kd + kd_per * (k / 2);
     h[k].kd_node = (KdNode*)(kb + (k % 2) * (kd_node + kd_vind));
     h[k].kd_vind = (int*)(kb + (k % 2) * (kd_node + kd_vind) + kd_node);
     h[k].kd_tmp = (int*)(kb + 2 * (kd_node + kd_vind));
@@ -1663,7 +1690,9 @@ static int s2m_alloc_lm(lego_s2m* m) {
   }
   const bool ok = hipMemcpy(d_scratch, h, sizeof(S2mScratch) * 2 * max_problems, hipMemcpyHostToDevice) == hipSuccess;
   delete[] h;
-  if (!ok) { hipFree(d_scratch); return LEGO_EDEVICE; }
+  if (!ok) return fail(LEGO_EDEVICE);
+  m->d_mem = d_mem;
+  m->d_kd = d_kd;
   m->d_scratch = d_scratch;
   return LEGO_OK;
 }
@@ -1973,9 +2002,9 @@ static int map_voxel_std_order(lego_s2m* m, int n, const lego_map_voxel_io* io, 
       return LEGO_EDEVICE;
     const int nbig = m->h_ctr[0];
     if (nbig == 0) break;
-    if (nbig > m->cap_big || nbig > 65535 || level > 64) return LEGO_EDEVICE;  // (bounded by construction)
+    if (nbig > m->cap_big || level > 64) return LEGO_EDEVICE;  // (bounded by construction)
     const int g64 = (nbig + 63) / 64;
-    const dim3 gch(m->vxs_maxch, nbig);
+    const dim3 gch((unsigned)((size_t)m->vxs_maxch * nbig));  // < 2^32: e / VXS_CH chunks at most
     if (hipMemsetAsync(ctr + 1, 0, 4, st) != hipSuccess) return LEGO_EDEVICE;
     hipLaunchKernelGGL(k_vxs_median, dim3(g64), dim3(64), 0, st, (const VxsSeg*)cur, (const int*)ctr, m->d_keys,
                        m->d_vals, m->d_pivot, m->d_cut);
@@ -1985,7 +2014,8 @@ static int map_voxel_std_order(lego_s2m* m, int n, const lego_map_voxel_io* io, 
                        (const unsigned*)m->d_keys, (const unsigned*)m->d_vals, (const unsigned*)m->d_pivot,
                        (const int*)m->d_cnt, m->vxs_maxch, m->d_xk, m->d_xv, m->d_rds, m->d_cut);
     hipLaunchKernelGGL(k_vxs_readback, gch, dim3(VXS_TPB), 0, st, (const VxsSeg*)cur, (const int*)ctr, m->d_keys,
-                       m->d_vals, (const unsigned*)m->d_xk, (const unsigned*)m->d_xv, (const int*)m->d_rds);
+                       m->d_vals, (const unsigned*)m->d_xk, (const unsigned*)m->d_xv, (const int*)m->d_rds,
+                       m->vxs_maxch);
     hipLaunchKernelGGL(k_vxs_split, dim3(g64), dim3(64), 0, st, (const VxsSeg*)cur, (const int*)ctr,
                        (const int*)m->d_cut, nxt, ctr + 1, m->d_small, ctr + 2, m->d_heap, ctr + 3);
     if (hipGetLastError() != hipSuccess) return LEGO_EDEVICE;
@@ -1999,9 +2029,9 @@ static int map_voxel_std_order(lego_s2m* m, int n, const lego_map_voxel_io* io, 
   if (nsmall > m->cap_small || nheap > m->cap_big) return LEGO_EDEVICE;
   if (nsmall > 0) {
     hipLaunchKernelGGL(k_vxs_small<16>, dim3(nsmall), dim3(64), 0, st, (const VxsSeg*)m->d_small, (const int*)(ctr + 2),
-                       m->d_keys, m->d_vals, m->d_xv);
+                       m->d_keys, m->d_vals, m->d_xk, m->d_xv);
     hipLaunchKernelGGL(k_vxs_small<32>, dim3(nsmall), dim3(64), 0, st, (const VxsSeg*)m->d_small, (const int*)(ctr + 2),
-                       m->d_keys, m->d_vals, m->d_xv);
+                       m->d_keys, m->d_vals, m->d_xk, m->d_xv);
   }
   if (nheap > 0)
     hipLaunchKernelGGL(k_vxs_heap, dim3(nheap), dim3(64), 0, st, (const VxsSeg*)m->d_heap, (const int*)(ctr + 3),

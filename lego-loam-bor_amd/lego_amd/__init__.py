@@ -84,6 +84,7 @@ def lib():
         L.lego_batch_set_groups.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_lag.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_probe.argtypes = [C.c_void_p, C.c_int32]
+        L.lego_batch_set_trajectory.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.lego_batch_probe_times.argtypes = [C.c_void_p, P(C.c_float), P(C.c_int32)]
         L.lego_batch_set_wide.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_wide.argtypes = [C.c_void_p]
@@ -239,6 +240,12 @@ class Batch:
     def set_groups(self, groups):
         """Launch the streams as `groups` slices on separate HIP streams (overlapping kernel tails)."""
         _check(lib().lego_batch_set_groups(self.h, int(groups)), "lego_batch_set_groups")
+
+    def set_trajectory(self, d_traj_ptr, max_scans):
+        """Per-scan odometry record (lego_batch_set_trajectory): a device array of S * max_scans * 12
+        float32 (transformCur, transformSum after each association); (0, 0) stops recording."""
+        _check(lib().lego_batch_set_trajectory(self.h, C.c_void_p(d_traj_ptr or None), int(max_scans)),
+               "lego_batch_set_trajectory")
 
     def set_probe(self, on=True):
         """Events around the projection and smoothness stages of every overlap-schedule step."""

@@ -398,9 +398,13 @@ int voxel_grid(const std::vector<Pt>& in, float leaf, std::vector<Pt>& out, bool
     int ijk0 = static_cast<int>(std::floor(in[i].x * inv) - static_cast<float>(min_b[0]));
     int ijk1 = static_cast<int>(std::floor(in[i].y * inv) - static_cast<float>(min_b[1]));
     int ijk2 = static_cast<int>(std::floor(in[i].z * inv) - static_cast<float>(min_b[2]));
-    int idx = ijk0 * divb_mul[0] + ijk1 * divb_mul[1] + ijk2 * divb_mul[2];
+    // PCL computes this in int and stores it as unsigned int; past 2^31 - 1 (extents its overflow gate,
+    // which multiplies the truncated (max - min) / leaf + 1, lets through) the int wraps: the same bits
+    // as this unsigned arithmetic, without the signed-overflow UB in the oracle itself
+    const unsigned idx = (unsigned)ijk0 * (unsigned)divb_mul[0] + (unsigned)ijk1 * (unsigned)divb_mul[1] +
+                         (unsigned)ijk2 * (unsigned)divb_mul[2];
     cloud_point_index_idx e;
-    e.idx = static_cast<unsigned int>(idx);
+    e.idx = idx;
     e.cloud_point_index = (unsigned int)i;
     iv.push_back(e);
   }

@@ -13,8 +13,9 @@
 // Build (where ROS Kinetic/Melodic, PCL and the reference's catkin package exist): replace
 // src/imageProjection.cpp and src/featureAssociation.cpp in LeGO-LOAM/CMakeLists.txt's lego_loam target
 // by ros/lego_nodes.cpp, add include/ and ros/ to its include directories and link
-// lego-loam-bor_amd/lego_amd/liblego_frontend.so.  Not compiled in this repository:
-// ROS is not installed here.
+// lego-loam-bor_amd/lego_amd/liblego_frontend.so.  ROS is not installed here: the
+// unit is syntax-checked against test-only declaration stubs of the ROS / PCL / tf symbols it uses
+// (tests/test_ros_unit_cpu.py, tests/native/ros_stubs/).
 #ifndef LEGO_AMD_ROS_NODES_H
 #define LEGO_AMD_ROS_NODES_H
 

@@ -6,7 +6,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "lego-loam-bor_amd")
-for p in (PKG, os.path.join(REPO, "oracle"), os.path.join(REPO, "tests"), os.path.join(REPO, "tests", "golden")):
+for p in (PKG, os.path.join(REPO, "oracle"), os.path.join(REPO, "tests"), os.path.join(REPO, "tests", "golden"), REPO):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -1,0 +1,80 @@
+"""The exact configuration bench.py times, against the oracle.
+
+bench.py's headline builds Batch(S = 256 VLP-16 sequences) with voxel_tie_order 0 and
+bench.configure_batch: lag 2, lego_batch_set_wide(-1) (the wide layout at 256 scans for this order), one
+caller stream; W warm-up steps, flush, K timed steps, flush.  The same batch here, with every scan's
+odometry recorded on the device (lego_batch_set_trajectory, which does not change the schedule): each of
+the 256 streams' transformCur / transformSum after every scan within 1e-4 of an independent oracle run
+(featureAssociation.cpp:1213-1270, 1286-1298), and exact parity of the last scan (projection, features,
+Last clouds) on a sample of streams.  The stable order runs its own bench schedule (lag 1, one-workgroup
+layout) the same way.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import bench
+import helpers as Hs
+import lego_amd as L
+from lego_amd import _abi as A
+from test_gpu_parity import assert_scan_parity, oracle_for
+
+pytestmark = pytest.mark.gpu
+
+S, W, K = 256, 3, 6
+
+
+def _oracle_sequence(params, pts, cnt, s):
+    orc = oracle_for(params)
+    traj, last = [], None
+    for k in range(W + K):
+        pr = orc.cloud_handler(pts[k * S + s, :cnt[k * S + s]])
+        fr = orc.feature_association()
+        traj.append(np.concatenate([fr["transform_cur"], fr["transform_sum"]]))
+        last = (pr, fr)
+    return np.array(traj, np.float64), last
+
+
+@pytest.mark.parametrize("order,wide", [(0, 1), (1, 0)])
+def test_bench_schedule_matches_oracle(gpu, order, wide):
+    import torch
+    params = L.params_vlp16(voxel_tie_order=order)
+    cfg = A.synth_cfg("vlp16")
+    cap = params.num_vertical_scans * params.num_horizontal_scans
+    seqs = np.repeat(np.arange(S, dtype=np.int32)[None, :], W + K, 0).reshape(-1)  # bench.py's sequences 0 .. S-1
+    scans = np.repeat(np.arange(W + K, dtype=np.int32)[:, None], S, 1).reshape(-1)
+    pts, cnt = A.synth_batch(cfg, seqs, scans)
+    d_pts = torch.from_numpy(pts).cuda()
+    d_off = torch.from_numpy((np.arange((W + K) * S, dtype=np.int64) * cap).reshape(W + K, S)).cuda()
+    d_cnt = torch.from_numpy(cnt.reshape(W + K, S).astype(np.int32)).cuda()
+    b = L.Batch(params, S, cap)
+    lag = bench.configure_batch(b, order)
+    assert lag == bench.default_lag(order) and b.wide() == wide  # the layout the bench line reports
+    traj = torch.zeros((S, W + K, 12), dtype=torch.float32, device="cuda")
+    b.set_trajectory(traj.data_ptr(), W + K)
+    stream = torch.cuda.current_stream()
+    for k in range(W):  # bench.timed(): warm-up, flush, timed steps, flush
+        b.step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
+    b.flush()
+    torch.cuda.synchronize()
+    for k in range(W, W + K):
+        b.step(d_pts.data_ptr(), d_off[k].data_ptr(), d_cnt[k].data_ptr(), stream.cuda_stream)
+    b.flush()
+    torch.cuda.synchronize()
+    got = traj.cpu().numpy().astype(np.float64)
+    poses, status = b.poses()
+    assert np.all((status & A.ST_UB_MASK) == 0)
+    with ThreadPoolExecutor(8) as ex:  # the oracle's ctypes calls release the GIL
+        ref = list(ex.map(lambda s: _oracle_sequence(params, pts, cnt, s), range(S)))
+    worst = max(float(np.abs(got[s] - ref[s][0]).max()) for s in range(S))
+    exact = sum(int(np.array_equal(got[s].astype(np.float32), ref[s][0].astype(np.float32))) for s in range(S))
+    print("order %d: %d streams x %d scans, max |d pose| %.3g, %d streams bit-identical" % (
+        order, S, W + K, worst, exact))
+    assert worst <= Hs.TF_TOL
+    np.testing.assert_array_equal(got[:, -1].astype(np.float32), poses)
+    for s in (0, 101, 202, S - 1):  # exact parity of the last scan on a sample
+        pg, fg = b.read(s)
+        pr, fr = ref[s][1]
+        assert_scan_parity((order, s), pg, pr, fg, fr)
+    b.close()

@@ -131,6 +131,33 @@ def test_voxel_overflow_then_normal_clouds(s2m, sequences, order):
     assert got[0][2] == 0x100 and got[4][2] == 0x100
 
 
+@pytest.mark.parametrize("order", [0, 1])
+def test_voxel_keys_past_2_31(s2m, order):
+    """Leaf indices of 2^31 and above: PCL's overflow gate multiplies the truncated extents
+    (dx = (max - min) / leaf + 1 = 1290 per axis, 1290^3 < 2^31 - 1: not flagged), while the indices use
+    floor(max / leaf) - floor(min / leaf) + 1 = 1291 per axis, so the largest leaf index is ~2.15e9.
+    The std::sort-order path's per-range sort takes keys below 2^31 - 1 and ranks such ranges first."""
+    s2m.set_voxel_tie_order(order)
+    rng = np.random.default_rng(31)
+    lo, hi = 0.005, 12.904  # leaf 0.01: lo / leaf = 0.5, hi / leaf = 1290.4, (hi - lo) / leaf = 1289.9
+    corners = np.array([[x, y, z, 1.0] for x in (lo, hi) for y in (lo, hi) for z in (lo, hi)], np.float32)
+    def cloud(n):
+        near_hi = hi - rng.uniform(0, 0.05, (n // 3, 3))  # top voxels: keys past 2^31
+        near_lo = lo + rng.uniform(0, 0.05, (n // 3, 3))
+        mid = rng.uniform(lo, hi, (n - 2 * (n // 3), 3))
+        p = np.concatenate([near_hi, near_lo, mid])
+        p = np.concatenate([p, rng.uniform(0, 1, (len(p), 1))], 1).astype(np.float32)
+        p = np.concatenate([corners, p, p[: n // 4]])  # repeated points: ties
+        return p[rng.permutation(len(p))]
+    clouds = [cloud(1500), cloud(6000), cloud(40000)]
+    got = _gpu_voxel(s2m, clouds, [0.01] * len(clouds))
+    for c, (o, on, st) in zip(clouds, got):
+        ref, rst = O.voxel_grid(c, 0.01, stable=order == 1)
+        assert rst == 0, "the cloud must pass PCL's overflow gate"
+        assert st == rst and on == len(ref), (len(c), on, len(ref))
+        assert np.array_equal(o.view(np.int32), ref.view(np.int32)), len(c)
+
+
 def test_voxel_std_order_key_sequences(s2m):
     """voxel_tie_order 0 on clouds whose leaf indices are chosen key sequences (points at x = key + 0.5, leaf 1):
     tie-heavy random keys up to 100k points (several device-wide levels, then one wave a range), sorted,

@@ -1,15 +1,18 @@
-"""Per-kernel duration summary from a rocprofv3 kernel trace of bench.py, split by bench phase.
+"""Per-kernel duration summary from a rocprofv3 kernel trace of bench.py, split by bench pass.
 
-  python tools/trace_split.py run_kernel_trace.csv OUT.csv [--steps K] [--warmup W]
+  python tools/trace_split.py run_kernel_trace.csv OUT.csv [--steps K] [--warmup W] [--roofline-reps R]
+      [--passes throughput,probe,timing]
 
-bench.py runs the W + K steps twice: first the throughput pass (the timed region; with lag 1 and one
-slice, k_publish / k_lm run on an internal stream concurrently with the next scan's front end, so a
-kernel's duration there includes sharing the GPU), then the per-stage timing pass (one stream, stages
-in sequence) whose last K launches give bench.py's stages_ms, and for k_project / k_fa_prep the
-roofline pass (R back-to-back pairs, --roofline-reps) that gives roofline.launch_ms.  rocprofv3's
---stats file averages all passes; this split reports them apart, so the timing pass can be compared
-with the bench line.  Launches are assigned to the passes in time order, per kernel (each kernel runs
-once per step in each pass).
+Run bench.py under the profiler with --no-alt-order --roofline-streams 0 --no-c5, so every launch of a
+given (kernel, grid) belongs to the one C3 batch.  bench.py then runs the W + K steps three times --
+the throughput pass (the timed region), the probe pass (events around the projection and smoothness
+stages: roofline.in_pipeline) and the per-stage timing pass (one stream, stages in sequence: stages_ms)
+-- and then launches the roofline pair (projection kernels + k_fa_prep4) R times back to back
+(roofline.launch_ms).  rocprofv3's --stats file averages all of them; this split reports them apart.
+Launches are assigned to the passes in time order, per (kernel, grid): every kernel of the step runs
+once per step in each pass (the pipeline is flushed at the end of each pass, so the lagged LM and
+publish launches of a pass's scans stay inside it).  A (kernel, grid) whose count does not fit is
+reported whole ("all").  The roofline rows' mean is what bench.py's roofline.launch_ms times with events.
 """
 import argparse
 import collections
@@ -23,34 +26,43 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--roofline-reps", type=int, default=20, help="bench.py's back-to-back roofline launches")
+    ap.add_argument("--passes", default="throughput,probe,timing")
     a = ap.parse_args()
     per = a.steps + a.warmup
+    names = a.passes.split(",")
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(a.trace)):
         name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
         if name.startswith("__amd") or "rocprim" in name:
             continue
-        grid = int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1)
+        grid = int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) // max(
+            int(r["Workgroup_Size_X"]) * int(r.get("Workgroup_Size_Y", 1) or 1), 1)
         acc[(name, grid)].append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
     rows = []
+    pair = collections.defaultdict(float)
     for (name, grid), v in sorted(acc.items()):
         v.sort()
         d = [x for _, x in v]
-        if len(d) == 2 * per:  # throughput pass, then the timing pass (measured: its last K)
-            parts = (("throughput_pass", d[a.warmup:per]), ("timing_pass", d[per + a.warmup:]))
-        elif len(d) == 2 * per + a.roofline_reps:  # + the roofline pass (k_project / k_fa_prep)
-            parts = (("throughput_pass", d[a.warmup:per]), ("timing_pass", d[per + a.warmup:2 * per]),
-                     ("roofline_pass", d[2 * per:]))
+        npass = len(names)
+        if len(d) in (npass * per, npass * per + a.roofline_reps):
+            parts = [("%s_pass" % nm, d[i * per + a.warmup:(i + 1) * per]) for i, nm in enumerate(names)]
+            if len(d) > npass * per:
+                parts.append(("roofline_pass", d[npass * per:]))
         else:
-            parts = (("all", d),)
+            parts = [("all", d)]
         for phase, x in parts:
-            rows.append([name, grid, phase, len(x), round(sum(x) / len(x), 2), round(min(x), 2), round(max(x), 2)])
+            avg = sum(x) / len(x)
+            rows.append([name, grid, phase, len(x), round(avg, 2), round(min(x), 2), round(max(x), 2)])
+            if phase == "roofline_pass":
+                pair["roofline_pass"] += avg
     with open(a.out, "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["kernel", "workgroups", "phase", "calls", "avg_us", "min_us", "max_us"])
         for r in rows:
             w.writerow(r)
-            print("%-24s wg=%6d %-16s calls=%3d avg %9.2f us  min %9.2f  max %9.2f" % tuple(r))
+            print("%-28s wg=%7d %-16s calls=%3d avg %9.2f us  min %9.2f  max %9.2f" % tuple(r))
+    if pair:
+        print("roofline pair (sum of the roofline_pass means): %.2f us" % pair["roofline_pass"])
 
 
 if __name__ == "__main__":
