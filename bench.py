@@ -449,6 +449,7 @@ def main():
     pair_ms = batch.time_hbm_stages(d_pts.data_ptr(), d_off[k_last].data_ptr(), d_cnt[k_last].data_ptr(),
                                     d_off[k_alt].data_ptr(), d_cnt[k_alt].data_ptr(),
                                     reps=args.roofline_reps, stream=stream.cuda_stream)
+    voxel_ms = batch.time_voxel(reps=10, stream=stream.cuda_stream)  # the VoxelGrid stage alone
     n_mean = float(host_cnt[W:].mean())
     # Algorithmic bytes, per launch of S scans:
     #   projection  B_proj = 16 N + 20 V H  (read x,y,z,i of every point; write range + cloud cell of every cell)
@@ -498,7 +499,7 @@ def main():
         "roofline": roofline,
         "stages_ms": {"project": round(stage[0], 4), "segment": round(stage[1], 4), "fa_prep": round(stage[2], 4),
                       "extract": round(stage[3], 4), "concat_publish": round(stage[4], 4),
-                      "lm": round(stage[5], 4)},
+                      "lm": round(stage[5], 4), "voxel_alone": round(voxel_ms, 4)},
         "other_voxel_tie_order": alt,
         "lm_status_bits": int(np.bitwise_or.reduce(status)),
         "trajectories_gathered": int(traj_all.shape[0]),

@@ -216,6 +216,11 @@ int  lego_batch_stage_times(lego_batch* b, float* ms6);
 int  lego_batch_time_hbm_stages(lego_batch* b, int32_t reps, const lego_point* d_points, const int64_t* d_offsets,
                                 const int32_t* d_counts, const int64_t* d_offsets_alt, const int32_t* d_counts_alt,
                                 void* hip_stream, float* ms_pair);
+/* Measurement: the VoxelGrid stage (PCL VoxelGrid of every ring's lessFlat cloud, featureAssociation.cpp:
+ * 377-379) of the batch's last step launched `reps` times back to back on hip_stream, alone on the device
+ * (it synchronises first); *ms = mean milliseconds a launch.  Idempotent (same staged input, same output).
+ * bench.py's stages_ms.voxel_alone. */
+int  lego_batch_time_voxel(lego_batch* b, int32_t reps, void* hip_stream, float* ms);
 /* While timing is enabled, steps run as one slice on the caller's stream (plus the VoxelGrid stream). */
 int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
 /* Measurement: while the probe is on, every overlap-schedule step records events around its projection

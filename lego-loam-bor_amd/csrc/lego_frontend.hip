@@ -909,6 +909,34 @@ int lego_batch_time_hbm_stages(lego_batch* b, int32_t reps, const lego_point* d_
   return rc;
 }
 
+int lego_batch_time_voxel(lego_batch* b, int32_t reps, void* hip_stream, float* ms) {
+  if (!b || reps < 1 || !ms) return LEGO_EINVAL;
+  if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
+  hipStream_t st = (hipStream_t)hip_stream;
+  int rc = flush_pending(b);
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;  // nothing else on the device
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return LEGO_EDEVICE;
+  if (hipEventCreate(&e1) != hipSuccess) {
+    hipEventDestroy(e0);
+    return LEGO_EDEVICE;
+  }
+  LgParams P = b->P;
+  P.s0 = 0;
+  P.par = b->last_par;  // the last step's staged lessFlat clouds and VoxelGrid output
+  if (hipEventRecord(e0, st) != hipSuccess) rc = LEGO_EDEVICE;
+  for (int r = 0; r < reps && !rc; ++r) rc = lg_launch_voxel(P, b->B, b->S, st);
+  if (!rc && hipEventRecord(e1, st) != hipSuccess) rc = LEGO_EDEVICE;
+  float t = 0.f;
+  if (!rc && hipEventSynchronize(e1) != hipSuccess) rc = LEGO_EDEVICE;
+  if (!rc && hipEventElapsedTime(&t, e0, e1) != hipSuccess) rc = LEGO_EDEVICE;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (!rc) *ms = t / reps;
+  return rc;
+}
+
 // Header of stream s (counts, orientation, state) into pinned memory, on st, then wait for it.
 struct ReadHdr {
   int32_t cnt[CNT_N];

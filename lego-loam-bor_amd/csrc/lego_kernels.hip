@@ -1898,15 +1898,19 @@ __global__ __launch_bounds__(FP4_NT) void k_fa_prep4(LgParams P, LgBufs B) {
 #define SEG_MAX 512
 #define RING_MAX 2048
 
-struct ExtractLds {  // k_voxel (and the sort test hooks): 13.5 KB per wave
+// The introsort emulation's scratch: stk, its range stack (one packed frame a word, sort_frame), and tab,
+// wave_partition_ranked's rank table (16-bit positions, (range length) / 2 of them).
+struct ExtractLds {  // k_voxel (and the sort test hooks): 14.5 KB per wave (11 waves a CU by LDS)
+  unsigned blk[RING_MAX / 32];  // final-block start bits of the introsort emulation; also the 15 words
+                                // final_window may read (and ignore) below vkey[0]
   union {
     struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;  // segment sort (test hook)
     unsigned vkey[RING_MAX];                                 // voxel keys
   } u;
   uint16_t vval[RING_MAX];      // lessFlat positions of the ring (relative to the ring start), sorted with vkey
-  unsigned blk[RING_MAX / 32];  // final-block start bits of the introsort emulation
-  int stk[3 * 64];
-  int tab[128];                 // lane-pairing / stop-queue scratch of the partitions
+                                // (also read, and ignored, by final_window past vkey[n - 1])
+  int stk[64];
+  int tab[RING_MAX / 4];
 };
 
 struct SegLds {  // k_sortseg: 5.6 KB per wave
@@ -1915,8 +1919,8 @@ struct SegLds {  // k_sortseg: 5.6 KB per wave
     uint16_t col[SEG_MAX + 16];                             // colInd around the segment (info words)
   } u;
   unsigned blk[RING_MAX / 32];
-  int stk[3 * 64];
-  int tab[128];
+  int stk[64];
+  int tab[SEG_MAX / 4];
 };
 
 template <typename T>
@@ -1938,7 +1942,7 @@ LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last,
   int v = in ? (int)a.val[first + lane] : 0;
   // __move_median_to_first(first, first+1, mid, last-1)
   const int im = m / 2, il = m - 1;
-  const K kx = __shfl(k, 1), ky = __shfl(k, im), kz = __shfl(k, il);
+  const K kx = rdlane(k, 1), ky = rdlane(k, im), kz = rdlane(k, il);  // (uniform lanes: no LDS crossbar)
   int sel;
   if (kx < ky) {
     if (ky < kz) sel = im;
@@ -1948,12 +1952,12 @@ LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last,
   else if (ky < kz) sel = il;
   else sel = im;
   {
-    const K k0 = __shfl(k, 0), ks = __shfl(k, sel);
-    const int v0 = __shfl(v, 0), vs = __shfl(v, sel);
+    const K k0 = rdlane(k, 0), ks = rdlane(k, sel);
+    const int v0 = __builtin_amdgcn_readlane(v, 0), vs = __builtin_amdgcn_readlane(v, sel);
     if (lane == 0) { k = ks; v = vs; }
     else if (lane == sel) { k = k0; v = v0; }
   }
-  const K pv = __shfl(k, 0);
+  const K pv = rdlane(k, 0);
   const bool lf = in && lane >= 1 && !(k < pv);
   const bool rf = in && lane >= 1 && !(pv < k);
   const unsigned long long bl = __ballot(lf), br = __ballot(rf);
@@ -2079,8 +2083,176 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
   }
 }
 
+// Compiler-only memory barrier between LDS phases of one wave: a wave's LDS operations execute in issue
+// order, so no wait is needed, only that the compiler keeps the order.
+LG_DEVICE void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
+// __move_median_to_first(first, first + 1, mid, last - 1) with the whole wave: lanes 0..3 read the four
+// elements in one LDS round trip, the choice is made on the scalar unit, two lanes write the swap.
+// Returns the pivot key.
+template <typename K, typename V>
+LG_DEVICE K wave_median_to_first(const SortView<K, V>& a, int first, int last) {
+  const int lane = lane_id();
+  const int x = first + 1, y = first + (last - first) / 2, z = last - 1;
+  const int src = lane == 0 ? first : lane == 1 ? x : lane == 2 ? y : z;
+  const K kv = a.key[src];
+  const V vv = a.val[src];
+  const K kx = rdlane(kv, 1), ky = rdlane(kv, 2), kz = rdlane(kv, 3);
+  int sl;  // lane (1..3) of the median
+  if (kx < ky) sl = ky < kz ? 2 : (kx < kz ? 3 : 1);
+  else sl = kx < kz ? 1 : (ky < kz ? 3 : 2);
+  const int sel = sl == 1 ? x : sl == 2 ? y : z;
+  const K kf = rdlane(kv, 0), ks = rdlane(kv, sl);
+  const V vf = (V)__builtin_amdgcn_readlane((int)vv, 0), vs = (V)__builtin_amdgcn_readlane((int)vv, sl);
+  if (lane == 0) { a.key[first] = ks; a.val[first] = vs; }
+  if (lane == 1) { a.key[sel] = kf; a.val[sel] = vf; }
+  wave_lds_fence();
+  return ks;
+}
+
+// __unguarded_partition_pivot on [first, last), 64 < last - first <= 2048, median-of-3 included,
+// without any sequential scan (the rank-pairing identity of lvl_sort / the map clouds' k_vxs_*:
+// lego_wavesort.h).  Per position p in (first, last): left stop lf = !(key < pivot), right stop
+// rf = !(pivot < key), A(p) = #lf in (first, p), B(p) = #rf in (p, last), D = A - B.  Hoare's loop swaps
+// the k-th left stop from the left with the k-th right stop from the right while the left one lies
+// below: left stop p is swapped iff D(p) < 0 (partner: the right stop of rank A), right stop q iff
+// D(q) > 0 (rank B), and the returned cut is the first p with (lf && D >= 0) || (rf && D > 0).
+// Positions are dealt in chunks of 64 (p = first + 1 + 64 j + lane): (A) the stop bits of every chunk
+// (all reads of a batch in flight) and, on the scalar unit, the stops before each chunk, (B) each
+// position's A and B; each swapped right stop records its position under its rank (posr[B]), the cut
+// is the first candidate, (C) each swapped left stop exchanges with the right stop posr[A] (pairs are
+// disjoint: the lanes need no order among themselves; 8 chunks' reads in flight).  The cost is a few
+// dependent LDS round trips a partition, which is what bounds a wave that shares its CU's LDS with ten
+// others.  Replaces a streamed version that paired the stops 64 positions at a time from both ends
+// (~1,000 cycles a chunk of dependent LDS round trips and permutes).
+// posr: LDS scratch of (last - first) / 2 16-bit entries.
+template <typename K, typename V>
+LG_DEVICE int wave_partition_ranked(const SortView<K, V>& a, int first, int last, uint16_t* posr) {
+  const int lane = lane_id();
+  const K pv = wave_median_to_first(a, first, last);
+  const int n1 = last - first - 1;      // positions (first, last)
+  const int c = (n1 + 63) >> 6;         // chunks, <= 32
+  const int p0 = first + 1 + lane;
+  unsigned lfm = 0u, rfm = 0u;          // bit j: this lane's position of chunk j is a left / right stop
+  int excl = 0;                         // lane j: stops before chunk j, lf | rf << 16
+  int runL = 0, runR = 0;               // (scalar) stops so far
+  for (int j0 = 0; j0 < c; j0 += 8) {
+    K kk[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) kk[u] = a.key[min(p0 + 64 * (j0 + u), last - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u;
+      if (j >= c) break;
+      const bool in = p0 + 64 * j < last;
+      const bool lf = in && !(kk[u] < pv), rf = in && !(pv < kk[u]);
+      lfm |= (unsigned)lf << j;
+      rfm |= (unsigned)rf << j;
+      excl = lane == j ? (runL | (runR << 16)) : excl;
+      runL += __popcll(__ballot(lf));
+      runR += __popcll(__ballot(rf));
+    }
+  }
+  const int totR = runR;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int cut = last;  // (a median-of-3 pivot always leaves a candidate)
+  bool found = false;
+  unsigned swl = 0u;  // bit j: this lane's position of chunk j is a swapped left stop
+  for (int j = 0; j < c; ++j) {
+    const int off = __builtin_amdgcn_readlane(excl, j);
+    const bool lf = (lfm >> j) & 1u, rf = (rfm >> j) & 1u;
+    const unsigned long long mL = __ballot(lf), mR = __ballot(rf);
+    const int A = (off & 0xffff) + __popcll(mL & below);
+    const int B = totR - (off >> 16) - __popcll(mR & below) - (int)rf;
+    const int D = A - B;
+    if (rf && D > 0) posr[B] = (uint16_t)(p0 + 64 * j - first);
+    swl |= (unsigned)(lf && D < 0) << j;
+    const unsigned long long cand = __ballot((lf && D >= 0) || (rf && D > 0));
+    if (!found && cand) {
+      found = true;
+      cut = first + 1 + 64 * j + (__ffsll((long long)cand) - 1);
+    }
+  }
+  wave_lds_fence();  // posr complete before phase C reads it
+  const int cmax = min(c, (cut - first - 1 + 63) >> 6);  // swapped left stops lie below the cut
+  for (int j0 = 0; j0 < cmax; j0 += 8) {
+    int q[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = min(j0 + u, c - 1);
+      const int off = __builtin_amdgcn_readlane(excl, j);
+      const int A = (off & 0xffff) + __popcll(__ballot((lfm >> j) & 1u) & below);
+      q[u] = posr[min(A, (last - first) / 2 - 1)];  // (meaningful where swapped)
+    }
+    K kq[8], kp[8];
+    V vq[8], vp[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u;
+      const bool sw = j < cmax && ((swl >> j) & 1u);
+      const int pp = sw ? p0 + 64 * j : first, qq = sw ? first + q[u] : first;
+      kp[u] = a.key[pp]; vp[u] = a.val[pp];
+      kq[u] = a.key[qq]; vq[u] = a.val[qq];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u;
+      if (j < cmax && ((swl >> j) & 1u)) {
+        const int pp = p0 + 64 * j, qq = first + q[u];
+        a.key[pp] = kq[u]; a.val[pp] = vq[u];
+        a.key[qq] = kp[u]; a.val[qq] = vp[u];
+      }
+    }
+  }
+  wave_lds_fence();
+  return cut;
+}
+
 template <int R, typename K, typename V>
 LG_DEVICE void final_bitonic(K* key, V* val, int n);
+
+// __final_insertion_sort of the post-partition array [0, n) (integral keys, n <= 64 R): the stable
+// order by key, and no element crosses a partition cut.  Every final range is either at most 16 long
+// or heap-sorted, and the ranges are ordered (each key of a range <= each key of the next), so a
+// position p moves by exactly #{q in (p, p + 15] : key_q < key_p} - #{q in [p - 15, p) : key_q > key_p}:
+// neighbours in other ranges never count, and a heap-sorted range does not move.  Row-major positions
+// (p = 64 r + lane: every read of a shifted window is conflict-free in LDS), 30 comparisons a
+// position, then one scatter; replaces a register bitonic sort of all n (key, position) pairs.
+// key[-15 .. n + 14] must be readable LDS (ExtractLds: blk before vkey, vval after it).
+template <int R, typename K, typename V>
+LG_DEVICE void final_window(K* key, V* val, int n) {
+  static_assert(std::is_integral<K>::value, "final_window: integral keys");
+  const int lane = lane_id();
+  K kr[R];
+  unsigned vn[R];  // value | new position << 16
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int p = 64 * r + lane;
+    const K* kp = key + min(p, n - 1);  // (one base address: the window's reads take immediate offsets)
+    const K k = kp[0];
+    int mv = 0;
+#pragma unroll
+    for (int d = 1; d <= 15; ++d) {
+      const K ka = kp[d], kb = kp[-d];
+      mv += (p + d < n && ka < k) ? 1 : 0;
+      mv -= (p - d >= 0 && k < kb) ? 1 : 0;
+    }
+    kr[r] = k;
+    vn[r] = (unsigned)val[min(p, n - 1)] | ((unsigned)(p + mv) << 16);
+    asm volatile("" : "+v"(vn[r]), "+v"(kr[r]));  // materialised here: the row's reads die with it
+    __builtin_amdgcn_sched_barrier(0);  // one row's 31 reads in flight at a time (registers)
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (64 * r + lane < n) {
+      const int np = (int)(vn[r] >> 16);
+      key[np] = kr[r];
+      val[np] = (V)(vn[r] & 0xffffu);
+    }
+  }
+  __syncthreads();
+}
 
 // final_reg: __final_insertion_sort is computed as a register sort by (key, position): it is stable
 // and never moves an element across a partition cut, so its result is the post-partition array
@@ -2094,15 +2266,18 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
   for (int w = lane; w < nwords; w += 64) blk[w] = 0u;
   __syncthreads();
   SortView<K, V> a{key, val};
-  int sp = 0;
   PROF_T(t_part0);
-  if (lane == 0) { stk[0] = 0; stk[1] = n; stk[2] = 2 * floor_log2(n); }
-  sp = 1;
-  __syncthreads();
+  // The range stack in registers: frame i in lane i (written and read by lane index on the scalar
+  // unit, no LDS round trip), one word a frame (first, last, depth): first and last <= 2048 (12 bits
+  // each), depth <= 22.  (stk: unused here; kept in the LDS layouts for the callers' layouts.)
+  (void)stk;
+  auto sort_frame = [](int f, int l, int d) { return f | (l << 12) | (d << 24); };
+  int frames = lane == 0 ? sort_frame(0, n, 2 * floor_log2(n)) : 0;
+  int sp = 1;
   while (sp > 0) {
     --sp;
-    int first = stk[3 * sp], last = stk[3 * sp + 1], depth = stk[3 * sp + 2];
-    __syncthreads();
+    const int fr = __builtin_amdgcn_readlane(frames, sp);
+    int first = fr & 0xfff, last = (fr >> 12) & 0xfff, depth = fr >> 24;
     while (last - first > 16) {
       if (depth == 0) {
         PROF_T(t_hs0);
@@ -2115,25 +2290,41 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
       }
       --depth;
       int cut;
+      PROF_T(t_pp0);
       if (last - first <= 64) {  // one chunk: partition in registers
         cut = wave_partition_small(a, first, last, tab);
+        PROF_ADD(51, t_pp0);
+#ifdef LG_PROFILE
+        if (lane == 0) atomicAdd(&PROF_SLOT(53), 1ull);
+#endif
       } else {
-
-        if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
-        __syncthreads();
-        cut = wave_partition_stream_reg(a, first, last);  // (every caller: one wave a workgroup)
-        __syncthreads();
+        cut = wave_partition_ranked(a, first, last, (uint16_t*)tab);  // (every caller: one wave a workgroup)
+        PROF_ADD(50, t_pp0);
+#ifdef LG_PROFILE
+        if (lane == 0) { atomicAdd(&PROF_SLOT(54), 1ull); atomicAdd(&PROF_SLOT(55), (unsigned long long)(last - first)); }
+#endif
       }
-      if (lane == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = last; stk[3 * sp + 2] = depth; }
+      frames = lane == sp ? sort_frame(cut, last, depth) : frames;  // (sp <= 2 * 11 + 1)
       ++sp;
       last = cut;
-      __syncthreads();
     }
-    if (lane == 0) blk[first >> 5] |= 1u << (first & 31);  // a final block starts here
-    __syncthreads();
+    if (!final_reg && lane == 0) blk[first >> 5] |= 1u << (first & 31);  // a final block starts here
   }
+  __syncthreads();
   PROF_ADD(6, t_part0);
   PROF_T(t_fin0);
+  if constexpr (std::is_integral<K>::value && sizeof(V) == 2) {
+    if (final_reg) {
+      if (n <= 64) final_window<1>(key, val, n);
+      else if (n <= 128) final_window<2>(key, val, n);
+      else if (n <= 256) final_window<4>(key, val, n);
+      else if (n <= 512) final_window<8>(key, val, n);
+      else if (n <= 1024) final_window<16>(key, val, n);
+      else final_window<32>(key, val, n);
+      PROF_ADD(11, t_fin0);
+      return;
+    }
+  }
   if (final_reg && (n <= 512 || std::is_integral<K>::value)) {
     if (n <= 64) final_bitonic<1>(key, val, n);
     else if (n <= 128) final_bitonic<2>(key, val, n);
@@ -4851,7 +5042,7 @@ __global__ __launch_bounds__(64) void k_sort_bench(const unsigned* keys, int n, 
   const int lane = lane_id();
   for (int i = lane; i < n; i += 64) { L.u.vkey[i] = keys[i]; L.vval[i] = (uint16_t)i; }
   __syncthreads();
-  wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
+  wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);  // as k_voxel
   if (lane == 0) out[blockIdx.x] = L.vval[n / 2];
 }
 template <int R>

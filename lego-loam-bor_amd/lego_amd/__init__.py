@@ -85,6 +85,7 @@ def lib():
         L.lego_batch_set_lag.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_probe.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_set_trajectory.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+        L.lego_batch_time_voxel.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, P(C.c_float)]
         L.lego_batch_probe_times.argtypes = [C.c_void_p, P(C.c_float), P(C.c_int32)]
         L.lego_batch_set_wide.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_wide.argtypes = [C.c_void_p]
@@ -240,6 +241,13 @@ class Batch:
     def set_groups(self, groups):
         """Launch the streams as `groups` slices on separate HIP streams (overlapping kernel tails)."""
         _check(lib().lego_batch_set_groups(self.h, int(groups)), "lego_batch_set_groups")
+
+    def time_voxel(self, reps=10, stream=0):
+        """Mean ms of the last step's VoxelGrid launch, alone on the device (lego_batch_time_voxel)."""
+        ms = C.c_float()
+        _check(lib().lego_batch_time_voxel(self.h, int(reps), C.c_void_p(stream or None), C.byref(ms)),
+               "lego_batch_time_voxel")
+        return ms.value
 
     def set_trajectory(self, d_traj_ptr, max_scans):
         """Per-scan odometry record (lego_batch_set_trajectory): a device array of S * max_scans * 12

@@ -22,7 +22,7 @@ for WHAT in "$@"; do
     tail -2 "$OUT/smoke.log"
   fi
   if [ "$WHAT" = quick ]; then
-    LEGO_REPORT_DIR=$OUT timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $QUICK_TESTS > "$OUT/gpu_quick.log" 2>&1
+    LEGO_REPORT_DIR=$OUT timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$QUICK_K" > "$OUT/gpu_quick.log" 2>&1
     tail -3 "$OUT/gpu_quick.log"
   fi
   if [ "$WHAT" = bench ]; then
@@ -43,6 +43,12 @@ for WHAT in "$@"; do
     timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_hdl" -o run -- python3 bench.py --kind hdl64 --steps 4 --warmup 2 --no-cpu-baseline --no-alt-order --roofline-streams 0 --no-c5 > "$OUT/fetch_hdl.log" 2>&1
     timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_hdl" -o run -- python3 bench.py --kind hdl64 --steps 4 --warmup 2 --no-cpu-baseline --no-alt-order --roofline-streams 0 --no-c5 > "$OUT/write_hdl.log" 2>&1
     echo pmc done
+  fi
+  if [ "$WHAT" = phase ]; then
+    for O in 0 1; do
+      LEGO_FRONTEND_LIB=lego-loam-bor_amd/lego_amd/liblego_frontend_prof.so timeout -k 10 300 python3 tools/phase_profile.py 256 $O > "$OUT/phase_order$O.txt" 2>&1
+      grep "voxel\|sort:" "$OUT/phase_order$O.txt" | head -8
+    done
   fi
   if [ "$WHAT" = hdl ]; then
     timeout -k 10 400 python3 bench.py --kind hdl64 $B --no-cpu-baseline --no-c5 > "$OUT/bench_hdl64.log" 2>&1

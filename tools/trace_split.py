@@ -35,8 +35,8 @@ def main():
         name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
         if name.startswith("__amd") or "rocprim" in name:
             continue
-        grid = int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) // max(
-            int(r["Workgroup_Size_X"]) * int(r.get("Workgroup_Size_Y", 1) or 1), 1)
+        grid = int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) * int(r.get("Grid_Size_Z", 1) or 1) // max(
+            int(r["Workgroup_Size_X"]) * int(r.get("Workgroup_Size_Y", 1) or 1) * int(r.get("Workgroup_Size_Z", 1) or 1), 1)
         acc[(name, grid)].append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
     rows = []
     pair = collections.defaultdict(float)
