@@ -289,6 +289,9 @@ int  lego_debug_prof(uint64_t* out256, int32_t reset);
 /* Kernel time of `blocks` concurrent one-wave copies of the device sort of h_keys (profile build);
  * mode 0 the stack emulation, 1 the level-synchronous one (n <= 2048). */
 int  lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, int32_t mode, float* ms);
+/* LDS co-residency probe (profile build; LEGO_ENOTSUP in the shipped library): mean ms of `blocks`
+ * one-wave blocks that each hold `bytes` of LDS and sleep ~20 us. */
+int  lego_debug_lds_probe(int32_t bytes, int32_t blocks, float* ms);
 /* Counter calibration (profile build; LEGO_ENOTSUP in the shipped library): k_project's input read
  * patterns (mode 0 12-byte buffer loads, 1 16-byte loads, 2 both passes) over S scans of device points
  * (offs / cnts as lego_batch_run's), out[S * 1024]. */

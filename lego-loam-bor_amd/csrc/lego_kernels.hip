@@ -1898,29 +1898,33 @@ __global__ __launch_bounds__(FP4_NT) void k_fa_prep4(LgParams P, LgBufs B) {
 #define SEG_MAX 512
 #define RING_MAX 2048
 
-// The introsort emulation's scratch: stk, its range stack (one packed frame a word, sort_frame), and tab,
-// wave_partition_ranked's rank table (16-bit positions, (range length) / 2 of them).
-struct ExtractLds {  // k_voxel (and the sort test hooks): 14.5 KB per wave (11 waves a CU by LDS)
-  unsigned blk[RING_MAX / 32];  // final-block start bits of the introsort emulation; also the 15 words
-                                // final_window may read (and ignore) below vkey[0]
+// LDS of one wave.  Measured on MI355X (tools/lds_probe.py): 11 one-wave workgroups share a CU at
+// 13,824 B each, not at 14,336; 12 not at 13,312 B.
+struct ExtractLds {  // k_voxel: 12.1 KB per wave (LDS allows 12 a CU)
+  unsigned pad[16];             // final_window reads (and ignores) up to 15 words below vkey[0]
   union {
-    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;  // segment sort (test hook)
-    unsigned vkey[RING_MAX];                                 // voxel keys
+    unsigned vkey[RING_MAX];    // voxel keys
   } u;
   uint16_t vval[RING_MAX];      // lessFlat positions of the ring (relative to the ring start), sorted with vkey
                                 // (also read, and ignored, by final_window past vkey[n - 1])
-  int stk[64];
-  int tab[RING_MAX / 4];
 };
 
-struct SegLds {  // k_sortseg: 5.6 KB per wave
+struct SortTestLds {  // the sort test hooks (lego_test_sort): every path of wave_std_sort
+  unsigned pad[16];
+  union {
+    struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;  // segment sort
+    unsigned vkey[RING_MAX];
+  } u;
+  uint16_t vval[RING_MAX];
+  unsigned blk[RING_MAX / 32];  // final-block start bits (the per-block insertion sorts)
+};
+
+struct SegLds {  // k_sortseg: 5.4 KB per wave
   union {
     struct { float skey[SEG_MAX]; int sval[SEG_MAX]; } seg;  // segment sort
     uint16_t col[SEG_MAX + 16];                             // colInd around the segment (info words)
   } u;
   unsigned blk[RING_MAX / 32];
-  int stk[64];
-  int tab[SEG_MAX / 4];
 };
 
 template <typename T>
@@ -1932,9 +1936,8 @@ LG_DEVICE T shfl_any(T v, int src) {
   return __builtin_bit_cast(T, __shfl(__builtin_bit_cast(int, v), src));
 }
 // __unguarded_partition_pivot on a range of 17..64 elements held one per lane; returns the cut.
-// tab: >= 128 ints of LDS scratch.
 template <typename K, typename V>
-LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last, int* tab) {
+LG_DEVICE int wave_partition_small(const SortView<K, V>& a, int first, int last) {
   const int lane = lane_id();
   const int m = last - first;
   const bool in = lane < m;
@@ -2083,131 +2086,6 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
   }
 }
 
-// Compiler-only memory barrier between LDS phases of one wave: a wave's LDS operations execute in issue
-// order, so no wait is needed, only that the compiler keeps the order.
-LG_DEVICE void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
-
-// __move_median_to_first(first, first + 1, mid, last - 1) with the whole wave: lanes 0..3 read the four
-// elements in one LDS round trip, the choice is made on the scalar unit, two lanes write the swap.
-// Returns the pivot key.
-template <typename K, typename V>
-LG_DEVICE K wave_median_to_first(const SortView<K, V>& a, int first, int last) {
-  const int lane = lane_id();
-  const int x = first + 1, y = first + (last - first) / 2, z = last - 1;
-  const int src = lane == 0 ? first : lane == 1 ? x : lane == 2 ? y : z;
-  const K kv = a.key[src];
-  const V vv = a.val[src];
-  const K kx = rdlane(kv, 1), ky = rdlane(kv, 2), kz = rdlane(kv, 3);
-  int sl;  // lane (1..3) of the median
-  if (kx < ky) sl = ky < kz ? 2 : (kx < kz ? 3 : 1);
-  else sl = kx < kz ? 1 : (ky < kz ? 3 : 2);
-  const int sel = sl == 1 ? x : sl == 2 ? y : z;
-  const K kf = rdlane(kv, 0), ks = rdlane(kv, sl);
-  const V vf = (V)__builtin_amdgcn_readlane((int)vv, 0), vs = (V)__builtin_amdgcn_readlane((int)vv, sl);
-  if (lane == 0) { a.key[first] = ks; a.val[first] = vs; }
-  if (lane == 1) { a.key[sel] = kf; a.val[sel] = vf; }
-  wave_lds_fence();
-  return ks;
-}
-
-// __unguarded_partition_pivot on [first, last), 64 < last - first <= 2048, median-of-3 included,
-// without any sequential scan (the rank-pairing identity of lvl_sort / the map clouds' k_vxs_*:
-// lego_wavesort.h).  Per position p in (first, last): left stop lf = !(key < pivot), right stop
-// rf = !(pivot < key), A(p) = #lf in (first, p), B(p) = #rf in (p, last), D = A - B.  Hoare's loop swaps
-// the k-th left stop from the left with the k-th right stop from the right while the left one lies
-// below: left stop p is swapped iff D(p) < 0 (partner: the right stop of rank A), right stop q iff
-// D(q) > 0 (rank B), and the returned cut is the first p with (lf && D >= 0) || (rf && D > 0).
-// Positions are dealt in chunks of 64 (p = first + 1 + 64 j + lane): (A) the stop bits of every chunk
-// (all reads of a batch in flight) and, on the scalar unit, the stops before each chunk, (B) each
-// position's A and B; each swapped right stop records its position under its rank (posr[B]), the cut
-// is the first candidate, (C) each swapped left stop exchanges with the right stop posr[A] (pairs are
-// disjoint: the lanes need no order among themselves; 8 chunks' reads in flight).  The cost is a few
-// dependent LDS round trips a partition, which is what bounds a wave that shares its CU's LDS with ten
-// others.  Replaces a streamed version that paired the stops 64 positions at a time from both ends
-// (~1,000 cycles a chunk of dependent LDS round trips and permutes).
-// posr: LDS scratch of (last - first) / 2 16-bit entries.
-template <typename K, typename V>
-LG_DEVICE int wave_partition_ranked(const SortView<K, V>& a, int first, int last, uint16_t* posr) {
-  const int lane = lane_id();
-  const K pv = wave_median_to_first(a, first, last);
-  const int n1 = last - first - 1;      // positions (first, last)
-  const int c = (n1 + 63) >> 6;         // chunks, <= 32
-  const int p0 = first + 1 + lane;
-  unsigned lfm = 0u, rfm = 0u;          // bit j: this lane's position of chunk j is a left / right stop
-  int excl = 0;                         // lane j: stops before chunk j, lf | rf << 16
-  int runL = 0, runR = 0;               // (scalar) stops so far
-  for (int j0 = 0; j0 < c; j0 += 8) {
-    K kk[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) kk[u] = a.key[min(p0 + 64 * (j0 + u), last - 1)];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j = j0 + u;
-      if (j >= c) break;
-      const bool in = p0 + 64 * j < last;
-      const bool lf = in && !(kk[u] < pv), rf = in && !(pv < kk[u]);
-      lfm |= (unsigned)lf << j;
-      rfm |= (unsigned)rf << j;
-      excl = lane == j ? (runL | (runR << 16)) : excl;
-      runL += __popcll(__ballot(lf));
-      runR += __popcll(__ballot(rf));
-    }
-  }
-  const int totR = runR;
-  const unsigned long long below = (1ull << lane) - 1ull;
-  int cut = last;  // (a median-of-3 pivot always leaves a candidate)
-  bool found = false;
-  unsigned swl = 0u;  // bit j: this lane's position of chunk j is a swapped left stop
-  for (int j = 0; j < c; ++j) {
-    const int off = __builtin_amdgcn_readlane(excl, j);
-    const bool lf = (lfm >> j) & 1u, rf = (rfm >> j) & 1u;
-    const unsigned long long mL = __ballot(lf), mR = __ballot(rf);
-    const int A = (off & 0xffff) + __popcll(mL & below);
-    const int B = totR - (off >> 16) - __popcll(mR & below) - (int)rf;
-    const int D = A - B;
-    if (rf && D > 0) posr[B] = (uint16_t)(p0 + 64 * j - first);
-    swl |= (unsigned)(lf && D < 0) << j;
-    const unsigned long long cand = __ballot((lf && D >= 0) || (rf && D > 0));
-    if (!found && cand) {
-      found = true;
-      cut = first + 1 + 64 * j + (__ffsll((long long)cand) - 1);
-    }
-  }
-  wave_lds_fence();  // posr complete before phase C reads it
-  const int cmax = min(c, (cut - first - 1 + 63) >> 6);  // swapped left stops lie below the cut
-  for (int j0 = 0; j0 < cmax; j0 += 8) {
-    int q[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j = min(j0 + u, c - 1);
-      const int off = __builtin_amdgcn_readlane(excl, j);
-      const int A = (off & 0xffff) + __popcll(__ballot((lfm >> j) & 1u) & below);
-      q[u] = posr[min(A, (last - first) / 2 - 1)];  // (meaningful where swapped)
-    }
-    K kq[8], kp[8];
-    V vq[8], vp[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j = j0 + u;
-      const bool sw = j < cmax && ((swl >> j) & 1u);
-      const int pp = sw ? p0 + 64 * j : first, qq = sw ? first + q[u] : first;
-      kp[u] = a.key[pp]; vp[u] = a.val[pp];
-      kq[u] = a.key[qq]; vq[u] = a.val[qq];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j = j0 + u;
-      if (j < cmax && ((swl >> j) & 1u)) {
-        const int pp = p0 + 64 * j, qq = first + q[u];
-        a.key[pp] = kq[u]; a.val[pp] = vq[u];
-        a.key[qq] = kp[u]; a.val[qq] = vp[u];
-      }
-    }
-  }
-  wave_lds_fence();
-  return cut;
-}
-
 template <int R, typename K, typename V>
 LG_DEVICE void final_bitonic(K* key, V* val, int n);
 
@@ -2218,7 +2096,7 @@ LG_DEVICE void final_bitonic(K* key, V* val, int n);
 // neighbours in other ranges never count, and a heap-sorted range does not move.  Row-major positions
 // (p = 64 r + lane: every read of a shifted window is conflict-free in LDS), 30 comparisons a
 // position, then one scatter; replaces a register bitonic sort of all n (key, position) pairs.
-// key[-15 .. n + 14] must be readable LDS (ExtractLds: blk before vkey, vval after it).
+// key[-15 .. n + 14] must be readable LDS (ExtractLds: pad before vkey, vval after it).
 template <int R, typename K, typename V>
 LG_DEVICE void final_window(K* key, V* val, int n) {
   static_assert(std::is_integral<K>::value, "final_window: integral keys");
@@ -2258,19 +2136,20 @@ LG_DEVICE void final_window(K* key, V* val, int n) {
 // and never moves an element across a partition cut, so its result is the post-partition array
 // stably sorted by key.  Needs key bit order == key order: unsigned keys, or float keys none
 // negative or NaN (the caller checks); n <= 2048 (unsigned) / 512 (float).
+// blk: the per-block insertion sorts' final-block bits (unused, may be null, with final_reg and integral keys)
 template <typename K, typename V>
-LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int* tab, bool final_reg = false) {
+LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, bool final_reg = false) {
   const int lane = lane_id();
   if (n <= 1) return;
   const int nwords = (n + 31) >> 5;
-  for (int w = lane; w < nwords; w += 64) blk[w] = 0u;
+  if (!final_reg)
+    for (int w = lane; w < nwords; w += 64) blk[w] = 0u;
   __syncthreads();
   SortView<K, V> a{key, val};
   PROF_T(t_part0);
   // The range stack in registers: frame i in lane i (written and read by lane index on the scalar
   // unit, no LDS round trip), one word a frame (first, last, depth): first and last <= 2048 (12 bits
-  // each), depth <= 22.  (stk: unused here; kept in the LDS layouts for the callers' layouts.)
-  (void)stk;
+  // each), depth <= 22.
   auto sort_frame = [](int f, int l, int d) { return f | (l << 12) | (d << 24); };
   int frames = lane == 0 ? sort_frame(0, n, 2 * floor_log2(n)) : 0;
   int sp = 1;
@@ -2290,19 +2169,13 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, int* stk, int
       }
       --depth;
       int cut;
-      PROF_T(t_pp0);
       if (last - first <= 64) {  // one chunk: partition in registers
-        cut = wave_partition_small(a, first, last, tab);
-        PROF_ADD(51, t_pp0);
-#ifdef LG_PROFILE
-        if (lane == 0) atomicAdd(&PROF_SLOT(53), 1ull);
-#endif
+        cut = wave_partition_small(a, first, last);
       } else {
-        cut = wave_partition_ranked(a, first, last, (uint16_t*)tab);  // (every caller: one wave a workgroup)
-        PROF_ADD(50, t_pp0);
-#ifdef LG_PROFILE
-        if (lane == 0) { atomicAdd(&PROF_SLOT(54), 1ull); atomicAdd(&PROF_SLOT(55), (unsigned long long)(last - first)); }
-#endif
+        if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
+        __syncthreads();
+        cut = wave_partition_stream_reg(a, first, last);  // (every caller: one wave a workgroup)
+        __syncthreads();
       }
       frames = lane == sp ? sort_frame(cut, last, depth) : frames;  // (sp <= 2 * 11 + 1)
       ++sp;
@@ -2670,7 +2543,7 @@ LG_DEVICE void sort_segment(Lds& L, int n, const TieOk& tie_ok = TieOk()) {
 #ifdef LG_PROFILE
     if (lane_id() == 0) atomicAdd(&PROF_SLOT(14), 1ull);
 #endif
-    wave_std_sort<float, int>(key, val, n, L.blk, L.stk, L.tab, !anomaly && n <= SEG_MAX);
+    wave_std_sort<float, int>(key, val, n, L.blk, !anomaly && n <= SEG_MAX);
   }
 }
 
@@ -2799,10 +2672,10 @@ LG_DEVICE void voxel_ring(const LgParams& P, const ScanView& v, Lds& L, int n, i
   __syncthreads();
   PROF_T(t_vs0);
   if constexpr (kMode == 0) {
-    wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, true);
+    wave_std_sort<unsigned, uint16_t>(vkey, vval, n, nullptr, true);
   } else if constexpr (kMode == 3) {
     if (P.voxel_stable) voxel_sort_stable<3>(vkey, vval, n);
-    else wave_std_sort<unsigned, uint16_t>(vkey, vval, n, L.blk, L.stk, L.tab, true);
+    else wave_std_sort<unsigned, uint16_t>(vkey, vval, n, nullptr, true);
   } else {
     voxel_sort_stable<kMode>(vkey, vval, n);
   }
@@ -4992,7 +4865,7 @@ void k_sort_test_lvl(unsigned* keys, int* vals, int n) {  // as k_voxel<4 / 5>
 }
 
 __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int n, int is_float) {
-  __shared__ ExtractLds L;
+  __shared__ SortTestLds L;
   const int lane = lane_id();
   for (int i = lane; i < n; i += 64) { L.u.vkey[i] = keys[i]; L.vval[i] = (uint16_t)vals[i]; }
   __syncthreads();
@@ -5003,9 +4876,9 @@ __global__ __launch_bounds__(64) void k_sort_test(unsigned* keys, int* vals, int
     for (int i = lane; i < n; i += 64) { keys[i] = (unsigned)__float_as_int(L.u.seg.skey[i]); vals[i] = L.u.seg.sval[i]; }
     return;
   } else if (is_float) {
-    wave_std_sort<float, uint16_t>((float*)L.u.vkey, L.vval, n, L.blk, L.stk, L.tab);
+    wave_std_sort<float, uint16_t>((float*)L.u.vkey, L.vval, n, L.blk);
   } else {
-    wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);  // as k_voxel
+    wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, nullptr, true);  // as k_voxel
   }
   for (int i = lane; i < n; i += 64) { keys[i] = L.u.vkey[i]; vals[i] = L.vval[i]; }
 }
@@ -5037,12 +4910,24 @@ extern "C" int lego_test_sort(uint32_t* h_keys, int32_t* h_vals, int32_t n, int3
 }
 
 #ifdef LG_PROFILE
+// kV 0: as k_voxel (partitions + final_window); 2: partitions + per-block insertion sorts; 3: final_window
+// alone; 4: final_bitonic alone (3 and 4 on the unpartitioned keys: their cost only)
+template <int kV>
 __global__ __launch_bounds__(64) void k_sort_bench(const unsigned* keys, int n, unsigned* out) {
-  __shared__ ExtractLds L;
+  __shared__ std::conditional_t<kV == 2, SortTestLds, ExtractLds> L;
   const int lane = lane_id();
   for (int i = lane; i < n; i += 64) { L.u.vkey[i] = keys[i]; L.vval[i] = (uint16_t)i; }
   __syncthreads();
-  wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, L.stk, L.tab, true);  // as k_voxel
+  if constexpr (kV == 0 || kV == 2) {
+    if constexpr (kV == 2) wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, L.blk, false);
+    else wave_std_sort<unsigned, uint16_t>(L.u.vkey, L.vval, n, nullptr, true);
+  } else if constexpr (kV == 3) {
+    if (n > 1024) final_window<32>(L.u.vkey, L.vval, n);
+    else final_window<16>(L.u.vkey, L.vval, n);
+  } else {
+    if (n > 1024) final_bitonic<32>(L.u.vkey, L.vval, n);
+    else final_bitonic<16>(L.u.vkey, L.vval, n);
+  }
   if (lane == 0) out[blockIdx.x] = L.vval[n / 2];
 }
 template <int R>
@@ -5129,7 +5014,10 @@ extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t 
   hipEventCreate(&a);
   hipEventCreate(&b);
   auto launch = [&]() {
-    if (mode == 0) hipLaunchKernelGGL(k_sort_bench, dim3(blocks), dim3(64), 0, 0, k, n, o);
+    if (mode == 0) hipLaunchKernelGGL(k_sort_bench<0>, dim3(blocks), dim3(64), 0, 0, k, n, o);
+    else if (mode == 2) hipLaunchKernelGGL(k_sort_bench<2>, dim3(blocks), dim3(64), 0, 0, k, n, o);
+    else if (mode == 3) hipLaunchKernelGGL(k_sort_bench<3>, dim3(blocks), dim3(64), 0, 0, k, n, o);
+    else if (mode == 4) hipLaunchKernelGGL(k_sort_bench<4>, dim3(blocks), dim3(64), 0, 0, k, n, o);
     else if (n > 1024) hipLaunchKernelGGL(k_sort_bench_lvl<32>, dim3(blocks), dim3(64), 0, 0, k, n, o);
     else if (n > 512) hipLaunchKernelGGL(k_sort_bench_lvl<16>, dim3(blocks), dim3(64), 0, 0, k, n, o);
     else hipLaunchKernelGGL(k_sort_bench_lvl<8>, dim3(blocks), dim3(64), 0, 0, k, n, o);
@@ -5147,6 +5035,39 @@ extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t 
   return LEGO_OK;
 #else
   (void)h_keys; (void)n; (void)blocks; (void)mode; (void)ms;
+  return LEGO_ENOTSUP;
+#endif
+}
+
+#ifdef LG_PROFILE
+// LDS allocation probe: one wave a block holding `bytes` of dynamic LDS, each sleeping ~20 us
+__global__ __launch_bounds__(64) void k_lds_probe(int* out) {
+  extern __shared__ int dyn[];
+  dyn[threadIdx.x] = threadIdx.x;
+  for (int i = 0; i < 400; ++i) __builtin_amdgcn_s_sleep(127);
+  if (threadIdx.x == 0) out[blockIdx.x] = dyn[1];
+}
+#endif
+// Diagnostics (profile build only): ms of `blocks` one-wave blocks of `bytes` LDS each (co-residency).
+extern "C" int lego_debug_lds_probe(int32_t bytes, int32_t blocks, float* ms) {
+#ifdef LG_PROFILE
+  int* o = nullptr;
+  hipMalloc((void**)&o, blocks * 4);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipLaunchKernelGGL(k_lds_probe, dim3(blocks), dim3(64), bytes, 0, o);
+  hipEventRecord(a, 0);
+  hipLaunchKernelGGL(k_lds_probe, dim3(blocks), dim3(64), bytes, 0, o);
+  hipEventRecord(b, 0);
+  hipEventSynchronize(b);
+  hipEventElapsedTime(ms, a, b);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  hipFree(o);
+  return LEGO_OK;
+#else
+  (void)bytes; (void)blocks; (void)ms;
   return LEGO_ENOTSUP;
 #endif
 }

@@ -26,7 +26,6 @@ NAMES = {0: "x:load+sort seg", 1: "x:sharp greedy", 2: "x:flat greedy", 3: "x:le
          32: "f:tile distort", 33: "f:tile LDS load", 34: "f:occl flags", 35: "f:smooth+picked",
          40: "lm:  it surf rows (w0)", 41: "lm:  it corner rows (w0)", 42: "lm:  it reduce (w0)",
          43: "lm:  it solve (w0)", 46: "lm:  corner nn", 47: "lm:  corner scans", 48: "lm:corner stage",
-         50: "  sort:ranked partitions", 51: "  sort:small partitions", 52: "  sort:ranked median",
          25: "s:init parents", 26: "s:edges+unite", 27: "s:find roots", 28: "s:sizes+rank+label", 29: "s:compaction", 31: "s:distortion"}
 
 
@@ -67,8 +66,6 @@ def main():
 
 
     print("heap-sort fallbacks %d per step" % (prof[24] / nsteps))
-    print("partitions per step: small (17-64) %d, ranked %d over %d positions" % (
-        prof[53] / nsteps, prof[54] / nsteps, prof[55] / nsteps))
     print("LM solves per scan: surf %.2f corner %.2f" % (prof[44] / nsteps / S, prof[45] / nsteps / S))
     V = params.num_vertical_scans
     print("per-ring extract wave cycles (mean / max over streams), ring 63 = first pass:")

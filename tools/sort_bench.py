@@ -25,15 +25,16 @@ def main():
     d = np.load(os.path.join(REPO, "tools", "data", "voxel_keys_heavy.npz"))
     for name in d.files:
         k = np.ascontiguousarray(d[name].astype(np.uint32))
-        for mode in (0, 1):
-            for blocks in (1, 256 * 11):
+        for mode in (0, 2, 3, 4, 1):
+            for blocks in (1, 4096):  # 4096: C3's rings a step (16 a CU)
                 ms = C.c_float()
                 rc = lib.lego_debug_sort_bench(k.ctypes.data_as(C.POINTER(C.c_uint32)), len(k), blocks, mode,
                                                C.byref(ms))
                 if rc != 0:
                     print("%-5s n=%5d mode %d: rc %d" % (name, len(k), mode, rc))
                     continue
-                print("%-5s n=%5d %-6s blocks=%5d  %.3f ms" % (name, len(k), ("stack", "level")[mode], blocks, ms.value))
+                print("%-5s n=%5d %-12s blocks=%5d  %.3f ms" % (
+                    name, len(k), ("stack", "level", "stack+blkins", "window only", "bitonic only")[mode], blocks, ms.value))
 
 
 if __name__ == "__main__":
