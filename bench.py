@@ -66,7 +66,7 @@ def parse():
                     help="projection / segmentation layout (lego_batch_set_wide): -1 automatic")
     ap.add_argument("--lag", type=int, default=None, choices=[0, 1, 2],
                     help="pipeline depth (lego_batch_set_lag): 1 = a step runs the previous scan's LM, 2 = the one "
-                         "before; default 2 for voxel_tie_order 0, 1 for order 1 (the faster of each, DESIGN §4)")
+                         "before; default automatic (DESIGN §4)")
     ap.add_argument("--voxel-tie-order", type=int, default=0, choices=[0, 1],
                     help="lego_params.voxel_tie_order of the measured path: 0 = libstdc++ std::sort order, "
                          "bit-identical to the GCC-built reference; 1 = VoxelGrid sums each voxel in point order "
@@ -187,20 +187,15 @@ def pmc_traffic(args, S, kernels):
     return int(sum(v["hbm_bytes"] for v in best[1])), os.path.relpath(best[0], REPO)
 
 
-def default_lag(order):
-    return 2 if order == 0 else 1
-
-
 def configure_batch(b, order, lag=None, wide=-1, groups=1):
     """The schedule every measured batch runs (and tests/test_gpu_bench_config.py pins against the
-    oracle): `groups` stream slices, pipeline depth `lag` (default: 2 for the reference's VoxelGrid
-    order, 1 for the stable one), projection / segmentation layout `wide` (-1: lego_batch_set_wide's
-    automatic choice).  Returns the lag set."""
-    lag = default_lag(order) if lag is None else lag
+    oracle): `groups` stream slices, pipeline depth `lag` (None: lego_batch_set_lag's automatic choice,
+    DESIGN §4), projection / segmentation layout `wide` (-1: lego_batch_set_wide's automatic choice).
+    Returns the lag in effect."""
     b.set_groups(groups)
-    b.set_lag(lag)
+    b.set_lag(-1 if lag is None else lag)
     b.set_wide(wide)
-    return lag
+    return b.lag()
 
 
 def roofline_kernels(wide):

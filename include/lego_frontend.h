@@ -235,16 +235,19 @@ int  lego_batch_probe_times(lego_batch* b, float* ms2, int32_t* steps);
  * overlap the others'.  Results do not depend on the grouping. */
 #define LEGO_MAX_GROUPS 4
 int  lego_batch_set_groups(lego_batch* b, int32_t groups);
-/* Pipeline depth of lego_batch_step: 0 = a step runs its own scan's LM, 1 (default) = the previous
- * scan's, 2 = the one before (the VoxelGrid of a scan gets two steps before its publish; one stream
- * group and timing off, else run as 1; see lego_batch_step).  Results do not depend on it. */
+/* Pipeline depth of lego_batch_step: 0 = a step runs its own scan's LM, 1 = the previous scan's, 2 = the
+ * one before (the VoxelGrid of a scan gets two steps before its publish; one stream group and timing
+ * off, else run as 1; see lego_batch_step), -1 (default) = automatic: 2 with voxel_tie_order 0 and at
+ * most half as many streams as compute units, else 1.  Results do not depend on it. */
 int  lego_batch_set_lag(lego_batch* b, int32_t lag);
+/* The pipeline depth in effect (0, 1 or 2), or LEGO_EINVAL. */
+int  lego_batch_lag(const lego_batch* b);
 /* Kernel layout of the projection and segmentation: 1 = wide (a scan's work over many workgroups,
  * per-scan images in HBM), 0 = one workgroup a scan with its images in LDS (only where they fit:
  * V <= 16, V*H < 32768; else LEGO_EINVAL), 2 = the one-workgroup projection with the wide
  * segmentation (where the projection's image fits LDS), -1 (default) = automatic: wide where the images
- * do not fit LDS, where fewer than (compute units / 8) streams are in flight, or with voxel_tie_order 0
- * and at most 2 streams a compute unit; else 0.  Results do not depend on it. */
+ * do not fit LDS or where at most (compute units / 8) streams are in flight; else 0.  Results do not
+ * depend on it. */
 int  lego_batch_set_wide(lego_batch* b, int32_t mode);
 /* The layout in effect (0, 1 or 2 as lego_batch_set_wide), or LEGO_EINVAL. */
 int  lego_batch_wide(const lego_batch* b);

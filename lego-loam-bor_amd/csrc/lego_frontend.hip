@@ -136,16 +136,20 @@ bool lg_lds_segment(const LgParams& P);
 // workgroup a scan cannot hold the images in LDS, and where too few scans are in flight to fill
 // the device with one workgroup each.
 // The wide layout (many small workgroups a scan) where the one-workgroup-a-scan kernels cannot hold the
-// scan in LDS, for few scans, and with the reference's VoxelGrid order up to 2 scans a CU: there the
-// VoxelGrid's and k_lm's long-lived waves sit on every CU, and a whole-CU k_project / k_segment_lds
-// workgroup waited for them to drain (C3 order 0, lag 2: 210-215k vs 194-199k scans/s with both
-// kernels whole-CU, 184k with only the projection so, mode 2).
+// scan in LDS and for few scans.  (Round 4 also took it for the reference's VoxelGrid order up to 2 scans
+// a CU, whose heavier VoxelGrid waves then held every CU against the whole-CU k_project / k_segment_lds;
+// with round 5's lighter VoxelGrid (105 VGPRs, 12.1 KB of LDS) the one-workgroup layout at lag 1 is the
+// faster one for both orders: C3 order 0 232.6-233.6k vs 220.9-222.2k scans/s)
 static int lg_wide_auto(const LgParams& P, int S) {
-  if (!lg_lds_projection(P) || !lg_lds_segment(P) || S * 8 <= P.ncu) return 1;
-  return (!P.voxel_stable && S <= 2 * P.ncu) ? 1 : 0;
+  return (!lg_lds_projection(P) || !lg_lds_segment(P) || S * 8 <= P.ncu) ? 1 : 0;
 }
 
 #define LG_PROBE_MAX 64  // probe events kept: the last LG_PROBE_MAX steps (lego_batch_probe_times)
+
+// Automatic pipeline depth: lag 2 for the reference's VoxelGrid order with at most half as many scans as
+// compute units (its slowest ring, a heap-sort fallback of ~1 ms, then needs more than one short step:
+// C5's 80 sequences 156k vs 104k scans/s), else lag 1 (C3's 256: 230-236k vs 214-216k).
+static int lg_lag_auto(const LgParams& P, int S) { return (!P.voxel_stable && 2 * S <= P.ncu) ? 2 : 1; }
 
 struct lego_batch {
   lego_params params;
@@ -183,6 +187,7 @@ struct lego_batch {
   //          slowest ring no longer holds the next one back.
   // lego_batch_flush (and every read) issues what is pending.
   int lag = 1;
+  int lag_req = -1;  // lego_batch_set_lag: -1 automatic (lg_lag_auto)
   hipStream_t vs[LEGO_MAX_GROUPS] = {};
   hipEvent_t ev_cat[LEGO_MAX_GROUPS] = {}, ev_vox[LEGO_MAX_GROUPS][LG_SLOTS] = {};
   hipEvent_t ev_cats[LG_SLOTS] = {};  // overlap schedule: k_concat of the scan in each slot
@@ -360,6 +365,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   b->P.max_points = max_points;
   b->wide_req = -1;
   b->P.wide = lg_wide_auto(P, n_streams);
+  b->lag = lg_lag_auto(P, n_streams);
   const size_t tiles = (VH + 1023) / 1024;  // SW_TILE
   rc = LEGO_OK;
 #define A(ptr, n) if (rc == LEGO_OK) rc = dalloc(&B.ptr, (n), o)
@@ -671,13 +677,16 @@ int lego_batch_set_groups(lego_batch* b, int32_t groups) {
 }
 
 int lego_batch_set_lag(lego_batch* b, int32_t lag) {
-  if (!b || lag < 0 || lag > 2) return LEGO_EINVAL;
+  if (!b || lag < -1 || lag > 2) return LEGO_EINVAL;
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   int rc = flush_pending(b);  // the pending work belongs to the old schedule
   if (rc) return rc;
-  b->lag = lag;
+  b->lag_req = lag;
+  b->lag = lag < 0 ? lg_lag_auto(b->P, b->S) : lag;
   return LEGO_OK;
 }
+
+int lego_batch_lag(const lego_batch* b) { return b ? b->lag : LEGO_EINVAL; }
 
 int lego_batch_set_wide(lego_batch* b, int32_t mode) {
   if (!b || mode < -1 || mode > 2) return LEGO_EINVAL;

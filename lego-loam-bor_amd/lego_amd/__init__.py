@@ -89,6 +89,7 @@ def lib():
         L.lego_batch_probe_times.argtypes = [C.c_void_p, P(C.c_float), P(C.c_int32)]
         L.lego_batch_set_wide.argtypes = [C.c_void_p, C.c_int32]
         L.lego_batch_wide.argtypes = [C.c_void_p]
+        L.lego_batch_lag.argtypes = [C.c_void_p]
         L.lego_batch_read_counts.argtypes = [C.c_void_p, P(C.c_int32)]
         L.lego_test_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int32, C.c_int32]
         L.lego_test_libm.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_int32, C.c_int32]
@@ -267,8 +268,13 @@ class Batch:
         return float(ms[0]), float(ms[1]), int(n.value)
 
     def set_lag(self, lag):
-        """Pipeline depth: 0 = a step runs its own scan's LM, 1 (default) = the previous scan's, 2 = the one before."""
+        """Pipeline depth: 0 = a step runs its own scan's LM, 1 = the previous scan's, 2 = the one before,
+        -1 automatic (the default)."""
         _check(lib().lego_batch_set_lag(self.h, int(lag)), "lego_batch_set_lag")
+
+    def lag(self):
+        """The pipeline depth in effect: 0, 1 or 2 (set_lag)."""
+        return int(lib().lego_batch_lag(self.h))
 
     def set_wide(self, mode):
         """Projection / segmentation layout: 1 wide (many workgroups a scan), 0 one workgroup a scan
