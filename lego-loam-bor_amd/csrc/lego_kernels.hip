@@ -39,6 +39,8 @@ using namespace lg;
 // 64 copies picked by block index so that the timer atomics do not serialise on one address.
 __device__ unsigned long long g_prof[256 * 64];
 #define PROF_SLOT(i) g_prof[(size_t)(i) * 64 + (blockIdx.x & 63)]
+// k_voxel's ring log of its last launch (profile build): per block {start, end, n | ring << 32, scan}
+__device__ unsigned long long g_ring_log[65536 * 4];
 #define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(slot, t0)                                           \
   do {                                                               \
@@ -2028,6 +2030,21 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
   while (true) {
     if (nqL == 0) {
       if (lo >= last) return min(last, lastR);  // unreachable for a median-of-3 pivot
+      // Skip, four chunks at a time, the chunks without a left stop (keys only: a run of keys below the
+      // pivot queues nothing).  A degenerate partition (a pivot near one end of the range, the VoxelGrid's
+      // heavy rings) otherwise streams its long side chunk by chunk through the queue permutes.
+      while (lo + 256 <= last) {
+        bool any[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) any[u] = !(a.key[lo + 64 * u + lane] < pv);
+        const unsigned long long b0 = __builtin_amdgcn_ballot_w64(any[0]), b1 = __builtin_amdgcn_ballot_w64(any[1]);
+        const unsigned long long b2 = __builtin_amdgcn_ballot_w64(any[2]), b3 = __builtin_amdgcn_ballot_w64(any[3]);
+        if (b0) break;
+        if (b1) { lo += 64; break; }
+        if (b2) { lo += 128; break; }
+        if (b3) { lo += 192; break; }
+        lo += 256;
+      }
       const int pL = lo + lane;
       const bool in = pL < last;
       const K k = a.key[in ? pL : first];
@@ -2044,6 +2061,18 @@ LG_DEVICE int wave_partition_stream_reg(const SortView<K, V>& a, int first, int 
       lo += 64;
     }
     if (nqR == 0) {
+      while (hi - 255 >= first) {  // the same for the right scan: chunks without a right stop
+        bool any[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) any[u] = !(pv < a.key[hi - 64 * u - lane]);
+        const unsigned long long b0 = __builtin_amdgcn_ballot_w64(any[0]), b1 = __builtin_amdgcn_ballot_w64(any[1]);
+        const unsigned long long b2 = __builtin_amdgcn_ballot_w64(any[2]), b3 = __builtin_amdgcn_ballot_w64(any[3]);
+        if (b0) break;
+        if (b1) { hi -= 64; break; }
+        if (b2) { hi -= 128; break; }
+        if (b3) { hi -= 192; break; }
+        hi -= 256;
+      }
       const int pR = hi - lane;
       const bool in = pR >= first;
       const K k = a.key[in ? pR : first];
@@ -2986,9 +3015,21 @@ void k_voxel(LgParams P, LgBufs B) {
   o.lflat = B.r_lflat + sb * P.H;  // output half P.par too (k_publish of this scan reads it)
   o.nLF = 0;
   o.status = 0;
+#ifdef LG_PROFILE
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz, one clock for all XCDs
+#endif
   PROF_T(t_vox0);
   voxel_wave<kMode>(P, v, L, n, o);
   PROF_ADD(4, t_vox0);
+#ifdef LG_PROFILE
+  if (lane_id() == 0 && b < 65536) {
+    unsigned long long* lg = g_ring_log + (size_t)b * 4;
+    lg[0] = rt0;
+    lg[1] = __builtin_amdgcn_s_memrealtime();
+    lg[2] = (unsigned long long)(unsigned)n | ((unsigned long long)(unsigned)rb << 32);
+    lg[3] = (unsigned long long)P.par;
+  }
+#endif
   if (lane_id() == 0) {
     B.r_vcount[sb] = o.nLF;
     B.r_vstatus[sb] = o.status;
@@ -5068,6 +5109,17 @@ extern "C" int lego_debug_lds_probe(int32_t bytes, int32_t blocks, float* ms) {
   return LEGO_OK;
 #else
   (void)bytes; (void)blocks; (void)ms;
+  return LEGO_ENOTSUP;
+#endif
+}
+
+extern "C" int lego_debug_ring_log(uint64_t* out, int32_t n_blocks) {  // k_voxel's last launch (profile build)
+#ifdef LG_PROFILE
+  if (!out || n_blocks < 0 || n_blocks > 65536) return LEGO_EINVAL;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ring_log), sizeof(uint64_t) * 4 * (size_t)n_blocks) == hipSuccess
+             ? LEGO_OK : LEGO_EDEVICE;
+#else
+  (void)out; (void)n_blocks;
   return LEGO_ENOTSUP;
 #endif
 }

@@ -75,6 +75,10 @@ template <typename K>
 LG_DEVICE K rdlane(K v, int l) {
   return __builtin_bit_cast(K, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
+template <typename K>
+LG_DEVICE K wshfl(K v, int src) {
+  return __builtin_bit_cast(K, __shfl(__builtin_bit_cast(int, v), src));
+}
 
 // __sort_heap (= repeated __pop_heap + __adjust_heap from the root) with the whole wave.
 // (Round 4 measured a variant with two ballots and the descent as a branch-free walk on the scalar
@@ -104,46 +108,152 @@ LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
   unsigned long long anc = 0ull;  // lanes of the node's in-window ancestors (excluding itself)
   for (int j = 1; j < lev; ++j) anc |= 1ull << ((1 << j) - 2 + (off >> (lev - j)));
   const unsigned long long bottom = ((1ull << 32) - 1ull) << 30;  // level-5 lanes
-  for (int len = last - first - 1; len >= 1; --len) {
-    // __pop_heap(first, first + len, first + len): value = a[len]; a[len] = a[0]; adjust from 0.
-    // The first window's read also brings the root (lane 62) and a[len] (lane 63).
-    const int lim = (len - 1) / 2;
-    const int only = (len & 1) == 0 ? len - 1 : -1;  // the only (left) child of node lim
-    int x = 0;     // window root (the hole when the window is entered)
-    int hole = 0;  // deepest node that took its child's element so far
-    K vk = K(0);
-    V vv = V(0);
-    while (true) {
-      const int node = (x << lev) + cst;
+  int len = last - first - 1;
+  if (len < 1) return;
+  // The top of the heap in registers: node t (levels 0-5) in lane t + 1, so lane l's children are lanes
+  // 2l, 2l + 1, siblings share a DPP pair and a node's in-register ancestors are lanes l >> 1, l >> 2, ..
+  const int tl = lane;
+  K tk = key[min(max(tl - 1, 0), len)];
+  V tv = val[min(max(tl - 1, 0), len)];
+  unsigned long long tanc = 0ull;  // in-register ancestors below the root
+  for (int j = tl >> 1; j >= 2; j >>= 1) tanc |= 1ull << j;
+  const bool todd = (tl & 1) != 0, ttop = tl >= 2;
+  const int c0 = 2 * tl;  // children lanes c0, c0 + 1 (lanes < 32)
+  if (len >= 127) {
+    // Heaps of 128 or more: levels 0-5 (nodes 0-62) stay in registers while the heap is at least that
+    // large, node t in lane t + 1 (so lane l's children are lanes 2l, 2l + 1 and siblings share a DPP pair);
+    // only the window below the level-5 path node (levels 6-10) is read from LDS.  Per pop: the top path
+    // by the same win / ancestor ballots, one LDS window, the moves as pulls from the moving child (a
+    // permute) and the window's writes.  The pop's value a[len] is read one pop ahead: the pop before can
+    // only change it by ending its hole there (a[len] is the last leaf), and then it is that pop's value.
+    const bool wlane = lane < 62;
+    K nvk = key[len];
+    V nvv = val[len];
+    for (; len >= 127; --len) {
+      const K vk = nvk;  // the pop's value; the root goes to its slot
+      const V vv = nvv;
+      nvk = key[len - 1];
+      nvv = val[len - 1];
+      const K rk = rdlane(tk, 1);
+      const V rv = (V)__builtin_amdgcn_readlane((int)tv, 1);
+      if (lane == 0) { key[len] = rk; val[len] = rv; }
+      // path through levels 1..5 (right unless right < left, as __adjust_heap)
+      const K ts = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, tk), 0xb1, 0xf, 0xf, false));
+      const bool twin = ttop & ((todd & !(tk < ts)) | (!todd & (ts < tk)));
+      const unsigned long long TW = __builtin_amdgcn_ballot_w64(twin);
+      const bool tonp = twin & ((TW & tanc) == tanc);
+      const unsigned long long TP = __builtin_amdgcn_ballot_w64(tonp);
+      const unsigned long long TM = __builtin_amdgcn_ballot_w64(tonp & !(tk < vk));  // moving top path nodes (a prefix)
+      const int x5l = 95 - __clzll((long long)(TP >> 32));  // the level-5 path lane
+      // window below node x5 (levels 6..10; every level-5 node has two children while len >= 127)
+      const int lim = (len - 1) / 2;
+      const int only = (len & 1) == 0 ? len - 1 : -1;
+      const int node = ((x5l - 1) << lev) + cst;
       const int par = (node - 1) >> 1;
-      const int nc = lane < 62 ? min(node, len - 1) : (lane == 62 ? x : len);
+      const int nc = wlane ? min(node, len - 1) : len - 1;
       const K kk = key[nc];
       const V vl = val[nc];
-      if (x == 0) {
-        vk = rdlane(kk, 63);
-        vv = (V)__builtin_amdgcn_readlane((int)vl, 63);
-        if (lane == 62) { key[len] = kk; val[len] = vl; }
-      }
-      const K ks = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, kk), 0xb1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]: the sibling
-      const bool wr = !(kk < ks), wl = ks < kk;
-      const bool win = lane < 62 && ((right && wr) || (!right && wl));
-      const unsigned long long W = __ballot(win);
-      const bool chain = (W & anc) == anc;
-      const bool onp = lane < 62 && chain && ((win && par < lim) || node == only);
-      const unsigned long long path = __ballot(onp);
-      const bool mv = onp && !(kk < vk);
-      const unsigned long long M = __ballot(mv);
-      if (mv) {
+      // the top: each path node takes its moving child's (old) element
+      const unsigned long long cm = tl < 32 ? (TM >> c0) & 3ull : 0ull;
+      const int src = cm ? c0 + (int)((cm & 1ull) ^ 1ull) : tl;
+      const K pk = wshfl(tk, src);
+      const V pv = (V)__shfl((int)tv, src);
+      const K ks = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, kk), 0xb1, 0xf, 0xf, false));
+      const bool win = wlane & ((right & !(kk < ks)) | (!right & (ks < kk)));
+      const unsigned long long W = __builtin_amdgcn_ballot_w64(win);
+      const bool onp = wlane & ((W & anc) == anc) & ((win & (par < lim)) | (node == only));
+      const bool mv = onp & !(kk < vk) & (((TM >> x5l) & 1ull) != 0ull);  // below a node that stays nothing moves
+      const unsigned long long M = __builtin_amdgcn_ballot_w64(mv);
+      if (mv & (lev > 1)) {  // (level 6's parent is x5, in registers)
         key[par] = kk;
         val[par] = vl;
       }
-      if (M) hole = __builtin_amdgcn_readlane(node, 63 - __clzll((long long)M));
-      if (M != path || !(M & bottom)) break;
-      x = hole;  // the path left the window through its bottom with every node moved
-      if (x > lim) break;
+      if (cm) { tk = pk; tv = pv; }
+      if (M & 3ull) {  // x5 takes its level-6 child
+        const int s6 = (int)((M & 1ull) ^ 1ull);
+        const K nk = rdlane(kk, s6);
+        const V nv = (V)__builtin_amdgcn_readlane((int)vl, s6);
+        if (tl == x5l) { tk = nk; tv = nv; }
+      }
+      if (M) {
+        int hole = __builtin_amdgcn_readlane(node, 63 - __clzll((long long)M));
+        // a window that the path leaves through its bottom with every node moved continues below
+        unsigned long long Mw = M, Pw = __builtin_amdgcn_ballot_w64(onp);
+        int xw = hole;
+        while (Mw == Pw && (Mw & bottom) && xw <= lim) {
+          const int node2 = (xw << lev) + cst;
+          const int par2 = (node2 - 1) >> 1;
+          const int nc2 = wlane ? min(node2, len - 1) : len - 1;
+          const K k2 = key[nc2];
+          const V v2 = val[nc2];
+          const K s2 = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, k2), 0xb1, 0xf, 0xf, false));
+          const bool win2 = wlane & ((right & !(k2 < s2)) | (!right & (s2 < k2)));
+          const unsigned long long W2 = __builtin_amdgcn_ballot_w64(win2);
+          const bool onp2 = wlane & ((W2 & anc) == anc) & ((win2 & (par2 < lim)) | (node2 == only));
+          const bool mv2 = onp2 & !(k2 < vk);
+          Pw = __builtin_amdgcn_ballot_w64(onp2);
+          Mw = __builtin_amdgcn_ballot_w64(mv2);
+          if (mv2) {
+            key[par2] = k2;
+            val[par2] = v2;
+          }
+          if (Mw) hole = __builtin_amdgcn_readlane(node2, 63 - __clzll((long long)Mw));
+          xw = hole;
+        }
+        if (lane == 0) { key[hole] = vk; val[hole] = vv; }
+        if (hole == len - 1) { nvk = vk; nvv = vv; }
+      } else {  // the deepest moved top node, or the root when none moves, takes the value
+        const int th = TM ? 63 - __clzll((long long)TM) : 1;
+        if (tl == th) { tk = vk; tv = vv; }
+      }
     }
-    if (lane == 0) { key[hole] = vk; val[hole] = vv; }
   }
+  // Heaps of at most 127: the whole heap in registers, the top as above and level 6 (nodes 63..126) in a
+  // second pair, node 63 + l in lane l (children of top lane l >= 32: bottom lanes 2l - 64, 2l - 63).  A
+  // pop reads no LDS: the value a[len] by a lane read, the top path by the ballots (with the reference's
+  // one-child node `only` and the two-children bound `lim`), level 6 below the level-5 path node, the
+  // moves as pulls; only the popped root is stored (at len, its sorted position).
+  K bk = key[min(63 + lane, len)];
+  V bv = val[min(63 + lane, len)];
+  const int bl = lane;
+  const bool bright = (bl & 1) != 0;
+  for (; len >= 1; --len) {
+    const K vk = len <= 62 ? rdlane(tk, len + 1) : rdlane(bk, len - 63);
+    const V vv = (V)__builtin_amdgcn_readlane(len <= 62 ? (int)tv : (int)bv, len <= 62 ? len + 1 : len - 63);
+    const K rk = rdlane(tk, 1);
+    const V rv = (V)__builtin_amdgcn_readlane((int)tv, 1);
+    if (lane == 0) { key[len] = rk; val[len] = rv; }
+    const int lim = (len - 1) / 2;
+    const int only = (len & 1) == 0 ? len - 1 : -1;  // the only (left) child of node lim
+    const K ts = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, tk), 0xb1, 0xf, 0xf, false));
+    const bool twin = ttop & ((todd & !(tk < ts)) | (!todd & (ts < tk)));
+    const unsigned long long TW = __builtin_amdgcn_ballot_w64(twin);
+    const bool tonp = ttop & ((TW & tanc) == tanc) & ((twin & ((tl >> 1) - 1 < lim)) | (tl - 1 == only));
+    const unsigned long long TP = __builtin_amdgcn_ballot_w64(tonp);
+    const unsigned long long TM = __builtin_amdgcn_ballot_w64(tonp & !(tk < vk));  // moving top path nodes
+    const bool x5m = (TM >> 32) != 0ull;  // the level-5 path node moved (only then can level 6 move)
+    const int x5l = x5m ? 95 - __clzll((long long)(TP >> 32)) : 0;
+    const K bs = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, bk), 0xb1, 0xf, 0xf, false));
+    const bool bwin = (bright & !(bk < bs)) | (!bright & (bs < bk));
+    const bool bonp = x5m & (32 + (bl >> 1) == x5l) & ((bwin & (31 + (bl >> 1) < lim)) | (63 + bl == only));
+    const unsigned long long BM = __builtin_amdgcn_ballot_w64(bonp & !(bk < vk));
+    // pulls from the moving child (old elements): top lanes < 32 from the top, level-5 lanes from level 6
+    const unsigned long long cm = tl < 32 ? (TM >> c0) & 3ull : (BM >> (c0 - 64)) & 3ull;
+    const int src = (cm ? c0 + (int)((cm & 1ull) ^ 1ull) : tl) & 63;
+    const K pt = wshfl(tk, src), pb = wshfl(bk, src);
+    const V qt = (V)__shfl((int)tv, src), qb = (V)__shfl((int)bv, src);
+    if (cm) {
+      tk = tl < 32 ? pt : pb;
+      tv = tl < 32 ? qt : qb;
+    }
+    if (BM) {  // the deepest moved node takes the value
+      if (bl == 63 - __clzll((long long)BM)) { bk = vk; bv = vv; }
+    } else {
+      const int th = TM ? 63 - __clzll((long long)TM) : 1;
+      if (tl == th) { tk = vk; tv = vv; }
+    }
+  }
+  if (lane == 0) { key[0] = rdlane(tk, 1); val[0] = (V)__builtin_amdgcn_readlane((int)tv, 1); }
   __syncthreads();
 }
 

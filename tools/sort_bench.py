@@ -22,14 +22,21 @@ import lego_amd as L  # noqa: E402
 def main():
     lib = L.lib()
     lib.lego_debug_sort_bench.argtypes = [C.POINTER(C.c_uint32), C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_float)]
+    lib.lego_debug_prof.argtypes = [C.POINTER(C.c_uint64), C.c_int32]
     d = np.load(os.path.join(REPO, "tools", "data", "voxel_keys_heavy.npz"))
     for name in d.files:
         k = np.ascontiguousarray(d[name].astype(np.uint32))
-        for mode in (0, 2, 3, 4, 1):
+        for mode in (0,):
             for blocks in (1, 4096):  # 4096: C3's rings a step (16 a CU)
                 ms = C.c_float()
+                prof = (C.c_uint64 * 256)()
+                lib.lego_debug_prof(prof, 1)
                 rc = lib.lego_debug_sort_bench(k.ctypes.data_as(C.POINTER(C.c_uint32)), len(k), blocks, mode,
                                                C.byref(ms))
+                lib.lego_debug_prof(prof, 0)
+                if blocks == 1 and rc == 0:  # phase split of the one copy (shader cycles; the bench may run it more than once)
+                    print("      phases (max one, cycles): partitions %d  heap fallback %d  heap pops %d  final %d" % (
+                        prof[192 + 6], prof[192 + 7], prof[192 + 36], prof[192 + 11]))
                 if rc != 0:
                     print("%-5s n=%5d mode %d: rc %d" % (name, len(k), mode, rc))
                     continue
