@@ -136,12 +136,14 @@ bool lg_lds_segment(const LgParams& P);
 // workgroup a scan cannot hold the images in LDS, and where too few scans are in flight to fill
 // the device with one workgroup each.
 // The wide layout (many small workgroups a scan) where the one-workgroup-a-scan kernels cannot hold the
-// scan in LDS and for few scans.  (Round 4 also took it for the reference's VoxelGrid order up to 2 scans
-// a CU, whose heavier VoxelGrid waves then held every CU against the whole-CU k_project / k_segment_lds;
-// with round 5's lighter VoxelGrid (105 VGPRs, 12.1 KB of LDS) the one-workgroup layout at lag 1 is the
-// faster one for both orders: C3 order 0 232.6-233.6k vs 220.9-222.2k scans/s)
+// scan in LDS, for few scans, and for the reference's VoxelGrid order with at most one scan a CU.  With
+// that order a scan's VoxelGrid launch (one wave a ring) runs ~0.85 ms, set by its few heap-sort-bound
+// rings; once it no longer waits behind the previous launch it overlaps the next scan's front end, and
+// one VoxelGrid wave on a SIMD already keeps the whole-CU k_project (4 x 110 VGPRs a SIMD) and
+// k_segment_lds (4 x 128) off that CU, while the wide kernels' small workgroups fill the room left
+// (round 5, same box: 235.1-237.8k vs 212.2-216.7k scans/s).
 static int lg_wide_auto(const LgParams& P, int S) {
-  return (!lg_lds_projection(P) || !lg_lds_segment(P) || S * 8 <= P.ncu) ? 1 : 0;
+  return (!lg_lds_projection(P) || !lg_lds_segment(P) || S * 8 <= P.ncu || (!P.voxel_stable && S <= P.ncu)) ? 1 : 0;
 }
 
 #define LG_PROBE_MAX 64  // probe events kept: the last LG_PROBE_MAX steps (lego_batch_probe_times)

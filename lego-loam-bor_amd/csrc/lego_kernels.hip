@@ -1214,7 +1214,10 @@ LG_DEVICE void segment_lds(const LgParams& P, const LgBufs& B, int* smem) {
   }
 }
 
-__global__ __launch_bounds__(1024) void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
+#ifndef LG_KP_ATTR
+#define LG_KP_ATTR
+#endif
+__global__ __launch_bounds__(1024) LG_KP_ATTR void k_project(LgParams P, LgBufs B, const float4* __restrict__ pts,
                                                   const int64_t* __restrict__ offs,
                                                   const int32_t* __restrict__ cnts) {
   extern __shared__ __attribute__((aligned(16))) int smem[];

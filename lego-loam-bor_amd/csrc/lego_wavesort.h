@@ -276,9 +276,13 @@ LG_DEVICE void heap_sort_wave(const SortView<K, V>& a, int first, int last) {
   PROF_T(t_pop0);
   // The pops are one dependent chain, usually the longest of the launch: let this wave win
   // instruction arbitration against the other waves of its SIMD while it runs them.
+#ifndef LG_AB_NOPRIO
   __builtin_amdgcn_s_setprio(3);
+#endif
   sort_heap_wave(a, first, last);
+#ifndef LG_AB_NOPRIO
   __builtin_amdgcn_s_setprio(0);
+#endif
   PROF_ADD(36, t_pop0);
 }
 
