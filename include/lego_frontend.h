@@ -292,6 +292,10 @@ int  lego_debug_prof(uint64_t* out256, int32_t reset);
 /* k_voxel's per-block log of its last launch (profile build): {start, end, n | ring id << 32, slot}, the
  * stamps from the 100 MHz real-time counter, 4 words a block. */
 int  lego_debug_ring_log(uint64_t* out, int32_t n_blocks);
+/* k_lm's per-block log of its last launch (profile build): {start, end (100 MHz real time), shader
+ * cycles of the surf / corner grid builds, searches and iteration blocks, surf / corner iterations,
+ * flat / sharp queries, surf / lessSharp Last sizes, 2 unused}, 16 words a block. */
+int  lego_debug_lm_log(uint64_t* out, int32_t n_blocks);
 /* Kernel time of `blocks` concurrent one-wave copies of the device sort of h_keys (profile build);
  * mode 0 the stack emulation, 1 the level-synchronous one (n <= 2048). */
 int  lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, int32_t mode, float* ms);

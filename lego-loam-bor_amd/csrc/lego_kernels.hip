@@ -41,6 +41,10 @@ __device__ unsigned long long g_prof[256 * 64];
 #define PROF_SLOT(i) g_prof[(size_t)(i) * 64 + (blockIdx.x & 63)]
 // k_voxel's ring log of its last launch (profile build): per block {start, end, n | ring << 32, scan}
 __device__ unsigned long long g_ring_log[65536 * 4];
+// k_lm's per-scan log of its last launch (profile build): {start, end (real time), phase cycles [6],
+// surf / corner iterations, flat / sharp queries, surf / lessSharp Last sizes}
+__device__ unsigned long long g_lm_log[4096 * 16];
+#define PROF_LM(i, t0) do { if (threadIdx.x == 0) L.plog[i] += __builtin_amdgcn_s_memtime() - (t0); } while (0)
 #define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(slot, t0)                                           \
   do {                                                               \
@@ -53,6 +57,7 @@ __device__ unsigned long long g_ring_log[65536 * 4];
 #else
 #define PROF_T(v) do {} while (0)
 #define PROF_ADD(slot, t0) do {} while (0)
+#define PROF_LM(i, t0) do {} while (0)
 #endif
 
 #include "lego_wavesort.h"  // heap_sort_wave, lvl_sort (after the phase-timer macros it uses)
@@ -3541,6 +3546,9 @@ struct LmLdsT {  // kMaxQ: feature queries of one loop (V * max(cap_sharp, cap_f
   int iters;     // iterations run by the loop so far
   int status;
   int skip;
+#ifdef LG_PROFILE
+  unsigned long long plog[8];  // k_lm's per-scan phase log (profile build): build / search / iterations a loop
+#endif
 };
 
 // candidate key compare: (dist, rank) lexicographic = sequential strict-< scan order
@@ -4213,11 +4221,20 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
   // uniform grid for the 1-NN: the surf cloud's cell table takes the LDS of the staged small cloud;
   // a small (staged) cloud gets a coarser table of its own
   int* gcell = small ? L.cgcell : L.u.gcell;
-  build_grid(L, small ? (const float4*)L.u.lastc : last_g, nl, gp, (sqrtf(P.nn_dist_sqr) + 0.01f) / 3.f, gcell,
-             small ? CGRID_MAX : GRID_MAX);
+  // A staged cloud of at most half the staging area keeps its grid-ordered copy in the other half, so its
+  // 1-NN walks read LDS instead of global memory (the corner cloud: ~450 points, four or five searches a
+  // loop); the grid itself is the same.
+  const bool gl = small && nl <= LM_LAST_LDS / 2;
+  float4* gpl = L.u.lastc + LM_LAST_LDS / 2;
+  if (gl)
+    build_grid(L, (const float4*)L.u.lastc, nl, gpl, (sqrtf(P.nn_dist_sqr) + 0.01f) / 3.f, gcell, CGRID_MAX);
+  else
+    build_grid(L, small ? (const float4*)L.u.lastc : last_g, nl, gp, (sqrtf(P.nn_dist_sqr) + 0.01f) / 3.f, gcell,
+               small ? CGRID_MAX : GRID_MAX);
   const float4* last = small ? (const float4*)L.u.lastc : last_g;
   ring_index(L, last, nl);
   PROF_ADD(surf ? 16 : 48, t_bg0);
+  PROF_LM(surf ? 0 : 1, t_bg0);
   if (tid == 0) { L.iters = 0; L.kd_built = 0; L.kdv.pts = last; L.kd_n = nl; }
   for (int iter = 0; iter < 25; iter += 5) {
     {  // search (all waves)
@@ -4240,7 +4257,8 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
         bool tie = false;
         const float4 qs = act ? L.sel[q] : make_float4(0.f, 0.f, 0.f, 0.f);
         int c;
-        c = grid_nn(L, gcell, gp, qs, P.nn_dist_sqr, tie, sub, tpq, act);
+        if (gl) c = grid_nn(L, gcell, (const float4*)gpl, qs, P.nn_dist_sqr, tie, sub, tpq, act);
+        else c = grid_nn(L, gcell, gp, qs, P.nn_dist_sqr, tie, sub, tpq, act);
         if (act && sub == 0) {
           L.ind1[q] = c;
           if (tie) {
@@ -4343,6 +4361,7 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
       }
       PROF_ADD(surf ? 38 : 47, t_rs0);
       PROF_ADD(9, t_srch0);
+      PROF_LM(surf ? 2 : 3, t_srch0);
     }
     PROF_T(t_acc0);
     if (wave_id() == 0) {  // iterations iter .. iter + 4 on wave 0
@@ -4392,6 +4411,7 @@ LG_DEVICE void lm_loop(const LgParams& P, Lds& L, LgState& S, const float4* __re
     }
     __syncthreads();
     PROF_ADD(10, t_acc0);
+    PROF_LM(surf ? 4 : 5, t_acc0);
     if (!L.flag) break;
   }
   iters = L.iters;
@@ -4475,6 +4495,10 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
   const float4* f_sharp = B.f_sharp + hs * V * P.cap_sharp;
   const float4* f_lsharp = B.f_lsharp + hs * V * P.cap_lsharp;
   const float4* f_flat = B.f_flat + hs * V * P.cap_flat;
+#ifdef LG_PROFILE
+  const unsigned long long rt_lm0 = __builtin_amdgcn_s_memrealtime();
+  if (tid < 8) L.plog[tid] = 0ull;
+#endif
   if (tid == 0) {
     S = B.state[s];
     L.status = fc[3];
@@ -4592,6 +4616,17 @@ __global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
     S.status = L.status;
     lm_record(P, B, s, S);
     B.state[s] = S;
+#ifdef LG_PROFILE
+    if (blockIdx.x < 4096) {
+      unsigned long long* lg = g_lm_log + (size_t)blockIdx.x * 16;
+      lg[0] = rt_lm0;
+      lg[1] = __builtin_amdgcn_s_memrealtime();
+      for (int k = 0; k < 6; ++k) lg[2 + k] = L.plog[k];
+      lg[8] = (unsigned)S.iters_surf; lg[9] = (unsigned)S.iters_corner;
+      lg[10] = (unsigned)n_flat; lg[11] = (unsigned)n_sharp;
+      lg[12] = (unsigned)S.n_surf_last; lg[13] = (unsigned)n_lsharp;
+    }
+#endif
   }
 }
 
@@ -5112,6 +5147,17 @@ extern "C" int lego_debug_lds_probe(int32_t bytes, int32_t blocks, float* ms) {
   return LEGO_OK;
 #else
   (void)bytes; (void)blocks; (void)ms;
+  return LEGO_ENOTSUP;
+#endif
+}
+
+extern "C" int lego_debug_lm_log(uint64_t* out, int32_t n_blocks) {  // k_lm's last launch (profile build)
+#ifdef LG_PROFILE
+  if (!out || n_blocks < 0 || n_blocks > 4096) return LEGO_EINVAL;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lm_log), sizeof(uint64_t) * 16 * (size_t)n_blocks) == hipSuccess
+             ? LEGO_OK : LEGO_EDEVICE;
+#else
+  (void)out; (void)n_blocks;
   return LEGO_ENOTSUP;
 #endif
 }
