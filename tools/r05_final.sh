@@ -36,4 +36,12 @@ if [ "$WHAT" = pmc ]; then
   python3 tools/pmc_summarize.py "$OUT/fetch" "$OUT/write" "$OUT/pmc.json" --workload vlp16 --streams 256
   python3 tools/pmc_summarize.py "$OUT/fetch_hdl" "$OUT/write_hdl" "$OUT/pmc_hdl64.json" --workload hdl64 --streams 256
 fi
+if [ "$WHAT" = latency ]; then  # config C2's mode: one scan in flight through the single-context C-ABI
+  for rep in 1 2; do
+    for O in 0 1; do
+      timeout -k 10 200 python3 tools/latency.py --voxel-order $O >> "$OUT/latency_one_scan.jsonl" 2>/dev/null
+    done
+  done
+  cat "$OUT/latency_one_scan.jsonl"
+fi
 echo done
