@@ -4482,8 +4482,15 @@ LG_DEVICE void lm_record(const LgParams& P, const LgBufs& B, int s, LgState& S) 
   S.n_assoc++;
 }
 
+// The VLP-16 layout (512 threads, two waves a SIMD) is held to 128 VGPRs (four waves a SIMD's worth; 49-66
+// registers spill to scratch): 2 x 128 of a SIMD's 512 registers leave
+// room for two VoxelGrid waves (105 VGPRs) beside it instead of one (177 VGPRs a wave otherwise); +0.9 % C3
+// order 0 in the pipeline (238.1k -> 240.3k scans/s, three A/B pairs on one box), +4.2 % order 1 (295.6k ->
+// 307.9k, two pairs) although k_lm alone is 5 % slower (0.53 -> 0.56 ms).  768 threads: unchanged.
+// (The compiler drops a request the block's own LDS makes unreachable: 5 for this layout, 4 for 768 threads.)
 template <int kNT, int kMaxQ, bool kF1>
-__global__ __launch_bounds__(kNT) void k_lm(LgParams P, LgBufs B) {
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kNT == 512 ? 4 : 1)))
+void k_lm(LgParams P, LgBufs B) {
   __shared__ LmLdsT<kMaxQ> L;
   __shared__ LgState S;
   const int s = P.s0 + blockIdx.x, tid = threadIdx.x;
