@@ -4482,14 +4482,15 @@ LG_DEVICE void lm_record(const LgParams& P, const LgBufs& B, int s, LgState& S) 
   S.n_assoc++;
 }
 
-// The VLP-16 layout (512 threads, two waves a SIMD) is held to 128 VGPRs (four waves a SIMD's worth; 49-66
-// registers spill to scratch): 2 x 128 of a SIMD's 512 registers leave
-// room for two VoxelGrid waves (105 VGPRs) beside it instead of one (177 VGPRs a wave otherwise); +0.9 % C3
-// order 0 in the pipeline (238.1k -> 240.3k scans/s, three A/B pairs on one box), +4.2 % order 1 (295.6k ->
-// 307.9k, two pairs) although k_lm alone is 5 % slower (0.53 -> 0.56 ms).  768 threads: unchanged.
-// (The compiler drops a request the block's own LDS makes unreachable: 5 for this layout, 4 for 768 threads.)
-template <int kNT, int kMaxQ, bool kF1>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kNT == 512 ? 4 : 1)))
+// kWpe: waves a SIMD the compiler budgets registers for.  With more than half a scan a CU in flight the VLP-16
+// layout (512 threads, two waves a SIMD) runs at 4 (128 VGPRs, 49-66 spilled to scratch): 2 x 128 of a SIMD's 512
+// registers leave room for two VoxelGrid waves (105 VGPRs) beside it instead of one (177 VGPRs a wave otherwise):
+// +0.9 % C3 order 0 in the pipeline (238.1k -> 240.3k scans/s, three A/B pairs on one box), +4.2 % order 1
+// (295.6k -> 307.9k, two pairs) although k_lm alone is 5 % slower (0.53 -> 0.56 ms).  With fewer scans (C5's 80
+// sequences: 157.4k -> 148.1k) the LM's own speed counts and kWpe stays 1.  (The compiler drops a request the
+// block's own LDS makes unreachable: 5 for this layout, 4 for 768 threads.)
+template <int kNT, int kMaxQ, bool kF1, int kWpe>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kWpe)))
 void k_lm(LgParams P, LgBufs B) {
   __shared__ LmLdsT<kMaxQ> L;
   __shared__ LgState S;
@@ -4765,14 +4766,19 @@ int lg_launch_lm(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
   // 553 -> 515 us, +4 % scans/s).  Few scans in flight (one scan: 2-3 % lower latency) and larger
   // sensors keep 768 threads (and LDS for 1,536 queries).
   const bool small = P.V * std::max(P.cap_sharp, P.cap_flat) <= 384 && S > 8;
-  if (small && !P.fp1)
-    hipLaunchKernelGGL((k_lm<512, 384, false>), dim3(S), dim3(512), 0, st, P, B);
+  const bool cap = 2 * S > P.ncu;  // more than half a scan a CU: share SIMDs with VoxelGrid waves (k_lm's kWpe)
+  if (small && cap && !P.fp1)
+    hipLaunchKernelGGL((k_lm<512, 384, false, 4>), dim3(S), dim3(512), 0, st, P, B);
+  else if (small && cap)
+    hipLaunchKernelGGL((k_lm<512, 384, true, 4>), dim3(S), dim3(512), 0, st, P, B);
+  else if (small && !P.fp1)
+    hipLaunchKernelGGL((k_lm<512, 384, false, 1>), dim3(S), dim3(512), 0, st, P, B);
   else if (small)
-    hipLaunchKernelGGL((k_lm<512, 384, true>), dim3(S), dim3(512), 0, st, P, B);
+    hipLaunchKernelGGL((k_lm<512, 384, true, 1>), dim3(S), dim3(512), 0, st, P, B);
   else if (!P.fp1)
-    hipLaunchKernelGGL((k_lm<768, 1536, false>), dim3(S), dim3(768), 0, st, P, B);
+    hipLaunchKernelGGL((k_lm<768, 1536, false, 1>), dim3(S), dim3(768), 0, st, P, B);
   else
-    hipLaunchKernelGGL((k_lm<768, 1536, true>), dim3(S), dim3(768), 0, st, P, B);
+    hipLaunchKernelGGL((k_lm<768, 1536, true, 1>), dim3(S), dim3(768), 0, st, P, B);
   LG_CHECK_LAUNCH();
   return LEGO_OK;
 }
