@@ -219,7 +219,7 @@ int  lego_batch_time_hbm_stages(lego_batch* b, int32_t reps, const lego_point* d
 /* Measurement: the VoxelGrid stage (PCL VoxelGrid of every ring's lessFlat cloud, featureAssociation.cpp:
  * 377-379) of the batch's last step launched `reps` times back to back on hip_stream, alone on the device
  * (it synchronises first); *ms = mean milliseconds a launch.  Idempotent (same staged input, same output).
- * bench.py's stages_ms.voxel_alone. */
+ * LEGO_EINVAL before the batch's first step (nothing staged).  bench.py's stages_ms.voxel_alone. */
 int  lego_batch_time_voxel(lego_batch* b, int32_t reps, void* hip_stream, float* ms);
 /* While timing is enabled, steps run as one slice on the caller's stream (plus the VoxelGrid stream). */
 int  lego_batch_set_timing(lego_batch* b, int32_t enabled);
@@ -240,7 +240,8 @@ int  lego_batch_set_groups(lego_batch* b, int32_t groups);
  * off, else run as 1; see lego_batch_step), -1 (default) = automatic: 2 with voxel_tie_order 0 and at
  * most half as many streams as compute units, else 1.  Results do not depend on it. */
 int  lego_batch_set_lag(lego_batch* b, int32_t lag);
-/* The pipeline depth in effect (0, 1 or 2), or LEGO_EINVAL. */
+/* The pipeline depth lego_batch_step runs (0, 1 or 2: a requested 2 reads 1 while the streams are sliced
+ * into groups > 1 or timing is on), or LEGO_EINVAL. */
 int  lego_batch_lag(const lego_batch* b);
 /* Kernel layout of the projection and segmentation: 1 = wide (a scan's work over many workgroups,
  * per-scan images in HBM), 0 = one workgroup a scan with its images in LDS (only where they fit:
@@ -286,28 +287,6 @@ int  lego_test_set_lm_state(lego_ctx* ctx, const float* transform_cur, const flo
  * found, -2: search stack overflow) and squared distances. */
 int  lego_test_kd_knn(const float* cloud, int32_t n, const float* queries, int32_t m, int32_t k, int32_t* idx,
                       float* dist);
-/* Diagnostic phase timers (shader cycles summed over waves) of a -DLG_PROFILE build
- * (liblego_frontend_prof.so); LEGO_ENOTSUP in the shipped library. */
-int  lego_debug_prof(uint64_t* out256, int32_t reset);
-/* k_voxel's per-block log of its last launch (profile build): {start, end, n | ring id << 32, slot}, the
- * stamps from the 100 MHz real-time counter, 4 words a block. */
-int  lego_debug_ring_log(uint64_t* out, int32_t n_blocks);
-/* k_lm's per-block log of its last launch (profile build): {start, end (100 MHz real time), shader
- * cycles of the surf / corner grid builds, searches and iteration blocks, surf / corner iterations,
- * flat / sharp queries, surf / lessSharp Last sizes, 2 unused}, 16 words a block. */
-int  lego_debug_lm_log(uint64_t* out, int32_t n_blocks);
-/* Kernel time of `blocks` concurrent one-wave copies of the device sort of h_keys (profile build);
- * mode 0 the stack emulation, 1 the level-synchronous one (n <= 2048). */
-int  lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, int32_t mode, float* ms);
-/* LDS co-residency probe (profile build; LEGO_ENOTSUP in the shipped library): mean ms of `blocks`
- * one-wave blocks that each hold `bytes` of LDS and sleep ~20 us. */
-int  lego_debug_lds_probe(int32_t bytes, int32_t blocks, float* ms);
-/* Counter calibration (profile build; LEGO_ENOTSUP in the shipped library): k_project's input read
- * patterns (mode 0 12-byte buffer loads, 1 16-byte loads, 2 both passes) over S scans of device points
- * (offs / cnts as lego_batch_run's), out[S * 1024]. */
-int  lego_debug_fetch_probe(int32_t mode, int32_t S, const void* pts, const int64_t* offs, const int32_t* cnts,
-                            float* out, void* stream);
-
 #ifdef __cplusplus
 }
 #endif

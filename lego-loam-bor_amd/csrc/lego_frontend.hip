@@ -193,6 +193,7 @@ struct lego_batch {
   hipStream_t vs[LEGO_MAX_GROUPS] = {};
   hipEvent_t ev_cat[LEGO_MAX_GROUPS] = {}, ev_vox[LEGO_MAX_GROUPS][LG_SLOTS] = {};
   hipEvent_t ev_cats[LG_SLOTS] = {};  // overlap schedule: k_concat of the scan in each slot
+  bool fe_ran = false;       // a front-end step has staged input since create / reset (lego_batch_time_voxel)
   int vox_alt = 0;           // lag 2: the stream of the next VoxelGrid launch (vs[0] / gs[0])
   int par = 0;               // staging slot of the next front-end scan
   int last_par = 0;          // slot of the last front-end scan (reads)
@@ -424,6 +425,10 @@ int lego_batch_reset(lego_batch* b) {
   b->epoch = 0;
   b->pend_pub = b->pend_lm = b->pend_lm_old = b->pend_ovl = false;
   b->par = b->last_par = 0;
+  b->fe_ran = false;
+  // the VoxelGrid's staged ring sizes and outputs: empty until a step stages them
+  if (hipMemset(B.lf_count, 0, LG_SLOTS * S * b->P.V * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemset(B.r_vcount, 0, LG_SLOTS * S * b->P.V * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.state, 0, S * sizeof(LgState)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.fe_state, 0, S * 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   if (hipMemset(B.counts, 0, S * CNT_N * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
@@ -688,7 +693,11 @@ int lego_batch_set_lag(lego_batch* b, int32_t lag) {
   return LEGO_OK;
 }
 
-int lego_batch_lag(const lego_batch* b) { return b ? b->lag : LEGO_EINVAL; }
+// The depth lego_batch_step runs: lag 2 runs as 1 when the streams are sliced (groups > 1) or timing is on.
+int lego_batch_lag(const lego_batch* b) {
+  if (!b) return LEGO_EINVAL;
+  return (b->lag >= 2 && (b->groups > 1 || b->timing)) ? 1 : b->lag;
+}
 
 int lego_batch_set_wide(lego_batch* b, int32_t mode) {
   if (!b || mode < -1 || mode > 2) return LEGO_EINVAL;
@@ -787,6 +796,7 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
     b->pend_ovl = true;
     b->last_par = b->par;
     b->par = (b->par + 1) % LG_SLOTS;
+    b->fe_ran = true;
     return LEGO_OK;
   }
   if (G <= 1) {
@@ -807,6 +817,7 @@ int lego_batch_step(lego_batch* b, const lego_point* d_points, const int64_t* d_
   }
   if (rc) return rc;
   advance_pipeline(b, lag, G);
+  b->fe_ran = true;
   return LEGO_OK;
 }
 
@@ -921,7 +932,7 @@ int lego_batch_time_hbm_stages(lego_batch* b, int32_t reps, const lego_point* d_
 }
 
 int lego_batch_time_voxel(lego_batch* b, int32_t reps, void* hip_stream, float* ms) {
-  if (!b || reps < 1 || !ms) return LEGO_EINVAL;
+  if (!b || reps < 1 || !ms || !b->fe_ran) return LEGO_EINVAL;  // no step has staged the VoxelGrid's input
   if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
   hipStream_t st = (hipStream_t)hip_stream;
   int rc = flush_pending(b);

@@ -2173,13 +2173,17 @@ LG_DEVICE void final_window(K* key, V* val, int n) {
 // and never moves an element across a partition cut, so its result is the post-partition array
 // stably sorted by key.  Needs key bit order == key order: unsigned keys, or float keys none
 // negative or NaN (the caller checks); n <= 2048 (unsigned) / 512 (float).
-// blk: the per-block insertion sorts' final-block bits (unused, may be null, with final_reg and integral keys)
+// blk: the per-block insertion sorts' final-block bits (unused, may be null, when the register final pass
+// serves the call: final_reg with integral keys, or with n <= 512)
 template <typename K, typename V>
 LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, bool final_reg = false) {
   const int lane = lane_id();
   if (n <= 1) return;
   const int nwords = (n + 31) >> 5;
-  if (!final_reg)
+  // the register final pass serves unsigned keys of any n <= 2048 and float keys of n <= 512; every
+  // other call falls through to the per-block insertion sorts below, which read blk
+  const bool reg_final = final_reg && (std::is_integral<K>::value || n <= 512);
+  if (!reg_final)
     for (int w = lane; w < nwords; w += 64) blk[w] = 0u;
   __syncthreads();
   SortView<K, V> a{key, val};
@@ -2218,7 +2222,7 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, bool final_re
       ++sp;
       last = cut;
     }
-    if (!final_reg && lane == 0) blk[first >> 5] |= 1u << (first & 31);  // a final block starts here
+    if (!reg_final && lane == 0) blk[first >> 5] |= 1u << (first & 31);  // a final block starts here
   }
   __syncthreads();
   PROF_ADD(6, t_part0);
@@ -2235,7 +2239,7 @@ LG_DEVICE void wave_std_sort(K* key, V* val, int n, unsigned* blk, bool final_re
       return;
     }
   }
-  if (final_reg && (n <= 512 || std::is_integral<K>::value)) {
+  if (reg_final) {
     if (n <= 64) final_bitonic<1>(key, val, n);
     else if (n <= 128) final_bitonic<2>(key, val, n);
     else if (n <= 256) final_bitonic<4>(key, val, n);
@@ -5080,23 +5084,19 @@ __global__ __launch_bounds__(1024) void k_fetch_probe(int mode, const float4* __
 
 #endif
 
+#ifdef LG_PROFILE  // the diagnostic entry points (include/lego_debug.h): profile build only
+#include "../../include/lego_debug.h"
 extern "C" int lego_debug_fetch_probe(int32_t mode, int32_t S, const void* pts, const int64_t* offs,
                                       const int32_t* cnts, float* out, void* stream) {
-#ifdef LG_PROFILE
   if (mode < 0 || mode > 2 || S < 1 || !pts || !offs || !cnts || !out) return LEGO_EINVAL;
   hipLaunchKernelGGL(k_fetch_probe, dim3(S), dim3(1024), 0, (hipStream_t)stream, mode, (const float4*)pts, offs,
                      cnts, out);
   return hipGetLastError() == hipSuccess ? LEGO_OK : LEGO_EDEVICE;
-#else
-  (void)mode; (void)S; (void)pts; (void)offs; (void)cnts; (void)out; (void)stream;
-  return LEGO_ENOTSUP;
-#endif
 }
 
 // Diagnostics (profile build only): time `blocks` concurrent copies of one device sort.
 // mode 0: the stack emulation (wave_std_sort), 1: the level-synchronous one (lvl_sort, R by size)
 extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t blocks, int32_t mode, float* ms) {
-#ifdef LG_PROFILE
   unsigned *k = nullptr, *o = nullptr;
   if (n < 1 || n > RING_MAX || blocks < 1 || (mode == 1 && n > 2048)) return LEGO_EINVAL;
   hipMalloc((void**)&k, n * 4);
@@ -5125,13 +5125,8 @@ extern "C" int lego_debug_sort_bench(const uint32_t* h_keys, int32_t n, int32_t 
   hipFree(k);
   hipFree(o);
   return LEGO_OK;
-#else
-  (void)h_keys; (void)n; (void)blocks; (void)mode; (void)ms;
-  return LEGO_ENOTSUP;
-#endif
 }
 
-#ifdef LG_PROFILE
 // LDS allocation probe: one wave a block holding `bytes` of dynamic LDS, each sleeping ~20 us
 __global__ __launch_bounds__(64) void k_lds_probe(int* out) {
   extern __shared__ int dyn[];
@@ -5139,10 +5134,8 @@ __global__ __launch_bounds__(64) void k_lds_probe(int* out) {
   for (int i = 0; i < 400; ++i) __builtin_amdgcn_s_sleep(127);
   if (threadIdx.x == 0) out[blockIdx.x] = dyn[1];
 }
-#endif
 // Diagnostics (profile build only): ms of `blocks` one-wave blocks of `bytes` LDS each (co-residency).
 extern "C" int lego_debug_lds_probe(int32_t bytes, int32_t blocks, float* ms) {
-#ifdef LG_PROFILE
   int* o = nullptr;
   hipMalloc((void**)&o, blocks * 4);
   hipEvent_t a, b;
@@ -5158,36 +5151,21 @@ extern "C" int lego_debug_lds_probe(int32_t bytes, int32_t blocks, float* ms) {
   hipEventDestroy(b);
   hipFree(o);
   return LEGO_OK;
-#else
-  (void)bytes; (void)blocks; (void)ms;
-  return LEGO_ENOTSUP;
-#endif
 }
 
-extern "C" int lego_debug_lm_log(uint64_t* out, int32_t n_blocks) {  // k_lm's last launch (profile build)
-#ifdef LG_PROFILE
+extern "C" int lego_debug_lm_log(uint64_t* out, int32_t n_blocks) {  // k_lm's last launch
   if (!out || n_blocks < 0 || n_blocks > 4096) return LEGO_EINVAL;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lm_log), sizeof(uint64_t) * 16 * (size_t)n_blocks) == hipSuccess
              ? LEGO_OK : LEGO_EDEVICE;
-#else
-  (void)out; (void)n_blocks;
-  return LEGO_ENOTSUP;
-#endif
 }
 
-extern "C" int lego_debug_ring_log(uint64_t* out, int32_t n_blocks) {  // k_voxel's last launch (profile build)
-#ifdef LG_PROFILE
+extern "C" int lego_debug_ring_log(uint64_t* out, int32_t n_blocks) {  // k_voxel's last launch
   if (!out || n_blocks < 0 || n_blocks > 65536) return LEGO_EINVAL;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ring_log), sizeof(uint64_t) * 4 * (size_t)n_blocks) == hipSuccess
              ? LEGO_OK : LEGO_EDEVICE;
-#else
-  (void)out; (void)n_blocks;
-  return LEGO_ENOTSUP;
-#endif
 }
 
 extern "C" int lego_debug_prof(uint64_t* out32, int32_t reset) {
-#ifdef LG_PROFILE
   std::vector<uint64_t> h(256 * 64, 0);
   if (out32) {
     if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_prof), sizeof(uint64_t) * h.size()) != hipSuccess) return LEGO_EDEVICE;
@@ -5203,8 +5181,5 @@ extern "C" int lego_debug_prof(uint64_t* out32, int32_t reset) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), h.data(), sizeof(uint64_t) * h.size()) != hipSuccess) return LEGO_EDEVICE;
   }
   return LEGO_OK;
-#else
-  (void)out32; (void)reset;
-  return LEGO_ENOTSUP;
-#endif
 }
+#endif  // LG_PROFILE

@@ -2004,7 +2004,11 @@ static int map_voxel_std_order(lego_s2m* m, int n, const lego_map_voxel_io* io, 
     if (nbig == 0) break;
     if (nbig > m->cap_big || level > 64) return LEGO_EDEVICE;  // (bounded by construction)
     const int g64 = (nbig + 63) / 64;
-    const dim3 gch((unsigned)((size_t)m->vxs_maxch * nbig));  // < 2^32: e / VXS_CH chunks at most
+    // one chunk block per (range, chunk of the longest possible range): vxs_maxch comes from the largest
+    // cloud, so the grid grows with nbig * max_map; HIP needs gridDim.x * blockDim.x < 2^32
+    const size_t nblk = (size_t)m->vxs_maxch * (size_t)nbig;
+    if (nblk * VXS_TPB >= (1ull << 32)) return LEGO_EINVAL;
+    const dim3 gch((unsigned)nblk);
     if (hipMemsetAsync(ctr + 1, 0, 4, st) != hipSuccess) return LEGO_EDEVICE;
     hipLaunchKernelGGL(k_vxs_median, dim3(g64), dim3(64), 0, st, (const VxsSeg*)cur, (const int*)ctr, m->d_keys,
                        m->d_vals, m->d_pivot, m->d_cut);

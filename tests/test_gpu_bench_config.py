@@ -7,7 +7,9 @@ stream; W warm-up steps, flush, K timed steps, flush.  The same batch here, with
 odometry recorded on the device (lego_batch_set_trajectory, which does not change the schedule): each of
 the 256 streams' transformCur / transformSum after every scan within 1e-4 of an independent oracle run
 (featureAssociation.cpp:1213-1270, 1286-1298), and exact parity of the last scan (projection, features,
-Last clouds) on a sample of streams.  The stable order (bench.py's other_voxel_tie_order) runs the same way.
+Last clouds) on a sample of streams.  The stable order (bench.py's other_voxel_tie_order) runs the same way,
+and so does the double libm model (fp_mode 1, shorter: its register-capped k_lm<512, 384, true, 4> runs only
+with more than half a scan a CU in flight, which no other fp_mode 1 test reaches).
 """
 from concurrent.futures import ThreadPoolExecutor
 
@@ -25,7 +27,7 @@ pytestmark = pytest.mark.gpu
 S, W, K = 256, 3, 6
 
 
-def _oracle_sequence(params, pts, cnt, s):
+def _oracle_sequence(params, pts, cnt, s, W=W, K=K):
     orc = oracle_for(params)
     traj, last = [], None
     for k in range(W + K):
@@ -36,10 +38,11 @@ def _oracle_sequence(params, pts, cnt, s):
     return np.array(traj, np.float64), last
 
 
-@pytest.mark.parametrize("order,wide", [(0, 1), (1, 0)])
-def test_bench_schedule_matches_oracle(gpu, order, wide):
+@pytest.mark.parametrize("order,wide,fp_mode", [(0, 1, 0), (1, 0, 0), (0, 1, 1)])
+def test_bench_schedule_matches_oracle(gpu, order, wide, fp_mode):
     import torch
-    params = L.params_vlp16(voxel_tie_order=order)
+    W, K = (3, 6) if fp_mode == 0 else (1, 3)
+    params = L.params_vlp16(voxel_tie_order=order, fp_mode=fp_mode)
     cfg = A.synth_cfg("vlp16")
     cap = params.num_vertical_scans * params.num_horizontal_scans
     seqs = np.repeat(np.arange(S, dtype=np.int32)[None, :], W + K, 0).reshape(-1)  # bench.py's sequences 0 .. S-1
@@ -66,15 +69,15 @@ def test_bench_schedule_matches_oracle(gpu, order, wide):
     poses, status = b.poses()
     assert np.all((status & A.ST_UB_MASK) == 0)
     with ThreadPoolExecutor(8) as ex:  # the oracle's ctypes calls release the GIL
-        ref = list(ex.map(lambda s: _oracle_sequence(params, pts, cnt, s), range(S)))
+        ref = list(ex.map(lambda s: _oracle_sequence(params, pts, cnt, s, W, K), range(S)))
     worst = max(float(np.abs(got[s] - ref[s][0]).max()) for s in range(S))
     exact = sum(int(np.array_equal(got[s].astype(np.float32), ref[s][0].astype(np.float32))) for s in range(S))
-    print("order %d: %d streams x %d scans, max |d pose| %.3g, %d streams bit-identical" % (
-        order, S, W + K, worst, exact))
+    print("order %d fp_mode %d: %d streams x %d scans, max |d pose| %.3g, %d streams bit-identical" % (
+        order, fp_mode, S, W + K, worst, exact))
     assert worst <= Hs.TF_TOL
     np.testing.assert_array_equal(got[:, -1].astype(np.float32), poses)
     for s in (0, 101, 202, S - 1):  # exact parity of the last scan on a sample
         pg, fg = b.read(s)
         pr, fr = ref[s][1]
-        assert_scan_parity((order, s), pg, pr, fg, fr)
+        assert_scan_parity((order, fp_mode, s), pg, pr, fg, fr)
     b.close()

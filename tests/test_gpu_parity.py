@@ -895,3 +895,35 @@ def test_segment_sort_ties_match_oracle(gpu):
         np.testing.assert_allclose(fg["transform_cur"], fr["transform_cur"], atol=Hs.TF_TOL, rtol=0)
         np.testing.assert_allclose(fg["transform_sum"], fr["transform_sum"], atol=Hs.TF_TOL, rtol=0)
     fe.close()
+
+
+def test_time_voxel_needs_a_step_and_lag_reports_effective_depth(gpu):
+    """lego_batch_time_voxel before any step has staged the VoxelGrid's input is refused (LEGO_EINVAL, no
+    launch over unset ring sizes), and is accepted after one; lego_batch_lag reports the depth the steps
+    run (a requested lag 2 runs as 1 with stream groups > 1)."""
+    import torch
+    params = L.params_vlp16()
+    cfg = A.synth_cfg("vlp16")
+    S = 4
+    cap = params.num_vertical_scans * params.num_horizontal_scans
+    b = L.Batch(params, S, cap)
+    with pytest.raises(L.LegoError):
+        b.time_voxel(reps=1)
+    pts, cnt = A.synth_batch(cfg, np.arange(S, dtype=np.int32), np.zeros(S, np.int32))
+    d_pts = torch.from_numpy(pts).cuda()
+    offs = torch.from_numpy(np.arange(S, dtype=np.int64) * cap).cuda()
+    cnts = torch.from_numpy(cnt.astype(np.int32)).cuda()
+    st = torch.cuda.current_stream().cuda_stream
+    b.step(d_pts.data_ptr(), offs.data_ptr(), cnts.data_ptr(), st)
+    b.sync()
+    assert b.time_voxel(reps=1) > 0
+    b.reset()
+    with pytest.raises(L.LegoError):
+        b.time_voxel(reps=1)
+    b.set_lag(2)
+    assert b.lag() == 2
+    b.set_groups(2)
+    assert b.lag() == 1
+    b.set_groups(1)
+    assert b.lag() == 2
+    b.close()
