@@ -107,8 +107,9 @@ struct LgBufs {  // device buffers, all indexed [stream][...]
   float4* cloud;         // [S][VH]  _full_cloud
   int8_t* ground;        // [S][VH]
   int32_t* label;        // [S][VH]
-  int32_t* winner;       // [S][VH]  wide mode: "later point wins" image, -1 between launches
+  int32_t* winner;       // [S][VH]  wide mode: "later point wins" image (tagged entries, column-major)
   int32_t* proj_mm;      // [S][2]   wide mode: first / last finite input point
+  int32_t* colcnt;       // [S][H]   wide mode: k_pw_slice's touches a column (k_pw_fix reads and clears it)
   int32_t* cc_parent;    // [S][VH]  wide mode: union-find parent (or -1: not eligible)
   int32_t* cc_cnt;       // [S][VH]  component size of a root, then its label
   unsigned long long* cc_mask;  // [S][VH]  rows of a root's non-seed members

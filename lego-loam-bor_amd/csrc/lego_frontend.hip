@@ -373,7 +373,7 @@ int lego_batch_create(const lego_params* p, int32_t device, int32_t n_streams, i
   rc = LEGO_OK;
 #define A(ptr, n) if (rc == LEGO_OK) rc = dalloc(&B.ptr, (n), o)
   A(range, S * VH); A(cloud, S * VH); A(ground, S * VH); A(label, S * VH);
-  A(winner, S * VH); A(proj_mm, S * 2); A(seg_tiles, S * tiles);
+  A(winner, S * VH); A(proj_mm, S * 2); A(colcnt, S * H); A(seg_tiles, S * tiles);
   A(cc_parent, S * VH); A(cc_cnt, S * VH); A(cc_mask, S * VH);
   A(scan_cand, S * H); A(orient, S * 4);
   A(seg_pts, S * VH); A(seg_range, S * VH); A(seg_col, S * VH); A(seg_ground, S * VH);
@@ -436,6 +436,7 @@ int lego_batch_reset(lego_batch* b) {
   // INT_MAX and last point -1 (every launch leaves them so)
   b->wepoch = 0;
   if (hipMemset(B.winner, 0, S * VH * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
+  if (hipMemset(B.colcnt, 0, S * b->P.H * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
   {
     std::vector<int32_t> mm(2 * S);
     for (size_t s = 0; s < S; ++s) { mm[2 * s] = 0x7fffffff; mm[2 * s + 1] = -1; }

@@ -203,7 +203,8 @@ LG_DEVICE float atan01_poly(float a) {
 // boundary), the range test from |p|^2 against [0.0099, 0.0101].  Returns the cell, -1 (rejected) or
 // -2: too close to a decision boundary to tell, the exact path decides.  The margins hold for
 // ang_res_y >= 0.1 deg and ang_res_x >= 0.1 deg (lg_fast_projection checks them).
-template <bool kColMajor = false>
+// kLayout: the cell as row * H + col (0), col * V + row (1: the wide winner image) or row << 16 | col (2)
+template <int kLayout = 0>
 LG_DEVICE int proj_cell_fast(const LgParams& P, float4 p) {
   const float d2 = p.x * p.x + p.y * p.y + p.z * p.z;
   if (!(d2 > 0.0101f)) return d2 < 0.0099f ? -1 : -2;
@@ -233,21 +234,24 @@ LG_DEVICE int proj_cell_fast(const LgParams& P, float4 p) {
   int columnIdn = (P.H - 2 * k) / 2;
   if (columnIdn >= P.H) columnIdn -= P.H;
   if (columnIdn < 0 || columnIdn >= P.H) return -1;
-  return kColMajor ? columnIdn * P.V + r0 : r0 * P.H + columnIdn;
+  return kLayout == 1 ? columnIdn * P.V + r0 : kLayout == 2 ? (r0 << 16) | columnIdn : r0 * P.H + columnIdn;
 }
 
 // groundRemoval's test (imageProjection.cpp:276-285): (double)(va - mount) <= 10 deg with va =
 // std::atan2(dZ, sqrt(s2)), s2 = dX*dX + dY*dY + dZ*dZ in float: atan2f(dZ, sqrtf(s2)) with the float
 // overloads (fp_mode 0); with ::sqrt(double) (fp_mode 1) the std::atan2(float, double) overload
 // promotes, va = (float)atan2(double(dZ), sqrt(double(s2))).  r = sqrt(s2) >= |dZ|, so the angle lies
-// in [-pi/4, pi/4].  A polynomial atan (error < 1e-6 rad with the reciprocal) decides every pair
-// farther than 1e-5 rad from the threshold in both models; the rest, and r == 0 or NaN (empty cells),
-// take the glibc-faithful path of the model.
+// in [-pi/4, pi/4].  A pair with an empty cell (NaN) is never ground (atan2 of a NaN is NaN in both
+// models).  A polynomial atan (error < 1e-6 rad with the reciprocal) decides every pair farther than
+// 1e-5 rad from the threshold in both models; the rest, and r == 0, take the glibc-faithful path of
+// the model.
 __attribute__((noinline)) __device__ bool ground_pair_exact(float dZ, float s2, float mount, int fp1) {  // one copy
   const float va = fp1 ? (float)atan2_d((double)dZ, sqrt((double)s2)) : atan2f_g(dZ, sqrtf(s2));
   return (double)(va - mount) <= 10 * DEG_TO_RAD_D;
 }
 LG_DEVICE bool ground_pair(float dZ, float s2, float mount, int fp1) {
+  // an empty cell (nanPoint) on either side: every model's angle is NaN and the test false
+  if (__builtin_isnan(dZ) || __builtin_isnan(s2)) return false;
   const double thr = 10 * DEG_TO_RAD_D;
   const float r = sqrtf(s2);
   if (r > 0.f && r < FLT_MAX) {
@@ -491,6 +495,7 @@ LG_DEVICE void project_lds(const LgParams& P, const LgBufs& B, const float4* __r
 // kNB batches of 8 points a lane per workgroup: 4 when many scans are in flight (fewer, longer
 // workgroups stream the input with the next batch's loads in flight), 1 for few scans (more
 // workgroups a scan).
+#ifndef LG_PW_SLICE  // the shipped wide projection: scatter + column pass
 #define PW_NT 256
 #define PW_PTS (PW_NT * 8)  // points a batch
 template <int kNB>
@@ -529,7 +534,7 @@ __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, cons
       if (i < n && isfinite_f(p.x) && isfinite_f(p.y) && isfinite_f(p.z)) {  // removeNaNFromPointCloud
         fmin = min(fmin, i);
         fmax = max(fmax, i);
-        c = P.fast_proj ? proj_cell_fast<true>(P, p)
+        c = P.fast_proj ? proj_cell_fast<1>(P, p)
                         : cell_cm(proj_cell_exact_ni(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, p), V, H);
         if (c >= 0) atomicMax(&winner[c], tag | (unsigned)i);
       }
@@ -556,14 +561,455 @@ __global__ __launch_bounds__(PW_NT) void k_pw_scatter(LgParams P, LgBufs B, cons
   }
 }
 
+#endif  // !LG_PW_SLICE
+
+// The column pass of one column j from its cells' points, NQ lanes a column, R rows a lane (V <= R * NQ):
+// lane q of the column holds rows Rq .. Rq + R - 1, pk[u] the x, y, z of row Rq + u (NaN for an empty
+// cell, nanPoint) and bit u of hm whether that row has a point.  Writes the range / cloud / ground cells
+// and the 2-D scan candidate of the column when `col` (lanes with !col take part in the shuffles only).
+// The pair (Rq - 1, Rq) of groundRemoval (:271-285) is settled by lane q with lane q - 1's last point
+// (shuffled up), and its result for row 16q - 1 goes back down; the 2-D scan candidate (:312-330) is the
+// (range, row) minimum over the lanes, which is what the sequential bottom-up scan with a strict `<` picks.
+template <int NQ, int R = 16>
+LG_DEVICE void pw_column_emit(const LgParams& P, const LgBufs& B, int s, int j, int q, bool col, const float3 (&pk)[R],
+                              unsigned hm) {
+  const int V = P.V, H = P.H, VH = P.VH, i0 = R * q;
+  float* range = B.range + (size_t)s * VH;
+  float4* cloud = B.cloud + (size_t)s * VH;
+  int8_t* ground = B.ground + (size_t)s * VH;
+  const double jfrac = (double)(float)j / 10000.0;
+  // groundRemoval (:271-285): pair (i-1, i) for 1 <= i <= G marks both rows
+  unsigned gm = 0u;  // bit u: row i0 + u
+  float3 below = make_float3(0.f, 0.f, 0.f);
+  if constexpr (NQ > 1) {
+    below.x = __shfl_up(pk[R - 1].x, 1, NQ);
+    below.y = __shfl_up(pk[R - 1].y, 1, NQ);
+    below.z = __shfl_up(pk[R - 1].z, 1, NQ);
+  }
+  bool down = false;  // pair (i0 - 1, i0) marks row i0 - 1, lane q - 1's last row
+  if (NQ > 1 && q > 0 && i0 <= P.G && col && i0 < V) {
+    const float dX = pk[0].x - below.x, dY = pk[0].y - below.y, dZ = pk[0].z - below.z;
+    if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) {
+      gm |= 1u;
+      down = true;
+    }
+  }
+#pragma unroll
+  for (int u = 1; u < R; ++u) {
+    const int i = i0 + u;
+    if (col && i < V && i <= P.G) {
+      const float dX = pk[u].x - pk[u - 1].x, dY = pk[u].y - pk[u - 1].y, dZ = pk[u].z - pk[u - 1].z;
+      if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) gm |= 3u << (u - 1);
+    }
+  }
+  if constexpr (NQ > 1) {
+    const int dn = __shfl_down((int)down, 1, NQ);
+    if (q + 1 < NQ && dn) gm |= 1u << (R - 1);
+  }
+  float min_range = 1000.f;
+  int id_min = 0x7fffffff;
+  if (col) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int i = i0 + u;
+      if (i >= V) continue;
+      const int c = i * H + j;
+      const float3 p = pk[u];
+      const bool h = (hm >> u) & 1u;
+      const float r = h ? sqrtf(p.x * p.x + p.y * p.y + p.z * p.z) : FLT_MAX;
+      st_nt(&range[c], r);
+      st_nt(&cloud[c], make_float4(p.x, p.y, p.z, h ? (float)((double)(float)i + jfrac) : 0.f));  // nanPoint: 0
+      const int g = (int)((gm >> u) & 1u);
+      ground[c] = (int8_t)g;
+      if (g != 1 && (double)p.z > 0.4 && (double)p.z < 1.2 && r < 40.f && r < min_range) {  // 2-D scan (:312-330)
+        min_range = r;
+        id_min = c;
+      }
+    }
+  }
+  if constexpr (NQ > 1) {
+#pragma unroll
+    for (int o = 1; o < NQ; o <<= 1) {
+      const float o_r = __shfl_xor(min_range, o, NQ);
+      const int o_c = __shfl_xor(id_min, o, NQ);
+      if (o_r < min_range || (o_r == min_range && o_c < id_min)) {
+        min_range = o_r;
+        id_min = o_c;
+      }
+    }
+  }
+  if (col && q == 0) B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
+}
+
+// findStartEndAngle (:234-249) of scan s from proj_mm, which is left reset for the next launch
+LG_DEVICE void pw_orient(const LgParams& P, const LgBufs& B, int s, const float4* in) {
+  const int fmin = B.proj_mm[2 * s], fmax = B.proj_mm[2 * s + 1];
+  B.proj_mm[2 * s] = 0x7fffffff;
+  B.proj_mm[2 * s + 1] = -1;
+  proj_orient(P, B, s, in, fmin, fmax);
+}
+
+#ifdef LG_PW_SLICE
+// ---- the wide projection in one read of the input (round 6; built with -DLG_PW_SLICE, not shipped) ------
+// Measured against the shipped scatter + column pass (tools/proj_time.py): correct (every wide
+// parity test) but slower: 0.15 vs 0.11 ms for 256 VLP-16 scans, 1.0 vs 0.55 ms for HDL-64E.
+// k_pw_slice: grid (slices of PWS_NT * kU consecutive input points, scans).  The input is in firing order
+// (azimuth-major), so a slice's points land in a narrow band of columns.  A slice resolves "later point
+// wins" (imageProjection.cpp:214-222) for its own points in an LDS image of that band (atomicMax of the
+// point's slot), keeps its points' x, y, z in LDS, and runs the column pass (pw_column_emit) of every
+// band column it touched: range / cloud / ground cells, the 2-D scan candidate.  Each point is read from
+// HBM once and each cell of an uncontested column written once.  Whether another slice also touched a
+// column is only known after every slice ran: each slice counts its touch in colcnt[column] (+1), and
+// publishes its band winners to the scan's winner image W (tagged atomicMax as k_pw_scatter) for the
+// PW_EDGE columns at either end of its band (+0x1000: "published"), where consecutive slices meet, and
+// for its whole band if it is the scan's first or last slice (the seam of the sweep).  A slice whose
+// band does not fit (input not in firing order) publishes every point to W and marks its columns
+// (bit 31).  k_pw_fix then settles every column: touched by exactly one band slice -> done; by none ->
+// empty cells; otherwise rebuilt from W, or, when a band slice touched it without publishing it (a
+// second sweep over the same azimuth), from a rescan of the scan's input for that column block.
+#define PWS_NT 256
+#define PW_EDGE 4  // band columns at either end of a slice published to the winner image
+
+// The exact path for 64 queued slots of a slice (lane l takes q[l]): the point read from the input, its
+// cell as row << 16 | col (or -1) into pcell.
+__attribute__((noinline)) __device__ void proj_drain_slot(float ang_bottom, float res_x, float res_y, int V, int H,
+                                                          const float4* in, int c0, const int* q, int* pcell) {
+  LgParams P;
+  P.ang_bottom = ang_bottom;
+  P.ang_res_x = res_x;
+  P.ang_res_y = res_y;
+  P.V = V;
+  P.H = H;
+  const int k = q[lane_id()];
+  const float4 p = in[c0 + k];
+  const int c = proj_cell_exact(P, make_float4(p.x, p.y, p.z, 0.f));
+  pcell[k] = c < 0 ? -1 : ((c / H) << 16) | (c - (c / H) * H);
+}
+
+#ifdef LG_PWS_STATS  // diagnostic builds only: [0] fallback slices [1] band slices [2] owned [3] empty
+                     // [4] contested complete [5] incomplete columns [6] rescan blocks
+__device__ unsigned long long g_pws[8];
+#define PWS_STAT(i, v) atomicAdd(&g_pws[i], (unsigned long long)(v))
+#else
+#define PWS_STAT(i, v) do {} while (0)
+#endif
+
+// k_pw_slice's LDS.  VM: rows (V <= VM); NBC: band columns held (a wider band: input out of firing order).
+template <int kU, int VM, int NBC>
+struct PwSliceLds {
+  static constexpr int PS = PWS_NT * kU;  // points a slice
+  static constexpr int NW = PWS_NT / 64;
+  static constexpr int VS = VM + 1;       // band image column stride (rows, then the touched flag)
+  int pcell[PS];                          // the slice's cells, row << 16 | col (-1: none)
+  int bwin[NBC * VS];                     // band image: winning slot a cell (-1: empty); [k * VS + VM]: touched
+  unsigned gbits[NBC * 2];                // ground rows of a band column (groundRemoval's pairs)
+  unsigned long long scan[NBC];           // 2-D scan candidate of a band column: range bits << 32 | cell
+  int queue[NW * PQ_CAP];
+  int red[4 * NW];
+};
+
+#ifndef LG_PWS_WPE
+#define LG_PWS_WPE 5
+#endif
+#define LG_PWS_ATTR __attribute__((amdgpu_waves_per_eu(LG_PWS_WPE)))
+template <int kU, int VM, int NBC>
+__global__ __launch_bounds__(PWS_NT) LG_PWS_ATTR void k_pw_slice(LgParams P, LgBufs B, const float4* __restrict__ pts,
+                                                                 const int64_t* __restrict__ offs,
+                                                                 const int32_t* __restrict__ cnts) {
+  using Lds = PwSliceLds<kU, VM, NBC>;
+  constexpr int PS = Lds::PS, NW = Lds::NW, VS = Lds::VS;
+  __shared__ Lds L;
+  const int s = P.s0 + blockIdx.y, tid = threadIdx.x;
+  const int V = P.V, H = P.H;
+  const int n = cnts[s];
+  const int c0 = blockIdx.x * PS;
+  if (c0 >= n) return;
+  const float4* in = pts + offs[s];
+  const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
+  int* queue = L.queue + wave_id() * PQ_CAP;
+  int qn = 0, fmin = 0x7fffffff, fmax = -1;
+  {
+    float3 pk[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) pk[u] = buffer_load_f3(rin, (uint32_t)(c0 + u * PWS_NT + tid) * 16u);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int slot = u * PWS_NT + tid, i = c0 + slot;
+      const float4 p = make_float4(pk[u].x, pk[u].y, pk[u].z, 0.f);
+      int c = -1;
+      if (i < n && isfinite_f(p.x) && isfinite_f(p.y) && isfinite_f(p.z)) {  // removeNaNFromPointCloud
+        fmin = min(fmin, i);
+        fmax = max(fmax, i);
+        if (P.fast_proj) {
+          c = proj_cell_fast<2>(P, p);
+        } else {
+          c = proj_cell_exact_ni(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, p);
+          c = c < 0 ? -1 : ((c / H) << 16) | (c - (c / H) * H);
+        }
+      }
+      L.pcell[slot] = c;
+      const unsigned long long amb = __ballot(c == -2);
+      if (c == -2) queue[qn + popc_below(amb)] = slot;
+      qn += __popcll(amb);
+      if (qn >= 64) {  // wave-uniform, rare: the oldest 64 take the exact path
+        proj_drain_slot(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, c0, queue + qn - 64, L.pcell);
+        qn -= 64;
+      }
+    }
+  }
+  if (qn > 0) {  // the rest (< 64): lanes past qn repeat entry 0 (the same write, harmless)
+    if (lane_id() >= qn) queue[lane_id()] = queue[0];
+    proj_drain_slot(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, in, c0, queue, L.pcell);
+  }
+  fmin = wave_min(fmin);
+  fmax = wave_max(fmax);
+  if (lane_id() == 0 && fmax >= 0) {  // findStartEndAngle's first / last finite point (k_pw_fix settles it)
+    atomicMin(&B.proj_mm[2 * s], fmin);
+    atomicMax(&B.proj_mm[2 * s + 1], fmax);
+  }
+  __syncthreads();
+#if defined(LG_PWS_CUT) && LG_PWS_CUT == 1
+  return;
+#endif
+  // The band: the slice's column range, directly or rotated by half a turn (a slice across the column
+  // wrap), whichever is narrower.  jr = (j + Hr) mod H, j = (jr + Hh) mod H.
+  const int Hh = H / 2, Hr = H - Hh;
+  int m0 = 0x7fffffff, x0 = -1, m1 = 0x7fffffff, x1 = -1;
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int c = L.pcell[u * PWS_NT + tid];
+    if (c >= 0) {
+      const int j = c & 0xffff, jr = j < Hh ? j + Hr : j - Hh;
+      m0 = min(m0, j); x0 = max(x0, j);
+      m1 = min(m1, jr); x1 = max(x1, jr);
+    }
+  }
+  m0 = wave_min(m0); x0 = wave_max(x0); m1 = wave_min(m1); x1 = wave_max(x1);
+  if (lane_id() == 0) {
+    L.red[4 * wave_id()] = m0; L.red[4 * wave_id() + 1] = x0; L.red[4 * wave_id() + 2] = m1; L.red[4 * wave_id() + 3] = x1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    m0 = min(m0, L.red[4 * w]); x0 = max(x0, L.red[4 * w + 1]);
+    m1 = min(m1, L.red[4 * w + 2]); x1 = max(x1, L.red[4 * w + 3]);
+  }
+  if (x0 < 0) return;  // no point of the slice has a cell (block-uniform)
+  const bool rot = x1 - m1 < x0 - m0;
+  const int base = rot ? m1 : m0, bw = (rot ? x1 - m1 : x0 - m0) + 1;
+  unsigned* W = (unsigned*)B.winner + (size_t)s * P.VH;
+  int* colcnt = B.colcnt + (size_t)s * H;
+  const unsigned tag = P.wtag;
+  if (tid == 0) PWS_STAT(bw > NBC ? 0 : 1, 1);
+  if (bw > NBC) {  // not in firing order: every point to the winner image, its columns marked
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int c = L.pcell[u * PWS_NT + tid];
+      if (c < 0) continue;
+      const int j = c & 0xffff;
+      atomicMax(&W[j * V + (c >> 16)], tag | (unsigned)(c0 + u * PWS_NT + tid));
+      atomicOr(&colcnt[j], (int)0x80000000);
+    }
+    return;
+  }
+  for (int e = tid; e < bw * VS; e += PWS_NT) {
+    const int k = e / VS;
+    L.bwin[e] = (e - k * VS == VM) ? 0 : -1;
+  }
+  for (int k = tid; k < bw; k += PWS_NT) {
+    L.gbits[2 * k] = 0u;
+    L.gbits[2 * k + 1] = 0u;
+    L.scan[k] = ~0ull;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int c = L.pcell[u * PWS_NT + tid];
+    if (c < 0) continue;
+    const int j = c & 0xffff;
+    const int k = (rot ? (j < Hh ? j + Hr : j - Hh) : j) - base;
+    atomicMax(&L.bwin[k * VS + (c >> 16)], u * PWS_NT + tid);  // later point wins
+    L.bwin[k * VS + VM] = 1;                                  // touched
+  }
+  __syncthreads();
+#if defined(LG_PWS_CUT) && LG_PWS_CUT == 2
+  return;
+#endif
+  auto colof = [&](int k) {
+    const int jv = base + k;
+    return rot ? (jv + Hh < H ? jv + Hh : jv + Hh - H) : jv;
+  };
+  const float qnan = __int_as_float(0x7fc00000);
+  // groundRemoval (:271-285): the pairs (r, r + 1), r < G, of every touched band column, in strips of 8 rows
+  // a lane (the winners' points read again from the input, which this workgroup has just read: L2)
+  const int G = P.G, nstrip = (G + 7) >> 3;
+  for (int e = tid; e < nstrip * bw; e += PWS_NT) {
+    const int st = e / bw, k = e - st * bw, r0 = st << 3;
+    if (!L.bwin[k * VS + VM]) continue;
+    float3 q[9];
+    unsigned hm = 0u;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      const int r = r0 + u;
+      const int w = (r <= G && r < V) ? L.bwin[k * VS + r] : -1;
+      hm |= (unsigned)(w >= 0) << u;
+      q[u] = buffer_load_f3(rin, w >= 0 ? (uint32_t)(c0 + w) * 16u : 0xffffffffu);
+    }
+    unsigned long long g = 0ull;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = r0 + u;
+      if (r < G && ((hm >> u) & 3u) == 3u) {  // (a pair with an empty cell is never ground)
+        const float dX = q[u + 1].x - q[u].x, dY = q[u + 1].y - q[u].y, dZ = q[u + 1].z - q[u].z;
+        if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) g |= 3ull << r;
+      }
+    }
+    if ((unsigned)g) atomicOr(&L.gbits[2 * k], (unsigned)g);
+    if ((unsigned)(g >> 32)) atomicOr(&L.gbits[2 * k + 1], (unsigned)(g >> 32));
+  }
+  __syncthreads();
+  // every cell of the touched band columns, row-major over the band (a row's consecutive columns in
+  // consecutive lanes): range / cloud / ground, the 2-D scan candidate (:312-330) by a 64-bit LDS min of
+  // (range, cell) — the sequential bottom-up scan with a strict `<` keeps the lowest row of equal ranges
+  float* range = B.range + (size_t)s * P.VH;
+  float4* cloud = B.cloud + (size_t)s * P.VH;
+  int8_t* ground = B.ground + (size_t)s * P.VH;
+  {
+    constexpr int EM = (VM * NBC + PWS_NT - 1) / PWS_NT;  // cells a lane at most
+    const int nc = V * bw;
+    int wv[EM];
+    float3 p3[EM];
+#pragma unroll
+    for (int t = 0; t < EM; ++t) {  // every gather in flight at once (one round trip)
+      const int e = tid + t * PWS_NT;
+      const int i = e / bw, k = e - i * bw;
+      wv[t] = (e < nc && L.bwin[k * VS + VM]) ? L.bwin[k * VS + i] : -2;  // -2: not a cell of a touched column
+      p3[t] = buffer_load_f3(rin, wv[t] >= 0 ? (uint32_t)(c0 + wv[t]) * 16u : 0xffffffffu);
+    }
+#pragma unroll
+    for (int t = 0; t < EM; ++t) {
+      if (wv[t] == -2) continue;
+      const int e = tid + t * PWS_NT;
+      const int i = e / bw, k = e - i * bw;
+      const int j = colof(k), c = i * H + j;
+      const bool h = wv[t] >= 0;
+      const float4 pc = h ? make_float4(p3[t].x, p3[t].y, p3[t].z, (float)((double)(float)i + (double)(float)j / 10000.0))
+                          : make_float4(qnan, qnan, qnan, 0.f);  // nanPoint: intensity 0
+      const float r = h ? sqrtf(p3[t].x * p3[t].x + p3[t].y * p3[t].y + p3[t].z * p3[t].z) : FLT_MAX;
+      const int g = (int)((L.gbits[2 * k + (i >> 5)] >> (i & 31)) & 1u);
+      st_nt(&range[c], r);
+      st_nt(&cloud[c], pc);
+      ground[c] = (int8_t)g;
+      if (g != 1 && (double)pc.z > 0.4 && (double)pc.z < 1.2 && r < 40.f)
+        atomicMin(&L.scan[k], ((unsigned long long)__float_as_uint(r) << 32) | (unsigned)c);
+    }
+  }
+  __syncthreads();
+  // per touched column: the scan candidate, its touch, and (at the band's ends, the scan's first / last
+  // slice) its winners to W
+  for (int k = tid; k < bw; k += PWS_NT) {
+    if (!L.bwin[k * VS + VM]) continue;
+    const int j = colof(k);
+    const unsigned long long sc = L.scan[k];
+    B.scan_cand[(size_t)s * H + j] = sc == ~0ull ? -1 : (int)(unsigned)sc;
+    const bool pub = k < PW_EDGE || k >= bw - PW_EDGE || c0 == 0 || c0 + PS >= n;
+    atomicAdd(&colcnt[j], pub ? 0x1001 : 1);
+    if (pub)
+      for (int i = 0; i < V; ++i) {
+        const int w = L.bwin[k * VS + i];
+        if (w >= 0) atomicMax(&W[j * V + i], tag | (unsigned)(c0 + w));
+      }
+  }
+}
+
+// k_pw_fix: grid (column blocks, scans), NQ lanes a column: reads and clears each column's colcnt and
+// settles the columns k_pw_slice left open: empty columns (no point) get their empty cells; contested
+// columns are rebuilt from the winner image W (each winner's point gathered from the input, as
+// k_pw_columns did for every column), or, where a band slice touched a column without publishing it,
+// from the winners of a rescan of the whole scan's input into the block's columns (LDS).  Block (0, s)
+// settles findStartEndAngle.
+template <int NQ, int PC_NT, int CPL>
+__global__ __launch_bounds__(PC_NT) void k_pw_fix(LgParams P, LgBufs B, const float4* __restrict__ pts,
+                                                  const int64_t* __restrict__ offs, const int32_t* __restrict__ cnts) {
+  constexpr int NC = PC_NT / NQ;  // columns a workgroup pass; CPL passes (every colcnt read up front)
+  constexpr int VS = 16 * NQ + 1;
+  __shared__ unsigned wl[NC * VS];
+  const int s = P.s0 + blockIdx.y, tid = threadIdx.x;
+  const int V = P.V, H = P.H;
+  const int jj = tid / NQ, q = tid % NQ, i0 = 16 * q;
+  int* colcnt = B.colcnt + (size_t)s * H;
+  static_assert(CPL >= 1 && CPL <= 4, "up to four column passes a workgroup");
+  unsigned v4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int rep = 0; rep < CPL; ++rep) {
+    const int j = (blockIdx.x * CPL + rep) * NC + jj;
+    v4[rep] = (j < H && q == 0) ? (unsigned)colcnt[j] : 0u;
+  }
+#pragma unroll
+  for (int rep = 0; rep < CPL; ++rep) {
+    const int j = (blockIdx.x * CPL + rep) * NC + jj;
+    if (j < H && q == 0) colcnt[j] = 0;
+    if constexpr (NQ > 1) v4[rep] = (unsigned)__shfl((int)v4[rep], lane_id() & ~(NQ - 1));
+  }
+  const int n = cnts[s];
+  const float4* in = pts + offs[s];
+  const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
+  const float qnan = __int_as_float(0x7fc00000);
+#pragma unroll 1
+  for (int rep = 0; rep < CPL; ++rep) {
+    const int jb = (blockIdx.x * CPL + rep) * NC, j = jb + jj;
+    const bool col = j < H;  // (whole lane groups: NQ divides 64)
+    const unsigned v = rep == 0 ? v4[0] : rep == 1 ? v4[1] : rep == 2 ? v4[2] : v4[3];
+    const unsigned t = v & 0xfffu, pb = (v >> 12) & 0xfffu;
+    const bool owned = (v >> 31) == 0u && t == 1u;  // one band slice, which wrote the column
+    const bool need = v != 0u && !owned;             // contested: rebuilt here
+    const bool incomplete = need && pb != t;         // a band slice touched it without publishing it
+    if (col && q == 0) PWS_STAT(owned ? 2 : v == 0u ? 3 : incomplete ? 5 : 4, 1);
+    const int any_inc = __syncthreads_or(incomplete);
+    const int any_work = __syncthreads_or(col && !owned);
+    if (!any_work) continue;  // (block-uniform)
+    if (tid == 0 && any_inc) PWS_STAT(6, 1);
+    if (any_inc) {  // rare: the block's winners from every point of the scan (exact cells)
+      for (int e = tid; e < NC * VS; e += PC_NT) wl[e] = 0u;
+      __syncthreads();
+      for (int i = tid; i < n; i += PC_NT) {
+        const float3 p3 = buffer_load_f3(rin, (uint32_t)i * 16u);
+        if (!(isfinite_f(p3.x) && isfinite_f(p3.y) && isfinite_f(p3.z))) continue;
+        const int c = proj_cell_exact_ni(P.ang_bottom, P.ang_res_x, P.ang_res_y, V, H, make_float4(p3.x, p3.y, p3.z, 0.f));
+        if (c < 0) continue;
+        const int r = c / H, jc = c - r * H;
+        if (jc >= jb && jc < jb + NC) atomicMax(&wl[(jc - jb) * VS + r], P.wtag | (unsigned)i);
+      }
+      __syncthreads();
+    }
+    const unsigned* W = (const unsigned*)B.winner + (size_t)s * P.VH + (size_t)(col ? j : 0) * V;
+    float3 pk[16];
+    unsigned hm = 0u;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = i0 + u;
+      unsigned w = 0u;
+      if (need && i < V) w = any_inc ? wl[jj * VS + i] : W[i];
+      const bool h = (w & 0xf0000000u) == P.wtag;
+      hm |= (unsigned)h << u;
+      pk[u] = buffer_load_f3(rin, h ? (w & 0x0fffffffu) * 16u : 0xffffffffu);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (!((hm >> u) & 1u)) pk[u] = make_float3(qnan, qnan, qnan);
+    pw_column_emit<NQ>(P, B, s, j, q, col && !owned, pk, hm);
+    if (any_inc) __syncthreads();  // wl is reused by the next pass
+  }
+  if (blockIdx.x == 0 && tid == 0) pw_orient(P, B, s, in);  // findStartEndAngle (:234-249)
+}
+#endif  // LG_PW_SLICE
+
+#ifndef LG_PW_SLICE
 // k_pw_columns: grid (column blocks of PW_NT, scans), one lane per column: the column pass of
 // k_project over the scan's winner image in HBM (each cell read once; entries without this launch's
 // tag are empty cells).  labelComponents' initial state is k_sw_local's.  Block (0, s) settles
 // findStartEndAngle from proj_mm.
-// NQ lanes a column, 16 rows a lane (V <= 16 * NQ): lane q of column j holds rows 16q .. 16q + 15.
-// The pair (16q - 1, 16q) of groundRemoval is settled by lane q with lane q - 1's last point (shuffled
-// up), and its result for row 16q - 1 goes back down; the 2-D scan candidate is the (range, row)
-// minimum over the lanes (the sequential bottom-up scan with a strict `<`).  PC_NT lanes a workgroup
+// NQ lanes a column (pw_column_emit).  PC_NT lanes a workgroup
 // (256; 128 for V <= 16, so that one scan still spreads over many workgroups), PC_NT / NQ columns, the
 // workgroup's columns of the column-major winner image staged in LDS with a
 // (V + 1)-word column stride.  Many small workgroups keep more waves in flight than one lane a column
@@ -597,9 +1043,6 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
   __syncthreads();
   const int n = cnts[s];
   const float4* in = pts + offs[s];
-  float* range = B.range + (size_t)s * VH;
-  float4* cloud = B.cloud + (size_t)s * VH;
-  int8_t* ground = B.ground + (size_t)s * VH;
   const float qnan = __int_as_float(0x7fc00000);
   const __amdgpu_buffer_rsrc_t rin = buffer_rsrc(in, (uint32_t)n * 16u);
   const int jj = tid / NQ, q = tid % NQ, i0 = 16 * q;
@@ -614,79 +1057,13 @@ __global__ __launch_bounds__(PC_NT) void k_pw_columns(LgParams P, LgBufs B, cons
     hm |= (unsigned)h << u;
     pk[u] = buffer_load_f3(rin, h ? (v & 0x0fffffffu) * 16u : 0xffffffffu);
   }
-  const float qnan3 = qnan;
 #pragma unroll
   for (int u = 0; u < 16; ++u)
-    if (!((hm >> u) & 1u)) pk[u] = make_float3(qnan3, qnan3, qnan3);
-  const double jfrac = (double)(float)j / 10000.0;
-  // groundRemoval (:271-285): pair (i-1, i) for 1 <= i <= G marks both rows
-  unsigned gm = 0u;  // bit u: row i0 + u
-  float3 below = make_float3(0.f, 0.f, 0.f);
-  if constexpr (NQ > 1) {
-    below.x = __shfl_up(pk[15].x, 1, NQ);
-    below.y = __shfl_up(pk[15].y, 1, NQ);
-    below.z = __shfl_up(pk[15].z, 1, NQ);
-  }
-  bool down = false;  // pair (i0 - 1, i0) marks row i0 - 1, lane q - 1's last row
-  if (NQ > 1 && q > 0 && i0 <= P.G && col && i0 < V) {
-    const float dX = pk[0].x - below.x, dY = pk[0].y - below.y, dZ = pk[0].z - below.z;
-    if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) {
-      gm |= 1u;
-      down = true;
-    }
-  }
-#pragma unroll
-  for (int u = 1; u < 16; ++u) {
-    const int i = i0 + u;
-    if (col && i < V && i <= P.G) {
-      const float dX = pk[u].x - pk[u - 1].x, dY = pk[u].y - pk[u - 1].y, dZ = pk[u].z - pk[u - 1].z;
-      if (ground_pair(dZ, dX * dX + dY * dY + dZ * dZ, P.mount, P.fp1)) gm |= 3u << (u - 1);
-    }
-  }
-  if constexpr (NQ > 1) {
-    const int dn = __shfl_down((int)down, 1, NQ);
-    if (q + 1 < NQ && dn) gm |= 1u << 15;
-  }
-  float min_range = 1000.f;
-  int id_min = 0x7fffffff;
-  if (col) {
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int i = i0 + u;
-      if (i >= V) continue;
-      const int c = i * H + j;
-      const float3 p = pk[u];
-      const bool h = (hm >> u) & 1u;
-      const float r = h ? sqrtf(p.x * p.x + p.y * p.y + p.z * p.z) : FLT_MAX;
-      st_nt(&range[c], r);
-      st_nt(&cloud[c], make_float4(p.x, p.y, p.z, h ? (float)((double)(float)i + jfrac) : 0.f));  // nanPoint: 0
-      const int g = (int)((gm >> u) & 1u);
-      ground[c] = (int8_t)g;
-      if (g != 1 && (double)p.z > 0.4 && (double)p.z < 1.2 && r < 40.f && r < min_range) {  // 2-D scan (:312-330)
-        min_range = r;
-        id_min = c;
-      }
-    }
-  }
-  if constexpr (NQ > 1) {
-#pragma unroll
-    for (int o = 1; o < NQ; o <<= 1) {
-      const float o_r = __shfl_xor(min_range, o, NQ);
-      const int o_c = __shfl_xor(id_min, o, NQ);
-      if (o_r < min_range || (o_r == min_range && o_c < id_min)) {
-        min_range = o_r;
-        id_min = o_c;
-      }
-    }
-  }
-  if (col && q == 0) B.scan_cand[(size_t)s * H + j] = (min_range < 1000.f) ? id_min : -1;
-  if (blockIdx.x == 0 && tid == 0) {  // findStartEndAngle (:234-249)
-    const int fmin = B.proj_mm[2 * s], fmax = B.proj_mm[2 * s + 1];
-    B.proj_mm[2 * s] = 0x7fffffff;
-    B.proj_mm[2 * s + 1] = -1;
-    proj_orient(P, B, s, in, fmin, fmax);
-  }
+    if (!((hm >> u) & 1u)) pk[u] = make_float3(qnan, qnan, qnan);
+  pw_column_emit<NQ>(P, B, s, j, q, col, pk, hm);
+  if (blockIdx.x == 0 && tid == 0) pw_orient(P, B, s, in);  // findStartEndAngle (:234-249)
 }
+#endif  // !LG_PW_SLICE
 
 // ============================================================================================
 // k_segment: labelComponents as connected components
@@ -4661,6 +5038,7 @@ bool lg_lds_segment(const LgParams& P) {  // k_segment_lds packing
 int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* pts, const int64_t* offs,
                       const int32_t* cnts, hipStream_t st) {
   if (P.wide == 1) {  // (mode 2: the one-workgroup projection, the wide segmentation)
+#ifndef LG_PW_SLICE
     if (S >= 64)
       hipLaunchKernelGGL(k_pw_scatter<4>, dim3((P.max_points + 4 * PW_PTS - 1) / (4 * PW_PTS), S), dim3(PW_NT), 0, st,
                          P, B, pts, offs, cnts);
@@ -4674,6 +5052,30 @@ int lg_launch_project(const LgParams& P, const LgBufs& B, int S, const float4* p
       hipLaunchKernelGGL((k_pw_columns<2, 256>), dim3((P.H + 127) / 128, S), dim3(256), 0, st, P, B, pts, offs, cnts);
     else
       hipLaunchKernelGGL((k_pw_columns<4, 256>), dim3((P.H + 63) / 64, S), dim3(256), 0, st, P, B, pts, offs, cnts);
+#else
+#ifndef LG_PWS_KU
+#define LG_PWS_KU 8
+#endif
+    constexpr int kU = LG_PWS_KU, PS = PWS_NT * kU;
+    const dim3 gs((P.max_points + PS - 1) / PS, S);
+#ifndef LG_PWS_CPL
+#define LG_PWS_CPL 1
+#endif
+    // band columns held: VLP-16's 2,048-point slices span ~100-175 columns, HDL-64E's ~30-40
+    if (P.V <= 16) {
+      hipLaunchKernelGGL((k_pw_slice<kU, 16, 192>), gs, dim3(PWS_NT), 0, st, P, B, pts, offs, cnts);
+      LG_CHECK_LAUNCH();
+      hipLaunchKernelGGL((k_pw_fix<1, 128, LG_PWS_CPL>), dim3((P.H + 128 * LG_PWS_CPL - 1) / (128 * LG_PWS_CPL), S), dim3(128), 0, st, P, B, pts, offs, cnts);
+    } else if (P.V <= 32) {
+      hipLaunchKernelGGL((k_pw_slice<kU, 32, 96>), gs, dim3(PWS_NT), 0, st, P, B, pts, offs, cnts);
+      LG_CHECK_LAUNCH();
+      hipLaunchKernelGGL((k_pw_fix<2, 256, LG_PWS_CPL>), dim3((P.H + 128 * LG_PWS_CPL - 1) / (128 * LG_PWS_CPL), S), dim3(256), 0, st, P, B, pts, offs, cnts);
+    } else {
+      hipLaunchKernelGGL((k_pw_slice<kU, 64, 48>), gs, dim3(PWS_NT), 0, st, P, B, pts, offs, cnts);
+      LG_CHECK_LAUNCH();
+      hipLaunchKernelGGL((k_pw_fix<4, 256, LG_PWS_CPL>), dim3((P.H + 64 * LG_PWS_CPL - 1) / (64 * LG_PWS_CPL), S), dim3(256), 0, st, P, B, pts, offs, cnts);
+    }
+#endif
   } else {  // !wide implies the LDS images fit (lego_batch_set_wide)
     size_t sm = (size_t)(P.VH + 64 + 16 * PQ_CAP) * 4;
     hipLaunchKernelGGL(k_project, dim3(S), dim3(1024), sm, st, P, B, pts, offs, cnts);
@@ -5183,3 +5585,14 @@ extern "C" int lego_debug_prof(uint64_t* out32, int32_t reset) {
   return LEGO_OK;
 }
 #endif  // LG_PROFILE
+
+#ifdef LG_PWS_STATS
+extern "C" int lego_debug_pws_stats(uint64_t* out8, int32_t reset) {
+  if (out8 && hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_pws), 64) != hipSuccess) return LEGO_EDEVICE;
+  if (reset) {
+    uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pws), z, 64) != hipSuccess) return LEGO_EDEVICE;
+  }
+  return LEGO_OK;
+}
+#endif

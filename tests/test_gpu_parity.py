@@ -171,6 +171,8 @@ def test_fast_ground_pair_decides_like_the_exact_path(gpu):
     rr[:64] = 0.0
     dz[64:128] = np.nan
     rr[64:128] = np.nan
+    dz[128:160] = np.nan  # one side of the pair empty
+    rr[160:192] = np.nan
     fp = C.POINTER(C.c_float)
     out = {}
     for which in (5, 6, 9, 10):  # fp_mode 0: fast + exact, exact; fp_mode 1: the same
@@ -729,13 +731,15 @@ def test_edge_inputs(gpu):
         fe.close()
 
 
-def test_projection_input_orders_lds_layout(gpu):
-    """The one-workgroup-a-scan layout (k_project, k_segment_lds) on inputs that are not in firing
-    order: a second sweep over the first (every cell claimed twice, the later point winning), reversed,
-    shuffled and rotated point orders, a ~400 deg sweep, and the edge clouds of test_edge_inputs (which
-    run the single-context, wide layout).  Every stream equals the oracle (projection bit-exact,
-    features, transform).  A projection that writes columns while the input still streams (measured
-    and not kept) must pass this test."""
+@pytest.mark.parametrize("wide", [0, 1])
+def test_projection_input_orders_lds_layout(gpu, wide):
+    """Both layouts (0: k_project, k_segment_lds; 1: k_pw_slice + k_pw_fix, k_sw_*) on inputs that are
+    not in firing order: a second sweep over the first (every cell claimed twice, the later point
+    winning; k_pw_fix's rescan of unpublished contested columns), reversed, shuffled (k_pw_slice's
+    out-of-band slices) and rotated point orders, a ~400 deg sweep (the seam), and the edge clouds of
+    test_edge_inputs.  Every stream equals the oracle (projection bit-exact, features, transform).  A
+    projection that writes columns while the input still streams (measured and not kept)
+    must pass this test."""
     import torch
     params = L.params_vlp16()
     cfg = A.synth_cfg("vlp16")
@@ -767,8 +771,8 @@ def test_projection_input_orders_lds_layout(gpu):
     offs = torch.from_numpy(np.arange(S, dtype=np.int64) * cap).cuda()
     cnts = torch.from_numpy(cnt).cuda()
     b = L.Batch(params, S, cap)
-    b.set_wide(0)
-    assert b.wide() == 0
+    b.set_wide(wide)
+    assert b.wide() == wide
     oracles = [oracle_for(params) for _ in range(S)]
     for k in range(steps):  # the same cloud again: the stale-state path across scans
         b.step(d_pts.data_ptr(), offs.data_ptr(), cnts.data_ptr(), torch.cuda.current_stream().cuda_stream)
