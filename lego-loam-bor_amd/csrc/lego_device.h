@@ -78,7 +78,7 @@ struct LgState {  // FeatureAssociation members that persist across scans (featu
   int pub_copy;          // k_publish stores the lessFlat cloud untransformed (checkSystemInitialization)
   int n_assoc;           // associations run on this stream since the reset (the trajectory record's index)
   int pad_;
-  double quat[4];
+  double quat[4];  // (unused: the odometry quaternion is computed on the host at readback, odom_quat)
   double pos[3];
 };
 

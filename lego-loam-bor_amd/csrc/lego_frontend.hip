@@ -960,6 +960,20 @@ int lego_batch_time_voxel(lego_batch* b, int32_t reps, void* hip_stream, float* 
   return rc;
 }
 
+// publishOdometry's orientation (featureAssociation.cpp:1287-1294): tf::createQuaternionMsgFromRollPitchYaw(
+// transformSum[2], -transformSum[0], -transformSum[1]) in double, then (-y, -z, x, w).  Computed here, on the
+// host with glibc's sin / cos (the reference's own), when the odometry is read back.
+static void odom_quat(const float* sum, double* q4) {
+  const double roll = sum[2], pitch = -(double)sum[0], yaw = -(double)sum[1];
+  const double hy = yaw * 0.5, hp = pitch * 0.5, hr = roll * 0.5;
+  const double cyw = cos(hy), syw = sin(hy), cp = cos(hp), sp = sin(hp), cr = cos(hr), sr = sin(hr);
+  const double qx = sr * cp * cyw - cr * sp * syw;
+  const double qy = cr * sp * cyw + sr * cp * syw;
+  const double qz = cr * cp * syw - sr * sp * cyw;
+  const double qw = cr * cp * cyw + sr * sp * syw;
+  q4[0] = -qy; q4[1] = -qz; q4[2] = qx; q4[3] = qw;
+}
+
 // Header of stream s (counts, orientation, state) into pinned memory, on st, then wait for it.
 struct ReadHdr {
   int32_t cnt[CNT_N];
@@ -1069,7 +1083,7 @@ static int read_assoc(lego_batch* b, int s, const ReadHdr* h, hipStream_t st, le
     o->transform_cur[i] = S.cur[i];
     o->transform_sum[i] = S.sum[i];
   }
-  for (int i = 0; i < 4; ++i) o->odom_orientation[i] = S.quat[i];
+  odom_quat(S.sum, o->odom_orientation);
   for (int i = 0; i < 3; ++i) o->odom_position[i] = S.pos[i];
   o->lm_iter_surf = S.iters_surf;
   o->lm_iter_corner = S.iters_corner;
@@ -1319,7 +1333,7 @@ int pack_assoc(lego_ctx* c, lego_association_out* o) {
     o->transform_cur[i] = S.cur[i];
     o->transform_sum[i] = S.sum[i];
   }
-  for (int i = 0; i < 4; ++i) o->odom_orientation[i] = S.quat[i];
+  odom_quat(S.sum, o->odom_orientation);
   for (int i = 0; i < 3; ++i) o->odom_position[i] = S.pos[i];
   o->lm_iter_surf = S.iters_surf;
   o->lm_iter_corner = S.iters_corner;

@@ -4969,14 +4969,9 @@ void k_lm(LgParams P, LgBufs B) {
     float tz = (T)sum[5] - (-sry_ * (T)x2 + cry_ * (T)z2);
     sum[0] = rx; sum[1] = ry; sum[2] = rz; sum[3] = tx; sum[4] = ty; sum[5] = tz;
     for (int k = 0; k < 6; ++k) S.cur[k] = L.cur[k];
-    double roll = sum[2], pitch = -(double)sum[0], yaw = -(double)sum[1];
-    double hy = yaw * 0.5, hp = pitch * 0.5, hr = roll * 0.5;
-    double cyw = cos(hy), syw = sin(hy), cp = cos(hp), sp = sin(hp), cr = cos(hr), sr = sin(hr);
-    double qx = sr * cp * cyw - cr * sp * syw;
-    double qy = cr * sp * cyw + sr * cp * syw;
-    double qz = cr * cp * syw - sr * sp * cyw;
-    double qw = cr * cp * cyw + sr * sp * syw;
-    S.quat[0] = -qy; S.quat[1] = -qz; S.quat[2] = qx; S.quat[3] = qw;
+    // publishOdometry's quaternion (:1287-1294, tf::createQuaternionMsgFromRollPitchYaw in double) is
+    // computed from transformSum on the host when the odometry is read (lego_frontend.hip odom_quat, glibc's
+    // sin / cos): six inlined double sin / cos here set k_lm's register peak (177 VGPRs)
     S.pos[0] = sum[3]; S.pos[1] = sum[4]; S.pos[2] = sum[5];
     S.iters_surf = it_s;
     S.iters_corner = it_c;

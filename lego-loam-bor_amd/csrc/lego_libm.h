@@ -10,8 +10,13 @@
 #ifdef __HIPCC__
 #include <hip/hip_runtime.h>
 #define LG_LIBM __host__ __device__ __forceinline__
+// Out of line (one copy a translation unit): the large-argument fallbacks, never taken for an LM angle.
+// Inlined, OCML's double sin / cos (Payne-Hanek reduction) set the register peak of every kernel that
+// evaluates a float sin / cos (k_lm: 177 VGPRs).
+#define LG_LIBM_COLD static __host__ __device__ __attribute__((noinline))
 #else
 #define LG_LIBM inline
+#define LG_LIBM_COLD static inline
 #endif
 
 namespace lg {
@@ -179,6 +184,10 @@ LG_LIBM double sincos_reduce(double x, int& n) {
   n = ((int32_t)r + 0x800000) >> 24;
   return __builtin_fma(-(double)n, 0x1.921fb54442d18p0, x);
 }
+LG_LIBM_COLD float sinf_big(float y) { return (float)sin((double)y); }
+LG_LIBM_COLD float cosf_big(float y) { return (float)cos((double)y); }
+LG_LIBM_COLD double sin_big(double x) { return sin(x); }
+LG_LIBM_COLD double cos_big(double x) { return cos(x); }
 LG_LIBM float sinf_g(float y) {
   const double x = (double)y;
   if (abstop12(y) < abstop12(0x1.921fb6p-1f)) {
@@ -191,7 +200,7 @@ LG_LIBM float sinf_g(float y) {
     const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;  // sign[] = {1, -1, -1, 1}
     return sincos_poly(r * sg, r * r, sincos_tab((n & 2) != 0), n);
   }
-  return (float)sin(x);
+  return sinf_big(y);
 }
 LG_LIBM float cosf_g(float y) {
   const double x = (double)y;
@@ -205,7 +214,7 @@ LG_LIBM float cosf_g(float y) {
     const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
     return sincos_poly(r * sg, r * r, sincos_tab((n & 2) != 0), n ^ 1);
   }
-  return (float)cos(x);
+  return cosf_big(y);
 }
 
 LG_LIBM bool isfinite_f(float x) { return (fbits(x) & 0x7f800000u) != 0x7f800000u; }
@@ -297,7 +306,7 @@ LG_LIBM double sin_d(double x) {  // s_sin.c
   const int32_t ix = dhi(x) & 0x7fffffff;
   if (ix <= 0x3fe921fb) return ksin_d(x, 0.0, 0);
   if (ix >= 0x7ff00000) return x - x;
-  if (ix >= 0x413921fb) return sin(x);  // |x| >= 2^20 * pi/2: never an angle here
+  if (ix >= 0x413921fb) return sin_big(x);  // |x| >= 2^20 * pi/2: never an angle here
   double y0, y1;
   const int n = rem_pio2_d(x, y0, y1);
   switch (n & 3) {
@@ -311,7 +320,7 @@ LG_LIBM double cos_d(double x) {  // s_cos.c
   const int32_t ix = dhi(x) & 0x7fffffff;
   if (ix <= 0x3fe921fb) return kcos_d(x, 0.0);
   if (ix >= 0x7ff00000) return x - x;
-  if (ix >= 0x413921fb) return cos(x);
+  if (ix >= 0x413921fb) return cos_big(x);
   double y0, y1;
   const int n = rem_pio2_d(x, y0, y1);
   switch (n & 3) {
