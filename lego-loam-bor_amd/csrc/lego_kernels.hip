@@ -3839,7 +3839,7 @@ LG_DEVICE void qr_solve3(const float* A_in, const float* b_in, float* x) {
   }
 }
 
-LG_DEVICE double eig_max_sym3(const float* Af) {
+__device__ __attribute__((noinline)) double eig_max_sym3(const float* Af) {  // (cold: out of line)
   double a[3][3];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) a[i][j] = Af[i * 3 + j];
@@ -4208,7 +4208,7 @@ LG_DEVICE int grid_nn(const Lds& L, const int* gcell, const float4* __restrict__
 // One wave: the reference's ring-limited linear scans for the 2nd (and 3rd) correspondence around
 // the accepted nearest neighbour `closest` (fa.cpp:514-564, 652-713).  surf = plane (3 points),
 // else line (2 points).
-LG_DEVICE void ring_scans(const LgParams& P, const float4* __restrict__ last, int nl, float4 sel, int fwd_bound,
+__device__ __attribute__((noinline)) void ring_scans(const LgParams& P, const float4* __restrict__ last, int nl, float4 sel, int fwd_bound,
                           bool surf, int closest, int& o2, int& o3, int& status) {
   const int lane = lane_id();
   o2 = -1; o3 = -1;
@@ -4870,6 +4870,38 @@ LG_DEVICE void lm_record(const LgParams& P, const LgBufs& B, int s, LgState& S) 
 // (295.6k -> 307.9k, two pairs) although k_lm alone is 5 % slower (0.53 -> 0.56 ms).  With fewer scans (C5's 80
 // sequences: 157.4k -> 148.1k) the LM's own speed counts and kWpe stays 1.  (The compiler drops a request the
 // block's own LDS makes unreachable: 5 for this layout, 4 for 768 threads.)
+// integrateTransformation (:1241-1270): transformSum from transformCur (AccumulateRotation :474-500)
+template <bool kF1>
+__device__ __attribute__((noinline)) void integrate_transformation(const float* cur, float* sum) {
+  typedef Fp<kF1> F;
+  typedef typename F::T T;
+  float cx = sum[0], cy = sum[1], cz = sum[2], lx = -cur[0], ly = -cur[1], lz = -cur[2];
+  // AccumulateRotation (:474-500)
+  const T clx = F::cs(lx), slx = F::sn(lx), cly = F::cs(ly), sly = F::sn(ly), clz = F::cs(lz), slz = F::sn(lz);
+  const T ccx = F::cs(cx), scx = F::sn(cx), ccy = F::cs(cy), scy = F::sn(cy), ccz = F::cs(cz), scz = F::sn(cz);
+  float srx = clx * ccx * sly * scz - ccx * ccz * slx - clx * cly * scx;
+  float ox = -F::as(srx);
+  float srycrx = slx * (ccy * scz - ccz * scx * scy) + clx * sly * (ccy * ccz + scx * scy * scz) + clx * cly * ccx * scy;
+  float crycrx = clx * cly * ccx * ccy - clx * sly * (ccz * scy - ccy * scx * scz) - slx * (scy * scz + ccy * ccz * scx);
+  const T cox = F::cs(ox);
+  float oy = F::at2((T)srycrx / cox, (T)crycrx / cox);
+  float srzcrx = scx * (clz * sly - cly * slx * slz) + ccx * scz * (cly * clz + slx * sly * slz) + clx * ccx * ccz * slz;
+  float crzcrx = clx * clz * ccx * ccz - ccx * scz * (cly * slz - clz * slx * sly) - scx * (sly * slz + cly * clz * slx);
+  float oz = F::at2((T)srzcrx / cox, (T)crzcrx / cox);
+  float rx = ox, ry = oy, rz = oz;
+  const T crz_ = F::cs(rz), srz_ = F::sn(rz), crx_ = F::cs(rx), srx_ = F::sn(rx), cry_ = F::cs(ry), sry_ = F::sn(ry);
+  float x1 = crz_ * (T)(cur[3]) - srz_ * (T)(cur[4]);
+  float y1 = srz_ * (T)(cur[3]) + crz_ * (T)(cur[4]);
+  float z1 = cur[5];
+  float x2 = x1;
+  float y2 = crx_ * (T)y1 - srx_ * (T)z1;
+  float z2 = srx_ * (T)y1 + crx_ * (T)z1;
+  float tx = (T)sum[3] - (cry_ * (T)x2 + sry_ * (T)z2);
+  float ty = sum[4] - y2;
+  float tz = (T)sum[5] - (-sry_ * (T)x2 + cry_ * (T)z2);
+  sum[0] = rx; sum[1] = ry; sum[2] = rz; sum[3] = tx; sum[4] = ty; sum[5] = tz;
+}
+
 template <int kNT, int kMaxQ, bool kF1, int kWpe>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kWpe)))
 void k_lm(LgParams P, LgBufs B) {
@@ -4937,42 +4969,15 @@ void k_lm(LgParams P, LgBufs B) {
     PROF_ADD(18, t_lc0);
   }
   __syncthreads();
-  // integrateTransformation (:1241-1270) + publishOdometry (:1286-1298)
+  // integrateTransformation (:1241-1270) + publishOdometry (:1286-1298), thread 0 (out of line: one lane's
+  // chain of libm calls, which inlined set the kernel's register peak)
   if (tid == 0) {
-    typedef Fp<kF1> F;
-    typedef typename F::T T;
-    const float* cur = L.cur;
-    float* sum = S.sum;
-    float cx = sum[0], cy = sum[1], cz = sum[2], lx = -cur[0], ly = -cur[1], lz = -cur[2];
-    // AccumulateRotation (:474-500)
-    const T clx = F::cs(lx), slx = F::sn(lx), cly = F::cs(ly), sly = F::sn(ly), clz = F::cs(lz), slz = F::sn(lz);
-    const T ccx = F::cs(cx), scx = F::sn(cx), ccy = F::cs(cy), scy = F::sn(cy), ccz = F::cs(cz), scz = F::sn(cz);
-    float srx = clx * ccx * sly * scz - ccx * ccz * slx - clx * cly * scx;
-    float ox = -F::as(srx);
-    float srycrx = slx * (ccy * scz - ccz * scx * scy) + clx * sly * (ccy * ccz + scx * scy * scz) + clx * cly * ccx * scy;
-    float crycrx = clx * cly * ccx * ccy - clx * sly * (ccz * scy - ccy * scx * scz) - slx * (scy * scz + ccy * ccz * scx);
-    const T cox = F::cs(ox);
-    float oy = F::at2((T)srycrx / cox, (T)crycrx / cox);
-    float srzcrx = scx * (clz * sly - cly * slx * slz) + ccx * scz * (cly * clz + slx * sly * slz) + clx * ccx * ccz * slz;
-    float crzcrx = clx * clz * ccx * ccz - ccx * scz * (cly * slz - clz * slx * sly) - scx * (sly * slz + cly * clz * slx);
-    float oz = F::at2((T)srzcrx / cox, (T)crzcrx / cox);
-    float rx = ox, ry = oy, rz = oz;
-    const T crz_ = F::cs(rz), srz_ = F::sn(rz), crx_ = F::cs(rx), srx_ = F::sn(rx), cry_ = F::cs(ry), sry_ = F::sn(ry);
-    float x1 = crz_ * (T)(cur[3]) - srz_ * (T)(cur[4]);
-    float y1 = srz_ * (T)(cur[3]) + crz_ * (T)(cur[4]);
-    float z1 = cur[5];
-    float x2 = x1;
-    float y2 = crx_ * (T)y1 - srx_ * (T)z1;
-    float z2 = srx_ * (T)y1 + crx_ * (T)z1;
-    float tx = (T)sum[3] - (cry_ * (T)x2 + sry_ * (T)z2);
-    float ty = sum[4] - y2;
-    float tz = (T)sum[5] - (-sry_ * (T)x2 + cry_ * (T)z2);
-    sum[0] = rx; sum[1] = ry; sum[2] = rz; sum[3] = tx; sum[4] = ty; sum[5] = tz;
+    integrate_transformation<kF1>(L.cur, S.sum);
     for (int k = 0; k < 6; ++k) S.cur[k] = L.cur[k];
     // publishOdometry's quaternion (:1287-1294, tf::createQuaternionMsgFromRollPitchYaw in double) is
     // computed from transformSum on the host when the odometry is read (lego_frontend.hip odom_quat, glibc's
-    // sin / cos): six inlined double sin / cos here set k_lm's register peak (177 VGPRs)
-    S.pos[0] = sum[3]; S.pos[1] = sum[4]; S.pos[2] = sum[5];
+    // sin / cos)
+    S.pos[0] = S.sum[3]; S.pos[1] = S.sum[4]; S.pos[2] = S.sum[5];
     S.iters_surf = it_s;
     S.iters_corner = it_c;
   }
