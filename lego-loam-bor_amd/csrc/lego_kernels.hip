@@ -1210,6 +1210,10 @@ LG_DEVICE float ori_branch2(float ori, float eo) {
 // i <= h, so a tile before h's tile is all branch 1 and one after it all branch 2.  Loads are
 // unconditional (index clamped) and issued together.  Block-uniform; scratch >= 16 ints.
 #define FP_U 8
+// fp_mode 1's orientation, (float)(-atan2(double y, double x)): out of line (one copy) — inlined FP_U times, the
+// double atan2 restatement set the register peak of k_sw_finish / k_segment_lds (38 / 18 VGPRs spilled) in
+// either mode
+__device__ __attribute__((noinline)) float neg_atan2_d(float y, float x) { return (float)(-atan2_d((double)y, (double)x)); }
 LG_DEVICE void distort_segmented(const LgParams& P, const LgBufs& B, int s, int M, int* scratch) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const float so = B.orient[s * 4 + 0], eo = B.orient[s * 4 + 1], od = B.orient[s * 4 + 2];
@@ -1223,7 +1227,7 @@ LG_DEVICE void distort_segmented(const LgParams& P, const LgBufs& B, int s, int 
     for (int u = 0; u < FP_U; ++u) pk[u] = seg[min(t0 + u * nt + tid, M - 1)];
 #pragma unroll
     for (int u = 0; u < FP_U; ++u)  // float ori = -atan2(point.x, point.z): point.x = y, point.z = x (:172)
-      ori[u] = P.fp1 ? (float)(-atan2_d((double)pk[u].y, (double)pk[u].x)) : -atan2f_g(pk[u].y, pk[u].x);
+      ori[u] = P.fp1 ? neg_atan2_d(pk[u].y, pk[u].x) : -atan2f_g(pk[u].y, pk[u].x);
     if (h == 0x7fffffff) {
       int hc = 0x7fffffff;
 #pragma unroll
