@@ -4867,13 +4867,6 @@ LG_DEVICE void lm_record(const LgParams& P, const LgBufs& B, int s, LgState& S) 
   S.n_assoc++;
 }
 
-// kWpe: waves a SIMD the compiler budgets registers for.  With more than half a scan a CU in flight the VLP-16
-// layout (512 threads, two waves a SIMD) runs at 4 (128 VGPRs, 49-66 spilled to scratch): 2 x 128 of a SIMD's 512
-// registers leave room for two VoxelGrid waves (105 VGPRs) beside it instead of one (177 VGPRs a wave otherwise):
-// +0.9 % C3 order 0 in the pipeline (238.1k -> 240.3k scans/s, three A/B pairs on one box), +4.2 % order 1
-// (295.6k -> 307.9k, two pairs) although k_lm alone is 5 % slower (0.53 -> 0.56 ms).  With fewer scans (C5's 80
-// sequences: 157.4k -> 148.1k) the LM's own speed counts and kWpe stays 1.  (The compiler drops a request the
-// block's own LDS makes unreachable: 5 for this layout, 4 for 768 threads.)
 // integrateTransformation (:1241-1270): transformSum from transformCur (AccumulateRotation :474-500)
 template <bool kF1>
 __device__ __attribute__((noinline)) void integrate_transformation(const float* cur, float* sum) {
@@ -4906,6 +4899,14 @@ __device__ __attribute__((noinline)) void integrate_transformation(const float* 
   sum[0] = rx; sum[1] = ry; sum[2] = rz; sum[3] = tx; sum[4] = ty; sum[5] = tz;
 }
 
+// kWpe: waves a SIMD the compiler budgets registers for.  With more than half a scan a CU in flight the VLP-16
+// layout (512 threads, two waves a SIMD) runs at 4 (128 VGPRs; 49-66 spilled to scratch in round 5, 11-12
+// since round 6's out-of-line cold paths): 2 x 128 of a SIMD's 512 registers leave room for two VoxelGrid
+// waves (105 VGPRs) beside it instead of one (155 VGPRs a wave otherwise, 177 in round 5): +0.9 % C3 order 0
+// in the pipeline (238.1k -> 240.3k scans/s, three A/B pairs on one box), +4.2 % order 1 (295.6k -> 307.9k,
+// two pairs) although k_lm alone is 5 % slower (0.53 -> 0.56 ms).  With fewer scans (C5's 80 sequences:
+// 157.4k -> 148.1k) the LM's own speed counts: kWpe 1 and, since round 6, 1,024 threads (lg_launch_lm).  (The
+// compiler drops a request the block's own LDS makes unreachable: 5 for this layout, 4 for 768 threads.)
 template <int kNT, int kMaxQ, bool kF1, int kWpe>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kWpe)))
 void k_lm(LgParams P, LgBufs B) {
@@ -5171,20 +5172,23 @@ int lg_launch_concat(const LgParams& P, const LgBufs& B, int S, hipStream_t st) 
 }
 
 int lg_launch_lm(const LgParams& P, const LgBufs& B, int S, hipStream_t st) {
-  // VLP-16-sized feature sets (<= 384 queries a loop) with many scans in flight: 512 threads and 66 KB
-  // of LDS leave room on the CU for the next scan's small front-end kernels (256 VLP-16 streams: k_lm
-  // 553 -> 515 us, +4 % scans/s).  Few scans in flight (one scan: 2-3 % lower latency) and larger
-  // sensors keep 768 threads (and LDS for 1,536 queries).
-  const bool small = P.V * std::max(P.cap_sharp, P.cap_flat) <= 384 && S > 8;
-  const bool cap = 2 * S > P.ncu;  // more than half a scan a CU: share SIMDs with VoxelGrid waves (k_lm's kWpe)
-  if (small && cap && !P.fp1)
+  // VLP-16-sized feature sets (<= 384 queries a loop):
+  //  * more than half a scan a CU in flight (C3's 256 streams): 512 threads compiled for four waves a SIMD
+  //    (128 VGPRs, 68 KB of LDS), so two VoxelGrid waves share each of its SIMDs;
+  //  * fewer (C5's shards, one scan in flight): each scan's LM latency sets the step, so 1,024 threads a
+  //    scan — twice the waves for the per-query ring scans, searches and grid builds (round 6: +7-10 % at
+  //    10-80 streams; 512 threads measured 0.581 vs 0.539 ms a step at 10 streams).
+  // Larger sensors keep 768 threads and LDS for 1,536 queries.
+  const bool vlp = P.V * std::max(P.cap_sharp, P.cap_flat) <= 384;
+  const bool cap = 2 * S > P.ncu;
+  if (vlp && cap && !P.fp1)
     hipLaunchKernelGGL((k_lm<512, 384, false, 4>), dim3(S), dim3(512), 0, st, P, B);
-  else if (small && cap)
+  else if (vlp && cap)
     hipLaunchKernelGGL((k_lm<512, 384, true, 4>), dim3(S), dim3(512), 0, st, P, B);
-  else if (small && !P.fp1)
-    hipLaunchKernelGGL((k_lm<512, 384, false, 1>), dim3(S), dim3(512), 0, st, P, B);
-  else if (small)
-    hipLaunchKernelGGL((k_lm<512, 384, true, 1>), dim3(S), dim3(512), 0, st, P, B);
+  else if (vlp && !P.fp1)
+    hipLaunchKernelGGL((k_lm<1024, 384, false, 1>), dim3(S), dim3(1024), 0, st, P, B);
+  else if (vlp)
+    hipLaunchKernelGGL((k_lm<1024, 384, true, 1>), dim3(S), dim3(1024), 0, st, P, B);
   else if (!P.fp1)
     hipLaunchKernelGGL((k_lm<768, 1536, false, 1>), dim3(S), dim3(768), 0, st, P, B);
   else
