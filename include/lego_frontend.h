@@ -20,6 +20,7 @@
 #ifndef LEGO_FRONTEND_H
 #define LEGO_FRONTEND_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -203,6 +204,19 @@ int  lego_batch_set_trajectory(lego_batch* b, float* d_traj, int32_t max_scans);
 int  lego_batch_read_counts(lego_batch* b, int32_t* out);
 /* Reset every stream to the freshly constructed state (systemInitedLM = false, transforms 0). */
 int  lego_batch_reset(lego_batch* b);
+/* Checkpoint / resume of stream s (shard warm-start, restart after a failure): the FeatureAssociation state one
+ * scan leaves for the next (featureAssociation.h:70-115: transformCur / transformSum, systemInitedLM,
+ * isDegenerate, the cycle count, the Last clouds and the kd-trees' staleness, the odometry) plus the
+ * persistent curvature / picked / label / smoothness vectors whose stale entries the next scan reads, in
+ * lego_batch_state_size bytes of host memory.  Save flushes the pending publish / LM first; load requires the
+ * same sensor layout (V, H, cap_lsharp; else LEGO_EINVAL) and may target another stream or batch.  A stream
+ * loaded from a checkpoint continues exactly as the saved stream would. */
+int  lego_batch_state_size(const lego_batch* b, size_t* bytes);
+int  lego_batch_save_state(lego_batch* b, int32_t s, void* host, size_t bytes);
+int  lego_batch_load_state(lego_batch* b, int32_t s, const void* host, size_t bytes);
+int  lego_ctx_state_size(const lego_ctx* ctx, size_t* bytes);
+int  lego_ctx_save_state(lego_ctx* ctx, void* host, size_t bytes);
+int  lego_ctx_load_state(lego_ctx* ctx, const void* host, size_t bytes);
 /* Kernel timing of the last step (ms, hipEvents on the step's stream, the pipelined path itself):
  * [0] project, [1] segment + distortion, [2] smoothness + occlusion, [3] feature extraction,
  * [4] concat + the pending lessFlat publish, [5] LM (of the previous scan with lag 1; the VoxelGrid

@@ -12,6 +12,7 @@
 #include <cfloat>
 #include <cstdlib>
 #include <new>
+#include <utility>
 #include <vector>
 
 #include "../../include/lego_frontend.h"
@@ -670,6 +671,96 @@ static int flush_pending(lego_batch* b) {
   }
   b->pend_pub = b->pend_lm = false;
   return LEGO_OK;
+}
+
+// ---- checkpoint / resume of one stream's FeatureAssociation state (featureAssociation.h:70-115) ----------
+// What one scan leaves for the next: LgState (transformCur / transformSum, systemInitedLM, isDegenerate, the
+// cycle count, the Last clouds' half and sizes, the kd-trees' staleness, the odometry), the initialisation
+// count of the front end (fe_state[1], adjustOutlierCloud's switch), both halves of the Last clouds, and the
+// persistent curvature / picked / label / smoothness vectors whose stale entries the next scan reads (SURVEY
+// App. B).  Everything else a step writes is rewritten by the next step.  k_extract's first-pass flag
+// (fp_sync) is reset by a load: it is compared with the loading batch's own launch epochs.
+struct LgCkptHdr {
+  uint32_t magic, version;
+  int32_t V, H, cap_lsharp, state_bytes;
+};
+static const uint32_t kCkptMagic = 0x4b43474cu;  // "LGCK"
+static size_t ckpt_bytes(const LgParams& P) {
+  const size_t VH = P.VH, cl = (size_t)P.V * P.cap_lsharp;
+  return sizeof(LgCkptHdr) + sizeof(LgState) + sizeof(int32_t) + 2 * cl * sizeof(float4) + 2 * VH * sizeof(float4) +
+         VH * (sizeof(float) + 1 + 1 + sizeof(int2));
+}
+
+int lego_batch_state_size(const lego_batch* b, size_t* bytes) {
+  if (!b || !bytes) return LEGO_EINVAL;
+  *bytes = ckpt_bytes(b->P);
+  return LEGO_OK;
+}
+
+// The stream's pieces in checkpoint order: (device pointer, bytes).
+static void ckpt_pieces(lego_batch* b, int s, std::vector<std::pair<void*, size_t>>& out) {
+  const LgParams& P = b->P;
+  const LgBufs& B = b->B;
+  const size_t VH = P.VH, cl = (size_t)P.V * P.cap_lsharp;
+  out.clear();
+  out.push_back({B.state + s, sizeof(LgState)});
+  out.push_back({B.fe_state + 2 * (size_t)s + 1, sizeof(int32_t)});
+  out.push_back({B.corner_last + (size_t)s * 2 * cl, 2 * cl * sizeof(float4)});
+  out.push_back({B.surf_last + (size_t)s * 2 * VH, 2 * VH * sizeof(float4)});
+  out.push_back({B.curv + (size_t)s * VH, VH * sizeof(float)});
+  out.push_back({B.picked + (size_t)s * VH, VH});
+  out.push_back({B.flabel + (size_t)s * VH, VH});
+  out.push_back({B.smooth + (size_t)s * VH, VH * sizeof(int2)});
+}
+
+int lego_batch_save_state(lego_batch* b, int32_t s, void* host, size_t bytes) {
+  if (!b || !host || s < 0 || s >= b->S || bytes < ckpt_bytes(b->P)) return LEGO_EINVAL;
+  if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
+  int rc = flush_pending(b);  // the stream's last scan published (its Last clouds, LgState)
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  LgCkptHdr h{kCkptMagic, 1u, b->P.V, b->P.H, b->P.cap_lsharp, (int32_t)sizeof(LgState)};
+  char* o = (char*)host;
+  memcpy(o, &h, sizeof(h));
+  o += sizeof(h);
+  std::vector<std::pair<void*, size_t>> pc;
+  ckpt_pieces(b, s, pc);
+  for (auto& q : pc) {
+    if (hipMemcpy(o, q.first, q.second, hipMemcpyDeviceToHost) != hipSuccess) return LEGO_EDEVICE;
+    o += q.second;
+  }
+  return LEGO_OK;
+}
+
+int lego_batch_load_state(lego_batch* b, int32_t s, const void* host, size_t bytes) {
+  if (!b || !host || s < 0 || s >= b->S || bytes < ckpt_bytes(b->P)) return LEGO_EINVAL;
+  LgCkptHdr h;
+  memcpy(&h, host, sizeof(h));
+  if (h.magic != kCkptMagic || h.version != 1u || h.V != b->P.V || h.H != b->P.H || h.cap_lsharp != b->P.cap_lsharp ||
+      h.state_bytes != (int32_t)sizeof(LgState))
+    return LEGO_EINVAL;  // another sensor layout or library version
+  if (hipSetDevice(b->device) != hipSuccess) return LEGO_EDEVICE;
+  int rc = flush_pending(b);  // no kernel of this batch may still write the stream
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  const char* o = (const char*)host + sizeof(h);
+  std::vector<std::pair<void*, size_t>> pc;
+  ckpt_pieces(b, s, pc);
+  for (auto& q : pc) {
+    if (hipMemcpy(q.first, o, q.second, hipMemcpyHostToDevice) != hipSuccess) return LEGO_EDEVICE;
+    o += q.second;
+  }
+  if (hipMemset(b->B.fp_sync + 2 * (size_t)s, 0, 2 * sizeof(int32_t)) != hipSuccess) return LEGO_EDEVICE;
+  if (hipDeviceSynchronize() != hipSuccess) return LEGO_EDEVICE;
+  return LEGO_OK;
+}
+
+int lego_ctx_state_size(const lego_ctx* c, size_t* bytes) { return c ? lego_batch_state_size(c->b, bytes) : LEGO_EINVAL; }
+int lego_ctx_save_state(lego_ctx* c, void* host, size_t bytes) {
+  return c ? lego_batch_save_state(c->b, 0, host, bytes) : LEGO_EINVAL;
+}
+int lego_ctx_load_state(lego_ctx* c, const void* host, size_t bytes) {
+  return c ? lego_batch_load_state(c->b, 0, host, bytes) : LEGO_EINVAL;
 }
 
 int lego_batch_set_groups(lego_batch* b, int32_t groups) {

@@ -91,6 +91,12 @@ def lib():
         L.lego_batch_wide.argtypes = [C.c_void_p]
         L.lego_batch_lag.argtypes = [C.c_void_p]
         L.lego_batch_read_counts.argtypes = [C.c_void_p, P(C.c_int32)]
+        L.lego_batch_state_size.argtypes = [C.c_void_p, P(C.c_size_t)]
+        L.lego_batch_save_state.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_size_t]
+        L.lego_batch_load_state.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_size_t]
+        L.lego_ctx_state_size.argtypes = [C.c_void_p, P(C.c_size_t)]
+        L.lego_ctx_save_state.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.lego_ctx_load_state.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.lego_test_sort.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_int32, C.c_int32]
         L.lego_test_libm.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_int32, C.c_int32]
         L.lego_test_project_cells.argtypes = [P(LegoParams), P(C.c_float), C.c_int32, P(C.c_int32), P(C.c_int32)]
@@ -150,6 +156,19 @@ def device_count():
     return int(lib().lego_device_count())
 
 
+def _save_state(size_fn, save_fn, h, *s):
+    n = C.c_size_t()
+    _check(size_fn(h, C.byref(n)), "state_size")
+    buf = np.zeros(n.value, np.uint8)
+    _check(save_fn(h, *s, buf.ctypes.data, n.value), "save_state")
+    return buf.tobytes()
+
+
+def _load_state(load_fn, h, data, *s):
+    buf = np.frombuffer(bytes(data), np.uint8).copy()
+    _check(load_fn(h, *s, buf.ctypes.data, buf.size), "load_state")
+
+
 class Frontend:
     """One sequence on one GPU: the drop-in for the reference's ImageProjection + FeatureAssociation."""
 
@@ -190,6 +209,14 @@ class Frontend:
             _check(lib().lego_feature_association_from(self.h, C.byref(pin), C.byref(out)),
                    "lego_feature_association_from")
         return association_to_dict(out)
+
+    def save_state(self):
+        """Checkpoint of the sequence's FeatureAssociation state (lego_ctx_save_state) as bytes."""
+        return _save_state(lib().lego_ctx_state_size, lib().lego_ctx_save_state, self.h)
+
+    def load_state(self, data):
+        """Resume from a checkpoint (lego_ctx_load_state); the next scans continue as the saved sequence's."""
+        _load_state(lib().lego_ctx_load_state, self.h, data)
 
     def set_lm_state(self, transform_cur, transform_sum, degenerate, corner_last, surf_last, tree_stale):
         """Test hook (lego_test_set_lm_state): the LM state the next association starts from."""
@@ -235,6 +262,14 @@ class Batch:
 
     def reset(self):
         _check(lib().lego_batch_reset(self.h), "lego_batch_reset")
+
+    def save_state(self, s):
+        """Checkpoint of stream s's FeatureAssociation state (lego_batch_save_state) as bytes."""
+        return _save_state(lib().lego_batch_state_size, lib().lego_batch_save_state, self.h, C.c_int32(int(s)))
+
+    def load_state(self, s, data):
+        """Stream s resumes from a checkpoint (lego_batch_load_state; any stream of a batch of the same sensor)."""
+        _load_state(lib().lego_batch_load_state, self.h, data, C.c_int32(int(s)))
 
     def set_timing(self, on=True):
         _check(lib().lego_batch_set_timing(self.h, 1 if on else 0), "lego_batch_set_timing")
