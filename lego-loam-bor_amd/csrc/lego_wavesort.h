@@ -117,8 +117,14 @@ LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
   V tv = val[min(max(tl - 1, 0), len)];
   unsigned long long tanc = 0ull;  // in-register ancestors below the root
   for (int j = tl >> 1; j >= 2; j >>= 1) tanc |= 1ull << j;
-  const bool todd = (tl & 1) != 0, ttop = tl >= 2;
   const int c0 = 2 * tl;  // children lanes c0, c0 + 1 (lanes < 32)
+  // The sibling tests as masks: a right child (odd lane, top, window and level 6 alike) wins unless
+  // right < left, a left one iff left < right -- two compares straight into scalar masks and scalar
+  // logic, then one 64-bit compare a lane against its ancestors-and-self mask -- instead of per-lane
+  // boolean arithmetic (with the block-stored roots: the heaviest ring's heap pops 1.46 M -> 1.30 M cycles,
+  // profiles/r06_heap_masks_ab.txt).
+  const unsigned long long kOdd = 0xAAAAAAAAAAAAAAAAull, kTop = ~3ull;
+  const unsigned long long tself = tanc | (1ull << tl);
   if (len >= 127) {
     // Heaps of 128 or more: levels 0-5 (nodes 0-62) stay in registers while the heap is at least that
     // large, node t in lane t + 1 (so lane l's children are lanes 2l, 2l + 1 and siblings share a DPP pair);
@@ -127,8 +133,16 @@ LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
     // permute) and the window's writes.  The pop's value a[len] is read one pop ahead: the pop before can
     // only change it by ending its hole there (a[len] is the last leaf), and then it is that pop's value.
     const bool wlane = lane < 62;
+    const unsigned long long kWin = (1ull << 62) - 1ull;
+    const unsigned long long wself = anc | (1ull << lane);
     K nvk = key[len];
     V nvv = val[len];
+    // The popped roots are kept a 64-slot block at a time (slot 64 q + l in lane l) and stored one block
+    // at once: no pop reads a slot above its heap, so a slot's store can wait (a whole-wave store per
+    // 64 pops instead of a one-lane store a pop).
+    const int top_len = len;
+    K ok = nvk;
+    V ov = nvv;
     for (; len >= 127; --len) {
       const K vk = nvk;  // the pop's value; the root goes to its slot
       const V vv = nvv;
@@ -136,14 +150,20 @@ LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
       nvv = val[len - 1];
       const K rk = rdlane(tk, 1);
       const V rv = (V)__builtin_amdgcn_readlane((int)tv, 1);
-      if (lane == 0) { key[len] = rk; val[len] = rv; }
+      const bool mine = lane == (len & 63);
+      ok = mine ? rk : ok;
+      ov = mine ? rv : ov;
+      if ((len & 63) == 0 && len + lane <= top_len) {  // block [len, len + 63] complete
+        key[len + lane] = ok;
+        val[len + lane] = ov;
+      }
       // path through levels 1..5 (right unless right < left, as __adjust_heap)
       const K ts = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, tk), 0xb1, 0xf, 0xf, false));
-      const bool twin = ttop & ((todd & !(tk < ts)) | (!todd & (ts < tk)));
-      const unsigned long long TW = __builtin_amdgcn_ballot_w64(twin);
-      const bool tonp = twin & ((TW & tanc) == tanc);
-      const unsigned long long TP = __builtin_amdgcn_ballot_w64(tonp);
-      const unsigned long long TM = __builtin_amdgcn_ballot_w64(tonp & !(tk < vk));  // moving top path nodes (a prefix)
+      const unsigned long long TGE = __builtin_amdgcn_ballot_w64(!(tk < ts));
+      const unsigned long long TLT = __builtin_amdgcn_ballot_w64(ts < tk);
+      const unsigned long long TW = ((TGE & kOdd) | (TLT & ~kOdd)) & kTop;
+      const unsigned long long TP = __builtin_amdgcn_ballot_w64((TW & tself) == tself);
+      const unsigned long long TM = TP & __builtin_amdgcn_ballot_w64(!(tk < vk));  // moving top path nodes (a prefix)
       const int x5l = 95 - __clzll((long long)(TP >> 32));  // the level-5 path lane
       // window below node x5 (levels 6..10; every level-5 node has two children while len >= 127)
       const int lim = (len - 1) / 2;
@@ -159,11 +179,14 @@ LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
       const K pk = wshfl(tk, src);
       const V pv = (V)__shfl((int)tv, src);
       const K ks = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, kk), 0xb1, 0xf, 0xf, false));
-      const bool win = wlane & ((right & !(kk < ks)) | (!right & (ks < kk)));
-      const unsigned long long W = __builtin_amdgcn_ballot_w64(win);
-      const bool onp = wlane & ((W & anc) == anc) & ((win & (par < lim)) | (node == only));
-      const bool mv = onp & !(kk < vk) & (((TM >> x5l) & 1ull) != 0ull);  // below a node that stays nothing moves
-      const unsigned long long M = __builtin_amdgcn_ballot_w64(mv);
+      // (the only child -- node len - 1, a leaf -- counts as winning: its clamped sibling read is itself)
+      const unsigned long long ONLY = __builtin_amdgcn_ballot_w64(node == only);
+      const unsigned long long W = ((((__builtin_amdgcn_ballot_w64(!(kk < ks)) & kOdd) |
+                                      (__builtin_amdgcn_ballot_w64(ks < kk) & ~kOdd)) & kWin) | ONLY);
+      const unsigned long long P = __builtin_amdgcn_ballot_w64((W & wself) == wself) &
+                                   (__builtin_amdgcn_ballot_w64(par < lim) | ONLY) & kWin;  // window path nodes
+      const unsigned long long M = P & __builtin_amdgcn_ballot_w64(!(kk < vk)) & (0ull - ((TM >> x5l) & 1ull));
+      const bool mv = ((M >> lane) & 1ull) != 0ull;  // (below a node that stays nothing moves)
       if (mv & (lev > 1)) {  // (level 6's parent is x5, in registers)
         key[par] = kk;
         val[par] = vl;
@@ -178,7 +201,7 @@ LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
       if (M) {
         int hole = __builtin_amdgcn_readlane(node, 63 - __clzll((long long)M));
         // a window that the path leaves through its bottom with every node moved continues below
-        unsigned long long Mw = M, Pw = __builtin_amdgcn_ballot_w64(onp);
+        unsigned long long Mw = M, Pw = P;
         int xw = hole;
         while (Mw == Pw && (Mw & bottom) && xw <= lim) {
           const int node2 = (xw << lev) + cst;
@@ -207,6 +230,13 @@ LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
         if (tl == th) { tk = vk; tv = vv; }
       }
     }
+    {  // the last, partial block: slots len + 1 .. (its end, or top_len)
+      const int p = len + 1, q = p & ~63;
+      if ((p & 63) != 0 && q + lane >= p && q + lane <= top_len) {
+        key[q + lane] = ok;
+        val[q + lane] = ov;
+      }
+    }
   }
   // Heaps of at most 127: the whole heap in registers, the top as above and level 6 (nodes 63..126) in a
   // second pair, node 63 + l in lane l (children of top lane l >= 32: bottom lanes 2l - 64, 2l - 63).  A
@@ -216,7 +246,6 @@ LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
   K bk = key[min(63 + lane, len)];
   V bv = val[min(63 + lane, len)];
   const int bl = lane;
-  const bool bright = (bl & 1) != 0;
   for (; len >= 1; --len) {
     const K vk = len <= 62 ? rdlane(tk, len + 1) : rdlane(bk, len - 63);
     const V vv = (V)__builtin_amdgcn_readlane(len <= 62 ? (int)tv : (int)bv, len <= 62 ? len + 1 : len - 63);
@@ -226,17 +255,22 @@ LG_DEVICE void sort_heap_wave(const SortView<K, V>& a, int first, int last) {
     const int lim = (len - 1) / 2;
     const int only = (len & 1) == 0 ? len - 1 : -1;  // the only (left) child of node lim
     const K ts = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, tk), 0xb1, 0xf, 0xf, false));
-    const bool twin = ttop & ((todd & !(tk < ts)) | (!todd & (ts < tk)));
-    const unsigned long long TW = __builtin_amdgcn_ballot_w64(twin);
-    const bool tonp = ttop & ((TW & tanc) == tanc) & ((twin & ((tl >> 1) - 1 < lim)) | (tl - 1 == only));
-    const unsigned long long TP = __builtin_amdgcn_ballot_w64(tonp);
-    const unsigned long long TM = __builtin_amdgcn_ballot_w64(tonp & !(tk < vk));  // moving top path nodes
+    // (the only child, a leaf, counts as winning; its parent is node lim, the last with children)
+    const unsigned long long TONLY = __builtin_amdgcn_ballot_w64(tl - 1 == only) & kTop;
+    const unsigned long long TW = ((((__builtin_amdgcn_ballot_w64(!(tk < ts)) & kOdd) |
+                                     (__builtin_amdgcn_ballot_w64(ts < tk) & ~kOdd)) & kTop) | TONLY);
+    const unsigned long long TP = __builtin_amdgcn_ballot_w64((TW & tself) == tself) &
+                                  (__builtin_amdgcn_ballot_w64((tl >> 1) - 1 < lim) | TONLY);
+    const unsigned long long TM = TP & __builtin_amdgcn_ballot_w64(!(tk < vk));  // moving top path nodes
     const bool x5m = (TM >> 32) != 0ull;  // the level-5 path node moved (only then can level 6 move)
-    const int x5l = x5m ? 95 - __clzll((long long)(TP >> 32)) : 0;
+    const int x5l = x5m ? 95 - __clzll((long long)(TP >> 32)) : 32;
+    // level 6: the pair below x5 (lanes 2 x5l - 64, + 1), both children when x5 < lim, else the only one
     const K bs = __builtin_bit_cast(K, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, bk), 0xb1, 0xf, 0xf, false));
-    const bool bwin = (bright & !(bk < bs)) | (!bright & (bs < bk));
-    const bool bonp = x5m & (32 + (bl >> 1) == x5l) & ((bwin & (31 + (bl >> 1) < lim)) | (63 + bl == only));
-    const unsigned long long BM = __builtin_amdgcn_ballot_w64(bonp & !(bk < vk));
+    const unsigned long long BW = (__builtin_amdgcn_ballot_w64(!(bk < bs)) & kOdd) |
+                                  (__builtin_amdgcn_ballot_w64(bs < bk) & ~kOdd);
+    const unsigned long long BONLY = __builtin_amdgcn_ballot_w64(63 + bl == only);
+    const unsigned long long BP = x5m ? (3ull << (2 * x5l - 64)) & ((x5l - 1 < lim ? BW : 0ull) | BONLY) : 0ull;
+    const unsigned long long BM = BP & __builtin_amdgcn_ballot_w64(!(bk < vk));
     // pulls from the moving child (old elements): top lanes < 32 from the top, level-5 lanes from level 6
     const unsigned long long cm = tl < 32 ? (TM >> c0) & 3ull : (BM >> (c0 - 64)) & 3ull;
     const int src = (cm ? c0 + (int)((cm & 1ull) ^ 1ull) : tl) & 63;
