@@ -23,6 +23,15 @@ def _ensure_built():
     subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "liblego_oracle.so"])
 
 
+def make_example(target):
+    """make examples/<target>, serialised across pytest-xdist workers (a worker relinking a tool that another
+    one is executing fails with ETXTBSY)."""
+    import fcntl
+    with open(os.path.join(REPO, "examples", ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), target])
+
+
 @pytest.fixture(scope="session", autouse=True)
 def built():
     _ensure_built()

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import helpers as Hs
+from conftest import make_example
 from lego_amd import _abi as A
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -16,7 +17,7 @@ EXE = os.path.join(REPO, "examples", "replay_pipeline")
 
 
 def build():
-    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "replay_pipeline"])
+    make_example("replay_pipeline")
 
 
 def write_scans(path, scans):
@@ -93,7 +94,7 @@ def test_rosbag_replay_equals_direct_replay(gpu, tmp_path):
     """The same sweeps replayed from a ROS bag (PointCloud2 decoded zero-copy, lego_rosbag.hpp) and from
     a plain file give the identical odometry line."""
     build()
-    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "bag_tool"])
+    make_example("bag_tool")
     cfg = A.synth_cfg("vlp16")
     scans = [A.synth_scan(cfg, 5, k) for k in range(5)]
     f = tmp_path / "s.bin"
@@ -137,7 +138,7 @@ def _problem():
 
 
 def test_scan2map_mirror_fails_loudly_without_device(tmp_path):
-    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "scan2map"])
+    make_example("scan2map")
     import lego_amd
     if lego_amd.device_count() > 0:
         pytest.skip("a HIP device is visible")
@@ -152,7 +153,7 @@ def test_scan2map_mirror_matches_oracle(gpu, tmp_path):
     """ScanToMapOptimization (the C++ mirror of MapOptimization's LM members and scan2MapOptimization)
     reproduces the oracle's optimised transformTobeMapped."""
     import oracle as O
-    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "scan2map"])
+    make_example("scan2map")
     pr = _problem()
     f = tmp_path / "p.bin"
     _write_problem(str(f), pr)
@@ -182,7 +183,7 @@ def _write_cycles(path, assocs):
 
 
 def test_mapping_mirror_fails_loudly_without_device(tmp_path):
-    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "mapping"])
+    make_example("mapping")
     import lego_amd
     if lego_amd.device_count() > 0:
         pytest.skip("a HIP device is visible")
@@ -198,7 +199,7 @@ def test_mapping_mirror_matches_oracle_loop(gpu, tmp_path):
     transformAftMapped every cycle and its key-frame count."""
     from lego_amd import mapping as M
     from test_gpu_mapping_loop import _emitted, mapping_step_oracle
-    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "mapping"])
+    make_example("mapping")
     assocs = _emitted(6, 26)
     f = tmp_path / "c.bin"
     _write_cycles(str(f), assocs)

@@ -16,7 +16,8 @@ TOOL = os.path.join(REPO, "examples", "bag_tool")
 
 
 def build():
-    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "examples"), "bag_tool"])
+    from conftest import make_example
+    make_example("bag_tool")
 
 
 def write_scans(path, scans):
