@@ -329,11 +329,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(args.dist_backend)
     ndev = torch.cuda.device_count()
     local_dev = local % max(ndev, 1)  # == local on a full node; lets a 1-GPU box rehearse N>1 with gloo
-    torch.cuda.set_device(local_dev)
+    torch.cuda.set_device(local_dev)  # before the process group: RCCL's barrier and collectives use this device
+    if world > 1:
+        dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", local_dev)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
