@@ -53,6 +53,9 @@ def build_frontend(force=False, profile=False):
             cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", target]
             print(" ".join(cmd), flush=True)
             subprocess.check_call(cmd)
+        print("[build] %s: rebuilt for %s" % (os.path.relpath(target, REPO), ARCH), flush=True)
+    else:
+        print("[build] %s: up to date (newer than every source and header)" % os.path.relpath(target, REPO), flush=True)
     return target
 
 
@@ -67,6 +70,8 @@ def build_synth(force=False):
 
 
 def build_all(force=False):
+    """force (or LEGO_FORCE_BUILD=1): recompile even when the libraries are newer than their sources."""
+    force = force or os.environ.get("LEGO_FORCE_BUILD") == "1"
     build_synth(force)
     build_frontend(force)
 
