@@ -1806,29 +1806,64 @@ LG_DEVICE void sw_classify(const LgParams& P, int c, int lab, int g, bool& pseg,
   }
 }
 
+// kRank (tiles of a scan <= SW_MAX_TILES): also ranks the tile's feasible roots in raster order and leaves
+// each root's rank in its label word, label[r] = -(2 + rank within the tile), 999999 for an infeasible
+// root, so k_sw_emit<true> labels every cell from its root's tile offset and no k_sw_rank launch is needed.
+// (Only a root's own tile writes its label word here; other tiles read the root's size / rows, untouched.)
+#define SW_MAX_TILES 1024
+template <bool kRank>
 __global__ __launch_bounds__(SW_NT) void k_sw_count(LgParams P, LgBufs B) {
-  __shared__ int red[3 * (SW_NT / 64)];
+  constexpr int NW = SW_NT / 64;
+  __shared__ int red[3 * NW];
+  __shared__ int wcnt[4 * NW];
   const int s = P.s0 + blockIdx.y, VH = P.VH;
   const int* parent = B.cc_parent + (size_t)s * VH;
   const int* ccnt = B.cc_cnt + (size_t)s * VH;
   const unsigned long long* cmsk = B.cc_mask + (size_t)s * VH;
   const int8_t* ground = B.ground + (size_t)s * VH;
+  int32_t* label = B.label + (size_t)s * VH;
   int nroot = 0, nseg = 0, nout = 0;
+  bool rt[4], rf[4];
+  unsigned long long mf[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int c = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
-    if (c >= VH) continue;
-    const int r = parent[c];
-    int lab = -1;
-    if (r >= 0) {
-      const bool feas = sw_feasible(P, ccnt[r], cmsk[r]);
-      lab = feas ? 1 : 999999;
-      nroot += (r == c && feas) ? 1 : 0;
+    rt[u] = rf[u] = false;
+    if (c < VH) {
+      const int r = parent[c];
+      int lab = -1;
+      if (r >= 0) {
+        const bool feas = sw_feasible(P, ccnt[r], cmsk[r]);
+        lab = feas ? 1 : 999999;
+        rt[u] = r == c;
+        rf[u] = rt[u] && feas;
+        nroot += rf[u] ? 1 : 0;
+      }
+      bool pseg, pout;
+      sw_classify(P, c, lab, ground[c], pseg, pout);
+      nseg += pseg;
+      nout += pout;
     }
-    bool pseg, pout;
-    sw_classify(P, c, lab, ground[c], pseg, pout);
-    nseg += pseg;
-    nout += pout;
+    if (kRank) mf[u] = __ballot(rf[u]);
+  }
+  if (kRank) {  // k_sw_rank's raster-order ranks, local to the tile
+    if (lane_id() == 0) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wcnt[u * NW + wave_id()] = __popcll(mf[u]);
+    }
+    __syncthreads();
+    int k = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int before = 0, tot = 0;
+      for (int w = 0; w < NW; ++w) {
+        const int v = wcnt[u * NW + w];
+        before += w < wave_id() ? v : 0;
+        tot += v;
+      }
+      if (rt[u]) label[blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x] = rf[u] ? -(2 + k + before + popc_below(mf[u])) : 999999;
+      k += tot;
+    }
   }
   nroot = wave_sum(nroot);
   nseg = wave_sum(nseg);
@@ -1900,8 +1935,10 @@ __global__ __launch_bounds__(SW_NT) void k_sw_rank(LgParams P, LgBufs B) {
   }
 }
 
+template <bool kRank>
 __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
   __shared__ int4 base;
+  __shared__ int tpre[kRank ? SW_MAX_TILES : 1];  // kRank: exclusive prefix of the feasible roots over the scan's tiles
   const int s = P.s0 + blockIdx.y, V = P.V, H = P.H, VH = P.VH;
   const int* parent = B.cc_parent + (size_t)s * VH;
   const int* clab = B.cc_cnt + (size_t)s * VH;
@@ -1918,7 +1955,25 @@ __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
   int32_t* ring_start = B.ring_start + (size_t)s * V;
   int32_t* ring_end = B.ring_end + (size_t)s * V;
   const bool swap_axes = B.fe_state[2 * s + 1] > 0;  // not the initialisation scan (:1414-1416)
-  const int4 b0 = sw_tile_base(B, s, &base);
+  if (kRank) {  // the scan's tile offsets of the feasible roots (wave 0: a lane per 16 tiles, then a wave scan)
+    if (wave_id() == 0) {
+      const int4* tc = B.seg_tiles + (size_t)s * gridDim.x;
+      const int nt = (int)gridDim.x, per = (nt + 63) / 64, t0 = lane_id() * per;
+      int own = 0;
+      for (int t = t0; t < min(t0 + per, nt); ++t) own += tc[t].x;
+      int incl = own;  // inclusive wave scan of the lanes' sums
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane_id() >= o) incl += v;
+      }
+      int a = incl - own;
+      for (int t = t0; t < min(t0 + per, nt); ++t) {
+        tpre[t] = a;
+        a += tc[t].x;
+      }
+    }
+  }
+  const int4 b0 = sw_tile_base(B, s, &base);  // (its barrier also publishes tpre)
   // The tile's 4 x SW_NT cells: every load of the four rounds in flight together, then one barrier
   // for the raster-order offsets of both compactions (wave counts of each round in LDS).
   __shared__ int wcnt[2 * 4 * (SW_NT / 64)];
@@ -1929,8 +1984,22 @@ __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
     r[u] = c[u] < VH ? parent[c[u]] : -1;
     g[u] = c[u] < VH ? ground[c[u]] : 0;
   }
+  if (kRank) {
+    // the root's label word: -(2 + rank in its tile) from k_sw_count<true>, or already the final label (its own
+    // tile's k_sw_emit may have stored it), or 999999; the first decodes to the label k_sw_rank would give
 #pragma unroll
-  for (int u = 0; u < 4; ++u) lab[u] = r[u] < 0 ? -1 : clab[r[u]];
+    for (int u = 0; u < 4; ++u) {
+      if (r[u] < 0) {
+        lab[u] = -1;
+      } else {
+        const int v = label[r[u]];
+        lab[u] = v <= -2 ? tpre[r[u] / SW_TILE] + (-v - 2) + 1 : v;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) lab[u] = r[u] < 0 ? -1 : clab[r[u]];
+  }
   bool pseg[4], pout[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -5100,11 +5169,17 @@ int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_sw_roots, g, dim3(SW_NT), 0, st, P, B);
     LG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_sw_count, g, dim3(SW_NT), 0, st, P, B);
-    LG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_sw_rank, g, dim3(SW_NT), 0, st, P, B);
-    LG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_sw_emit, g, dim3(SW_NT), 0, st, P, B);
+    if (g.x <= SW_MAX_TILES) {  // the roots ranked inside k_sw_count (one launch fewer on the front end's chain)
+      hipLaunchKernelGGL(k_sw_count<true>, g, dim3(SW_NT), 0, st, P, B);
+      LG_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_sw_emit<true>, g, dim3(SW_NT), 0, st, P, B);
+    } else {
+      hipLaunchKernelGGL(k_sw_count<false>, g, dim3(SW_NT), 0, st, P, B);
+      LG_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_sw_rank, g, dim3(SW_NT), 0, st, P, B);
+      LG_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_sw_emit<false>, g, dim3(SW_NT), 0, st, P, B);
+    }
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_sw_finish<1024>, dim3(S), dim3(1024), 0, st, P, B, (int)g.x);
   } else {
