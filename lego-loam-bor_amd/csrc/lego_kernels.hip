@@ -1620,9 +1620,9 @@ __global__ __launch_bounds__(1024) void k_segment_lds(LgParams P, LgBufs B) {
 //   k_sw_local   union of the edges inside 2-D tiles in LDS (parent := tile-local root)
 //   k_sw_bound   union of the edges crossing tile borders (and the wrap), on the global parent[]
 //   k_sw_roots   full path compression; size and non-seed row mask of every root
-//   k_sw_count   per tile: feasible roots, segmented cells, outliers
-//   k_sw_rank    label of every root: 1 + its raster rank among feasible roots, or 999999
-//   k_sw_emit    label image and the raster-order compaction (:358-396) at tile offsets
+//   k_sw_count   per tile: feasible roots, segmented cells, outliers; each root's rank within its tile
+//   k_sw_emit    label image (a root's label: 1 + its raster rank among the scan's feasible roots, or
+//                999999) and the raster-order compaction (:358-396) at tile offsets
 //   k_sw_finish  one workgroup a scan: 2-D scan compaction, adjustDistortion, counts
 #define SW_NT 256
 #define SW_TILE (SW_NT * 4)
@@ -1806,12 +1806,11 @@ LG_DEVICE void sw_classify(const LgParams& P, int c, int lab, int g, bool& pseg,
   }
 }
 
-// kRank (tiles of a scan <= SW_MAX_TILES): also ranks the tile's feasible roots in raster order and leaves
-// each root's rank in its label word, label[r] = -(2 + rank within the tile), 999999 for an infeasible
-// root, so k_sw_emit<true> labels every cell from its root's tile offset and no k_sw_rank launch is needed.
-// (Only a root's own tile writes its label word here; other tiles read the root's size / rows, untouched.)
-#define SW_MAX_TILES 1024
-template <bool kRank>
+// Also ranks the tile's feasible roots in raster order and leaves each root's rank in its label word,
+// label[r] = -(2 + rank within the tile), 999999 for an infeasible root, so k_sw_emit labels every cell from
+// its root's tile offset (no separate ranking launch).  Only a root's own tile writes its label word here;
+// other tiles read the root's size / rows, which stay untouched.
+#define SW_MAX_TILES ((64 * 2048) / SW_TILE)  // lego_params_validate: V <= 64, H <= 2048
 __global__ __launch_bounds__(SW_NT) void k_sw_count(LgParams P, LgBufs B) {
   constexpr int NW = SW_NT / 64;
   __shared__ int red[3 * NW];
@@ -1844,9 +1843,9 @@ __global__ __launch_bounds__(SW_NT) void k_sw_count(LgParams P, LgBufs B) {
       nseg += pseg;
       nout += pout;
     }
-    if (kRank) mf[u] = __ballot(rf[u]);
+    mf[u] = __ballot(rf[u]);
   }
-  if (kRank) {  // k_sw_rank's raster-order ranks, local to the tile
+  {  // raster-order ranks of the feasible roots, local to the tile
     if (lane_id() == 0) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) wcnt[u * NW + wave_id()] = __popcll(mf[u]);
@@ -1893,55 +1892,12 @@ LG_DEVICE int4 sw_tile_base(const LgBufs& B, int s, int4* sh) {
   return *sh;
 }
 
-__global__ __launch_bounds__(SW_NT) void k_sw_rank(LgParams P, LgBufs B) {
-  __shared__ int4 base;
-  constexpr int NW = SW_NT / 64;
-  __shared__ int wcnt[4 * NW];
-  const int s = P.s0 + blockIdx.y, VH = P.VH;
-  const int* parent = B.cc_parent + (size_t)s * VH;
-  int* ccnt = B.cc_cnt + (size_t)s * VH;
-  const unsigned long long* cmsk = B.cc_mask + (size_t)s * VH;
-  const int k0 = sw_tile_base(B, s, &base).x;
-  // the four rounds' loads in flight together, one barrier for the raster-order ranks
-  int c[4];
-  bool root[4], feas[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    c[u] = blockIdx.x * SW_TILE + u * SW_NT + threadIdx.x;
-    root[u] = c[u] < VH && parent[c[u]] == c[u];
-  }
-  unsigned long long mf[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    feas[u] = root[u] && sw_feasible(P, ccnt[c[u]], cmsk[c[u]]);
-    mf[u] = __ballot(feas[u]);
-  }
-  if (lane_id() == 0) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) wcnt[u * NW + wave_id()] = __popcll(mf[u]);
-  }
-  __syncthreads();
-  int k = k0;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    int before = 0, tot = 0;
-    for (int w = 0; w < NW; ++w) {
-      const int v = wcnt[u * NW + w];
-      before += w < wave_id() ? v : 0;
-      tot += v;
-    }
-    if (root[u]) ccnt[c[u]] = feas[u] ? k + before + popc_below(mf[u]) + 1 : 999999;  // the root's word now holds its label
-    k += tot;
-  }
-}
 
-template <bool kRank>
 __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
   __shared__ int4 base;
-  __shared__ int tpre[kRank ? SW_MAX_TILES : 1];  // kRank: exclusive prefix of the feasible roots over the scan's tiles
+  __shared__ int tpre[SW_MAX_TILES];  // exclusive prefix of the feasible roots over the scan's tiles
   const int s = P.s0 + blockIdx.y, V = P.V, H = P.H, VH = P.VH;
   const int* parent = B.cc_parent + (size_t)s * VH;
-  const int* clab = B.cc_cnt + (size_t)s * VH;
   const int8_t* ground = B.ground + (size_t)s * VH;
   const float* range = B.range + (size_t)s * VH;
   const float4* cloud = B.cloud + (size_t)s * VH;
@@ -1955,7 +1911,7 @@ __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
   int32_t* ring_start = B.ring_start + (size_t)s * V;
   int32_t* ring_end = B.ring_end + (size_t)s * V;
   const bool swap_axes = B.fe_state[2 * s + 1] > 0;  // not the initialisation scan (:1414-1416)
-  if (kRank) {  // the scan's tile offsets of the feasible roots (wave 0: a lane per 16 tiles, then a wave scan)
+  {  // the scan's tile offsets of the feasible roots (wave 0: a lane per (tiles / 64) tiles, then a wave scan)
     if (wave_id() == 0) {
       const int4* tc = B.seg_tiles + (size_t)s * gridDim.x;
       const int nt = (int)gridDim.x, per = (nt + 63) / 64, t0 = lane_id() * per;
@@ -1984,9 +1940,9 @@ __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
     r[u] = c[u] < VH ? parent[c[u]] : -1;
     g[u] = c[u] < VH ? ground[c[u]] : 0;
   }
-  if (kRank) {
-    // the root's label word: -(2 + rank in its tile) from k_sw_count<true>, or already the final label (its own
-    // tile's k_sw_emit may have stored it), or 999999; the first decodes to the label k_sw_rank would give
+  {
+    // the root's label word: -(2 + rank in its tile) from k_sw_count, or already the final label (its own tile's
+    // k_sw_emit may have stored it), or 999999; the first decodes to 1 + the root's raster rank in the scan
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (r[u] < 0) {
@@ -1996,9 +1952,6 @@ __global__ __launch_bounds__(SW_NT) void k_sw_emit(LgParams P, LgBufs B) {
         lab[u] = v <= -2 ? tpre[r[u] / SW_TILE] + (-v - 2) + 1 : v;
       }
     }
-  } else {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) lab[u] = r[u] < 0 ? -1 : clab[r[u]];
   }
   bool pseg[4], pout[4];
 #pragma unroll
@@ -5169,17 +5122,10 @@ int lg_launch_segment(const LgParams& P, const LgBufs& B, int S, hipStream_t st)
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_sw_roots, g, dim3(SW_NT), 0, st, P, B);
     LG_CHECK_LAUNCH();
-    if (g.x <= SW_MAX_TILES) {  // the roots ranked inside k_sw_count (one launch fewer on the front end's chain)
-      hipLaunchKernelGGL(k_sw_count<true>, g, dim3(SW_NT), 0, st, P, B);
-      LG_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_sw_emit<true>, g, dim3(SW_NT), 0, st, P, B);
-    } else {
-      hipLaunchKernelGGL(k_sw_count<false>, g, dim3(SW_NT), 0, st, P, B);
-      LG_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_sw_rank, g, dim3(SW_NT), 0, st, P, B);
-      LG_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_sw_emit<false>, g, dim3(SW_NT), 0, st, P, B);
-    }
+    if (g.x > SW_MAX_TILES) return LEGO_EINVAL;  // (unreachable for validated parameters)
+    hipLaunchKernelGGL(k_sw_count, g, dim3(SW_NT), 0, st, P, B);  // counts + the tile-local root ranks
+    LG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_sw_emit, g, dim3(SW_NT), 0, st, P, B);
     LG_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_sw_finish<1024>, dim3(S), dim3(1024), 0, st, P, B, (int)g.x);
   } else {
